@@ -1,0 +1,358 @@
+"""Experiment configuration (expconf): parsing, defaults and validation.
+
+Reference: `schemas/expconf/v0/*.json` (JSON-schema with defaults/unions) and
+`harness/determined/_experiment_config.py`. The same YAML documents are accepted; instead of a
+JSON-schema engine (none is installed here) the schema is a small declarative table below, which
+fills defaults, checks types/enums/ranges and reports every error at once.
+"""
+import copy
+from typing import Any, Dict, List, Optional, Tuple
+
+import yaml
+
+from determined_clone_amd.errors import InvalidConfigurationException
+
+LENGTH_UNITS = ("batches", "records", "epochs")
+
+
+def _length_ok(v: Any) -> bool:
+    return (isinstance(v, dict) and len(v) == 1 and next(iter(v)) in LENGTH_UNITS
+            and isinstance(next(iter(v.values())), int) and next(iter(v.values())) >= 0)
+
+
+# --------------------------------------------------------------------------- schema tables
+# field -> (allowed python types, default)
+TOP_LEVEL: Dict[str, Tuple[Tuple[type, ...], Any]] = {
+    "bind_mounts": ((list,), []),
+    "checkpoint_policy": ((str,), "best"),
+    "checkpoint_storage": ((dict,), None),
+    "data": ((dict,), {}),
+    "data_layer": ((dict,), None),
+    "debug": ((bool,), False),
+    "description": ((str,), None),
+    "entrypoint": ((str, list), None),
+    "environment": ((dict,), {}),
+    "hyperparameters": ((dict,), {}),
+    "internal": ((type(None),), None),
+    "labels": ((list,), []),
+    "log_policies": ((list,), []),
+    "max_restarts": ((int,), 5),
+    "min_checkpoint_period": ((dict,), {"batches": 0}),
+    "min_validation_period": ((dict,), {"batches": 0}),
+    "name": ((str,), None),
+    "optimizations": ((dict,), {}),
+    "pbs": ((dict,), {}),
+    "perform_initial_validation": ((bool,), False),
+    "profiling": ((dict,), {}),
+    "project": ((str,), ""),
+    "records_per_epoch": ((int,), 0),
+    "reproducibility": ((dict,), {}),
+    "resources": ((dict,), {}),
+    "scheduling_unit": ((int,), 100),
+    "searcher": ((dict,), None),
+    "security": ((dict,), None),
+    "slurm": ((dict,), {}),
+    "tensorboard_storage": ((dict,), None),
+    "workspace": ((str,), ""),
+}
+
+OPTIMIZATIONS = {
+    "aggregation_frequency": ((int,), 1),
+    "auto_tune_tensor_fusion": ((bool,), False),
+    "average_aggregated_gradients": ((bool,), True),
+    "average_training_metrics": ((bool,), True),
+    "gradient_compression": ((bool,), False),
+    "grad_updates_size_file": ((str,), None),
+    "mixed_precision": ((str,), "O0"),
+    "tensor_fusion_cycle_time": ((int,), 1),
+    "tensor_fusion_threshold": ((int,), 64),
+}
+
+RESOURCES = {
+    "agent_label": ((str,), None),
+    "devices": ((list,), []),
+    "max_slots": ((int,), None),
+    "native_parallel": ((bool,), False),
+    "priority": ((int,), None),
+    "resource_pool": ((str,), ""),
+    "shm_size": ((int, str), None),
+    "slots": ((int,), None),
+    "slots_per_trial": ((int,), 1),
+    "weight": ((int, float), 1),
+    "is_single_node": ((bool,), None),
+}
+
+REPRODUCIBILITY = {"experiment_seed": ((int,), None)}
+
+ENVIRONMENT = {
+    "image": ((str, dict), None),
+    "environment_variables": ((list, dict), []),
+    "pod_spec": ((dict,), None),
+    "registry_auth": ((dict,), None),
+    "force_pull_image": ((bool,), False),
+    "add_capabilities": ((list,), []),
+    "drop_capabilities": ((list,), []),
+    "proxy_ports": ((list,), []),
+}
+
+PROFILING = {
+    "enabled": ((bool,), False),
+    "begin_on_batch": ((int,), 0),
+    "end_after_batch": ((int,), None),
+    "sync_timings": ((bool,), True),
+}
+
+SEARCHER_COMMON = {
+    "name": ((str,), None),
+    "metric": ((str,), None),
+    "smaller_is_better": ((bool,), True),
+    "source_trial_id": ((int,), None),
+    "source_checkpoint_uuid": ((str,), None),
+}
+
+SEARCHERS: Dict[str, Dict[str, Tuple[Tuple[type, ...], Any]]] = {
+    "single": {"max_length": ((dict, int), None)},
+    "random": {"max_length": ((dict, int), None), "max_trials": ((int,), None),
+               "max_concurrent_trials": ((int,), 16)},
+    "grid": {"max_length": ((dict, int), None), "max_concurrent_trials": ((int,), 16)},
+    "async_halving": {"max_length": ((dict, int), None), "max_trials": ((int,), None),
+                      "num_rungs": ((int,), None), "divisor": ((int, float), 4),
+                      "max_concurrent_trials": ((int,), 16), "stop_once": ((bool,), False),
+                      "time_metric": ((str,), None), "max_time": ((int,), None)},
+    "adaptive_asha": {"max_length": ((dict, int), None), "max_trials": ((int,), None),
+                      "bracket_rungs": ((list,), []), "mode": ((str,), "standard"),
+                      "divisor": ((int, float), 4), "max_rungs": ((int,), 5),
+                      "max_concurrent_trials": ((int,), 16), "stop_once": ((bool,), False),
+                      "time_metric": ((str,), None), "max_time": ((int,), None)},
+    "custom": {"unit": ((str,), None)},
+}
+SEARCHER_ALIASES = {"asha": "async_halving"}
+
+CHECKPOINT_STORAGE_COMMON = {
+    "save_experiment_best": ((int,), 0),
+    "save_trial_best": ((int,), 1),
+    "save_trial_latest": ((int,), 1),
+}
+CHECKPOINT_STORAGE = {
+    "shared_fs": {"host_path": ((str,), None), "storage_path": ((str,), None),
+                  "container_path": ((str,), None), "checkpoint_path": ((str,), None),
+                  "tensorboard_path": ((str,), None), "propagation": ((str,), "rprivate")},
+    "directory": {"container_path": ((str,), None)},
+    "s3": {"bucket": ((str,), None), "access_key": ((str,), None), "secret_key": ((str,), None),
+           "endpoint_url": ((str,), None), "prefix": ((str,), None)},
+    "gcs": {"bucket": ((str,), None), "prefix": ((str,), None)},
+    "azure": {"container": ((str,), None), "connection_string": ((str,), None),
+              "account_url": ((str,), None), "credential": ((str,), None)},
+}
+
+HPARAM_TYPES = ("const", "int", "double", "log", "categorical")
+
+
+# --------------------------------------------------------------------------- helpers
+def _apply(section: Dict[str, Any], table: Dict[str, Tuple[Tuple[type, ...], Any]], where: str,
+           errors: List[str], allow_extra: bool = False) -> Dict[str, Any]:
+    out = dict(section)
+    for key, (types, default) in table.items():
+        if key not in out or out[key] is None:
+            out[key] = copy.deepcopy(default)
+            continue
+        v = out[key]
+        if float in types and isinstance(v, int) and not isinstance(v, bool):
+            continue
+        if bool not in types and isinstance(v, bool) and int in types:
+            errors.append(f"{where}.{key}: expected {'/'.join(t.__name__ for t in types)}, got bool")
+        elif not isinstance(v, types):
+            errors.append(f"{where}.{key}: expected {'/'.join(t.__name__ for t in types)}, "
+                          f"got {type(v).__name__}")
+    if not allow_extra:
+        for key in section:
+            if key not in table:
+                errors.append(f"{where}: unknown field '{key}'")
+    return out
+
+
+def _check_hparam(name: str, hp: Any, errors: List[str], path: str) -> Any:
+    """Normalise one hyperparameter definition (bare values become const; nested dicts without
+    ``type`` are nested hyperparameter groups)."""
+    where = f"{path}.{name}"
+    if not isinstance(hp, dict):
+        return {"type": "const", "val": hp}
+    if "type" not in hp:
+        return {k: _check_hparam(k, v, errors, where) for k, v in hp.items()}
+    t = hp["type"]
+    if t not in HPARAM_TYPES:
+        errors.append(f"{where}: unknown hyperparameter type '{t}'")
+        return hp
+    if t == "const":
+        if "val" not in hp:
+            errors.append(f"{where}: const hyperparameter needs 'val'")
+    elif t in ("int", "double", "log"):
+        for k in ("minval", "maxval"):
+            if k not in hp:
+                errors.append(f"{where}: {t} hyperparameter needs '{k}'")
+        if t == "log" and "base" not in hp:
+            hp = dict(hp, base=10.0)
+        if "minval" in hp and "maxval" in hp and hp["minval"] > hp["maxval"]:
+            errors.append(f"{where}: minval > maxval")
+        if t == "int" and any(not isinstance(hp.get(k), int) for k in ("minval", "maxval") if k in hp):
+            errors.append(f"{where}: int hyperparameter bounds must be integers")
+        if "count" in hp and (not isinstance(hp["count"], int) or hp["count"] < 1):
+            errors.append(f"{where}: count must be a positive integer")
+    elif t == "categorical":
+        vals = hp.get("vals")
+        if not isinstance(vals, list) or not vals:
+            errors.append(f"{where}: categorical hyperparameter needs non-empty 'vals'")
+    return hp
+
+
+def normalize_length(v: Any, where: str, errors: List[str]) -> Optional[Dict[str, int]]:
+    if v is None:
+        return None
+    if isinstance(v, int) and not isinstance(v, bool):
+        return {"batches": v}  # legacy unitless max_length
+    if not _length_ok(v):
+        errors.append(f"{where}: expected a length like {{batches: N}}, {{records: N}} or {{epochs: N}}")
+        return None
+    return dict(v)
+
+
+# --------------------------------------------------------------------------- entry points
+def parse(text_or_dict: Any) -> Dict[str, Any]:
+    if isinstance(text_or_dict, (str, bytes)):
+        cfg = yaml.safe_load(text_or_dict) or {}
+    else:
+        cfg = copy.deepcopy(text_or_dict)
+    if not isinstance(cfg, dict):
+        raise InvalidConfigurationException(["config must be a mapping"])
+    return cfg
+
+
+def complete(config: Any, cluster_defaults: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+    """Fill every default and validate; raises InvalidConfigurationException listing all errors."""
+    cfg = parse(config)
+    if cluster_defaults:
+        from determined_clone_amd.util import merge_dicts
+
+        cfg = merge_dicts(cluster_defaults, cfg)
+    errors: List[str] = []
+    cfg = _apply(cfg, TOP_LEVEL, "config", errors)
+    if cfg["checkpoint_policy"] not in ("best", "all", "none"):
+        errors.append("config.checkpoint_policy: must be one of best/all/none")
+    if cfg["max_restarts"] is not None and cfg["max_restarts"] < 0:
+        errors.append("config.max_restarts: must be >= 0")
+    cfg["optimizations"] = _apply(cfg["optimizations"] or {}, OPTIMIZATIONS, "optimizations", errors)
+    if cfg["optimizations"]["aggregation_frequency"] < 1:
+        errors.append("optimizations.aggregation_frequency: must be >= 1")
+    if cfg["optimizations"]["mixed_precision"] not in ("O0", "O1", "O2", "O3"):
+        errors.append("optimizations.mixed_precision: must be O0..O3")
+    cfg["resources"] = _apply(cfg["resources"] or {}, RESOURCES, "resources", errors)
+    if cfg["resources"]["slots_per_trial"] < 0:
+        errors.append("resources.slots_per_trial: must be >= 0")
+    cfg["reproducibility"] = _apply(cfg["reproducibility"] or {}, REPRODUCIBILITY, "reproducibility", errors)
+    cfg["environment"] = _apply(cfg["environment"] or {}, ENVIRONMENT, "environment", errors,
+                                allow_extra=True)
+    cfg["profiling"] = _apply(cfg["profiling"] or {}, PROFILING, "profiling", errors)
+    for key in ("min_validation_period", "min_checkpoint_period"):
+        cfg[key] = normalize_length(cfg[key], key, errors) or {"batches": 0}
+
+    # checkpoint storage
+    cs = cfg.get("checkpoint_storage")
+    if cs is not None:
+        t = cs.get("type")
+        if t not in CHECKPOINT_STORAGE:
+            errors.append(f"checkpoint_storage.type: unknown storage type '{t}'")
+        else:
+            table = dict(CHECKPOINT_STORAGE_COMMON, **CHECKPOINT_STORAGE[t])
+            table["type"] = ((str,), t)
+            cs = _apply(cs, table, "checkpoint_storage", errors)
+            if t == "shared_fs" and not cs.get("host_path"):
+                errors.append("checkpoint_storage.host_path: required for shared_fs")
+            if t == "directory" and not cs.get("container_path"):
+                errors.append("checkpoint_storage.container_path: required for directory")
+            cfg["checkpoint_storage"] = cs
+
+    # hyperparameters
+    hps = cfg.get("hyperparameters") or {}
+    cfg["hyperparameters"] = {k: _check_hparam(k, v, errors, "hyperparameters") for k, v in hps.items()}
+
+    # searcher
+    s = cfg.get("searcher")
+    if s is None:
+        errors.append("config.searcher: required")
+    else:
+        name = SEARCHER_ALIASES.get(s.get("name"), s.get("name"))
+        if name not in SEARCHERS:
+            errors.append(f"searcher.name: unknown searcher '{s.get('name')}'")
+        else:
+            table = dict(SEARCHER_COMMON, **SEARCHERS[name])
+            s = _apply(dict(s, name=name), table, "searcher", errors)
+            if name != "custom" and not s.get("metric"):
+                errors.append("searcher.metric: required")
+            if "max_length" in table:
+                if s.get("max_length") is None and not s.get("max_time"):
+                    errors.append("searcher.max_length: required")
+                s["max_length"] = normalize_length(s.get("max_length"), "searcher.max_length", errors)
+            if name in ("random", "async_halving", "adaptive_asha") and not s.get("max_trials"):
+                errors.append("searcher.max_trials: required")
+            if name == "async_halving" and not s.get("num_rungs"):
+                errors.append("searcher.num_rungs: required")
+            if name == "adaptive_asha" and s.get("mode") not in ("aggressive", "standard", "conservative"):
+                errors.append("searcher.mode: must be aggressive/standard/conservative")
+            if name in ("async_halving", "adaptive_asha") and s.get("divisor", 4) <= 1:
+                errors.append("searcher.divisor: must be > 1")
+            if name == "grid":
+                _check_grid(cfg["hyperparameters"], errors)
+            cfg["searcher"] = s
+    # log policies
+    for i, lp in enumerate(cfg["log_policies"]):
+        if not isinstance(lp, dict) or "pattern" not in lp:
+            errors.append(f"log_policies[{i}]: needs a 'pattern'")
+    if errors:
+        raise InvalidConfigurationException(errors)
+    return cfg
+
+
+def _check_grid(hps: Dict[str, Any], errors: List[str], path: str = "hyperparameters") -> None:
+    for k, hp in hps.items():
+        if not isinstance(hp, dict):
+            continue
+        if "type" not in hp:
+            _check_grid(hp, errors, f"{path}.{k}")
+        elif hp["type"] in ("int", "double", "log") and "count" not in hp:
+            errors.append(f"{path}.{k}: grid search needs 'count' for {hp['type']} hyperparameters")
+
+
+def searcher_unit(config: Dict[str, Any]) -> Optional[str]:
+    s = config.get("searcher") or {}
+    ml = s.get("max_length")
+    if isinstance(ml, dict) and ml:
+        return next(iter(ml))
+    if s.get("name") == "custom":
+        return s.get("unit")
+    return None
+
+
+def searcher_max_length(config: Dict[str, Any]) -> Optional[int]:
+    ml = (config.get("searcher") or {}).get("max_length")
+    if isinstance(ml, dict) and ml:
+        return int(next(iter(ml.values())))
+    return None
+
+
+def global_batch_size(config: Dict[str, Any], hparams: Dict[str, Any]) -> Optional[int]:
+    gbs = hparams.get("global_batch_size")
+    return int(gbs) if gbs is not None else None
+
+
+def length_to_batches(length: Dict[str, int], global_batch: Optional[int],
+                      records_per_epoch: int) -> int:
+    (unit, n), = length.items()
+    if unit == "batches":
+        return n
+    if global_batch is None or global_batch <= 0:
+        raise ValueError(f"converting {unit} to batches needs hyperparameters.global_batch_size")
+    if unit == "records":
+        return (n + global_batch - 1) // global_batch
+    if records_per_epoch <= 0:
+        raise ValueError("converting epochs to batches needs records_per_epoch")
+    return (n * records_per_epoch + global_batch - 1) // global_batch

@@ -1,0 +1,169 @@
+"""``core.init()`` and ``core.Context`` (reference: `harness/determined/core/_context.py`)."""
+import logging
+import os
+import pathlib
+import signal
+import sys
+import threading
+import traceback
+import types
+from typing import Any, Dict, Optional, Union
+
+from determined_clone_amd import _info, errors
+from determined_clone_amd.common import api, storage
+from determined_clone_amd.core._checkpoint import CheckpointContext, DummyCheckpointContext
+from determined_clone_amd.core._distributed import DistributedContext, DummyDistributedContext
+from determined_clone_amd.core._heartbeat import _Heartbeat
+from determined_clone_amd.core._preempt import DummyPreemptContext, PreemptContext, PreemptMode
+from determined_clone_amd.core._searcher import (DummySearcherContext, SearcherContext,
+                                                 _parse_searcher_units)
+from determined_clone_amd.core._train import DummyTrainContext, EarlyExitReason, TrainContext
+
+logger = logging.getLogger("determined_clone_amd.core")
+
+
+class TensorboardMode:
+    AUTO = "AUTO"
+    MANUAL = "MANUAL"
+
+
+class Context:
+    """Composition of checkpoint / distributed / preempt / searcher / train contexts."""
+
+    def __init__(self, checkpoint: CheckpointContext, distributed: Optional[DistributedContext] = None,
+                 preempt: Optional[PreemptContext] = None, train: Optional[TrainContext] = None,
+                 searcher: Optional[SearcherContext] = None,
+                 info: Optional[_info.ClusterInfo] = None, experimental: Any = None,
+                 _tensorboard_manager: Any = None, _heartbeat: Optional[_Heartbeat] = None,
+                 _session: Any = None) -> None:
+        self.checkpoint = checkpoint
+        self.distributed = distributed or DummyDistributedContext()
+        self.preempt = preempt or DummyPreemptContext(self.distributed)
+        self.train = train or DummyTrainContext()
+        self.searcher = searcher or DummySearcherContext(self.distributed)
+        self.info = info
+        from determined_clone_amd.core._experimental import (DummyExperimentalCoreContext,
+                                                             ExperimentalCoreContext)
+
+        self.experimental = experimental or DummyExperimentalCoreContext()
+        self._tensorboard_manager = _tensorboard_manager
+        self._heartbeat = _heartbeat
+        self._session = _session
+
+    def start(self) -> None:
+        self.preempt.start()
+        if self._tensorboard_manager is not None:
+            self._tensorboard_manager.start()
+        if self._heartbeat is not None:
+            self._heartbeat.start()
+
+    def __enter__(self) -> "Context":
+        self.start()
+        return self
+
+    def close(self, exc_type: Optional[type] = None, exc_val: Optional[BaseException] = None,
+              exc_tb: Optional[types.TracebackType] = None) -> None:
+        self.preempt.close()
+        self.distributed.close()
+        if self._tensorboard_manager is not None:
+            self._tensorboard_manager.close()
+        if self._heartbeat is not None:
+            self._heartbeat.close(exc_type, exc_val, exc_tb)
+
+    def __exit__(self, exc_type: Optional[type], exc_val: Optional[BaseException],
+                 exc_tb: Optional[types.TracebackType]) -> None:
+        self.close(exc_type, exc_val, exc_tb)
+        if isinstance(exc_val, errors.InvalidHP):
+            self.train.report_early_exit(EarlyExitReason.INVALID_HP)
+            logger.info("InvalidHP detected, converting to exit(0)")
+            sys.exit(0)
+
+
+def _install_stacktrace_on_sigusr1() -> None:
+    if not hasattr(signal, "SIGUSR1") or threading.current_thread() is not threading.main_thread():
+        return
+    old = None
+
+    def handler(signum: Any, frame: Any) -> None:
+        traceback.print_stack(frame, file=sys.stderr)
+        if callable(old):
+            old(signum, frame)
+
+    old = signal.signal(signal.SIGUSR1, handler)
+
+
+def _get_storage_manager(checkpoint_storage: Optional[Union[str, Dict[str, Any]]]) -> Optional[storage.StorageManager]:
+    if checkpoint_storage is None:
+        return None
+    if isinstance(checkpoint_storage, str):
+        return storage.from_string(checkpoint_storage)
+    if isinstance(checkpoint_storage, dict):
+        return storage.build(checkpoint_storage)
+    raise TypeError("checkpoint_storage must be a string, dictionary, or None")
+
+
+def _default_local_storage() -> str:
+    return os.environ.get("DET_LOCAL_STORAGE", os.path.join(os.path.expanduser("~"), ".local",
+                                                            "share", "determined_clone_amd"))
+
+
+def _dummy_init(*, distributed: Optional[DistributedContext] = None,
+                checkpoint_storage: Optional[Union[str, Dict[str, Any]]] = None,
+                tensorboard_path: Optional[pathlib.Path] = None,
+                preempt_mode: PreemptMode = PreemptMode.WorkersAskChief) -> Context:
+    distributed = distributed or DummyDistributedContext()
+    preempt = DummyPreemptContext(distributed, preempt_mode)
+    sm = _get_storage_manager(checkpoint_storage)
+    if sm is None:
+        base = _default_local_storage()
+        logger.info(f"no storage manager provided; storing checkpoints in {base}")
+        sm = storage.SharedFSStorageManager(base)
+    _install_stacktrace_on_sigusr1()
+    return Context(distributed=distributed, checkpoint=DummyCheckpointContext(distributed, sm),
+                   preempt=preempt, train=DummyTrainContext(tensorboard_path),
+                   searcher=DummySearcherContext(distributed))
+
+
+def init(*, distributed: Optional[DistributedContext] = None,
+         checkpoint_storage: Optional[Union[str, Dict[str, Any]]] = None,
+         preempt_mode: PreemptMode = PreemptMode.WorkersAskChief,
+         tensorboard_mode: str = TensorboardMode.AUTO) -> Context:
+    """Build a Core API context. Off-cluster (no ClusterInfo) returns a local context that keeps
+    checkpoints on disk and logs metrics."""
+    info = _info.get_cluster_info()
+    if info is None:
+        return _dummy_init(distributed=distributed, checkpoint_storage=checkpoint_storage,
+                           preempt_mode=preempt_mode)
+    session = api.Session(info.master_url, info.session_token)
+    if distributed is None and (len(info.container_addrs) > 1 or len(info.slot_ids) > 1):
+        raise ValueError("you must provide a valid DistributedContext for a multi-slot task")
+    distributed = distributed or DummyDistributedContext()
+    train = searcher = tb = None
+    sm = _get_storage_manager(checkpoint_storage)
+    if info.task_type == "TRIAL":
+        cfg = info.trial._config
+        from determined_clone_amd import tensorboard
+
+        tb = tensorboard.build(info.cluster_id, str(info.trial.experiment_id),
+                               str(info.trial.trial_id), cfg.get("checkpoint_storage") or {},
+                               rank=distributed.rank)
+        writer = tb.metric_writer() if (tb is not None and tensorboard_mode == TensorboardMode.AUTO) else None
+        train = TrainContext(session, info.trial.trial_id, info.trial._trial_run_id,
+                             info.trial.experiment_id, distributed, tensorboard_mode, tb, writer)
+        searcher = SearcherContext(session, distributed, info.trial.trial_id,
+                                   info.trial._trial_run_id, info.allocation_id,
+                                   _parse_searcher_units(cfg))
+        if sm is None:
+            sm = storage.build(cfg["checkpoint_storage"])
+    elif sm is None:
+        sm = storage.SharedFSStorageManager(_default_local_storage())
+    checkpoint = CheckpointContext(distributed, sm, session, info.task_id, info.allocation_id,
+                                   tensorboard_manager=tb)
+    preempt = PreemptContext(session, info.allocation_id, distributed, preempt_mode)
+    from determined_clone_amd.core._experimental import ExperimentalCoreContext
+
+    exp = ExperimentalCoreContext(session, info.trial.trial_id) if info.task_type == "TRIAL" else None
+    _install_stacktrace_on_sigusr1()
+    return Context(checkpoint=checkpoint, distributed=distributed, preempt=preempt, train=train,
+                   searcher=searcher, info=info, experimental=exp, _tensorboard_manager=tb,
+                   _session=session)

@@ -1,0 +1,135 @@
+"""ResNet-50 (v1.5) for the headline benchmark trial.
+
+The reference benchmarks torchvision's ``resnet50`` inside a PyTorchTrial
+(`examples/deepspeed_autotune/torchvision/`); torchvision is not part of this image, so the
+architecture is defined here. It is laid out for MI355X rather than copied:
+
+* activations are NHWC (``channels_last``) bf16 end to end, so MIOpen picks its NHWC
+  implicit-GEMM (MFMA) convolutions and no layout transposes run between layers;
+* every ``BatchNorm -> (+ residual) -> ReLU`` tail is ONE module, ``BatchNormAct2d``, which on a
+  GPU runs the hand-written NHWC HIP kernels in ``ops/csrc/batchnorm.hip`` (stats + apply + add +
+  ReLU in two passes over HBM instead of four separate PyTorch ops); BN affine params and running
+  stats stay fp32 while activations are bf16;
+* the stem max-pool and the classifier are plain PyTorch ops (they are <2 % of step time).
+"""
+from typing import List, Optional, Type
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from determined_clone_amd.ops import batchnorm as bn_ops
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """BatchNorm2d with an optional fused residual add and ReLU.
+
+    ``forward(x, residual=None)`` computes ``act(bn(x) + residual)``. Parameters/buffers have the
+    same names as ``nn.BatchNorm2d`` so state dicts interchange with torchvision checkpoints.
+    """
+
+    def __init__(self, num_features: int, relu: bool = True, eps: float = 1e-5,
+                 momentum: float = 0.1) -> None:
+        super().__init__(num_features, eps=eps, momentum=momentum)
+        self.relu = relu
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        return bn_ops.batch_norm_act(
+            x,
+            self.weight,
+            self.bias,
+            self.running_mean,
+            self.running_var,
+            residual=residual,
+            training=self.training,
+            momentum=self.momentum,
+            eps=self.eps,
+            relu=self.relu,
+            num_batches_tracked=self.num_batches_tracked,
+        )
+
+
+def _conv(cin: int, cout: int, k: int, stride: int = 1) -> nn.Conv2d:
+    return nn.Conv2d(cin, cout, kernel_size=k, stride=stride, padding=k // 2, bias=False)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, width: int, stride: int = 1) -> None:
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = _conv(cin, width, 1)
+        self.bn1 = BatchNormAct2d(width)
+        self.conv2 = _conv(width, width, 3, stride)  # v1.5: stride on the 3x3
+        self.bn2 = BatchNormAct2d(width)
+        self.conv3 = _conv(width, cout, 1)
+        self.bn3 = BatchNormAct2d(cout)  # bn3 + residual + relu fused
+        self.downsample: Optional[nn.Module] = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(
+                _conv(cin, cout, 1, stride), BatchNormAct2d(cout, relu=False)
+            )
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), residual=identity)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers: List[int], num_classes: int = 1000,
+                 block: Type[Bottleneck] = Bottleneck, zero_init_residual: bool = True) -> None:
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = BatchNormAct2d(64)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        cin = 64
+        stages = []
+        for i, (n, width) in enumerate(zip(layers, [64, 128, 256, 512])):
+            blocks = []
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                blocks.append(block(cin, width, stride))
+                cin = width * block.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        self.fc = nn.Linear(cin, num_classes)
+
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+
+def resnet50(num_classes: int = 1000) -> ResNet:
+    return ResNet([3, 4, 6, 3], num_classes=num_classes)
+
+
+def resnet18_bottleneck_tiny(num_classes: int = 10) -> ResNet:
+    """A 4-block bottleneck ResNet for fast CPU tests of the same code path."""
+    return ResNet([1, 1, 1, 1], num_classes=num_classes)
+
+
+def to_mi355x_layout(model: nn.Module, dtype: torch.dtype = torch.bfloat16) -> nn.Module:
+    """Convert a ResNet to the MI355X training layout: NHWC, conv/fc weights in ``dtype``,
+    BatchNorm affine params and running stats kept in fp32 (the fused BN kernels read them as
+    fp32)."""
+    model = model.to(memory_format=torch.channels_last)
+    for m in model.modules():
+        if isinstance(m, (nn.Conv2d, nn.Linear)):
+            m.to(dtype)
+    return model

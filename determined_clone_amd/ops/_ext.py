@@ -1,0 +1,43 @@
+"""Loader for the in-tree HIP extension ``determined_clone_amd.ops._C``.
+
+GPU tensors ALWAYS go through the HIP kernels: if the extension is missing on a machine with a GPU
+the op raises (no silent eager fallback). CPU tensors use the PyTorch reference implementations
+that the GPU numerics tests compare against.
+"""
+import importlib
+import os
+from typing import Any, Optional
+
+_C: Optional[Any] = None
+_err: Optional[BaseException] = None
+
+
+def load() -> Any:
+    global _C, _err
+    if _C is not None:
+        return _C
+    import torch  # noqa: F401  (loads libc10_hip / libamdhip64 before the extension)
+
+    try:
+        _C = importlib.import_module("determined_clone_amd.ops._C")
+    except ImportError as e:  # pragma: no cover - exercised only when the build is missing
+        _err = e
+        if os.environ.get("DCA_AUTOBUILD", "1") == "1":
+            from determined_clone_amd.ops import build
+
+            build.build()
+            _C = importlib.import_module("determined_clone_amd.ops._C")
+        else:
+            raise ImportError(
+                "determined_clone_amd.ops._C is not built; run "
+                "`python -m determined_clone_amd.ops.build`"
+            ) from e
+    return _C
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except Exception:
+        return False

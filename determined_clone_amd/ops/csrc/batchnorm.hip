@@ -1,0 +1,338 @@
+// Fused NHWC BatchNorm (+ residual add) (+ ReLU) forward/backward for MI355X.
+//
+// Replaces the reference's cuDNN BatchNorm + separate add/ReLU kernels in the ResNet-50 trial
+// (reference: torchvision resnet50 driven by harness/determined/pytorch/_pytorch_trial.py).
+// Activations are channels_last, i.e. a row-major [M = N*H*W][C] matrix, C % 8 == 0.
+//
+// Training forward = 3 launches, 2 passes over x:
+//   bn_reduce<FWD>   : per-block partial (sum x, sum x^2) per channel          (reads x)
+//   bn_finalize_fwd  : channel-parallel combine of partials in fp64, running stats update,
+//                      per-channel scale/shift, num_batches_tracked += 1
+//   bn_apply_fwd     : y = act(x*scale + shift [+ res])                        (reads x[,res], writes y)
+// Training backward = 3 launches, 2 passes:
+//   bn_reduce<BWD>   : partial (sum dy', sum dy'*(x-mean)), dy' = relu ? dy*(y>0) : dy
+//   bn_finalize_bwd  : dgamma, dbeta and the affine form dx = k1*dy' + k2*x + k3
+//   bn_apply_bwd     : dx (and d_residual = dy' when the residual add was fused)
+// Every lane moves 8 channels (16 B of bf16) per access; reductions are deterministic.
+#include "common.h"
+
+namespace dca {
+
+enum class BnDtype : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+namespace {
+
+constexpr int kBlock = 256;
+
+// Geometry shared by the reduce kernels. TPR = threads per row (8 channels each), RPI = rows per
+// block iteration, channel groups on grid.y when C/8 > 256.
+struct ReduceGeom {
+  int tpr, rpi, cgroups;
+};
+inline ReduceGeom reduce_geom(int C) {
+  int c8 = C / 8;
+  ReduceGeom g;
+  g.tpr = c8 < kBlock ? c8 : kBlock;
+  // tpr must divide 256 for the row mapping; fall back to the largest power of two <= c8.
+  while (kBlock % g.tpr != 0) --g.tpr;
+  g.rpi = kBlock / g.tpr;
+  g.cgroups = (c8 + g.tpr - 1) / g.tpr;
+  return g;
+}
+
+template <typename T, bool BWD>
+__global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
+    const void* __restrict__ x, const void* __restrict__ dy, const void* __restrict__ y,
+    const float* __restrict__ mean, int64_t M, int C, int tpr, int rpi, bool relu,
+    float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][tpr*16]
+  const int tid = threadIdx.x;
+  const int lc = tid % tpr, r0 = tid / tpr;
+  const int c = (blockIdx.y * tpr + lc) * 8;
+  const bool active = c < C;
+  float s[8], q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
+  float mu[8];
+  if (BWD && active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mu[k] = mean[c + k];
+  }
+  if (active) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * rpi;
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * rpi + r0; r < M; r += stride) {
+      const int64_t off = r * C + c;
+      float xv[8];
+      Vec8<T>::load(reinterpret_cast<const char*>(x) + off * Vec8<T>::bytes, xv);
+      if (!BWD) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s[k] += xv[k]; q[k] = fmaf(xv[k], xv[k], q[k]); }
+      } else {
+        float g[8];
+        Vec8<T>::load(reinterpret_cast<const char*>(dy) + off * Vec8<T>::bytes, g);
+        if (relu) {
+          float yv[8];
+          Vec8<T>::load(reinterpret_cast<const char*>(y) + off * Vec8<T>::bytes, yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { s[k] += g[k]; q[k] = fmaf(g[k], xv[k] - mu[k], q[k]); }
+      }
+    }
+  }
+  // Combine the rpi row-groups that share channels through LDS.
+  const int width = tpr * 16;
+  float* mine = lds + r0 * width + lc * 16;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { mine[k] = s[k]; mine[8 + k] = q[k]; }
+  __syncthreads();
+  for (int o = tid; o < width; o += kBlock) {
+    float acc = 0.f;
+    for (int r = 0; r < rpi; ++r) acc += lds[r * width + o];
+    const int lco = o / 16, k = o % 16;
+    const int ch = (blockIdx.y * tpr + lco) * 8 + (k & 7);
+    if (ch < C) partial[(static_cast<int64_t>(blockIdx.x) * 2 + (k >> 3)) * C + ch] = acc;
+  }
+}
+
+// Channel-parallel combine of the per-block partials: block = 256 threads = 8 channels x 32
+// slices of the partial list, fp64 accumulation.
+__device__ __forceinline__ void combine_partials(const float* __restrict__ partial, int B, int C,
+                                                 double* red, double& s_out, double& q_out,
+                                                 int& ch_out) {
+  const int tid = threadIdx.x;
+  const int cl = tid & 7, sl = tid >> 3;
+  const int ch = blockIdx.x * 8 + cl;
+  double s = 0.0, q = 0.0;
+  if (ch < C) {
+    for (int b = sl; b < B; b += 32) {
+      s += partial[(static_cast<int64_t>(b) * 2) * C + ch];
+      q += partial[(static_cast<int64_t>(b) * 2 + 1) * C + ch];
+    }
+  }
+  red[tid] = s;
+  red[256 + tid] = q;
+  __syncthreads();
+  if (sl == 0) {
+    for (int j = 1; j < 32; ++j) { s += red[j * 8 + cl]; q += red[256 + j * 8 + cl]; }
+  }
+  s_out = s; q_out = q; ch_out = ch;
+}
+
+__global__ __launch_bounds__(kBlock) void bn_finalize_fwd_kernel(
+    const float* __restrict__ partial, int B, int C, int64_t M, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ running_mean,
+    float* __restrict__ running_var, float momentum, float eps, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd, float* __restrict__ scale, float* __restrict__ shift,
+    int64_t* __restrict__ num_batches) {
+  __shared__ double red[512];
+  double s, q;
+  int ch;
+  combine_partials(partial, B, C, red, s, q, ch);
+  if ((threadIdx.x >> 3) == 0 && ch < C) {
+    const double mean = s / static_cast<double>(M);
+    double var = q / static_cast<double>(M) - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = static_cast<float>(1.0 / sqrt(var + static_cast<double>(eps)));
+    const float g = gamma ? gamma[ch] : 1.f, bt = beta ? beta[ch] : 0.f;
+    save_mean[ch] = static_cast<float>(mean);
+    save_invstd[ch] = invstd;
+    scale[ch] = g * invstd;
+    shift[ch] = bt - static_cast<float>(mean) * g * invstd;
+    if (running_mean) {
+      const double unbiased = M > 1 ? var * static_cast<double>(M) / static_cast<double>(M - 1) : var;
+      running_mean[ch] = (1.f - momentum) * running_mean[ch] + momentum * static_cast<float>(mean);
+      running_var[ch] = (1.f - momentum) * running_var[ch] + momentum * static_cast<float>(unbiased);
+    }
+  }
+  if (num_batches && blockIdx.x == 0 && threadIdx.x == 0) *num_batches += 1;
+}
+
+__global__ __launch_bounds__(kBlock) void bn_finalize_bwd_kernel(
+    const float* __restrict__ partial, int B, int C, int64_t M, const float* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float* __restrict__ coef /* [3][C] */) {
+  __shared__ double red[512];
+  double s, q;
+  int ch;
+  combine_partials(partial, B, C, red, s, q, ch);
+  if ((threadIdx.x >> 3) == 0 && ch < C) {
+    const float is = invstd[ch];
+    const float g = gamma ? gamma[ch] : 1.f;
+    const float sdy = static_cast<float>(s);
+    const float sdyx = static_cast<float>(q);  // sum dy' * (x - mean)
+    if (dgamma) dgamma[ch] = sdyx * is;
+    if (dbeta) dbeta[ch] = sdy;
+    const float invM = 1.f / static_cast<float>(M);
+    const float k1 = g * is;
+    const float k2 = -k1 * is * is * sdyx * invM;
+    const float k3 = -k1 * sdy * invM - k2 * mean[ch];
+    coef[ch] = k1;
+    coef[C + ch] = k2;
+    coef[2 * C + ch] = k3;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
+    const void* __restrict__ x, const void* __restrict__ res, void* __restrict__ y,
+    const float* __restrict__ scale, const float* __restrict__ shift, int64_t nvec, int c8,
+    bool relu) {
+  // nvec < 2^31 is checked on the host: 32-bit index math (a 64-bit modulo is a long
+  // software sequence on CDNA), 64-bit byte offsets.
+  const uint32_t stride = gridDim.x * blockDim.x, n = static_cast<uint32_t>(nvec);
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += stride) {
+    const int c = static_cast<int>(v % static_cast<uint32_t>(c8)) * 8;
+    float xv[8];
+    Vec8<T>::load(reinterpret_cast<const char*>(x) + static_cast<int64_t>(v) * 8 * Vec8<T>::bytes, xv);
+    const float4* sc = reinterpret_cast<const float4*>(scale + c);
+    const float4* sh = reinterpret_cast<const float4*>(shift + c);
+    const float4 a0 = sc[0], a1 = sc[1], b0 = sh[0], b1 = sh[1];
+    const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = fmaf(xv[k], a[k], b[k]);
+    if (res) {
+      float rv[8];
+      Vec8<T>::load(reinterpret_cast<const char*>(res) + static_cast<int64_t>(v) * 8 * Vec8<T>::bytes, rv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] += rv[k];
+    }
+    if (relu) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = fmaxf(o[k], 0.f);
+    }
+    Vec8<T>::store(reinterpret_cast<char*>(y) + static_cast<int64_t>(v) * 8 * Vec8<T>::bytes, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
+    const void* __restrict__ dy, const void* __restrict__ y, const void* __restrict__ x,
+    const float* __restrict__ coef, void* __restrict__ dx, void* __restrict__ dres, int64_t nvec,
+    int c8, int C, bool relu) {
+  // nvec < 2^31 is checked on the host: 32-bit index math (a 64-bit modulo is a long
+  // software sequence on CDNA), 64-bit byte offsets.
+  const uint32_t stride = gridDim.x * blockDim.x, n = static_cast<uint32_t>(nvec);
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += stride) {
+    const int c = static_cast<int>(v % static_cast<uint32_t>(c8)) * 8;
+    const int64_t off = static_cast<int64_t>(v) * 8 * Vec8<T>::bytes;
+    float g[8], xv[8];
+    Vec8<T>::load(reinterpret_cast<const char*>(dy) + off, g);
+    if (relu) {
+      float yv[8];
+      Vec8<T>::load(reinterpret_cast<const char*>(y) + off, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+    Vec8<T>::load(reinterpret_cast<const char*>(x) + off, xv);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      o[k] = fmaf(coef[c + k], g[k], fmaf(coef[C + c + k], xv[k], coef[2 * C + c + k]));
+    Vec8<T>::store(reinterpret_cast<char*>(dx) + off, o);
+    if (dres) Vec8<T>::store(reinterpret_cast<char*>(dres) + off, g);
+  }
+}
+
+inline int reduce_blocks(int64_t M, int C, const ReduceGeom& g) {
+  // Aim at ~64K elements per workgroup, 256..1024 workgroups in x (x cgroups in y).
+  int64_t total = M * static_cast<int64_t>(C);
+  int64_t b = (total + 65535) / 65536;
+  if (b < 256) b = 256;
+  if (b > 1024) b = 1024;
+  int64_t rows_iter = (M + g.rpi - 1) / g.rpi;
+  if (b > rows_iter) b = rows_iter;
+  if (b < 1) b = 1;
+  return static_cast<int>(b);
+}
+
+template <typename T>
+void launch_reduce(bool bwd, const void* x, const void* dy, const void* y, const float* mean,
+                   int64_t M, int C, bool relu, float* partial, int B, const ReduceGeom& g,
+                   hipStream_t st) {
+  dim3 grid(B, g.cgroups);
+  size_t lds = static_cast<size_t>(g.rpi) * g.tpr * 16 * sizeof(float);
+  if (bwd)
+    hipLaunchKernelGGL((bn_reduce_kernel<T, true>), grid, dim3(kBlock), lds, st, x, dy, y, mean,
+                       M, C, g.tpr, g.rpi, relu, partial);
+  else
+    hipLaunchKernelGGL((bn_reduce_kernel<T, false>), grid, dim3(kBlock), lds, st, x, dy, y, mean,
+                       M, C, g.tpr, g.rpi, relu, partial);
+}
+
+}  // namespace
+
+// Workspace floats needed by bn_forward_train / bn_backward_train for (M, C).
+int64_t bn_workspace_floats(int64_t M, int C) {
+  ReduceGeom g = reduce_geom(C);
+  int B = reduce_blocks(M, C, g);
+  return static_cast<int64_t>(B) * 2 * C + 4 * static_cast<int64_t>(C);
+}
+
+void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
+                      const float* gamma, const float* beta, float* running_mean,
+                      float* running_var, float momentum, float eps, bool relu, float* save_mean,
+                      float* save_invstd, int64_t* num_batches, float* workspace,
+                      hipStream_t st) {
+  ReduceGeom g = reduce_geom(C);
+  int B = reduce_blocks(M, C, g);
+  float* partial = workspace;
+  float* scale = workspace + static_cast<int64_t>(B) * 2 * C;
+  float* shift = scale + C;
+  switch (dt) {
+    case BnDtype::kBF16: launch_reduce<BF16>(false, x, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
+    case BnDtype::kF16: launch_reduce<F16>(false, x, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
+    default: launch_reduce<F32>(false, x, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
+  }
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
+                     C, M, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
+                     save_invstd, scale, shift, num_batches);
+  const int64_t nvec = M * C / 8;
+  const int grid = stream_grid(nvec, kBlock);
+  switch (dt) {
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
+    default: hipLaunchKernelGGL(bn_apply_fwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
+  }
+}
+
+// Inference-mode forward with precomputed per-channel scale/shift (fp32, [C] each).
+void bn_forward_affine(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
+                       const float* scale, const float* shift, bool relu, hipStream_t st) {
+  const int64_t nvec = M * C / 8;
+  const int grid = stream_grid(nvec, kBlock);
+  switch (dt) {
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
+    default: hipLaunchKernelGGL(bn_apply_fwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
+  }
+}
+
+void bn_backward_train(BnDtype dt, const void* dy, const void* y, const void* x, int64_t M, int C,
+                       const float* gamma, const float* save_mean, const float* save_invstd,
+                       bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
+                       float* workspace, hipStream_t st) {
+  ReduceGeom g = reduce_geom(C);
+  int B = reduce_blocks(M, C, g);
+  float* partial = workspace;
+  float* coef = workspace + static_cast<int64_t>(B) * 2 * C;  // [3][C]
+  switch (dt) {
+    case BnDtype::kBF16: launch_reduce<BF16>(true, x, dy, y, save_mean, M, C, relu, partial, B, g, st); break;
+    case BnDtype::kF16: launch_reduce<F16>(true, x, dy, y, save_mean, M, C, relu, partial, B, g, st); break;
+    default: launch_reduce<F32>(true, x, dy, y, save_mean, M, C, relu, partial, B, g, st); break;
+  }
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
+                     C, M, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+  const int64_t nvec = M * C / 8;
+  const int grid = stream_grid(nvec, kBlock);
+  switch (dt) {
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_bwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, dy, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_bwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, dy, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
+    default: hipLaunchKernelGGL(bn_apply_bwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, dy, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
+  }
+}
+
+}  // namespace dca

@@ -1,0 +1,298 @@
+// Python bindings of the determined_clone_amd HIP kernels (`determined_clone_amd.ops._C`).
+// Tensor checks live here; the .hip translation units only see raw pointers and a hipStream_t so
+// they compile without the torch headers.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+
+#include <hip/hip_runtime.h>
+
+namespace dca {
+enum class BnDtype : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+enum class OptDtype : int { kF32 = 0, kBF16 = 1, kF16 = 2, kNone = 3 };
+
+int64_t bn_workspace_floats(int64_t M, int C);
+void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
+                      const float* gamma, const float* beta, float* running_mean,
+                      float* running_var, float momentum, float eps, bool relu, float* save_mean,
+                      float* save_invstd, int64_t* num_batches, float* workspace, hipStream_t st);
+void bn_forward_affine(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
+                       const float* scale, const float* shift, bool relu, hipStream_t st);
+void bn_backward_train(BnDtype dt, const void* dy, const void* y, const void* x, int64_t M, int C,
+                       const float* gamma, const float* save_mean, const float* save_invstd,
+                       bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
+                       float* workspace, hipStream_t st);
+
+int sumsq_partial_blocks(int64_t n);
+void sumsq_partial(OptDtype g, const void* grad, int64_t n, float* partial, int blocks,
+                   hipStream_t st);
+void norm_finalize(const float* partial, int nparts, const float* loss_scale, float extra_scale,
+                   float max_norm, float* out, hipStream_t st);
+void sgd_step(OptDtype gdt, OptDtype pdt, float* master, void* model, const void* grad, float* mom,
+              int64_t n, float lr, float momentum, float dampening, float wd, bool nesterov,
+              bool first_step, float gscale, const float* dev_scale, hipStream_t st);
+void adam_step(OptDtype gdt, OptDtype pdt, float* master, void* model, const void* grad, float* m,
+               float* v, int64_t n, float lr, float beta1, float beta2, float eps, float wd,
+               bool adamw, float bc1, float bc2, float gscale, const float* dev_scale,
+               hipStream_t st);
+void lamb_step(OptDtype gdt, OptDtype pdt, float* master, void* model, const void* grad, float* m,
+               float* v, float* ubuf, const int64_t* cstart, const int* clen, const int* cseg,
+               int nchunks, const int* seg_chunk_begin, int nseg, float* part_w, float* part_u,
+               float* ratio, float lr, float beta1, float beta2, float eps, float wd, float bc1,
+               float bc2, float gscale, const float* dev_scale, hipStream_t st);
+void scaler_update(float* state, const float* dev_scale, float growth, float backoff, int interval,
+                   hipStream_t st);
+void scale_inplace(OptDtype dt, void* x, int64_t n, float s, const float* dev_scale,
+                   hipStream_t st);
+}  // namespace dca
+
+namespace {
+
+using torch::Tensor;
+using OptT = c10::optional<Tensor>;
+
+// PyTorch-ROCm exposes GPUs as device type "cuda"; its HIP stream/guard wrappers masquerade.
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+
+dca::BnDtype bn_dtype(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kBFloat16: return dca::BnDtype::kBF16;
+    case at::kHalf: return dca::BnDtype::kF16;
+    case at::kFloat: return dca::BnDtype::kF32;
+    default: TORCH_CHECK(false, "batchnorm: unsupported dtype ", t.scalar_type());
+  }
+}
+
+dca::OptDtype opt_dtype(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kBFloat16: return dca::OptDtype::kBF16;
+    case at::kHalf: return dca::OptDtype::kF16;
+    case at::kFloat: return dca::OptDtype::kF32;
+    default: TORCH_CHECK(false, "optimizer: unsupported dtype ", t.scalar_type());
+  }
+}
+
+template <typename T>
+T* ptr_or_null(const OptT& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<T>() : nullptr;
+}
+const void* vptr_or_null(const OptT& t) {
+  return t.has_value() && t->defined() ? t->data_ptr() : nullptr;
+}
+
+// Rows x channels view of an NHWC (channels_last) 4-D tensor or a contiguous [.., C] tensor.
+std::pair<int64_t, int> rows_channels(const Tensor& x) {
+  int C = x.dim() >= 2 ? static_cast<int>(x.size(1)) : static_cast<int>(x.size(0));
+  if (x.dim() == 4) {
+    TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "batchnorm: 4-D input must be channels_last contiguous");
+  } else {
+    TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "batchnorm: input must be NHWC 4-D or [N, C]");
+  }
+  TORCH_CHECK(C % 8 == 0, "batchnorm: channels must be a multiple of 8, got ", C);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(M * C / 8 < (int64_t(1) << 31), "batchnorm: tensor too large for one launch");
+  return {M, C};
+}
+
+std::vector<Tensor> bn_fwd_train(const Tensor& x, const OptT& residual, const OptT& weight,
+                                 const OptT& bias, const OptT& running_mean,
+                                 const OptT& running_var, const OptT& num_batches, double momentum,
+                                 double eps, bool relu) {
+  CHECK_DEV(x);
+  const c10::DeviceGuard guard(x.device());
+  auto [M, C] = rows_channels(x);
+  if (residual.has_value()) {
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->strides() == x.strides() &&
+                    residual->scalar_type() == x.scalar_type(),
+                "batchnorm: residual must match input shape/layout/dtype");
+  }
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor y = torch::empty_like(x);
+  Tensor save_mean = torch::empty({C}, fopt), save_invstd = torch::empty({C}, fopt);
+  Tensor ws = torch::empty({dca::bn_workspace_floats(M, C)}, fopt);
+  dca::bn_forward_train(bn_dtype(x), x.data_ptr(), vptr_or_null(residual), y.data_ptr(), M, C,
+                        ptr_or_null<float>(weight), ptr_or_null<float>(bias),
+                        ptr_or_null<float>(running_mean), ptr_or_null<float>(running_var),
+                        static_cast<float>(momentum), static_cast<float>(eps), relu,
+                        save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                        ptr_or_null<int64_t>(num_batches), ws.data_ptr<float>(), cur_stream());
+  return {y, save_mean, save_invstd};
+}
+
+Tensor bn_fwd_affine(const Tensor& x, const OptT& residual, const Tensor& scale,
+                     const Tensor& shift, bool relu) {
+  CHECK_DEV(x);
+  CHECK_F32(scale);
+  CHECK_F32(shift);
+  const c10::DeviceGuard guard(x.device());
+  auto [M, C] = rows_channels(x);
+  Tensor sc = scale.contiguous(), sh = shift.contiguous();
+  Tensor y = torch::empty_like(x);
+  dca::bn_forward_affine(bn_dtype(x), x.data_ptr(), vptr_or_null(residual), y.data_ptr(), M, C,
+                         sc.data_ptr<float>(), sh.data_ptr<float>(), relu, cur_stream());
+  return y;
+}
+
+std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const OptT& y,
+                                 const OptT& weight, const Tensor& save_mean,
+                                 const Tensor& save_invstd, bool relu, bool need_dres,
+                                 bool need_dweight) {
+  CHECK_DEV(x);
+  const c10::DeviceGuard guard(x.device());
+  auto [M, C] = rows_channels(x);
+  Tensor dy = dy_in.dim() == 4 ? dy_in.contiguous(at::MemoryFormat::ChannelsLast) : dy_in.contiguous();
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "batchnorm bwd: grad dtype mismatch");
+  TORCH_CHECK(!relu || (y.has_value() && y->defined()), "batchnorm bwd: relu needs the output");
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor dx = torch::empty_like(x);
+  Tensor dres = need_dres ? torch::empty_like(x) : Tensor();
+  Tensor dgamma = need_dweight ? torch::empty({C}, fopt) : Tensor();
+  Tensor dbeta = need_dweight ? torch::empty({C}, fopt) : Tensor();
+  Tensor ws = torch::empty({dca::bn_workspace_floats(M, C)}, fopt);
+  dca::bn_backward_train(bn_dtype(x), dy.data_ptr(), relu ? y->data_ptr() : nullptr, x.data_ptr(),
+                         M, C, ptr_or_null<float>(weight), save_mean.data_ptr<float>(),
+                         save_invstd.data_ptr<float>(), relu, dx.data_ptr(),
+                         need_dres ? dres.data_ptr() : nullptr,
+                         need_dweight ? dgamma.data_ptr<float>() : nullptr,
+                         need_dweight ? dbeta.data_ptr<float>() : nullptr, ws.data_ptr<float>(),
+                         cur_stream());
+  return {dx, dgamma, dbeta, dres};
+}
+
+// Global gradient norm over one flat buffer: returns a 3-float device tensor
+// [grad multiplier, found_inf, norm] (see optim.hip norm_finalize_kernel).
+Tensor grad_norm_scale(const std::vector<Tensor>& grads, const OptT& loss_scale, double extra_scale,
+                       double max_norm) {
+  TORCH_CHECK(!grads.empty(), "grad_norm_scale: no gradients");
+  const c10::DeviceGuard guard(grads[0].device());
+  auto fopt = grads[0].options().dtype(at::kFloat);
+  std::vector<int> blocks;
+  int total = 0;
+  for (auto& g : grads) {
+    CHECK_DEV(g);
+    TORCH_CHECK(g.is_contiguous(), "grad_norm_scale: flat gradient buffers must be contiguous");
+    blocks.push_back(dca::sumsq_partial_blocks(g.numel()));
+    total += blocks.back();
+  }
+  Tensor partial = torch::empty({total}, fopt);
+  Tensor out = torch::empty({3}, fopt);
+  int off = 0;
+  for (size_t i = 0; i < grads.size(); ++i) {
+    dca::sumsq_partial(opt_dtype(grads[i]), grads[i].data_ptr(), grads[i].numel(),
+                       partial.data_ptr<float>() + off, blocks[i], cur_stream());
+    off += blocks[i];
+  }
+  dca::norm_finalize(partial.data_ptr<float>(), total, ptr_or_null<float>(loss_scale),
+                     static_cast<float>(extra_scale), static_cast<float>(max_norm),
+                     out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+void check_flat(const Tensor& master, const Tensor& grad, const OptT& model) {
+  CHECK_DEV(master);
+  CHECK_F32(master);
+  TORCH_CHECK(master.is_contiguous() && grad.is_contiguous(), "flat buffers must be contiguous");
+  TORCH_CHECK(grad.numel() == master.numel(), "grad/master size mismatch");
+  if (model.has_value() && model->defined())
+    TORCH_CHECK(model->numel() == master.numel() && model->is_contiguous(), "model buffer mismatch");
+}
+
+void sgd(const Tensor& master, const OptT& model, const Tensor& grad, const OptT& mom, double lr,
+         double momentum, double dampening, double wd, bool nesterov, bool first_step,
+         double gscale, const OptT& dev_scale) {
+  check_flat(master, grad, model);
+  const c10::DeviceGuard guard(master.device());
+  TORCH_CHECK(momentum == 0.0 || (mom.has_value() && mom->numel() == master.numel()),
+              "sgd: momentum buffer required");
+  dca::sgd_step(opt_dtype(grad),
+                model.has_value() && model->defined() ? opt_dtype(*model) : dca::OptDtype::kNone,
+                master.data_ptr<float>(), model.has_value() && model->defined() ? model->data_ptr() : nullptr,
+                grad.data_ptr(), ptr_or_null<float>(mom), master.numel(), static_cast<float>(lr),
+                static_cast<float>(momentum), static_cast<float>(dampening), static_cast<float>(wd),
+                nesterov, first_step, static_cast<float>(gscale), ptr_or_null<float>(dev_scale),
+                cur_stream());
+}
+
+void adam(const Tensor& master, const OptT& model, const Tensor& grad, const Tensor& m,
+          const Tensor& v, double lr, double beta1, double beta2, double eps, double wd, bool adamw,
+          int64_t step, double gscale, const OptT& dev_scale) {
+  check_flat(master, grad, model);
+  const c10::DeviceGuard guard(master.device());
+  const double bc1 = 1.0 - std::pow(beta1, static_cast<double>(step));
+  const double bc2 = 1.0 - std::pow(beta2, static_cast<double>(step));
+  dca::adam_step(opt_dtype(grad),
+                 model.has_value() && model->defined() ? opt_dtype(*model) : dca::OptDtype::kNone,
+                 master.data_ptr<float>(), model.has_value() && model->defined() ? model->data_ptr() : nullptr,
+                 grad.data_ptr(), m.data_ptr<float>(), v.data_ptr<float>(), master.numel(),
+                 static_cast<float>(lr), static_cast<float>(beta1), static_cast<float>(beta2),
+                 static_cast<float>(eps), static_cast<float>(wd), adamw, static_cast<float>(bc1),
+                 static_cast<float>(bc2), static_cast<float>(gscale), ptr_or_null<float>(dev_scale),
+                 cur_stream());
+}
+
+// chunks: int64 [3][nchunks] = (start, len, seg) on device; seg_begin: int32 [nseg+1] on device.
+void lamb(const Tensor& master, const OptT& model, const Tensor& grad, const Tensor& m,
+          const Tensor& v, const Tensor& ubuf, const Tensor& cstart, const Tensor& clen,
+          const Tensor& cseg, const Tensor& seg_begin, double lr, double beta1, double beta2,
+          double eps, double wd, int64_t step, double gscale, const OptT& dev_scale) {
+  check_flat(master, grad, model);
+  const c10::DeviceGuard guard(master.device());
+  const int nchunks = static_cast<int>(cstart.numel());
+  const int nseg = static_cast<int>(seg_begin.numel()) - 1;
+  auto fopt = master.options();
+  Tensor pw = torch::empty({nchunks}, fopt), pu = torch::empty({nchunks}, fopt);
+  Tensor ratio = torch::empty({nseg}, fopt);
+  const double bc1 = 1.0 - std::pow(beta1, static_cast<double>(step));
+  const double bc2 = 1.0 - std::pow(beta2, static_cast<double>(step));
+  dca::lamb_step(opt_dtype(grad),
+                 model.has_value() && model->defined() ? opt_dtype(*model) : dca::OptDtype::kNone,
+                 master.data_ptr<float>(), model.has_value() && model->defined() ? model->data_ptr() : nullptr,
+                 grad.data_ptr(), m.data_ptr<float>(), v.data_ptr<float>(), ubuf.data_ptr<float>(),
+                 cstart.data_ptr<int64_t>(), clen.data_ptr<int>(), cseg.data_ptr<int>(), nchunks,
+                 seg_begin.data_ptr<int>(), nseg, pw.data_ptr<float>(), pu.data_ptr<float>(),
+                 ratio.data_ptr<float>(), static_cast<float>(lr), static_cast<float>(beta1),
+                 static_cast<float>(beta2), static_cast<float>(eps), static_cast<float>(wd),
+                 static_cast<float>(bc1), static_cast<float>(bc2), static_cast<float>(gscale),
+                 ptr_or_null<float>(dev_scale), cur_stream());
+}
+
+void amp_scaler_update(const Tensor& state, const Tensor& dev_scale, double growth, double backoff,
+                       int64_t interval) {
+  CHECK_DEV(state);
+  const c10::DeviceGuard guard(state.device());
+  dca::scaler_update(state.data_ptr<float>(), dev_scale.data_ptr<float>(),
+                     static_cast<float>(growth), static_cast<float>(backoff),
+                     static_cast<int>(interval), cur_stream());
+}
+
+void scale_(const Tensor& x, double s, const OptT& dev_scale) {
+  CHECK_DEV(x);
+  TORCH_CHECK(x.is_contiguous(), "scale_: contiguous buffer required");
+  const c10::DeviceGuard guard(x.device());
+  dca::scale_inplace(opt_dtype(x), x.data_ptr(), x.numel(), static_cast<float>(s),
+                     ptr_or_null<float>(dev_scale), cur_stream());
+}
+
+}  // namespace
+
+// Extra kernel families register themselves from their own translation units.
+void register_transformer_ops(pybind11::module& m);
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "determined_clone_amd MI355X (gfx950) HIP kernels";
+  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_fwd_affine", &bn_fwd_affine);
+  m.def("bn_bwd_train", &bn_bwd_train);
+  m.def("grad_norm_scale", &grad_norm_scale);
+  m.def("sgd", &sgd);
+  m.def("adam", &adam);
+  m.def("lamb", &lamb);
+  m.def("amp_scaler_update", &amp_scaler_update);
+  m.def("scale_", &scale_);
+  register_transformer_ops(m);
+}

@@ -1,0 +1,136 @@
+// Shared device helpers for the determined_clone_amd HIP kernels (gfx950 / CDNA4 only).
+//
+// Conventions used by every kernel in this directory:
+//  * wave64: lane = threadIdx.x & 63, block sizes are multiples of 64;
+//  * memory-bound kernels move 16 bytes per lane per access (8 x bf16 / 4 x fp32), never scalar
+//    bf16 (cdna_hip_programming.md Guideline 13);
+//  * reductions are deterministic: per-block partials -> a second, channel-parallel pass
+//    (no float atomics, so results are bitwise reproducible run to run).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dca {
+
+constexpr int kWave = 64;
+
+// ---------------------------------------------------------------- bf16 / fp16 bit helpers
+__device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// fp32 -> bf16 round-to-nearest-even (NaN stays NaN).
+__device__ __forceinline__ uint32_t f2bf_bits(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return f2bf_bits(lo) | (f2bf_bits(hi) << 16);
+}
+
+__device__ __forceinline__ float h2f(uint32_t bits) {
+  const uint16_t h = static_cast<uint16_t>(bits);
+  _Float16 f;
+  __builtin_memcpy(&f, &h, 2);
+  return static_cast<float>(f);
+}
+__device__ __forceinline__ uint16_t f2h(float f) {
+  const _Float16 h = static_cast<_Float16>(f);
+  uint16_t u;
+  __builtin_memcpy(&u, &h, 2);
+  return u;
+}
+
+// ---------------------------------------------------------------- 8-element vector I/O
+// Type tags: element storage for the templated kernels.
+struct BF16 { using raw = uint16_t; };
+struct F16 { using raw = uint16_t; };
+struct F32 { using raw = float; };
+
+template <typename T> struct Vec8;
+
+template <> struct Vec8<BF16> {
+  __device__ __forceinline__ static void load(const void* p, float (&v)[8]) {
+    uint4 q = *reinterpret_cast<const uint4*>(p);
+    v[0] = bf16_lo(q.x); v[1] = bf16_hi(q.x); v[2] = bf16_lo(q.y); v[3] = bf16_hi(q.y);
+    v[4] = bf16_lo(q.z); v[5] = bf16_hi(q.z); v[6] = bf16_lo(q.w); v[7] = bf16_hi(q.w);
+  }
+  __device__ __forceinline__ static void store(void* p, const float (&v)[8]) {
+    uint4 q;
+    q.x = pack_bf16x2(v[0], v[1]); q.y = pack_bf16x2(v[2], v[3]);
+    q.z = pack_bf16x2(v[4], v[5]); q.w = pack_bf16x2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(p) = q;
+  }
+  static constexpr int bytes = 2;
+};
+
+template <> struct Vec8<F16> {
+  __device__ __forceinline__ static void load(const void* p, float (&v)[8]) {
+    uint4 q = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = h2f(static_cast<uint16_t>(w[i] & 0xffffu));
+      v[2 * i + 1] = h2f(static_cast<uint16_t>(w[i] >> 16));
+    }
+  }
+  __device__ __forceinline__ static void store(void* p, const float (&v)[8]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = static_cast<uint32_t>(f2h(v[2 * i])) | (static_cast<uint32_t>(f2h(v[2 * i + 1])) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  static constexpr int bytes = 2;
+};
+
+template <> struct Vec8<F32> {
+  __device__ __forceinline__ static void load(const void* p, float (&v)[8]) {
+    const float4* q = reinterpret_cast<const float4*>(p);
+    float4 a = q[0], b = q[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ static void store(void* p, const float (&v)[8]) {
+    float4* q = reinterpret_cast<float4*>(p);
+    q[0] = make_float4(v[0], v[1], v[2], v[3]);
+    q[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  static constexpr int bytes = 4;
+};
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `scratch` needs blockDim.x/64 floats. Result valid in
+// every thread.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += scratch[i];
+  return t;
+}
+
+// Memory-bound grid size: enough workgroups to fill 256 CUs several times, grid-stride the rest.
+inline int stream_grid(int64_t work_items, int block) {
+  int64_t g = (work_items + block - 1) / block;
+  if (g > 256 * 8) g = 256 * 8;
+  if (g < 1) g = 1;
+  return static_cast<int>(g);
+}
+
+}  // namespace dca

@@ -1,0 +1,184 @@
+"""TensorBoard support without a TensorFlow dependency.
+
+Reference: `harness/determined/tensorboard/*` (TensorboardManager that syncs event files to
+checkpoint storage, metric writers for TF/PyTorch). TensorBoard/TF are not installed here, so the
+event-file format is written natively: TFRecord framing (length, masked CRC32C) around hand-encoded
+``Event``/``Summary`` protobuf messages (scalars). Files are readable by stock TensorBoard.
+"""
+import os
+import pathlib
+import shutil
+import socket
+import struct
+import threading
+import time
+from typing import Any, Callable, Dict, Optional
+
+# ----------------------------------------------------------------------------- CRC32C
+_CRC_TABLE = []
+for _i in range(256):
+    _c = _i
+    for _ in range(8):
+        _c = (_c >> 1) ^ 0x82F63B78 if _c & 1 else _c >> 1
+    _CRC_TABLE.append(_c)
+
+
+def crc32c(data: bytes) -> int:
+    c = 0xFFFFFFFF
+    tbl = _CRC_TABLE
+    for b in data:
+        c = tbl[(c ^ b) & 0xFF] ^ (c >> 8)
+    return c ^ 0xFFFFFFFF
+
+
+def _masked_crc(data: bytes) -> int:
+    c = crc32c(data)
+    return (((c >> 15) | (c << 17)) + 0xA282EAD8) & 0xFFFFFFFF
+
+
+# ----------------------------------------------------------------------------- protobuf encoding
+def _varint(n: int) -> bytes:
+    out = bytearray()
+    n &= (1 << 64) - 1
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        if n:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _field(num: int, wire: int) -> bytes:
+    return _varint((num << 3) | wire)
+
+
+def _bytes_field(num: int, payload: bytes) -> bytes:
+    return _field(num, 2) + _varint(len(payload)) + payload
+
+
+def encode_scalar_event(tag: str, value: float, step: int, wall_time: Optional[float] = None) -> bytes:
+    val = _bytes_field(1, tag.encode()) + _field(2, 5) + struct.pack("<f", float(value))
+    summary = _bytes_field(1, val)
+    ev = _field(1, 1) + struct.pack("<d", wall_time or time.time())
+    ev += _field(2, 0) + _varint(int(step))
+    ev += _bytes_field(5, summary)
+    return ev
+
+
+def encode_file_version_event() -> bytes:
+    return _field(1, 1) + struct.pack("<d", time.time()) + _bytes_field(3, b"brain.Event:2")
+
+
+def frame(record: bytes) -> bytes:
+    header = struct.pack("<Q", len(record))
+    return header + struct.pack("<I", _masked_crc(header)) + record + struct.pack("<I", _masked_crc(record))
+
+
+def read_records(path: str):
+    """Iterate raw records of an event file (used by tests and the tensorboard fetcher)."""
+    with open(path, "rb") as f:
+        while True:
+            header = f.read(12)
+            if len(header) < 12:
+                return
+            (n,) = struct.unpack("<Q", header[:8])
+            data = f.read(n)
+            f.read(4)
+            yield data
+
+
+class EventFileWriter:
+    def __init__(self, logdir: str, suffix: str = "") -> None:
+        os.makedirs(logdir, exist_ok=True)
+        name = f"events.out.tfevents.{int(time.time())}.{socket.gethostname()}{suffix}"
+        self.path = os.path.join(logdir, name)
+        self._f = open(self.path, "ab")
+        self._lock = threading.Lock()
+        self._write(encode_file_version_event())
+
+    def _write(self, rec: bytes) -> None:
+        with self._lock:
+            self._f.write(frame(rec))
+
+    def add_scalar(self, tag: str, value: float, step: int) -> None:
+        self._write(encode_scalar_event(tag, value, step))
+
+    def flush(self) -> None:
+        with self._lock:
+            self._f.flush()
+
+    def close(self) -> None:
+        with self._lock:
+            self._f.close()
+
+
+class MetricWriter:
+    """Writes reported training/validation metrics as scalars (reference: metric_writers)."""
+
+    def __init__(self, logdir: str) -> None:
+        self._w = EventFileWriter(logdir)
+
+    def on_metrics(self, group: str, steps_completed: int, metrics: Dict[str, Any]) -> None:
+        from determined_clone_amd.util import is_numerical_scalar, to_python
+
+        prefix = "Determined/" if group == "training" else f"Determined/{group}_"
+        for k, v in metrics.items():
+            if is_numerical_scalar(v):
+                self._w.add_scalar(prefix + k, float(to_python(v)), steps_completed)
+        self._w.flush()
+
+    def close(self) -> None:
+        self._w.close()
+
+
+class TensorboardManager:
+    """Owns the local tensorboard directory of a trial and syncs it into storage."""
+
+    def __init__(self, base_path: pathlib.Path, sync_path: Optional[pathlib.Path]) -> None:
+        self.base_path = pathlib.Path(base_path)
+        self.sync_path = sync_path
+        self.base_path.mkdir(parents=True, exist_ok=True)
+        self._writer: Optional[MetricWriter] = None
+
+    def metric_writer(self) -> MetricWriter:
+        if self._writer is None:
+            self._writer = MetricWriter(str(self.base_path))
+        return self._writer
+
+    def start(self) -> None:
+        pass
+
+    def sync(self, selector: Optional[Callable[[str], bool]] = None, mangler: Any = None) -> None:
+        if self.sync_path is None:
+            return
+        self.sync_path.mkdir(parents=True, exist_ok=True)
+        for p in self.base_path.rglob("*"):
+            if p.is_file() and (selector is None or selector(str(p))):
+                dst = self.sync_path / p.relative_to(self.base_path)
+                dst.parent.mkdir(parents=True, exist_ok=True)
+                shutil.copy2(p, dst)
+
+    def close(self) -> None:
+        if self._writer is not None:
+            self._writer.close()
+        self.sync()
+
+
+def build(cluster_id: str, experiment_id: str, trial_id: str, storage_config: Dict[str, Any],
+          rank: int = 0) -> Optional[TensorboardManager]:
+    base = pathlib.Path(os.environ.get("DET_TENSORBOARD_DIR", f"/tmp/tensorboard-{experiment_id}-{trial_id}"))
+    sync = None
+    if storage_config.get("type") in ("shared_fs", "directory"):
+        root = storage_config.get("host_path") or storage_config.get("container_path")
+        if storage_config.get("storage_path"):
+            root = os.path.join(root, storage_config["storage_path"])
+        sync = pathlib.Path(root) / "tensorboard" / cluster_id / "experiment" / experiment_id / "trial" / trial_id
+    if rank != 0:
+        return None
+    return TensorboardManager(base, sync)
+
+
+def get_metric_writer(logdir: str) -> MetricWriter:
+    return MetricWriter(logdir)

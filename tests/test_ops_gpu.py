@@ -1,0 +1,164 @@
+"""Numerics of the HIP kernels vs plain PyTorch fp32 references (run on an MI355X)."""
+import pytest
+import torch
+
+from determined_clone_amd.ops import _ext, batchnorm
+from determined_clone_amd.ops import optim as fopt
+
+pytestmark = pytest.mark.gpu
+
+
+def _ext_loaded():
+    C = _ext.load()
+    assert C.__file__.endswith("_C.so")
+    return C
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 7), (2, 2048, 3, 3), (16, 24, 5, 5)])
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_bn_act_forward_backward(dtype, shape, relu, res):
+    _ext_loaded()
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    dev = "cuda"
+    x = (torch.randn(shape, device=dev) * 2 + 0.5).to(dtype).contiguous(memory_format=torch.channels_last)
+    r = torch.randn(shape, device=dev).to(dtype).contiguous(memory_format=torch.channels_last) if res else None
+    w = torch.rand(C, device=dev) + 0.5
+    b = torch.randn(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    nbt = torch.zeros((), dtype=torch.long, device=dev)
+    x1 = x.clone().requires_grad_(True)
+    w1, b1 = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    r1 = r.clone().requires_grad_(True) if res else None
+    y = batchnorm.batch_norm_act(x1, w1, b1, rm, rv, residual=r1, training=True, momentum=0.1,
+                                 eps=1e-5, relu=relu, num_batches_tracked=nbt)
+    # fp32 reference
+    x2 = x.float().clone().requires_grad_(True)
+    w2, b2 = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    r2 = r.float().clone().requires_grad_(True) if res else None
+    rm2, rv2 = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    y2 = batchnorm.reference_batch_norm_act(x2, w2, b2, rm2, rv2, r2, True, 0.1, 1e-5, relu)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), y2, atol=tol * 4, rtol=tol)
+    torch.testing.assert_close(rm, rm2, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(rv, rv2, atol=1e-3, rtol=1e-3)
+    assert int(nbt) == (1 if C % 8 == 0 else 1)
+    g = torch.randn_like(y2)
+    y.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
+    y2.backward(g)
+    # bf16 grads: compare against the fp32 reference computed from the same rounded inputs
+    torch.testing.assert_close(x1.grad.float(), x2.grad, atol=tol * 10, rtol=tol * 5)
+    torch.testing.assert_close(w1.grad, w2.grad, atol=tol * 50, rtol=tol * 5)
+    torch.testing.assert_close(b1.grad, b2.grad, atol=tol * 50, rtol=tol * 5)
+    if res:
+        torch.testing.assert_close(r1.grad.float(), r2.grad, atol=tol * 4, rtol=tol)
+
+
+def test_bn_eval_affine():
+    _ext_loaded()
+    x = torch.randn(4, 64, 8, 8, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w, b = torch.rand(64, device="cuda"), torch.randn(64, device="cuda")
+    rm, rv = torch.randn(64, device="cuda"), torch.rand(64, device="cuda") + 0.5
+    with torch.no_grad():
+        y = batchnorm.batch_norm_act(x, w, b, rm, rv, training=False, relu=True)
+        y2 = batchnorm.reference_batch_norm_act(x.float(), w, b, rm, rv, None, False, 0.1, 1e-5, True)
+    torch.testing.assert_close(y.float(), y2, atol=3e-2, rtol=2e-2)
+
+
+def _params(dtype):
+    torch.manual_seed(1)
+    ps = [torch.nn.Parameter(torch.randn(s, device="cuda").to(dtype)) for s in [(37,), (64, 3, 3, 3), (1000, 17), (5,)]]
+    return ps
+
+
+@pytest.mark.parametrize("kind", ["sgd", "sgd_nesterov", "adam", "adamw"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fused_optimizers_match_torch(kind, dtype):
+    _ext_loaded()
+    ps = _params(dtype)
+    ref = [torch.nn.Parameter(p.detach().float().clone()) for p in ps]
+    if kind.startswith("sgd"):
+        kw = dict(lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=kind == "sgd_nesterov")
+        fused = fopt.FusedSGD(ps, **kw)
+        tref = torch.optim.SGD(ref, **kw)
+    elif kind == "adam":
+        fused = fopt.FusedAdam(ps, lr=1e-2, weight_decay=1e-3)
+        tref = torch.optim.Adam(ref, lr=1e-2, weight_decay=1e-3)
+    else:
+        fused = fopt.FusedAdamW(ps, lr=1e-2, weight_decay=1e-2)
+        tref = torch.optim.AdamW(ref, lr=1e-2, weight_decay=1e-2)
+    for step in range(4):
+        grads = [torch.randn(p.shape, device="cuda") for p in ps]
+        for p, g in zip(ps, grads):
+            p.grad.copy_(g.to(dtype))
+        for p, g in zip(ref, grads):
+            p.grad = g.to(dtype).float()
+        fused.step()
+        tref.step()
+    for st in fused.flat.values():
+        for seg in st.buf.segments:
+            got = st.buf.view(st.master, seg)
+            want = ref[seg.index].detach()
+            torch.testing.assert_close(got, want, atol=1e-5, rtol=1e-5)
+            torch.testing.assert_close(seg.param.detach().float(), want, atol=2e-2, rtol=1e-2)
+
+
+def test_grad_clip_and_found_inf():
+    _ext_loaded()
+    ps = _params(torch.float32)
+    opt = fopt.FusedSGD(ps, lr=1.0)
+    for p in ps:
+        p.grad.fill_(1.0)
+    n = sum(p.numel() for p in ps)
+    before = [p.detach().clone() for p in ps]
+    opt.prepare_grads(max_norm=1.0)
+    assert abs(float(opt.last_grad_norm) - n ** 0.5) / n ** 0.5 < 1e-5
+    opt.step()
+    delta = torch.cat([(b - p.detach()).flatten() for b, p in zip(before, ps)])
+    assert abs(float(delta.norm()) - 1.0) < 1e-4
+    # inf gradient -> step skipped
+    ps[0].grad[0] = float("inf")
+    snap = [p.detach().clone() for p in ps]
+    opt.prepare_grads(max_norm=1.0)
+    assert float(opt.found_inf) == 1.0
+    opt.step()
+    for s, p in zip(snap, ps):
+        assert torch.equal(s, p.detach())
+
+
+def test_lamb_matches_reference():
+    _ext_loaded()
+    ps = _params(torch.float32)
+    ref = [torch.nn.Parameter(p.detach().clone().cpu()) for p in ps]
+    f = fopt.FusedLAMB(ps, lr=1e-2, weight_decay=0.01)
+    r = fopt.FusedLAMB(ref, lr=1e-2, weight_decay=0.01)  # CPU path = reference math
+    for _ in range(3):
+        grads = [torch.randn(p.shape) for p in ps]
+        for p, g in zip(ps, grads):
+            p.grad.copy_(g.cuda())
+        for p, g in zip(ref, grads):
+            p.grad.copy_(g)
+        f.step()
+        r.step()
+    for p, q in zip(ps, ref):
+        torch.testing.assert_close(p.detach().cpu(), q.detach(), atol=1e-5, rtol=1e-4)
+
+
+def test_device_grad_scaler():
+    _ext_loaded()
+    ps = _params(torch.float32)
+    opt = fopt.FusedSGD(ps, lr=0.1)
+    sc = fopt.DeviceGradScaler(init_scale=1024.0, growth_interval=1)
+    for p in ps:
+        p.grad.fill_(1024.0)
+    before = [p.detach().clone() for p in ps]
+    sc.step(opt)
+    sc.update()
+    assert sc.get_scale() == 2048.0
+    for b, p in zip(before, ps):
+        torch.testing.assert_close(b - p.detach(), torch.full_like(b, 0.1))
+    ps[1].grad.fill_(float("nan"))
+    sc.step(opt)
+    sc.update()
+    assert sc.get_scale() == 1024.0
