@@ -1,0 +1,139 @@
+"""Headline benchmark: ResNet-50 PyTorchTrial training throughput (images/sec) on MI355X.
+
+BASELINE.json metric: "images/sec ResNet-50 PyTorchTrial at 1/2/4/8 MI355X". The step that is
+timed is the real PyTorchTrial path of this framework: ``pytorch.Trainer.fit`` ->
+``_PyTorchTrialController`` -> ``trial.train_batch`` (forward, ``context.backward`` with bucketed
+RCCL all-reduce overlapped with backward, ``context.step_optimizer`` with the fused HIP SGD) on
+ResNet-50 v1.5 (random init, 25.6M params), bf16 NHWC activations, fp32 master weights, synthetic
+224x224 ImageNet-shaped data resident in HBM. Weak scaling: 256 images per GPU per step.
+
+Usage: ``python bench.py [--gpus N --steps K --warmup W]``; for N>1 launch under
+``torch.distributed.run`` (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from the env).
+Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+# Ship MIOpen's find/perf databases with the repo so a fresh box skips convolution tuning.
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(HERE, "tools", "miopen", "db"))
+os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(HERE, "tools", "miopen", "cache"))
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from determined_clone_amd import pytorch  # noqa: E402
+from determined_clone_amd.models import resnet  # noqa: E402
+
+METRIC = "images/sec ResNet-50 PyTorchTrial"
+BASELINE_VALUE = None  # BASELINE.json "published" is empty
+
+
+class ResNet50BenchTrial(pytorch.PyTorchTrial):
+    def __init__(self, context: pytorch.PyTorchTrialContext) -> None:
+        self.context = context
+        hp = context.get_hparams()
+        self.per_slot = context.get_per_slot_batch_size()
+        self.warmup = int(hp["warmup"])
+        self.steps = int(hp["steps"])
+        model = resnet.to_mi355x_layout(resnet.resnet50())
+        self.model = context.wrap_model(model)
+        lr = 0.1 * context.get_global_batch_size() / 256
+        opt = torch.optim.SGD(self.model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5)
+        self.opt = context.wrap_optimizer(opt)
+        self.t0 = self.t1 = None
+
+    def _mark(self) -> float:
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if self.context.distributed.size > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        return time.perf_counter()
+
+    def train_batch(self, batch, epoch_idx: int, batch_idx: int):
+        if batch_idx == self.warmup:
+            self.t0 = self._mark()
+        images, labels = batch
+        logits = self.model(images)
+        loss = F.cross_entropy(logits.float(), labels)
+        self.context.backward(loss)
+        self.context.step_optimizer(self.opt)
+        if batch_idx == self.warmup + self.steps - 1:
+            self.t1 = self._mark()
+        return {"loss": loss}
+
+    def evaluate_batch(self, batch, batch_idx: int):
+        images, labels = batch
+        logits = self.model(images)
+        return {"val_loss": F.cross_entropy(logits.float(), labels)}
+
+    def _data(self, n_batches: int, length: int) -> pytorch.DataLoader:
+        dev = self.context.device
+        g = torch.Generator(device="cpu").manual_seed(1234 + self.context.distributed.rank)
+        batches = []
+        for _ in range(n_batches):
+            x = torch.randn(self.per_slot, 3, 224, 224, generator=g).to(dev, torch.bfloat16)
+            x = x.contiguous(memory_format=torch.channels_last)
+            y = torch.randint(0, 1000, (self.per_slot,), generator=g).to(dev)
+            batches.append((x, y))
+        # batch_size=None: each item already is a per-slot batch resident in HBM.
+        ds = pytorch.DeviceBatchDataset(batches, length * self.context.distributed.size)
+        return pytorch.DataLoader(ds, batch_size=None)
+
+    def build_training_data_loader(self):
+        return self._data(4, 10000)
+
+    def build_validation_data_loader(self):
+        return self._data(1, 1)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if torch.cuda.is_available():
+        torch.backends.cudnn.benchmark = True
+    hparams = {"global_batch_size": args.batch * world, "warmup": args.warmup, "steps": args.steps}
+    exp_conf = {"optimizations": {"aggregation_frequency": 1, "average_training_metrics": True}}
+    with pytorch.init(hparams=hparams, exp_conf=exp_conf) as ctx:
+        trial = ResNet50BenchTrial(ctx)
+        trainer = pytorch.Trainer(trial, ctx)
+        total = args.warmup + args.steps
+        trainer.fit(max_length=pytorch.Batch(total), reporting_period=pytorch.Batch(total),
+                    checkpoint_policy="none")
+        dt = trial.t1 - trial.t0
+        ms = dt / args.steps * 1000.0
+        if ctx.distributed.size > 1:
+            ms = max(ctx.distributed.allgather(ms))
+        imgs = args.batch * world * args.steps / (ms * args.steps / 1000.0)
+        if ctx.distributed.rank == 0:
+            out = {
+                "metric": METRIC, "value": round(imgs, 1), "unit": "images/sec",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None if BASELINE_VALUE is None else round(imgs / BASELINE_VALUE, 3),
+                "dtype": "bf16", "data": "synthetic (random 224x224x3 images + labels resident in HBM, random-init weights)",
+                "config": {"model": "resnet50", "global_batch": args.batch * world, "seq_len": None,
+                           "image_size": 224, "parallelism": f"dp{world}",
+                           "trial": "PyTorchTrial", "optimizer": "SGD momentum (fused HIP)",
+                           "slots_per_trial": world},
+            }
+            print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

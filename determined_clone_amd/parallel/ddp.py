@@ -1,0 +1,227 @@
+"""Data-parallel gradient synchronisation over RCCL (xGMI), overlapped with backward.
+
+Replaces the reference's Horovod ``DistributedOptimizer`` / torch ``DistributedDataParallel``
+(`harness/determined/pytorch/_pytorch_context.py` wrap_model / wrap_optimizer / backward).
+
+Design (MI355X-first):
+* gradients live in the flat buffers of a :class:`~.flat.FlatParamSpace`; a bucket is a contiguous
+  slice of that buffer, so RCCL all-reduces it IN PLACE — no pack/unpack copies;
+* the flat layout is reverse registration order, so buckets become ready roughly in index order as
+  backward proceeds; a post-accumulate-grad hook per parameter counts down its bucket and buckets
+  are launched strictly in index order (identical collective order on every rank);
+* bucket size is chosen for point-to-point xGMI rings: the first bucket is small (1 MiB) so
+  communication starts as soon as the last layers' grads exist, the rest are ``bucket_mb`` (default
+  32 MiB — at ~50 GB/s of per-peer ring bandwidth a 32 MiB bucket is ~0.7 ms, well above the
+  ~30 us collective latency yet small enough that the tail bucket after the last layer is short);
+* averaging is folded into the fused optimizer's grad multiplier (no extra pass) when possible;
+* ``comm_dtype`` (optimizations.gradient_compression) casts fp32 grads to bf16 for the wire.
+"""
+import contextlib
+import logging
+from typing import Any, Iterator, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from determined_clone_amd.parallel.flat import FlatBuffer, FlatParamSpace
+
+logger = logging.getLogger("determined_clone_amd.parallel")
+
+MiB = 1 << 20
+
+
+class _Bucket:
+    __slots__ = ("buf", "start", "end", "nparams", "pending", "work", "comm", "launched")
+
+    def __init__(self, buf: FlatBuffer, start: int, end: int, nparams: int) -> None:
+        self.buf = buf
+        self.start = start
+        self.end = end
+        self.nparams = nparams
+        self.pending = nparams
+        self.work: Any = None
+        self.comm: Optional[torch.Tensor] = None
+        self.launched = False
+
+
+class GradientSync:
+    def __init__(self, space: FlatParamSpace, group: Any = None, bucket_mb: float = 32.0,
+                 first_bucket_mb: float = 1.0, comm_dtype: Optional[torch.dtype] = None,
+                 average: bool = True) -> None:
+        self.space = space
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.comm_dtype = comm_dtype
+        self.average = average
+        self.fold_average = False  # set by the context when the fused optimizer scales grads
+        self.enabled = True
+        self.buckets: List[_Bucket] = []
+        self._param_bucket = {}
+        self._next = 0
+        self._hooks = []
+        self._build(bucket_mb, first_bucket_mb)
+        self._register_hooks()
+
+    # ------------------------------------------------------------------ setup
+    def _build(self, bucket_mb: float, first_mb: float) -> None:
+        for buf in self.space.buffers.values():
+            esz = buf.grad.element_size()
+            cap = first_mb * MiB
+            start = None
+            count = 0
+            last_end = 0
+            for seg in buf.segments:
+                if start is None:
+                    start = seg.offset
+                seg_end = seg.offset + ((seg.numel + 63) // 64) * 64
+                count += 1
+                self._param_bucket[id(seg.param)] = len(self.buckets)
+                last_end = seg_end
+                if (seg_end - start) * esz >= cap:
+                    self.buckets.append(_Bucket(buf, start, seg_end, count))
+                    start, count = None, 0
+                    cap = bucket_mb * MiB
+            if start is not None:
+                self.buckets.append(_Bucket(buf, start, last_end, count))
+        logger.debug(f"gradient sync: {len(self.buckets)} buckets, world={self.world}")
+
+    def _register_hooks(self) -> None:
+        for p in self.space.params():
+            if hasattr(p, "register_post_accumulate_grad_hook"):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    # ------------------------------------------------------------------ runtime
+    def _on_grad(self, p: torch.Tensor) -> None:
+        if not self.enabled or self.world == 1:
+            return
+        bi = self._param_bucket.get(id(p))
+        if bi is None:
+            return
+        buf = self.space.buffer_of(p)
+        seg = self.space.segment(p)
+        view_ptr = buf.grad.data_ptr() + seg.offset * buf.grad.element_size()
+        if p.grad is not None and p.grad.data_ptr() != view_ptr:
+            v = buf.view(buf.grad, seg)
+            v.copy_(p.grad)
+            p.grad = v
+        b = self.buckets[bi]
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch_ready()
+
+    def _launch_ready(self) -> None:
+        while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
+            self._launch(self.buckets[self._next])
+            self._next += 1
+
+    def _op(self) -> Any:
+        if self.average and not self.fold_average and dist.get_backend(self.group) == "nccl":
+            return dist.ReduceOp.AVG
+        return dist.ReduceOp.SUM
+
+    def _launch(self, b: _Bucket) -> None:
+        t = b.buf.grad[b.start:b.end]
+        if self.comm_dtype is not None and t.dtype != self.comm_dtype:
+            b.comm = t.to(self.comm_dtype)
+            t = b.comm
+        b.work = dist.all_reduce(t, op=self._op(), group=self.group, async_op=True)
+        b.launched = True
+
+    def finish(self) -> None:
+        """Launch buckets that never became ready (unused params) and wait for all; called after
+        backward and before the optimizer step."""
+        if self.world == 1 or not self.enabled:
+            return
+        for b in self.buckets[self._next:]:
+            if not b.launched:
+                self._launch(b)
+        self._next = len(self.buckets)
+        manual_div = self.average and not self.fold_average and self._op() == dist.ReduceOp.SUM
+        for b in self.buckets:
+            if b.work is not None:
+                b.work.wait()
+            if b.comm is not None:
+                b.buf.grad[b.start:b.end].copy_(b.comm)
+                b.comm = None
+            if manual_div:
+                b.buf.grad[b.start:b.end].div_(self.world)
+            b.work = None
+            b.launched = False
+            b.pending = b.nparams
+        self._next = 0
+
+    def reset(self) -> None:
+        for b in self.buckets:
+            b.pending = b.nparams
+            b.launched = False
+            b.work = None
+        self._next = 0
+
+    @contextlib.contextmanager
+    def no_sync(self) -> Iterator[None]:
+        old = self.enabled
+        self.enabled = False
+        try:
+            yield
+        finally:
+            self.enabled = old
+
+    def remove(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def broadcast_module_state(module: torch.nn.Module, group: Any = None, src: int = 0) -> None:
+    """Make every rank start from rank ``src``'s parameters and buffers (flat buffers go as one
+    collective each; loose tensors are coalesced per dtype)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    tensors = [p.data for p in module.parameters()] + [b for b in module.buffers()]
+    _broadcast_coalesced(tensors, group, src)
+
+
+def _broadcast_coalesced(tensors: List[torch.Tensor], group: Any, src: int) -> None:
+    by_dtype = {}
+    seen = set()
+    for t in tensors:
+        key = (t.data_ptr(), t.numel(), t.dtype)
+        if key in seen:
+            continue
+        seen.add(key)
+        by_dtype.setdefault((t.dtype, t.device), []).append(t)
+    for (dtype, device), ts in by_dtype.items():
+        flat = torch.cat([t.reshape(-1) for t in ts]) if len(ts) > 1 else ts[0].reshape(-1).clone()
+        if dist.get_backend(group) == "gloo" and flat.is_cuda:
+            cpu = flat.cpu()
+            dist.broadcast(cpu, src, group=group)
+            flat = cpu.to(device)
+        else:
+            dist.broadcast(flat, src, group=group)
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n
+
+
+def allreduce_loose_grads(params: List[torch.Tensor], group: Any = None, average: bool = True) -> None:
+    """All-reduce gradients that are not part of a flat space (coalesced per dtype)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    world = dist.get_world_size(group)
+    grads = [p.grad for p in params if p.grad is not None]
+    by_dtype = {}
+    for g in grads:
+        by_dtype.setdefault(g.dtype, []).append(g)
+    for ts in by_dtype.values():
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        dist.all_reduce(flat, group=group)
+        if average:
+            flat.div_(world)
+        off = 0
+        for t in ts:
+            n = t.numel()
+            t.copy_(flat[off:off + n].view_as(t))
+            off += n

@@ -31,8 +31,8 @@ class DataLoader:
         if isinstance(dataset, torch.utils.data.IterableDataset):
             raise ValueError("IterableDatasets are not supported by DataLoader(); shard/repeat/skip "
                              "them yourself and return a torch DataLoader from the trial instead")
-        if batch_sampler is None and batch_size is None:
-            raise ValueError("batch_sampler=None and batch_size=None is not supported")
+        # batch_size=None (no auto-collation: every item is already a batch) is supported here,
+        # unlike the reference; the sampler chain then shards/repeats/skips whole batches.
         if num_workers < 0:
             raise ValueError("num_workers option should be non-negative")
         if timeout < 0:
