@@ -25,20 +25,20 @@ class _BNActTrain(torch.autograd.Function):
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, num_batches, momentum,
                 eps, relu):
         C = _ext.load()
-        y, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
-                                         num_batches, momentum, eps, relu)
-        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        y, mean, invstd, mask = C.bn_fwd_train(x, residual, weight, bias, running_mean,
+                                               running_var, num_batches, momentum, eps, relu)
+        # The ReLU decision is kept as a bitmask (1/16 of y) instead of y itself.
+        ctx.save_for_backward(x, mask if relu else None, weight, mean, invstd)
         ctx.relu = relu
         ctx.has_res = residual is not None
-        ctx.mark_non_differentiable(mean, invstd)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, mean, invstd = ctx.saved_tensors
+        x, mask, weight, mean, invstd = ctx.saved_tensors
         need_w = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         dx, dgamma, dbeta, dres = _ext.load().bn_bwd_train(
-            dy, x, y, weight, mean, invstd, ctx.relu, ctx.has_res, need_w)
+            dy, x, mask, weight, mean, invstd, ctx.relu, ctx.has_res, need_w)
         return (dx, dgamma if need_w else None, dbeta if need_w else None,
                 dres if ctx.has_res else None, None, None, None, None, None, None)
 

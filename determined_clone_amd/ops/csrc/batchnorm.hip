@@ -10,7 +10,9 @@
 //                      per-channel scale/shift, num_batches_tracked += 1
 //   bn_apply_fwd     : y = act(x*scale + shift [+ res])                        (reads x[,res], writes y)
 // Training backward = 3 launches, 2 passes:
-//   bn_reduce<BWD>   : partial (sum dy', sum dy'*(x-mean)), dy' = relu ? dy*(y>0) : dy
+//   bn_reduce<BWD>   : partial (sum dy', sum dy'*(x-mean)), dy' = relu ? dy*mask : dy
+// The forward stores the ReLU decision as a 1-bit-per-element mask (1/16 of the bf16 output), so
+// the backward never re-reads y.
 //   bn_finalize_bwd  : dgamma, dbeta and the affine form dx = k1*dy' + k2*x + k3
 //   bn_apply_bwd     : dx (and d_residual = dy' when the residual add was fused)
 // Every lane moves 8 channels (16 B of bf16) per access; reductions are deterministic.
@@ -42,7 +44,7 @@ inline ReduceGeom reduce_geom(int C) {
 
 template <typename T, bool BWD>
 __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
-    const void* __restrict__ x, const void* __restrict__ dy, const void* __restrict__ y,
+    const void* __restrict__ x, const void* __restrict__ dy, const uint8_t* __restrict__ mask,
     const float* __restrict__ mean, int64_t M, int C, int tpr, int rpi, bool relu,
     float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][tpr*16]
@@ -71,10 +73,9 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
         float g[8];
         Vec8<T>::load(reinterpret_cast<const char*>(dy) + off * Vec8<T>::bytes, g);
         if (relu) {
-          float yv[8];
-          Vec8<T>::load(reinterpret_cast<const char*>(y) + off * Vec8<T>::bytes, yv);
+          const uint32_t m = mask[off >> 3];  // one ReLU bit per element, 8 channels per byte
 #pragma unroll
-          for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+          for (int k = 0; k < 8; ++k) g[k] = ((m >> k) & 1u) ? g[k] : 0.f;
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) { s[k] += g[k]; q[k] = fmaf(g[k], xv[k] - mu[k], q[k]); }
@@ -178,7 +179,7 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
     const void* __restrict__ x, const void* __restrict__ res, void* __restrict__ y,
     const float* __restrict__ scale, const float* __restrict__ shift, int64_t nvec, int c8,
-    bool relu) {
+    bool relu, uint8_t* __restrict__ mask) {
   // nvec < 2^31 is checked on the host: 32-bit index math (a 64-bit modulo is a long
   // software sequence on CDNA), 64-bit byte offsets.
   const uint32_t stride = gridDim.x * blockDim.x, n = static_cast<uint32_t>(nvec);
@@ -201,8 +202,13 @@ __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
       for (int k = 0; k < 8; ++k) o[k] += rv[k];
     }
     if (relu) {
+      uint32_t bits = 0;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = fmaxf(o[k], 0.f);
+      for (int k = 0; k < 8; ++k) {
+        bits |= (o[k] > 0.f ? 1u : 0u) << k;
+        o[k] = fmaxf(o[k], 0.f);
+      }
+      if (mask) mask[v] = static_cast<uint8_t>(bits);
     }
     Vec8<T>::store(reinterpret_cast<char*>(y) + static_cast<int64_t>(v) * 8 * Vec8<T>::bytes, o);
   }
@@ -210,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
-    const void* __restrict__ dy, const void* __restrict__ y, const void* __restrict__ x,
+    const void* __restrict__ dy, const uint8_t* __restrict__ mask, const void* __restrict__ x,
     const float* __restrict__ coef, void* __restrict__ dx, void* __restrict__ dres, int64_t nvec,
     int c8, int C, bool relu) {
   // nvec < 2^31 is checked on the host: 32-bit index math (a 64-bit modulo is a long
@@ -222,10 +228,9 @@ __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
     float g[8], xv[8];
     Vec8<T>::load(reinterpret_cast<const char*>(dy) + off, g);
     if (relu) {
-      float yv[8];
-      Vec8<T>::load(reinterpret_cast<const char*>(y) + off, yv);
+      const uint32_t m = mask[v];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+      for (int k = 0; k < 8; ++k) g[k] = ((m >> k) & 1u) ? g[k] : 0.f;
     }
     Vec8<T>::load(reinterpret_cast<const char*>(x) + off, xv);
     float o[8];
@@ -250,7 +255,7 @@ inline int reduce_blocks(int64_t M, int C, const ReduceGeom& g) {
 }
 
 template <typename T>
-void launch_reduce(bool bwd, const void* x, const void* dy, const void* y, const float* mean,
+void launch_reduce(bool bwd, const void* x, const void* dy, const uint8_t* y, const float* mean,
                    int64_t M, int C, bool relu, float* partial, int B, const ReduceGeom& g,
                    hipStream_t st) {
   dim3 grid(B, g.cgroups);
@@ -275,7 +280,7 @@ int64_t bn_workspace_floats(int64_t M, int C) {
 void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
                       const float* gamma, const float* beta, float* running_mean,
                       float* running_var, float momentum, float eps, bool relu, float* save_mean,
-                      float* save_invstd, int64_t* num_batches, float* workspace,
+                      float* save_invstd, int64_t* num_batches, uint8_t* mask, float* workspace,
                       hipStream_t st) {
   ReduceGeom g = reduce_geom(C);
   int B = reduce_blocks(M, C, g);
@@ -293,25 +298,26 @@ void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64
   const int64_t nvec = M * C / 8;
   const int grid = stream_grid(nvec, kBlock);
   switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
-    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
-    default: hipLaunchKernelGGL(bn_apply_fwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
+    default: hipLaunchKernelGGL(bn_apply_fwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
   }
 }
 
 // Inference-mode forward with precomputed per-channel scale/shift (fp32, [C] each).
 void bn_forward_affine(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
                        const float* scale, const float* shift, bool relu, hipStream_t st) {
+  uint8_t* mask = nullptr;
   const int64_t nvec = M * C / 8;
   const int grid = stream_grid(nvec, kBlock);
   switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
-    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
-    default: hipLaunchKernelGGL(bn_apply_fwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu); break;
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
+    default: hipLaunchKernelGGL(bn_apply_fwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
   }
 }
 
-void bn_backward_train(BnDtype dt, const void* dy, const void* y, const void* x, int64_t M, int C,
+void bn_backward_train(BnDtype dt, const void* dy, const uint8_t* y, const void* x, int64_t M, int C,
                        const float* gamma, const float* save_mean, const float* save_invstd,
                        bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
                        float* workspace, hipStream_t st) {

@@ -16,10 +16,11 @@ int64_t bn_workspace_floats(int64_t M, int C);
 void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
                       const float* gamma, const float* beta, float* running_mean,
                       float* running_var, float momentum, float eps, bool relu, float* save_mean,
-                      float* save_invstd, int64_t* num_batches, float* workspace, hipStream_t st);
+                      float* save_invstd, int64_t* num_batches, uint8_t* mask, float* workspace,
+                      hipStream_t st);
 void bn_forward_affine(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
                        const float* scale, const float* shift, bool relu, hipStream_t st);
-void bn_backward_train(BnDtype dt, const void* dy, const void* y, const void* x, int64_t M, int C,
+void bn_backward_train(BnDtype dt, const void* dy, const uint8_t* mask, const void* x, int64_t M, int C,
                        const float* gamma, const float* save_mean, const float* save_invstd,
                        bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
                        float* workspace, hipStream_t st);
@@ -115,13 +116,16 @@ std::vector<Tensor> bn_fwd_train(const Tensor& x, const OptT& residual, const Op
   Tensor y = torch::empty_like(x);
   Tensor save_mean = torch::empty({C}, fopt), save_invstd = torch::empty({C}, fopt);
   Tensor ws = torch::empty({dca::bn_workspace_floats(M, C)}, fopt);
+  Tensor mask = relu ? torch::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
   dca::bn_forward_train(bn_dtype(x), x.data_ptr(), vptr_or_null(residual), y.data_ptr(), M, C,
                         ptr_or_null<float>(weight), ptr_or_null<float>(bias),
                         ptr_or_null<float>(running_mean), ptr_or_null<float>(running_var),
                         static_cast<float>(momentum), static_cast<float>(eps), relu,
                         save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
-                        ptr_or_null<int64_t>(num_batches), ws.data_ptr<float>(), cur_stream());
-  return {y, save_mean, save_invstd};
+                        ptr_or_null<int64_t>(num_batches),
+                        relu ? mask.data_ptr<uint8_t>() : nullptr, ws.data_ptr<float>(),
+                        cur_stream());
+  return {y, save_mean, save_invstd, mask};
 }
 
 Tensor bn_fwd_affine(const Tensor& x, const OptT& residual, const Tensor& scale,
@@ -138,7 +142,7 @@ Tensor bn_fwd_affine(const Tensor& x, const OptT& residual, const Tensor& scale,
   return y;
 }
 
-std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const OptT& y,
+std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const OptT& mask,
                                  const OptT& weight, const Tensor& save_mean,
                                  const Tensor& save_invstd, bool relu, bool need_dres,
                                  bool need_dweight) {
@@ -147,14 +151,15 @@ std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const Opt
   auto [M, C] = rows_channels(x);
   Tensor dy = dy_in.dim() == 4 ? dy_in.contiguous(at::MemoryFormat::ChannelsLast) : dy_in.contiguous();
   TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "batchnorm bwd: grad dtype mismatch");
-  TORCH_CHECK(!relu || (y.has_value() && y->defined()), "batchnorm bwd: relu needs the output");
+  TORCH_CHECK(!relu || (mask.has_value() && mask->defined() && mask->numel() == M * C / 8),
+              "batchnorm bwd: relu needs the forward's ReLU bitmask");
   auto fopt = x.options().dtype(at::kFloat);
   Tensor dx = torch::empty_like(x);
   Tensor dres = need_dres ? torch::empty_like(x) : Tensor();
   Tensor dgamma = need_dweight ? torch::empty({C}, fopt) : Tensor();
   Tensor dbeta = need_dweight ? torch::empty({C}, fopt) : Tensor();
   Tensor ws = torch::empty({dca::bn_workspace_floats(M, C)}, fopt);
-  dca::bn_backward_train(bn_dtype(x), dy.data_ptr(), relu ? y->data_ptr() : nullptr, x.data_ptr(),
+  dca::bn_backward_train(bn_dtype(x), dy.data_ptr(), relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(),
                          M, C, ptr_or_null<float>(weight), save_mean.data_ptr<float>(),
                          save_invstd.data_ptr<float>(), relu, dx.data_ptr(),
                          need_dres ? dres.data_ptr() : nullptr,

@@ -1,0 +1,103 @@
+"""Multi-process data-parallel correctness on CPU (gloo, world_size 2)."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank: int, world: int, port: int) -> None:
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "LOCAL_WORLD_SIZE": str(world)})
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _model() -> torch.nn.Module:
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+
+
+def _data(n=8):
+    g = torch.Generator().manual_seed(42)
+    return torch.randn(n, 16, generator=g), torch.randn(n, 4, generator=g)
+
+
+def _worker_sync(rank: int, world: int, port: int, fused: bool, agg: int, out_dir: str) -> None:
+    _init(rank, world, port)
+    from determined_clone_amd import core, pytorch
+
+    dist_ctx = core.DistributedContext.from_torch_distributed()
+    with pytorch.init(hparams={}, distributed=dist_ctx, aggregation_frequency=agg,
+                      exp_conf={"optimizations": {}}) as ctx:
+        model = ctx.wrap_model(_model())
+        opt = ctx.wrap_optimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), fused=fused)
+        x, y = _data(8 * agg)
+        for step in range(3):
+            for micro in range(agg):
+                ctx._current_batch_idx = step * agg + micro
+                lo = (micro * world + rank) * 4
+                xb, yb = x[lo:lo + 4], y[lo:lo + 4]
+                loss = torch.nn.functional.mse_loss(model(xb), yb)
+                ctx.backward(loss)
+                ctx.step_optimizer(opt)
+        torch.save({k: v.detach().clone() for k, v in model.state_dict().items()},
+                   os.path.join(out_dir, f"r{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+def _reference(agg: int):
+    model = _model()
+    opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9)
+    x, y = _data(8 * agg)
+    for step in range(3):
+        opt.zero_grad()
+        for micro in range(agg):
+            xb, yb = x[micro * 8:(micro + 1) * 8], y[micro * 8:(micro + 1) * 8]
+            (torch.nn.functional.mse_loss(model(xb), yb) / agg).backward()
+        opt.step()
+    return model.state_dict()
+
+
+@pytest.mark.parametrize("fused,agg", [(False, 1), (True, 1), (True, 2), (False, 2)])
+def test_data_parallel_matches_single_process(fused, agg):
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker_sync, args=(world, _free_port(), fused, agg, d), nprocs=world,
+                           start_method="spawn")
+        ref = _reference(agg)
+        r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)
+        for k in ref:
+            torch.testing.assert_close(r0[k], r1[k], atol=0, rtol=0)
+            torch.testing.assert_close(r0[k], ref[k], atol=1e-5, rtol=1e-5)
+
+
+def _worker_core(rank: int, world: int, port: int, out_dir: str) -> None:
+    _init(rank, world, port)
+    from determined_clone_amd import core
+
+    d = core.DistributedContext.from_torch_distributed()
+    assert d.allgather(rank) == [0, 1]
+    g = d.gather(rank * 10)
+    assert (g == [0, 10]) if rank == 0 else g is None
+    assert d.broadcast("chief" if rank == 0 else None) == "chief"
+    assert d.allgather_local(rank) == [0, 1]
+    open(os.path.join(out_dir, f"ok{rank}"), "w").close()
+    torch.distributed.destroy_process_group()
+
+
+def test_core_distributed_context_collectives():
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker_core, args=(2, _free_port(), d), nprocs=2, start_method="spawn")
+        assert os.path.exists(os.path.join(d, "ok0")) and os.path.exists(os.path.join(d, "ok1"))

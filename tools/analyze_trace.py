@@ -1,0 +1,68 @@
+"""Summarise a rocprofv3 kernel trace over the last N training steps.
+
+Steps are delimited by the fused SGD kernel (one launch per param group per step). Prints the
+per-step GPU busy time and the top kernels by time, grouped into categories."""
+import csv
+import re
+import sys
+from collections import defaultdict
+
+
+def category(name: str) -> str:
+    n = name
+    if "bn_" in n and "dca" in n:
+        return "dca BatchNorm(+add+ReLU)"
+    if "sgd_kernel" in n or "adam_kernel" in n or "lamb" in n or "sumsq" in n or "norm_finalize" in n:
+        return "dca optimizer"
+    if "igemm_fwd" in n or "conv_fwd" in n or "ConvFwd" in n or ("fwd" in n and "conv" in n.lower()):
+        return "conv fwd (MIOpen)"
+    if "igemm_bwd" in n or "bwd_data" in n or ("conv" in n.lower() and "bwd" in n and "weight" not in n):
+        return "conv bwd-data (MIOpen)"
+    if "wrw" in n or "bwd_weight" in n:
+        return "conv bwd-weight (MIOpen)"
+    if "gemm" in n.lower() or "Cijk" in n:
+        return "gemm (fc)"
+    if "fillBuffer" in n or "copyBuffer" in n:
+        return "memset/copy"
+    if "elementwise" in n or "Functor" in n:
+        return "torch elementwise"
+    if "reduce" in n.lower():
+        return "torch reduce"
+    return "other"
+
+
+def main(path: str, steps: int = 3, step_marker: str = "sgd_kernel", per_step: int = 2) -> None:
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if step_marker in r["Kernel_Name"]]
+    # the fused optimizer launches once per (dtype buffer, param group): `per_step` per step
+    marks = marks[per_step - 1::per_step]
+    if len(marks) < steps + 1:
+        print("not enough steps in trace")
+        return
+    lo, hi = marks[-steps - 1] + 1, marks[-1] + 1
+    seg = rows[lo:hi]
+    t0 = int(seg[0]["Start_Timestamp"])
+    t1 = int(seg[-1]["End_Timestamp"])
+    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg)
+    by_cat = defaultdict(float)
+    by_name = defaultdict(lambda: [0.0, 0])
+    for r in seg:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        by_cat[category(r["Kernel_Name"])] += d
+        k = by_name[r["Kernel_Name"][:110]]
+        k[0] += d
+        k[1] += 1
+    print(f"steps={steps} wall/step={(t1 - t0) / 1e6 / steps:.3f} ms  gpu-busy/step={busy / 1e6 / steps:.3f} ms "
+          f"kernels/step={len(seg) / steps:.0f}")
+    print("\nby category (ms/step):")
+    for c, v in sorted(by_cat.items(), key=lambda x: -x[1]):
+        print(f"  {c:32s} {v / steps:8.3f}  {100 * v / (busy / 1e6):5.1f}%")
+    print("\ntop kernels (ms/step, calls/step):")
+    for n, (v, c) in sorted(by_name.items(), key=lambda x: -x[1][0])[:25]:
+        print(f"  {v / steps:8.3f} {c / steps:5.0f}  {n}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 3,
+         per_step=int(sys.argv[3]) if len(sys.argv) > 3 else 2)
