@@ -1,0 +1,270 @@
+"""Agent: reports this host's MI355X slots to the master and runs tasks on them.
+
+Reference: `agent/internal` (Go; Docker container runtime, rocm-smi/nvidia-smi detection).
+Here a task is a process group (no Docker in this image): the agent fetches the task's context
+directory from the master, sets ``HIP_VISIBLE_DEVICES`` to the assigned slots, ``DET_*`` env and
+the cluster-info document, starts ``exec.launch``, ships stdout/stderr lines to the master, and
+reports RUNNING / TERMINATED(exit code). Kill = SIGTERM to the process group, SIGKILL after a
+grace period.
+
+Devices: KFD topology via the native module (`native/scheduler.cpp: detect_kfd_gpus`), falling
+back to ``rocm-smi --json``; CPU-only hosts expose ``--artificial-slots`` CPU slots.
+"""
+import argparse
+import base64
+import json
+import logging
+import os
+import shutil
+import signal
+import socket
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+import uuid
+from typing import Any, Dict, List, Optional
+
+from determined_clone_amd.common.api import Session
+
+logger = logging.getLogger("determined_clone_amd.agent")
+
+FRAMEWORK_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def detect_devices(artificial_slots: int = 0) -> List[Dict[str, Any]]:
+    if artificial_slots > 0:
+        return [{"id": i, "uuid": f"cpu-{i}", "type": "cpu", "brand": "artificial"} for i in range(artificial_slots)]
+    devs: List[Dict[str, Any]] = []
+    try:
+        from determined_clone_amd.native import load
+
+        for g in load().detect_kfd_gpus(""):
+            devs.append({"id": int(g["index"]), "uuid": g.get("unique_id") or g["index"],
+                         "type": "rocm", "brand": "AMD", "gfx_target": g.get("gfx_target"),
+                         "cu_count": int(g.get("cu_count") or 0),
+                         "vram_bytes": int(g.get("vram_bytes") or 0)})
+    except Exception as e:  # pragma: no cover - no native module / no KFD
+        logger.debug(f"KFD detection failed: {e}")
+    if not devs and shutil.which("rocm-smi"):
+        try:
+            out = subprocess.run(["rocm-smi", "--showuniqueid", "--showbus", "--json"],
+                                 capture_output=True, text=True, timeout=30).stdout
+            for k, v in sorted(json.loads(out).items()):
+                if k.startswith("card"):
+                    devs.append({"id": int(k[4:]), "uuid": v.get("Unique ID", k), "type": "rocm",
+                                 "brand": "AMD"})
+        except Exception:  # pragma: no cover
+            pass
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+    if vis and devs:
+        keep = {int(x) for x in vis.split(",") if x.strip().isdigit()}
+        devs = [d for d in devs if d["id"] in keep]
+    if not devs:
+        devs = [{"id": 0, "uuid": "cpu-0", "type": "cpu", "brand": "cpu"}]
+    return devs
+
+
+class _Task:
+    def __init__(self, spec: Dict[str, Any], proc: subprocess.Popen, workdir: str) -> None:
+        self.spec = spec
+        self.proc = proc
+        self.workdir = workdir
+        self.killed = False
+
+
+class Agent:
+    def __init__(self, master_url: str, agent_id: Optional[str] = None, pool: str = "default",
+                 artificial_slots: int = 0, label: str = "", username: str = "admin",
+                 password: str = "", workdir: Optional[str] = None) -> None:
+        self.session = Session(master_url)
+        tok = self.session.post("/api/v1/auth/login", {"username": username, "password": password})["token"]
+        self.session.token = tok
+        self.master_url = self.session.master
+        self.id = agent_id or socket.gethostname()
+        self.pool = pool
+        self.label = label
+        self.devices = detect_devices(artificial_slots)
+        self.tasks: Dict[str, _Task] = {}
+        self.workdir = workdir or tempfile.mkdtemp(prefix="det-clone-agent-")
+        self._stop = threading.Event()
+        self._lock = threading.Lock()
+
+    def register(self) -> None:
+        self.session.post("/api/v1/agents/register", {
+            "agent_id": self.id, "slots": self.devices, "resource_pool": self.pool,
+            "label": self.label, "addresses": ["127.0.0.1"]})
+
+    # ------------------------------------------------------------------ task lifecycle
+    def _start(self, spec: Dict[str, Any]) -> None:
+        alloc = spec["allocation_id"]
+        task_id = spec["task_id"]
+        wd = os.path.join(self.workdir, alloc.replace("/", "_"))
+        ctx_dir = os.path.join(wd, "context")
+        os.makedirs(ctx_dir, exist_ok=True)
+        try:
+            blob = self.session.get(f"/api/v1/tasks/{task_id}/context").get("b64_tgz")
+            if blob:
+                from determined_clone_amd.util import untar_to
+
+                untar_to(base64.b64decode(blob), ctx_dir)
+        except Exception as e:
+            logger.warning(f"could not fetch context for {task_id}: {e}")
+        info = dict(spec["cluster_info"])
+        info["agent_id"] = self.id
+        info["slot_ids"] = list(spec.get("slots") or [])
+        info["gpu_uuids"] = [d["uuid"] for d in self.devices if d["id"] in set(spec.get("slots") or [])
+                             and d["type"] == "rocm"]
+        if spec.get("num_containers", 1) > 1:
+            info["rendezvous"] = {"container_addrs": ["127.0.0.1"] * spec["num_containers"],
+                                  "container_rank": spec.get("container_rank", 0)}
+        env = dict(os.environ)
+        user_env = (spec.get("environment") or {}).get("environment_variables") or {}
+        if isinstance(user_env, list):
+            user_env = dict(x.split("=", 1) for x in user_env if "=" in x)
+        elif isinstance(user_env, dict) and ("rocm" in user_env or "cpu" in user_env or "cuda" in user_env):
+            user_env = dict(x.split("=", 1) for x in (user_env.get("rocm") or user_env.get("cpu") or []) if "=" in x)
+        env.update({str(k): str(v) for k, v in user_env.items()})
+        env["DET_CLUSTER_INFO"] = json.dumps(info)
+        env["DET_CONTEXT_DIR"] = ctx_dir
+        env["DET_MASTER"] = self.master_url
+        env["DET_AGENT_ID"] = self.id
+        env["DET_ALLOCATION_ID"] = alloc
+        env["DET_TASK_ID"] = task_id
+        env["PYTHONUNBUFFERED"] = "1"
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        env["PYTHONPATH"] = os.pathsep.join([ctx_dir, FRAMEWORK_ROOT] + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
+        slots = spec.get("slots") or []
+        if any(d["type"] == "rocm" for d in self.devices):
+            env["HIP_VISIBLE_DEVICES"] = ",".join(str(s) for s in slots) if slots else ""
+        else:
+            env["DET_SLOTS"] = str(max(len(slots), 1))
+        if spec["kind"] == "TRIAL":
+            cmd = [sys.executable, "-m", "determined_clone_amd.exec.launch"]
+        else:
+            cmd = list(spec.get("entrypoint") or ["true"])
+            if cmd and cmd[0] in ("python", "python3"):
+                cmd[0] = sys.executable
+        proc = subprocess.Popen(cmd, cwd=ctx_dir, env=env, stdout=subprocess.PIPE,
+                                stderr=subprocess.STDOUT, start_new_session=True)
+        t = _Task(spec, proc, wd)
+        with self._lock:
+            self.tasks[alloc] = t
+        self._event(alloc, "RUNNING")
+        threading.Thread(target=self._pump, args=(t,), daemon=True).start()
+
+    def _pump(self, t: _Task) -> None:
+        alloc = t.spec["allocation_id"]
+        task_id = t.spec["task_id"]
+        buf: List[Dict[str, Any]] = []
+        last = time.time()
+
+        def flush() -> None:
+            nonlocal buf, last
+            if buf:
+                try:
+                    self.session.post("/api/v1/task/logs", {"logs": buf})
+                except Exception as e:
+                    logger.warning(f"log shipping failed: {e}")
+                buf = []
+            last = time.time()
+
+        for raw in iter(t.proc.stdout.readline, b""):
+            line = raw.decode(errors="replace").rstrip("\n")
+            rank = None
+            if line.startswith("[rank"):
+                try:
+                    rank = int(line[line.index("=") + 1: line.index("]")])
+                except ValueError:
+                    rank = None
+            buf.append({"task_id": task_id, "allocation_id": alloc, "agent_id": self.id,
+                        "log": line, "timestamp": time.time(), "rank_id": rank,
+                        "container_id": str(t.spec.get("container_rank", 0))})
+            if len(buf) >= 200 or time.time() - last > 1.0:
+                flush()
+        code = t.proc.wait()
+        flush()
+        with self._lock:
+            self.tasks.pop(alloc, None)
+        self._event(alloc, "TERMINATED", code if not t.killed else (code or 137))
+        shutil.rmtree(t.workdir, ignore_errors=True)
+
+    def _kill(self, alloc: str, grace: float = 10.0) -> None:
+        t = self.tasks.get(alloc)
+        if t is None:
+            return
+        t.killed = True
+        try:
+            os.killpg(t.proc.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            return
+
+        def hard() -> None:
+            time.sleep(grace)
+            if t.proc.poll() is None:
+                try:
+                    os.killpg(t.proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+
+        threading.Thread(target=hard, daemon=True).start()
+
+    def _event(self, alloc: str, state: str, exit_code: Optional[int] = None) -> None:
+        try:
+            self.session.post(f"/api/v1/agents/{self.id}/events",
+                              {"allocation_id": alloc, "state": state, "exit_code": exit_code})
+        except Exception as e:
+            logger.warning(f"event report failed: {e}")
+
+    # ------------------------------------------------------------------ main loop
+    def run(self) -> None:
+        self.register()
+        while not self._stop.is_set():
+            try:
+                acts = self.session.get(f"/api/v1/agents/{self.id}/actions",
+                                        params={"timeout_seconds": 5}, timeout=30)["actions"]
+            except Exception as e:
+                logger.warning(f"master unreachable: {e}; re-registering")
+                time.sleep(1)
+                try:
+                    self.register()
+                except Exception:
+                    pass
+                continue
+            for a in acts:
+                try:
+                    if a["type"] == "start":
+                        self._start(a["spec"])
+                    elif a["type"] == "kill":
+                        self._kill(a["allocation_id"])
+                except Exception:
+                    logger.exception(f"failed to handle action {a.get('type')}")
+                    if a.get("type") == "start":
+                        self._event(a["spec"]["allocation_id"], "TERMINATED", 1)
+
+    def start_background(self) -> "Agent":
+        self.register()
+        threading.Thread(target=self.run, daemon=True, name=f"agent-{self.id}").start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        for alloc in list(self.tasks):
+            self._kill(alloc, grace=2.0)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser("det-clone-agent")
+    ap.add_argument("--master-url", default=os.environ.get("DET_MASTER", "http://127.0.0.1:8080"))
+    ap.add_argument("--agent-id", default=None)
+    ap.add_argument("--resource-pool", default="default")
+    ap.add_argument("--artificial-slots", type=int, default=0)
+    ap.add_argument("--label", default="")
+    args = ap.parse_args()
+    logging.basicConfig(level=logging.INFO)
+    Agent(args.master_url, args.agent_id, args.resource_pool, args.artificial_slots, args.label).run()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,572 @@
+"""The master process state: DB, resource manager, experiments, allocations, agents, logs.
+
+Reference: `master/internal/core.go` (Master), `task/allocation*.go` (allocations, preemption
+signals, rendezvous), `checkpoint_gc.go`, `webhooks`, `command` (NTSC tasks).
+"""
+import hashlib
+import json
+import logging
+import os
+import secrets
+import shutil
+import threading
+import time
+import uuid
+from typing import Any, Dict, List, Optional, Tuple
+
+from determined_clone_amd.config import expconf
+from determined_clone_amd.master.db import DB, dec, now
+from determined_clone_amd.master.experiment import (ACTIVE, PAUSED, TERMINAL, Experiment, Trial,
+                                                    experiment_row_to_api, trial_row_to_api)
+from determined_clone_amd.master.rm import AgentState, AllocationRequest, ResourceManager
+
+logger = logging.getLogger("determined_clone_amd.master")
+
+
+def hash_password(pw: str) -> str:
+    return hashlib.sha512(("determined-clone-amd" + pw).encode()).hexdigest()
+
+
+class Allocation:
+    def __init__(self, alloc_id: str, task_id: str, kind: str, exp: Optional[Experiment] = None,
+                 trial: Optional[Trial] = None, spec: Optional[Dict[str, Any]] = None) -> None:
+        self.id = alloc_id
+        self.task_id = task_id
+        self.kind = kind  # TRIAL | COMMAND | SHELL | NOTEBOOK | TENSORBOARD | CHECKPOINT_GC
+        self.exp = exp
+        self.trial = trial
+        self.spec = spec or {}
+        self.state = "PENDING"
+        self.preempt = threading.Event()
+        self.preempt_acked = False
+        self.ready = False
+        self.placements: List[Dict[str, Any]] = []
+        self.exited = False
+        self.exit_code: Optional[int] = None
+        self.containers_running = 0
+        self.allgather: Dict[str, Any] = {}
+        self.allgather_cv = threading.Condition()
+        self.proxy_address: Optional[str] = None
+
+
+class Webhooks:
+    """Outgoing webhooks on experiment/trial state changes (reference: internal/webhooks)."""
+
+    def __init__(self, master: "Master") -> None:
+        self.master = master
+
+    def _fire(self, trigger: str, payload: Dict[str, Any]) -> None:
+        hooks = self.master.db.all("SELECT * FROM webhooks")
+        if not hooks:
+            return
+        import requests
+
+        for h in hooks:
+            triggers = dec(h["triggers"], []) or []
+            if not any(tr.get("trigger_type") == trigger and
+                       (tr.get("condition", {}).get("state") in (None, payload.get("state")))
+                       for tr in triggers):
+                continue
+            body = payload if h["webhook_type"] != "SLACK" else {"text": json.dumps(payload)}
+
+            def send(url: str = h["url"], b: Dict[str, Any] = body) -> None:
+                try:
+                    requests.post(url, json=b, timeout=5)
+                except Exception as e:  # pragma: no cover - best effort
+                    logger.warning(f"webhook {url} failed: {e}")
+
+            threading.Thread(target=send, daemon=True).start()
+
+    def experiment_event(self, exp: Experiment, state: str) -> None:
+        self._fire("EXPERIMENT_STATE_CHANGE", {"type": "EXPERIMENT_STATE_CHANGE",
+                                               "experiment_id": exp.id, "state": state})
+
+    def trial_event(self, exp: Experiment, t: Trial, state: str) -> None:
+        self._fire("TRIAL_STATE_CHANGE", {"type": "TRIAL_STATE_CHANGE", "experiment_id": exp.id,
+                                          "trial_id": t.id, "state": state})
+
+
+class Master:
+    def __init__(self, db_path: str = ":memory:", scheduler: str = "priority", fit: str = "best",
+                 preemption: bool = True, checkpoint_storage: Optional[Dict[str, Any]] = None,
+                 cluster_name: str = "default", master_url: str = "http://127.0.0.1:8080") -> None:
+        self.db = DB(db_path)
+        self.cluster_id = self.db.kv_get("cluster_id") or str(uuid.uuid4())
+        self.db.kv_set("cluster_id", self.cluster_id)
+        self.cluster_name = cluster_name
+        self.master_url = master_url
+        self.checkpoint_storage = checkpoint_storage or {
+            "type": "shared_fs", "host_path": os.path.join(os.path.expanduser("~"), ".det-clone-ckpts")}
+        self.rm = ResourceManager(scheduler, fit, preemption, on_start=self._on_alloc_start,
+                                  on_preempt=self._on_alloc_preempt)
+        self.experiments: Dict[int, Experiment] = {}
+        self.allocations: Dict[str, Allocation] = {}
+        self.tasks: Dict[str, Dict[str, Any]] = {}
+        self.webhooks = Webhooks(self)
+        self.lock = threading.RLock()
+        self.log_cv = threading.Condition()
+        self.start_time = time.time()
+        self._bootstrap_users()
+        self._restore()
+
+    # ------------------------------------------------------------------ users / auth
+    def _bootstrap_users(self) -> None:
+        if not self.db.one("SELECT id FROM users WHERE username='admin'"):
+            self.db.insert("users", {"username": "admin", "password_hash": hash_password(""),
+                                     "admin": 1, "active": 1, "created": now()})
+            self.db.insert("users", {"username": "determined", "password_hash": hash_password(""),
+                                     "admin": 0, "active": 1, "created": now()})
+        if not self.db.one("SELECT id FROM workspaces WHERE id=1"):
+            self.db.insert("workspaces", {"name": "Uncategorized", "user_id": 1, "created": now()})
+            self.db.insert("projects", {"name": "Uncategorized", "workspace_id": 1, "user_id": 1,
+                                        "created": now()})
+
+    def login(self, username: str, password: str) -> Tuple[str, Dict[str, Any]]:
+        u = self.db.one("SELECT * FROM users WHERE username=?", [username])
+        if u is None or u["password_hash"] != hash_password(password or "") or not u["active"]:
+            raise PermissionError("invalid credentials")
+        token = secrets.token_hex(24)
+        self.db.insert("sessions", {"token": token, "user_id": u["id"], "expiry": now() + 7 * 86400})
+        return token, self.user_api(u)
+
+    def user_for_token(self, token: Optional[str]) -> Optional[Dict[str, Any]]:
+        if not token:
+            return None
+        s = self.db.one("SELECT * FROM sessions WHERE token=?", [token])
+        if s is None or s["expiry"] < now():
+            return None
+        return self.db.one("SELECT * FROM users WHERE id=?", [s["user_id"]])
+
+    @staticmethod
+    def user_api(u: Dict[str, Any]) -> Dict[str, Any]:
+        return {"id": u["id"], "username": u["username"], "display_name": u.get("display_name"),
+                "admin": bool(u["admin"]), "active": bool(u["active"]),
+                "agent_user_group": {"agent_uid": u.get("agent_uid"), "agent_user": u.get("agent_user")}}
+
+    # ------------------------------------------------------------------ experiments
+    def create_experiment(self, config_text: Any, model_def: Optional[bytes] = None,
+                          parent_id: Optional[int] = None, activate: bool = True,
+                          project_id: Optional[int] = None, owner_id: int = 1,
+                          template: Optional[str] = None, unmanaged: bool = False) -> Experiment:
+        raw = expconf.parse(config_text)
+        if template:
+            t = self.db.one("SELECT config FROM templates WHERE name=?", [template])
+            if t is None:
+                raise KeyError(f"template {template} not found")
+            from determined_clone_amd.util import merge_dicts
+
+            raw = merge_dicts(dec(t["config"], {}), raw)
+        if raw.get("checkpoint_storage") is None:
+            raw["checkpoint_storage"] = dict(self.checkpoint_storage)
+        cfg = expconf.complete(raw)
+        seed = cfg["reproducibility"].get("experiment_seed")
+        if seed is None:
+            seed = int(time.time() * 1000) % (2 ** 31)
+            cfg["reproducibility"]["experiment_seed"] = seed
+        if project_id is None:
+            project_id = 1
+            if cfg.get("workspace") and cfg.get("project"):
+                ws = self.db.one("SELECT id FROM workspaces WHERE name=?", [cfg["workspace"]])
+                if ws:
+                    p = self.db.one("SELECT id FROM projects WHERE workspace_id=? AND name=?", [ws["id"], cfg["project"]])
+                    if p:
+                        project_id = p["id"]
+        job_id = str(uuid.uuid4())
+        eid = self.db.insert("experiments", {
+            "config": cfg, "original_config": json.dumps(raw), "model_definition": model_def,
+            "state": ACTIVE if activate else PAUSED, "start_time": now(), "parent_id": parent_id,
+            "owner_id": owner_id, "project_id": project_id, "job_id": job_id,
+            "unmanaged": int(unmanaged)})
+        exp = Experiment(self, eid, cfg, seed, job_id)
+        if not activate:
+            exp.state = PAUSED
+        with self.lock:
+            self.experiments[eid] = exp
+        self.tasks[job_id] = {"type": "EXPERIMENT", "experiment_id": eid}
+        if not unmanaged:
+            exp.start()
+        return exp
+
+    def get_experiment(self, eid: int) -> Experiment:
+        e = self.experiments.get(int(eid))
+        if e is None:
+            raise KeyError(f"experiment {eid} not found")
+        return e
+
+    def experiment_api(self, eid: int) -> Dict[str, Any]:
+        row = self.db.one("SELECT * FROM experiments WHERE id=?", [eid])
+        if row is None:
+            raise KeyError(f"experiment {eid} not found")
+        d = experiment_row_to_api(row, self.experiments.get(int(eid)))
+        d["num_trials"] = self.db.one("SELECT COUNT(*) AS n FROM trials WHERE experiment_id=?", [eid])["n"]
+        return d
+
+    def trial_by_id(self, trial_id: int) -> Trial:
+        row = self.db.one("SELECT experiment_id, request_id FROM trials WHERE id=?", [trial_id])
+        if row is None:
+            raise KeyError(f"trial {trial_id} not found")
+        exp = self.get_experiment(row["experiment_id"])
+        return exp.trials[row["request_id"]]
+
+    def trial_api(self, trial_id: int) -> Dict[str, Any]:
+        row = self.db.one("SELECT * FROM trials WHERE id=?", [trial_id])
+        if row is None:
+            raise KeyError(f"trial {trial_id} not found")
+        t = None
+        e = self.experiments.get(row["experiment_id"])
+        if e is not None:
+            t = e.trials.get(row["request_id"])
+        return trial_row_to_api(row, t)
+
+    def _restore(self) -> None:
+        for row in self.db.all("SELECT * FROM experiments"):
+            cfg = dec(row["config"], {})
+            exp = Experiment(self, row["id"], cfg, cfg["reproducibility"]["experiment_seed"], row["job_id"])
+            exp.state = row["state"]
+            self.experiments[row["id"]] = exp
+            self.tasks[row["job_id"]] = {"type": "EXPERIMENT", "experiment_id": row["id"]}
+            snap = row.get("searcher_snapshot")
+            if snap and row["state"] not in TERMINAL:
+                try:
+                    exp.restore(json.loads(snap))
+                except Exception:
+                    logger.exception(f"could not restore experiment {row['id']}")
+            elif snap:
+                s = json.loads(snap)
+                exp.best_metric = s.get("best_metric")
+
+    # ------------------------------------------------------------------ allocations
+    def register_allocation(self, alloc_id: str, exp: Experiment, trial: Trial) -> None:
+        with self.lock:
+            self.allocations[alloc_id] = Allocation(alloc_id, trial.task_id, "TRIAL", exp, trial)
+
+    def _on_alloc_start(self, req: AllocationRequest) -> None:
+        a = self.allocations.get(req.alloc_id)
+        if a is None:
+            self.rm.release(req.alloc_id)
+            return
+        a.placements = req.placements
+        a.state = "ASSIGNED"
+        self.db.update("allocations", "allocation_id", a.id,
+                       {"state": "ASSIGNED", "agent_ids": [p["agent_id"] for p in req.placements]})
+        if a.kind == "TRIAL":
+            a.trial.allocation_state = "ASSIGNED"
+            spec = self._trial_spec(a)
+        else:
+            spec = dict(a.spec)
+        spec["allocation_id"] = a.id
+        spec["task_id"] = a.task_id
+        n_containers = len(req.placements)
+        a.containers_running = n_containers
+        for rank, p in enumerate(req.placements):
+            agent = self.rm.agents.get(p["agent_id"])
+            if agent is None:
+                continue
+            s = dict(spec)
+            s["slots"] = p["slots"]
+            s["container_rank"] = rank
+            s["num_containers"] = n_containers
+            agent.push({"type": "start", "spec": s})
+
+    def _on_alloc_preempt(self, req: AllocationRequest) -> None:
+        self.preempt_allocation(req.alloc_id)
+
+    def preempt_allocation(self, alloc_id: str) -> None:
+        a = self.allocations.get(alloc_id)
+        if a is None:
+            return
+        if a.state in ("PENDING",):
+            # never started: just drop it
+            self.rm.release(alloc_id)
+            self._allocation_done(a, 0, "preempted before start")
+            return
+        a.preempt.set()
+
+    def kill_allocation(self, alloc_id: str) -> None:
+        a = self.allocations.get(alloc_id)
+        if a is None:
+            return
+        if a.state == "PENDING":
+            self.rm.release(alloc_id)
+            self._allocation_done(a, 137, "killed")
+            return
+        for p in a.placements:
+            agent = self.rm.agents.get(p["agent_id"])
+            if agent:
+                agent.push({"type": "kill", "allocation_id": alloc_id})
+
+    def container_event(self, agent_id: str, alloc_id: str, state: str,
+                        exit_code: Optional[int] = None) -> None:
+        a = self.allocations.get(alloc_id)
+        if a is None:
+            return
+        if state == "RUNNING":
+            a.state = "RUNNING"
+            if a.trial is not None:
+                a.trial.allocation_state = "RUNNING"
+            self.db.update("allocations", "allocation_id", alloc_id, {"state": "RUNNING"})
+        elif state == "TERMINATED":
+            with self.lock:
+                a.containers_running -= 1
+                if exit_code not in (0, None):
+                    a.exit_code = exit_code
+                elif a.exit_code is None:
+                    a.exit_code = 0
+                if a.containers_running > 0:
+                    if exit_code not in (0, None):
+                        # failure detection: one container died -> kill the rest
+                        self.kill_allocation(alloc_id)
+                    return
+            self.rm.release(alloc_id)
+            self._allocation_done(a, a.exit_code or 0, "")
+
+    def _allocation_done(self, a: Allocation, exit_code: int, reason: str) -> None:
+        if a.exited:
+            return
+        a.exited = True
+        a.exit_code = exit_code
+        self.db.update("allocations", "allocation_id", a.id,
+                       {"state": "TERMINATED", "end_time": now(), "exit_reason": reason or str(exit_code)})
+        with self.log_cv:
+            self.log_cv.notify_all()
+        if a.kind == "TRIAL":
+            a.exp.allocation_exited(a.trial, exit_code, reason)
+        else:
+            t = self.tasks.get(a.task_id)
+            if t is not None:
+                t["state"] = "TERMINATED"
+                t["exit_code"] = exit_code
+            self.db.update("tasks", "task_id", a.task_id, {"state": "TERMINATED", "end_time": now()})
+
+    def _trial_spec(self, a: Allocation) -> Dict[str, Any]:
+        exp, t = a.exp, a.trial
+        cfg = exp.config
+        steps = t.steps_completed
+        info = {
+            "master_url": self.master_url, "cluster_id": self.cluster_id, "agent_id": "",
+            "slot_ids": [], "task_id": t.task_id, "allocation_id": a.id,
+            "session_token": self._task_token(), "task_type": "TRIAL",
+            "latest_checkpoint": t.latest_checkpoint,
+            "trial": {"trial_id": t.id, "experiment_id": exp.id, "trial_seed": t.seed,
+                      "hparams": t.hparams, "config": cfg, "steps_completed": steps,
+                      "trial_run_id": t.run_id, "debug": bool(cfg.get("debug"))},
+        }
+        ep = cfg.get("entrypoint")
+        return {"kind": "TRIAL", "cluster_info": info, "entrypoint": ep,
+                "environment": cfg.get("environment", {}), "experiment_id": exp.id,
+                "slots_per_trial": exp.slots_per_trial}
+
+    def _task_token(self) -> str:
+        u = self.db.one("SELECT id FROM users WHERE username='determined'") or {"id": 1}
+        token = secrets.token_hex(24)
+        self.db.insert("sessions", {"token": token, "user_id": u["id"], "expiry": now() + 30 * 86400})
+        return token
+
+    # ------------------------------------------------------------------ NTSC tasks (commands)
+    def launch_command(self, kind: str, entrypoint: List[str], slots: int = 0,
+                       priority: int = 42, pool: str = "default", env: Optional[Dict[str, str]] = None,
+                       owner_id: int = 1, context: Optional[bytes] = None,
+                       name: Optional[str] = None) -> Dict[str, Any]:
+        task_id = str(uuid.uuid4())
+        alloc_id = f"{task_id}.0"
+        spec = {"kind": kind, "entrypoint": entrypoint, "environment": {"environment_variables": env or {}},
+                "cluster_info": {"master_url": self.master_url, "cluster_id": self.cluster_id,
+                                 "agent_id": "", "slot_ids": [], "task_id": task_id,
+                                 "allocation_id": alloc_id, "session_token": self._task_token(),
+                                 "task_type": kind}}
+        self.db.upsert("tasks", {"task_id": task_id, "task_type": kind, "job_id": task_id,
+                                 "start_time": now(), "state": "QUEUED", "owner_id": owner_id,
+                                 "config": {"entrypoint": entrypoint, "slots": slots, "name": name}})
+        if context is not None:
+            self.db.kv_set(f"context:{task_id}", context.hex())
+        self.tasks[task_id] = {"type": kind, "task_id": task_id, "state": "QUEUED",
+                               "entrypoint": entrypoint, "slots": slots, "name": name or kind.lower()}
+        with self.lock:
+            self.allocations[alloc_id] = Allocation(alloc_id, task_id, kind, spec=spec)
+        self.rm.allocate(AllocationRequest(alloc_id, task_id, task_id, slots, priority, 1.0, pool,
+                                           preemptible=False, name=name or kind.lower()))
+        return {"id": task_id, "allocation_id": alloc_id, "state": "QUEUED", "type": kind}
+
+    # ------------------------------------------------------------------ agents
+    def register_agent(self, body: Dict[str, Any]) -> None:
+        a = AgentState(body["agent_id"], body.get("slots", []), body.get("resource_pool") or "default",
+                       body.get("label") or "", body.get("addresses"))
+        self.rm.register_agent(a)
+
+    # ------------------------------------------------------------------ checkpoints
+    def report_checkpoint(self, body: Dict[str, Any]) -> None:
+        md = body.get("metadata") or {}
+        task_id = body.get("task_id") or ""
+        trial_id = exp_id = None
+        steps = md.get("steps_completed")
+        for e in self.experiments.values():
+            for t in e.trials.values():
+                if t.task_id == task_id:
+                    trial_id, exp_id = t.id, e.id
+                    if steps is not None and steps >= t.steps_completed:
+                        t.latest_checkpoint = body["uuid"]
+                        t.steps_completed = int(steps)
+                        self.db.update("trials", "id", t.id, {"latest_checkpoint": body["uuid"],
+                                                              "steps_completed": int(steps)})
+        size = sum(int(v) for v in (body.get("resources") or {}).values() if isinstance(v, (int, float)))
+        self.db.upsert("checkpoints", {
+            "uuid": body["uuid"], "task_id": task_id, "allocation_id": body.get("allocation_id"),
+            "trial_id": trial_id, "experiment_id": exp_id, "report_time": now(),
+            "state": body.get("state", "COMPLETED"), "resources": body.get("resources") or {},
+            "metadata": md, "steps_completed": steps, "size": size})
+
+    def checkpoint_api(self, row: Dict[str, Any]) -> Dict[str, Any]:
+        md = dec(row.get("metadata"), {})
+        val = None
+        if row.get("trial_id") is not None and row.get("steps_completed") is not None:
+            m = self.db.one("SELECT metrics FROM metrics WHERE trial_id=? AND grp='validation' AND "
+                            "steps_completed=? ORDER BY id DESC LIMIT 1", [row["trial_id"], row["steps_completed"]])
+            if m:
+                val = dec(m["metrics"], {})
+        return {"uuid": row["uuid"], "task_id": row.get("task_id"),
+                "allocation_id": row.get("allocation_id"), "report_time": row.get("report_time"),
+                "state": row.get("state"), "resources": dec(row.get("resources"), {}),
+                "metadata": md, "training": {"trial_id": row.get("trial_id"),
+                                             "experiment_id": row.get("experiment_id"),
+                                             "validation_metrics": {"avg_metrics": val} if val else {},
+                                             "steps_completed": row.get("steps_completed")},
+                "size": row.get("size", 0)}
+
+    def _storage_for(self, exp: Experiment):
+        from determined_clone_amd.common import storage
+
+        try:
+            return storage.build(exp.config["checkpoint_storage"])
+        except Exception:
+            return None
+
+    def delete_checkpoints(self, uuids: List[str], exp: Optional[Experiment] = None) -> None:
+        for u in uuids:
+            row = self.db.one("SELECT * FROM checkpoints WHERE uuid=?", [u])
+            if row is None:
+                continue
+            e = exp or (self.experiments.get(row["experiment_id"]) if row.get("experiment_id") else None)
+            sm = self._storage_for(e) if e else None
+            if sm is not None:
+                try:
+                    sm.delete(u)
+                except Exception:
+                    logger.exception(f"failed deleting checkpoint {u}")
+            self.db.update("checkpoints", "uuid", u, {"state": "DELETED"})
+
+    def _gc_candidates(self, exp: Experiment, trial: Optional[Trial]) -> List[str]:
+        cs = exp.config.get("checkpoint_storage") or {}
+        keep_exp_best = int(cs.get("save_experiment_best", 0))
+        keep_trial_best = int(cs.get("save_trial_best", 1))
+        keep_trial_latest = int(cs.get("save_trial_latest", 1))
+        metric = exp.config["searcher"].get("metric")
+        sib = exp.smaller_is_better
+        rows = self.db.all("SELECT * FROM checkpoints WHERE experiment_id=? AND state='COMPLETED'", [exp.id])
+        if trial is not None:
+            rows = [r for r in rows if r["trial_id"] == trial.id]
+
+        def score(r: Dict[str, Any]) -> Optional[float]:
+            m = self.db.one("SELECT metrics FROM metrics WHERE trial_id=? AND grp='validation' AND "
+                            "steps_completed=? ORDER BY id DESC LIMIT 1", [r["trial_id"], r["steps_completed"]])
+            if not m or not metric:
+                return None
+            v = (dec(m["metrics"], {}) or {}).get(metric)
+            return float(v) if isinstance(v, (int, float)) else None
+
+        keep = set()
+        by_trial: Dict[int, List[Dict[str, Any]]] = {}
+        for r in rows:
+            by_trial.setdefault(r["trial_id"], []).append(r)
+        scored = [(score(r), r) for r in rows]
+        ranked = sorted([x for x in scored if x[0] is not None], key=lambda x: x[0] if sib else -x[0])
+        for _, r in ranked[:keep_exp_best]:
+            keep.add(r["uuid"])
+        for tid, rs in by_trial.items():
+            rs_sorted = sorted(rs, key=lambda r: (r["steps_completed"] or 0, r["report_time"] or 0))
+            for r in rs_sorted[-keep_trial_latest:] if keep_trial_latest else []:
+                keep.add(r["uuid"])
+            tr = sorted([(s, r) for s, r in scored if r["trial_id"] == tid and s is not None],
+                        key=lambda x: x[0] if sib else -x[0])
+            for _, r in tr[:keep_trial_best]:
+                keep.add(r["uuid"])
+        return [r["uuid"] for r in rows if r["uuid"] not in keep]
+
+    def checkpoint_gc_trial(self, exp: Experiment, t: Trial) -> None:
+        pass  # GC runs once per experiment (experiment-best needs every trial's metrics)
+
+    def checkpoint_gc_experiment(self, exp: Experiment) -> None:
+        try:
+            self.delete_checkpoints(self._gc_candidates(exp, None), exp)
+        except Exception:
+            logger.exception("checkpoint GC failed")
+
+    # ------------------------------------------------------------------ metrics
+    def report_metrics(self, trial_id: int, body: Dict[str, Any]) -> None:
+        m = body.get("metrics") or {}
+        grp = body.get("group", "training")
+        steps = int(m.get("steps_completed", 0))
+        avg = m.get("avg_metrics") or {}
+        self.db.insert("metrics", {"trial_id": trial_id, "trial_run_id": m.get("trial_run_id", 0),
+                                   "grp": grp, "steps_completed": steps, "metrics": avg,
+                                   "batch_metrics": m.get("batch_metrics"), "end_time": now()})
+        row = self.db.one("SELECT summary_metrics, experiment_id FROM trials WHERE id=?", [trial_id]) or {}
+        summary = dec(row.get("summary_metrics"), {}) or {}
+        sec = summary.setdefault(f"{grp}_metrics" if grp in ("training", "validation") else grp, {})
+        for k, v in avg.items():
+            if isinstance(v, (int, float)) and not isinstance(v, bool):
+                s = sec.setdefault(k, {"count": 0, "sum": 0.0, "min": v, "max": v, "last": v, "type": "number"})
+                s["count"] += 1
+                s["sum"] += v
+                s["min"] = min(s["min"], v)
+                s["max"] = max(s["max"], v)
+                s["last"] = v
+        fields: Dict[str, Any] = {"summary_metrics": summary}
+        if grp == "validation":
+            fields["latest_validation_steps"] = steps
+            exp = self.experiments.get(row.get("experiment_id"))
+            if exp is not None:
+                metric = exp.config["searcher"].get("metric")
+                v = avg.get(metric)
+                if isinstance(v, (int, float)):
+                    cur = self.db.one("SELECT best_validation FROM trials WHERE id=?", [trial_id])["best_validation"]
+                    if cur is None or (v < cur if exp.smaller_is_better else v > cur):
+                        fields["best_validation"] = float(v)
+        self.db.update("trials", "id", trial_id, fields)
+
+    # ------------------------------------------------------------------ logs
+    def post_logs(self, logs: List[Dict[str, Any]]) -> None:
+        for lg in logs:
+            self.db.insert("task_logs", {"task_id": lg.get("task_id"), "allocation_id": lg.get("allocation_id"),
+                                         "agent_id": lg.get("agent_id"), "container_id": lg.get("container_id"),
+                                         "rank_id": lg.get("rank_id"), "timestamp": lg.get("timestamp") or now(),
+                                         "level": lg.get("level", "INFO"), "log": lg.get("log", ""),
+                                         "source": lg.get("source", "task"), "stdtype": lg.get("stdtype", "stdout")})
+        self._apply_log_policies(logs)
+        with self.log_cv:
+            self.log_cv.notify_all()
+
+    def _apply_log_policies(self, logs: List[Dict[str, Any]]) -> None:
+        """expconf ``log_policies``: regex on trial logs -> exclude_node / cancel_retries
+        (reference: master/internal/logpattern)."""
+        import re
+
+        for lg in logs:
+            a = self.allocations.get(lg.get("allocation_id") or "")
+            if a is None or a.exp is None:
+                continue
+            for pol in a.exp.config.get("log_policies") or []:
+                pat = pol.get("pattern")
+                if not pat or not re.search(pat, lg.get("log", "")):
+                    continue
+                action = pol.get("action") or {}
+                atype = action.get("type") if isinstance(action, dict) else action
+                if atype == "cancel_retries" and a.trial is not None:
+                    a.trial.restarts = 10 ** 6
+                elif atype == "exclude_node" and lg.get("agent_id"):
+                    req = self.rm.pending.get(a.id) or self.rm.running.get(a.id)
+                    if req is not None and lg["agent_id"] not in req.blocked_agents:
+                        req.blocked_agents.append(lg["agent_id"])
+
+    def task_logs(self, task_id: str, after_id: int = 0, limit: int = 10000) -> List[Dict[str, Any]]:
+        return self.db.all("SELECT * FROM task_logs WHERE task_id=? AND id>? ORDER BY id LIMIT ?",
+                           [task_id, after_id, limit])

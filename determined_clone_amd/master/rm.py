@@ -1,0 +1,267 @@
+"""Agent resource manager (reference: `master/internal/rm/agentrm`).
+
+Keeps the live view of agents/slots and allocation requests, and asks the native C++ scheduler
+(`native/scheduler.cpp`) for decisions on every change. Decisions are applied here (slots marked
+busy) and handed to the master via callbacks: ``on_start(alloc, placements)`` and
+``on_preempt(alloc)``.
+"""
+import logging
+import threading
+import time
+from typing import Any, Callable, Dict, List, Optional
+
+from determined_clone_amd.native import load as load_native
+
+logger = logging.getLogger("determined_clone_amd.master.rm")
+
+
+class AgentState:
+    def __init__(self, agent_id: str, slots: List[Dict[str, Any]], pool: str = "default",
+                 label: str = "", addresses: Optional[List[str]] = None) -> None:
+        self.id = agent_id
+        self.slots = slots  # [{"id": int, "uuid": str, "type": "rocm"|"cpu", "brand": str}]
+        self.pool = pool
+        self.label = label
+        self.addresses = addresses or ["127.0.0.1"]
+        self.enabled = True
+        self.draining = False
+        self.slot_enabled = [True] * len(slots)
+        self.slot_owner = [""] * len(slots)
+        self.zero_slot_used = 0
+        self.last_seen = time.time()
+        self.registered = time.time()
+        self.actions: List[Dict[str, Any]] = []
+        self.cv = threading.Condition()
+
+    def push(self, action: Dict[str, Any]) -> None:
+        with self.cv:
+            self.actions.append(action)
+            self.cv.notify_all()
+
+    def pop_all(self, timeout: float) -> List[Dict[str, Any]]:
+        with self.cv:
+            if not self.actions:
+                self.cv.wait(timeout)
+            out, self.actions = self.actions, []
+            return out
+
+    def to_dict(self) -> Dict[str, Any]:
+        return {
+            "id": self.id, "resource_pool": self.pool, "label": self.label,
+            "enabled": self.enabled, "draining": self.draining, "addresses": self.addresses,
+            "registered_time": self.registered, "last_seen": self.last_seen,
+            "slots": {str(i): {"id": str(s["id"]), "device": s, "enabled": self.slot_enabled[i],
+                               "container": ({"id": self.slot_owner[i]} if self.slot_owner[i] else None)}
+                      for i, s in enumerate(self.slots)},
+        }
+
+
+class AllocationRequest:
+    def __init__(self, alloc_id: str, task_id: str, job_id: str, slots: int, priority: int = 42,
+                 weight: float = 1.0, pool: str = "default", preemptible: bool = True,
+                 label: str = "", name: str = "") -> None:
+        self.alloc_id = alloc_id
+        self.task_id = task_id
+        self.job_id = job_id
+        self.slots = slots
+        self.priority = priority
+        self.weight = weight
+        self.pool = pool
+        self.preemptible = preemptible
+        self.label = label
+        self.name = name
+        self.submit_time = time.time()
+        self.job_position = 0
+        self.blocked_agents: List[str] = []
+        self.placements: List[Dict[str, Any]] = []
+        self.start_time: Optional[float] = None
+        self.preempt_requested = False
+
+
+class ResourceManager:
+    def __init__(self, scheduler: str = "priority", fit: str = "best", preemption: bool = True,
+                 on_start: Optional[Callable[[AllocationRequest], None]] = None,
+                 on_preempt: Optional[Callable[[AllocationRequest], None]] = None) -> None:
+        self._N = load_native()
+        self.policy = scheduler
+        self.fit = fit
+        self.preemption = preemption
+        self._sched = self._N.Scheduler(scheduler, fit, preemption)
+        self.agents: Dict[str, AgentState] = {}
+        self.pending: Dict[str, AllocationRequest] = {}
+        self.running: Dict[str, AllocationRequest] = {}
+        self.on_start = on_start
+        self.on_preempt = on_preempt
+        self._lock = threading.RLock()
+
+    # ------------------------------------------------------------------ agents
+    def register_agent(self, agent: AgentState) -> None:
+        with self._lock:
+            old = self.agents.get(agent.id)
+            if old is not None:
+                agent.slot_owner = old.slot_owner if len(old.slot_owner) == len(agent.slots) else agent.slot_owner
+                agent.enabled = old.enabled
+            self.agents[agent.id] = agent
+        self.schedule()
+
+    def remove_agent(self, agent_id: str) -> List[AllocationRequest]:
+        with self._lock:
+            self.agents.pop(agent_id, None)
+            lost = [r for r in self.running.values() if any(p["agent_id"] == agent_id for p in r.placements)]
+            for r in lost:
+                self.running.pop(r.alloc_id, None)
+            return lost
+
+    def set_agent_enabled(self, agent_id: str, enabled: bool, drain: bool = False) -> None:
+        with self._lock:
+            a = self.agents[agent_id]
+            a.enabled = enabled
+            a.draining = drain and not enabled
+            if not enabled and not drain:
+                for r in list(self.running.values()):
+                    if any(p["agent_id"] == agent_id for p in r.placements) and self.on_preempt:
+                        r.preempt_requested = True
+                        self.on_preempt(r)
+        self.schedule()
+
+    def set_slot_enabled(self, agent_id: str, slot: int, enabled: bool) -> None:
+        with self._lock:
+            self.agents[agent_id].slot_enabled[slot] = enabled
+        self.schedule()
+
+    # ------------------------------------------------------------------ requests
+    def allocate(self, req: AllocationRequest) -> None:
+        with self._lock:
+            self.pending[req.alloc_id] = req
+        self.schedule()
+
+    def release(self, alloc_id: str) -> None:
+        with self._lock:
+            self.pending.pop(alloc_id, None)
+            r = self.running.pop(alloc_id, None)
+            if r is not None:
+                for p in r.placements:
+                    a = self.agents.get(p["agent_id"])
+                    if a is None:
+                        continue
+                    if not p["slots"]:
+                        a.zero_slot_used = max(0, a.zero_slot_used - 1)
+                    for s in p["slots"]:
+                        if s < len(a.slot_owner) and a.slot_owner[s] == alloc_id:
+                            a.slot_owner[s] = ""
+        self.schedule()
+
+    def set_job_priority(self, job_id: str, priority: Optional[int] = None,
+                         weight: Optional[float] = None, position: Optional[int] = None) -> None:
+        with self._lock:
+            for r in list(self.pending.values()) + list(self.running.values()):
+                if r.job_id == job_id:
+                    if priority is not None:
+                        r.priority = priority
+                    if weight is not None:
+                        r.weight = weight
+                    if position is not None:
+                        r.job_position = position
+        self.schedule()
+
+    # ------------------------------------------------------------------ scheduling
+    def _snapshot(self):
+        N = self._N
+        agents = []
+        for a in self.agents.values():
+            na = N.Agent()
+            na.id = a.id
+            na.num_slots = len(a.slots)
+            na.slot_owner = list(a.slot_owner)
+            na.slot_enabled = list(a.slot_enabled)
+            na.enabled = a.enabled and not a.draining
+            na.pool = a.pool
+            na.label = a.label
+            na.zero_slot_used = a.zero_slot_used
+            agents.append(na)
+        pend = []
+        for r in self.pending.values():
+            nr = N.Request()
+            nr.alloc_id, nr.job_id, nr.slots = r.alloc_id, r.job_id, r.slots
+            nr.priority, nr.weight, nr.submit_time = r.priority, r.weight, r.submit_time
+            nr.job_position, nr.preemptible, nr.pool = r.job_position, r.preemptible, r.pool
+            nr.label, nr.blocked_agents = r.label, list(r.blocked_agents)
+            pend.append(nr)
+        run = []
+        for r in self.running.values():
+            nr = N.Running()
+            nr.alloc_id, nr.job_id, nr.slots = r.alloc_id, r.job_id, r.slots
+            nr.priority, nr.weight = r.priority, r.weight
+            nr.start_time = r.start_time or 0.0
+            nr.preemptible = r.preemptible and not r.preempt_requested
+            run.append(nr)
+        return agents, pend, run
+
+    def schedule(self) -> None:
+        starts: List[AllocationRequest] = []
+        preempts: List[AllocationRequest] = []
+        with self._lock:
+            if not self.pending:
+                return
+            # each resource pool is scheduled independently
+            pools = {a.pool for a in self.agents.values()} | {r.pool for r in self.pending.values()}
+            agents, pend, run = self._snapshot()
+            for pool in pools:
+                pa = [a for a in agents if a.pool == pool]
+                pp = [r for r in pend if r.pool == pool]
+                if not pp:
+                    continue
+                pr = [r for r in run if self.running[r.alloc_id].pool == pool]
+                d = self._sched.schedule(pa, pp, pr)
+                for alloc_id, placements in d.start:
+                    req = self.pending.pop(alloc_id)
+                    req.placements = [{"agent_id": p.agent_id, "slots": list(p.slots)} for p in placements]
+                    req.start_time = time.time()
+                    for p in req.placements:
+                        a = self.agents[p["agent_id"]]
+                        if not p["slots"]:
+                            a.zero_slot_used += 1
+                        for s in p["slots"]:
+                            a.slot_owner[s] = alloc_id
+                    self.running[alloc_id] = req
+                    starts.append(req)
+                for alloc_id in d.preempt:
+                    r = self.running.get(alloc_id)
+                    if r is not None and not r.preempt_requested:
+                        r.preempt_requested = True
+                        preempts.append(r)
+        for r in starts:
+            if self.on_start:
+                self.on_start(r)
+        for r in preempts:
+            if self.on_preempt:
+                self.on_preempt(r)
+
+    # ------------------------------------------------------------------ views
+    def pools(self) -> List[Dict[str, Any]]:
+        with self._lock:
+            out = {}
+            for a in self.agents.values():
+                p = out.setdefault(a.pool, {"name": a.pool, "num_agents": 0, "slots_available": 0,
+                                            "slots_used": 0, "scheduler_type": self.policy,
+                                            "scheduler_fitting_policy": self.fit,
+                                            "slot_type": "rocm" if any(s.get("type") == "rocm" for s in a.slots) else "cpu"})
+                p["num_agents"] += 1
+                p["slots_available"] += sum(1 for e in a.slot_enabled if e)
+                p["slots_used"] += sum(1 for o in a.slot_owner if o)
+            return list(out.values()) or [{"name": "default", "num_agents": 0, "slots_available": 0,
+                                           "slots_used": 0, "scheduler_type": self.policy,
+                                           "scheduler_fitting_policy": self.fit, "slot_type": "cpu"}]
+
+    def queue(self) -> List[Dict[str, Any]]:
+        with self._lock:
+            rows = []
+            for state, d in (("SCHEDULED", self.running), ("QUEUED", self.pending)):
+                for r in d.values():
+                    rows.append({"allocation_id": r.alloc_id, "task_id": r.task_id, "job_id": r.job_id,
+                                 "name": r.name, "state": state, "slots": r.slots,
+                                 "priority": r.priority, "weight": r.weight,
+                                 "resource_pool": r.pool, "submission_time": r.submit_time,
+                                 "position": r.job_position})
+            rows.sort(key=lambda x: (x["state"] != "SCHEDULED", x["priority"], x["position"], x["submission_time"]))
+            return rows

@@ -1,0 +1,145 @@
+"""End-to-end: in-process master + agent (CPU artificial slots) running real trial processes.
+
+Mirrors the reference's e2e_tests (experiment create -> trials -> metrics/checkpoints ->
+completion; ASHA search with concurrent trials; pause/activate; kill)."""
+import base64
+import os
+import shutil
+import tempfile
+import time
+
+import pytest
+
+from determined_clone_amd.agent import Agent
+from determined_clone_amd.common.api import Session
+from determined_clone_amd.master import Master, MasterServer
+from determined_clone_amd.util import tar_directory
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+MODEL_DEF = '''
+import torch
+from determined_clone_amd import pytorch
+
+class Ones(torch.utils.data.Dataset):
+    def __len__(self):
+        return 64
+    def __getitem__(self, i):
+        return torch.tensor([1.0]), torch.tensor([1.0])
+
+class OneVar(pytorch.PyTorchTrial):
+    def __init__(self, context):
+        self.context = context
+        m = torch.nn.Linear(1, 1, bias=False)
+        m.weight.data.fill_(0.0)
+        self.model = context.wrap_model(m)
+        lr = context.get_hparam("lr")
+        self.opt = context.wrap_optimizer(torch.optim.SGD(self.model.parameters(), lr=lr))
+    def train_batch(self, batch, epoch_idx, batch_idx):
+        x, y = batch
+        loss = torch.nn.functional.mse_loss(self.model(x), y)
+        self.context.backward(loss)
+        self.context.step_optimizer(self.opt)
+        return {"loss": loss}
+    def evaluate_batch(self, batch, batch_idx):
+        x, y = batch
+        return {"val_loss": torch.nn.functional.mse_loss(self.model(x), y)}
+    def build_training_data_loader(self):
+        return pytorch.DataLoader(Ones(), batch_size=self.context.get_per_slot_batch_size())
+    def build_validation_data_loader(self):
+        return pytorch.DataLoader(Ones(), batch_size=16)
+'''
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    tmp = tempfile.mkdtemp(prefix="det-e2e-")
+    m = Master(os.path.join(tmp, "m.db"), checkpoint_storage={"type": "shared_fs", "host_path": os.path.join(tmp, "ckpt")})
+    srv = MasterServer(m, "127.0.0.1", 0).start()
+    agent = Agent(m.master_url, "agent-0", artificial_slots=4).start_background()
+    s = Session(m.master_url)
+    s.token = s.post("/api/v1/auth/login", {"username": "admin", "password": ""})["token"]
+    ctx = os.path.join(tmp, "ctx")
+    os.makedirs(ctx)
+    with open(os.path.join(ctx, "model_def.py"), "w") as f:
+        f.write(MODEL_DEF)
+    yield m, s, ctx, tmp
+    agent.stop()
+    srv.stop()
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _create(s, ctx, cfg):
+    body = {"config": cfg, "model_definition": base64.b64encode(tar_directory(ctx)).decode()}
+    return s.post("/api/v1/experiments", body)["experiment"]["id"]
+
+
+def _wait(s, eid, states=("COMPLETED", "CANCELED", "ERROR"), timeout=240):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        st = s.get(f"/api/v1/experiments/{eid}")["experiment"]["state"]
+        if st in states:
+            return st
+        time.sleep(0.5)
+    raise TimeoutError(f"experiment {eid} still {st}")
+
+
+BASE = """
+name: e2e
+entrypoint: model_def:OneVar
+hyperparameters:
+  global_batch_size: 4
+  lr: 0.01
+max_restarts: 0
+min_validation_period: {batches: 4}
+scheduling_unit: 4
+"""
+
+
+def test_single_experiment_completes_with_metrics_and_checkpoint(cluster):
+    m, s, ctx, _ = cluster
+    eid = _create(s, ctx, BASE + "searcher: {name: single, metric: val_loss, max_length: {batches: 8}}\n")
+    assert _wait(s, eid) == "COMPLETED"
+    trials = s.get(f"/api/v1/experiments/{eid}/trials")["trials"]
+    assert len(trials) == 1 and trials[0]["state"] == "COMPLETED"
+    tid = trials[0]["id"]
+    val = s.get(f"/api/v1/trials/{tid}/metrics", params={"group": "validation"})["metrics"]
+    assert [v["steps_completed"] for v in val] == [4, 8]
+    ck = s.get(f"/api/v1/experiments/{eid}/checkpoints")["checkpoints"]
+    assert ck and ck[-1]["metadata"]["steps_completed"] == 8
+    logs = s.get(f"/api/v1/trials/{tid}/logs")["logs"]
+    assert any("validated" in l["log"] for l in logs)
+
+
+def test_asha_search_runs_concurrent_trials(cluster):
+    m, s, ctx, _ = cluster
+    cfg = BASE.replace("lr: 0.01", "lr: {type: log, minval: -3, maxval: -1}") + \
+        "searcher: {name: adaptive_asha, metric: val_loss, max_length: {batches: 16}, max_trials: 6, " \
+        "max_rungs: 2, divisor: 2, mode: aggressive, max_concurrent_trials: 4}\n"
+    eid = _create(s, ctx, cfg)
+    assert _wait(s, eid, timeout=400) == "COMPLETED"
+    trials = s.get(f"/api/v1/experiments/{eid}/trials")["trials"]
+    assert len(trials) == 6
+    assert all(t["state"] == "COMPLETED" for t in trials)
+    longest = max(t["steps_completed"] or 0 for t in trials)
+    assert longest == 16
+
+
+def test_pause_activate_and_kill(cluster):
+    m, s, ctx, _ = cluster
+    eid = _create(s, ctx, BASE + "searcher: {name: single, metric: val_loss, max_length: {batches: 400}}\n")
+    time.sleep(4)
+    s.post(f"/api/v1/experiments/{eid}/pause")
+    assert _wait(s, eid, states=("PAUSED",)) == "PAUSED"
+    s.post(f"/api/v1/experiments/{eid}/activate")
+    time.sleep(2)
+    s.post(f"/api/v1/experiments/{eid}/kill")
+    assert _wait(s, eid) == "CANCELED"
+
+
+def test_invalid_config_rejected(cluster):
+    m, s, ctx, _ = cluster
+    from determined_clone_amd.errors import APIException
+
+    with pytest.raises(APIException):
+        _create(s, ctx, "entrypoint: x:y\nsearcher: {name: single}\n")
