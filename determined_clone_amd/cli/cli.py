@@ -1,0 +1,688 @@
+"""``det`` command-line interface (reference: `harness/determined/cli/*.py`).
+
+Same command tree as the reference where it applies (experiment/e, trial/t, checkpoint, model,
+template/tpl, agent/a, slot/s, task, command/cmd, shell, notebook, tensorboard, user/u, workspace,
+project, job, resource-pool, master, deploy local, version), talking to the master's REST API.
+"""
+import argparse
+import base64
+import json
+import os
+import pathlib
+import sys
+import time
+from typing import Any, Callable, Dict, List, Optional
+
+import yaml
+
+from determined_clone_amd import __version__
+from determined_clone_amd.common.api import Session
+from determined_clone_amd.errors import APIException
+
+AUTH_FILE = pathlib.Path(os.environ.get("DET_CLONE_AUTH", pathlib.Path.home() / ".det-clone" / "auth.json"))
+
+
+# ---------------------------------------------------------------------------- session helpers
+def _load_tokens() -> Dict[str, Any]:
+    try:
+        return json.loads(AUTH_FILE.read_text())
+    except (OSError, ValueError):
+        return {}
+
+
+def _save_tokens(d: Dict[str, Any]) -> None:
+    AUTH_FILE.parent.mkdir(parents=True, exist_ok=True)
+    AUTH_FILE.write_text(json.dumps(d))
+    os.chmod(AUTH_FILE, 0o600)
+
+
+def session(args: argparse.Namespace, login: bool = True) -> Session:
+    s = Session(args.master)
+    toks = _load_tokens().get(s.master, {})
+    user = args.user or toks.get("active_user") or "admin"
+    tok = (toks.get("tokens") or {}).get(user)
+    if tok:
+        s.token = tok
+        try:
+            s.get("/api/v1/me")
+            return s
+        except APIException:
+            s.token = None
+    if login:
+        pw = os.environ.get("DET_PASS", "")
+        r = s.post("/api/v1/auth/login", {"username": user, "password": pw})
+        s.token = r["token"]
+        d = _load_tokens()
+        d.setdefault(s.master, {}).setdefault("tokens", {})[user] = s.token
+        d[s.master]["active_user"] = user
+        _save_tokens(d)
+    return s
+
+
+def render_table(rows: List[Dict[str, Any]], cols: List[str], as_json: bool = False) -> None:
+    if as_json:
+        print(json.dumps(rows, indent=2, default=str))
+        return
+    if not rows:
+        print("(none)")
+        return
+    widths = {c: max(len(c), *(len(_fmt(r.get(c))) for r in rows)) for c in cols}
+    print("  ".join(c.upper().ljust(widths[c]) for c in cols))
+    print("  ".join("-" * widths[c] for c in cols))
+    for r in rows:
+        print("  ".join(_fmt(r.get(c)).ljust(widths[c]) for c in cols))
+
+
+def _fmt(v: Any) -> str:
+    if v is None:
+        return ""
+    if isinstance(v, float):
+        if v > 1e9:
+            return time.strftime("%Y-%m-%d %H:%M:%S", time.localtime(v))
+        return f"{v:.6g}"
+    if isinstance(v, (dict, list)):
+        return json.dumps(v, default=str)
+    return str(v)
+
+
+# ---------------------------------------------------------------------------- user / master
+def user_login(args):
+    s = Session(args.master)
+    import getpass
+
+    pw = args.password if args.password is not None else (os.environ.get("DET_PASS") or getpass.getpass("Password: "))
+    r = s.post("/api/v1/auth/login", {"username": args.username, "password": pw})
+    d = _load_tokens()
+    d.setdefault(s.master, {}).setdefault("tokens", {})[args.username] = r["token"]
+    d[s.master]["active_user"] = args.username
+    _save_tokens(d)
+    print(f"logged in as {args.username}")
+
+
+def user_logout(args):
+    d = _load_tokens()
+    m = Session(args.master).master
+    d.pop(m, None)
+    _save_tokens(d)
+
+
+def user_whoami(args):
+    print(f"You are logged in as user '{session(args).get('/api/v1/me')['user']['username']}'")
+
+
+def user_list(args):
+    render_table(session(args).get("/api/v1/users")["users"], ["id", "username", "admin", "active"], args.json)
+
+
+def user_create(args):
+    session(args).post("/api/v1/users", {"user": {"username": args.username, "admin": args.admin},
+                                          "password": args.password or ""})
+
+
+def user_set_active(active: bool):
+    def f(args):
+        s = session(args)
+        u = [x for x in s.get("/api/v1/users")["users"] if x["username"] == args.username][0]
+        s.patch(f"/api/v1/users/{u['id']}", {"active": active})
+    return f
+
+
+def user_change_password(args):
+    s = session(args)
+    name = args.target_user or s.get("/api/v1/me")["user"]["username"]
+    u = [x for x in s.get("/api/v1/users")["users"] if x["username"] == name][0]
+    s.post(f"/api/v1/users/{u['id']}/password", {"password": args.password})
+
+
+def master_info(args):
+    print(json.dumps(session(args, login=False).get("/api/v1/master"), indent=2))
+
+
+def master_config(args):
+    print(yaml.safe_dump(session(args).get("/api/v1/master/config")["config"]))
+
+
+def version(args):
+    print(f"client: {__version__}")
+    try:
+        print(f"master: {Session(args.master).get('/api/v1/master')['version']}")
+    except Exception:
+        print("master: unreachable")
+
+
+# ---------------------------------------------------------------------------- experiments
+def _read_config(path: str) -> Dict[str, Any]:
+    with open(path) as f:
+        return yaml.safe_load(f) or {}
+
+
+def experiment_create(args):
+    from determined_clone_amd.util import tar_directory
+
+    cfg = _read_config(args.config_file)
+    for kv in args.config or []:
+        k, _, v = kv.partition("=")
+        d = cfg
+        parts = k.split(".")
+        for p in parts[:-1]:
+            d = d.setdefault(p, {})
+        d[parts[-1]] = yaml.safe_load(v)
+    if args.test:
+        return _local_test(cfg, args.model_def)
+    body: Dict[str, Any] = {"config": cfg, "activate": not args.paused}
+    if args.model_def:
+        body["model_definition"] = base64.b64encode(tar_directory(args.model_def)).decode()
+    if args.template:
+        body["template"] = args.template
+    if args.project_id:
+        body["project_id"] = args.project_id
+    s = session(args)
+    exp = s.post("/api/v1/experiments", body)["experiment"]
+    print(f"Created experiment {exp['id']}")
+    if args.follow_first_trial:
+        _follow_first_trial(s, exp["id"])
+
+
+def _local_test(cfg: Dict[str, Any], context: Optional[str]) -> None:
+    """``--test``: validate the config and run one batch of train + validate locally."""
+    from determined_clone_amd import pytorch
+    from determined_clone_amd.config import expconf
+    from determined_clone_amd.exec.harness import load_trial_class
+
+    full = expconf.complete(cfg)
+    if context:
+        os.environ["DET_CONTEXT_DIR"] = os.path.abspath(context)
+    hp = {k: (v.get("val") if isinstance(v, dict) and v.get("type") == "const" else
+              v.get("minval") if isinstance(v, dict) and "minval" in v else
+              (v.get("vals") or [None])[0] if isinstance(v, dict) and "vals" in v else v)
+          for k, v in full["hyperparameters"].items()}
+    cls = load_trial_class(full["entrypoint"])
+    with pytorch.init(hparams=hp, exp_conf=full) as ctx:
+        pytorch.Trainer(cls(ctx), ctx).fit(max_length=pytorch.Batch(1), test_mode=True,
+                                           checkpoint_policy="none")
+    print("Model definition test succeeded")
+
+
+def _follow_first_trial(s: Session, eid: int) -> None:
+    tid = None
+    while tid is None:
+        ts = s.get(f"/api/v1/experiments/{eid}/trials")["trials"]
+        if ts:
+            tid = ts[0]["id"]
+        else:
+            time.sleep(1)
+    _follow_logs(s, f"/api/v1/trials/{tid}/logs")
+
+
+def _follow_logs(s: Session, path: str, follow: bool = True, tail: Optional[int] = None) -> None:
+    after = 0
+    first = True
+    while True:
+        r = s.get(path, params={"after_id": after, "follow": "true" if follow else "false",
+                                "timeout_seconds": 5})
+        logs = r["logs"]
+        if first and tail is not None:
+            logs = logs[-tail:]
+        first = False
+        for l in logs:
+            print(l["log"])
+            after = max(after, l["id"])
+        if not follow or (r.get("done") and not r["logs"]):
+            return
+
+
+def experiment_list(args):
+    params = {}
+    if not args.all:
+        params["archived"] = "false"
+    exps = session(args).get("/api/v1/experiments", params=params)["experiments"]
+    render_table(exps, ["id", "name", "state", "progress", "start_time", "end_time", "searcher_type",
+                        "resource_pool"], args.json)
+
+
+def experiment_describe(args):
+    s = session(args)
+    e = s.get(f"/api/v1/experiments/{args.experiment_id}")["experiment"]
+    if args.json:
+        trials = s.get(f"/api/v1/experiments/{args.experiment_id}/trials")["trials"]
+        print(json.dumps({"experiment": e, "trials": trials}, indent=2, default=str))
+        return
+    render_table([e], ["id", "name", "state", "progress", "start_time", "end_time", "searcher_type", "labels"])
+    print()
+    trials = s.get(f"/api/v1/experiments/{args.experiment_id}/trials")["trials"]
+    render_table(trials, ["id", "state", "hparams", "steps_completed", "best_validation", "restarts",
+                          "latest_checkpoint"])
+
+
+def experiment_config(args):
+    print(yaml.safe_dump(session(args).get(f"/api/v1/experiments/{args.experiment_id}")["config"]))
+
+
+def experiment_action(action: str):
+    def f(args):
+        session(args).post(f"/api/v1/experiments/{args.experiment_id}/{action}")
+        print(f"{action}: experiment {args.experiment_id}")
+    return f
+
+
+def experiment_delete(args):
+    session(args).delete(f"/api/v1/experiments/{args.experiment_id}")
+
+
+def experiment_set(field: str):
+    def f(args):
+        session(args).patch(f"/api/v1/experiments/{args.experiment_id}", {field: args.value})
+    return f
+
+
+def experiment_label(add: bool):
+    def f(args):
+        s = session(args)
+        labels = s.get(f"/api/v1/experiments/{args.experiment_id}")["experiment"]["labels"] or []
+        labels = sorted(set(labels) | {args.label}) if add else [l for l in labels if l != args.label]
+        s.patch(f"/api/v1/experiments/{args.experiment_id}", {"labels": labels})
+    return f
+
+
+def experiment_list_trials(args):
+    render_table(session(args).get(f"/api/v1/experiments/{args.experiment_id}/trials")["trials"],
+                 ["id", "state", "hparams", "steps_completed", "best_validation"], args.json)
+
+
+def experiment_list_checkpoints(args):
+    cks = session(args).get(f"/api/v1/experiments/{args.experiment_id}/checkpoints",
+                            params={"sort_by": "searcher_metric"} if args.best else {})["checkpoints"]
+    if args.best:
+        cks = cks[:args.best]
+    rows = [{"uuid": c["uuid"], "trial_id": c["training"]["trial_id"],
+             "steps_completed": c["training"]["steps_completed"], "state": c["state"],
+             "validation": ((c["training"].get("validation_metrics") or {}).get("avg_metrics"))} for c in cks]
+    render_table(rows, ["uuid", "trial_id", "steps_completed", "state", "validation"], args.json)
+
+
+def experiment_wait(args):
+    s = session(args)
+    while True:
+        st = s.get(f"/api/v1/experiments/{args.experiment_id}")["experiment"]["state"]
+        if st in ("COMPLETED", "CANCELED", "ERROR"):
+            print(st)
+            sys.exit(0 if st == "COMPLETED" else 1)
+        time.sleep(args.polling_interval)
+
+
+def experiment_download(args):
+    s = session(args)
+    cks = s.get(f"/api/v1/experiments/{args.experiment_id}/checkpoints", params={"sort_by": "searcher_metric"})["checkpoints"]
+    for c in cks[:args.top_n]:
+        _download_checkpoint(s, c["uuid"], os.path.join(args.output_dir, c["uuid"]))
+
+
+def preview_search(args):
+    r = session(args).post("/api/v1/preview-hp-search", {"config": _read_config(args.config_file)})
+    sim = r["simulation"]
+    print(f"Using search method {_read_config(args.config_file)['searcher']['name']}: {sim['trials']} trials")
+    rows = [{"trials": n, "training_lengths": k} for k, n in sim["results"].items()]
+    render_table(rows, ["trials", "training_lengths"])
+
+
+# ---------------------------------------------------------------------------- trials / checkpoints
+def trial_describe(args):
+    s = session(args)
+    t = s.get(f"/api/v1/trials/{args.trial_id}")["trial"]
+    if args.json:
+        print(json.dumps(t, indent=2, default=str))
+        return
+    render_table([t], ["id", "experiment_id", "state", "steps_completed", "best_validation", "restarts", "hparams"])
+    if args.metrics:
+        ms = s.get(f"/api/v1/trials/{args.trial_id}/metrics")["metrics"]
+        render_table([{"group": m["group"], "steps": m["steps_completed"], "metrics": m["metrics"]} for m in ms],
+                     ["group", "steps", "metrics"])
+
+
+def trial_logs(args):
+    _follow_logs(session(args), f"/api/v1/trials/{args.trial_id}/logs", follow=args.follow, tail=args.tail)
+
+
+def trial_kill(args):
+    session(args).post(f"/api/v1/trials/{args.trial_id}/kill")
+
+
+def _download_checkpoint(s: Session, uuid: str, out: str) -> None:
+    from determined_clone_amd.common import storage
+
+    c = s.get(f"/api/v1/checkpoints/{uuid}")["checkpoint"]
+    sm = storage.build(c.get("storage") or {"type": "shared_fs", "host_path": "/tmp"})
+    sm.download(uuid, out)
+    print(f"downloaded checkpoint {uuid} to {out}")
+
+
+def checkpoint_describe(args):
+    print(json.dumps(session(args).get(f"/api/v1/checkpoints/{args.uuid}")["checkpoint"], indent=2, default=str))
+
+
+def checkpoint_download(args):
+    _download_checkpoint(session(args), args.uuid, args.output_dir or os.path.join("checkpoints", args.uuid))
+
+
+def checkpoint_delete(args):
+    session(args).request("DELETE", "/api/v1/checkpoints", body={"checkpoint_uuids": args.uuids})
+
+
+# ---------------------------------------------------------------------------- model registry
+def model_create(args):
+    m = session(args).post("/api/v1/models", {"name": args.name, "description": args.description or ""})["model"]
+    print(f"Created model {m['name']} (id {m['id']})")
+
+
+def model_list(args):
+    render_table(session(args).get("/api/v1/models")["models"], ["id", "name", "description", "num_versions", "archived"], args.json)
+
+
+def model_describe(args):
+    r = session(args).get(f"/api/v1/models/{args.name}/versions")
+    render_table([r["model"]], ["id", "name", "description", "num_versions"])
+    render_table([{"version": v["version"], "checkpoint": v["checkpoint"]["uuid"], "name": v["name"]}
+                  for v in r["model_versions"]], ["version", "checkpoint", "name"])
+
+
+def model_register(args):
+    v = session(args).post(f"/api/v1/models/{args.name}/versions", {"checkpoint_uuid": args.uuid})["model_version"]
+    print(f"Registered version {v['version']} of model {args.name}")
+
+
+def model_delete(args):
+    session(args).delete(f"/api/v1/models/{args.name}")
+
+
+# ---------------------------------------------------------------------------- templates
+def template_list(args):
+    render_table(session(args).get("/api/v1/templates")["templates"], ["name", "config"], args.json)
+
+
+def template_describe(args):
+    print(yaml.safe_dump(session(args).get(f"/api/v1/templates/{args.name}")["template"]["config"]))
+
+
+def template_set(args):
+    session(args).put(f"/api/v1/templates/{args.name}", {"config": _read_config(args.template_file)})
+    print(f"Set template {args.name}")
+
+
+def template_remove(args):
+    session(args).delete(f"/api/v1/templates/{args.name}")
+
+
+# ---------------------------------------------------------------------------- cluster
+def agent_list(args):
+    rows = []
+    for a in session(args).get("/api/v1/agents")["agents"]:
+        rows.append({"id": a["id"], "resource_pool": a["resource_pool"], "enabled": a["enabled"],
+                     "slots": len(a["slots"]), "containers": sum(1 for s in a["slots"].values() if s["container"])})
+    render_table(rows, ["id", "resource_pool", "enabled", "slots", "containers"], args.json)
+
+
+def agent_enable(enable: bool):
+    def f(args):
+        session(args).post(f"/api/v1/agents/{args.agent_id}/{'enable' if enable else 'disable'}",
+                           {"drain": bool(getattr(args, "drain", False))})
+    return f
+
+
+def slot_list(args):
+    rows = []
+    for a in session(args).get("/api/v1/agents")["agents"]:
+        for sid, sl in a["slots"].items():
+            rows.append({"agent_id": a["id"], "slot_id": sid, "enabled": sl["enabled"],
+                         "type": sl["device"].get("type"), "uuid": sl["device"].get("uuid"),
+                         "allocation": (sl["container"] or {}).get("id")})
+    render_table(rows, ["agent_id", "slot_id", "enabled", "type", "uuid", "allocation"], args.json)
+
+
+def slot_enable(enable: bool):
+    def f(args):
+        session(args).post(f"/api/v1/agents/{args.agent_id}/slots/{args.slot_id}/{'enable' if enable else 'disable'}")
+    return f
+
+
+def resource_pool_list(args):
+    render_table(session(args).get("/api/v1/resource-pools")["resource_pools"],
+                 ["name", "num_agents", "slots_available", "slots_used", "scheduler_type", "slot_type"], args.json)
+
+
+def job_list(args):
+    render_table(session(args).get("/api/v1/job-queues")["jobs"],
+                 ["job_id", "name", "state", "slots", "priority", "weight", "resource_pool", "position"], args.json)
+
+
+def job_update(args):
+    u: Dict[str, Any] = {"job_id": args.job_id}
+    if args.priority is not None:
+        u["priority"] = args.priority
+    if args.weight is not None:
+        u["weight"] = args.weight
+    session(args).post("/api/v1/job-queues", {"updates": [u]})
+
+
+def task_list(args):
+    render_table(session(args).get("/api/v1/tasks")["tasks"], ["task_id", "type", "state", "name"], args.json)
+
+
+def task_logs(args):
+    _follow_logs(session(args), f"/api/v1/tasks/{args.task_id}/logs", follow=args.follow)
+
+
+def cmd_run(kind: str, path: str):
+    def f(args):
+        s = session(args)
+        body: Dict[str, Any] = {"config": {"resources": {"slots": args.slots}}}
+        if getattr(args, "entrypoint", None):
+            body["entrypoint"] = args.entrypoint
+        if getattr(args, "experiment_ids", None):
+            body["experiment_ids"] = args.experiment_ids
+        if getattr(args, "context", None):
+            from determined_clone_amd.util import tar_directory
+
+            body["files"] = base64.b64encode(tar_directory(args.context)).decode()
+        t = s.post(f"/api/v1/{path}", body)[path[:-1]]
+        print(f"Launched {kind.lower()} {t['id']}")
+        if kind == "COMMAND" and not args.detach:
+            _follow_logs(s, f"/api/v1/tasks/{t['id']}/logs")
+    return f
+
+
+def cmd_list(path: str):
+    def f(args):
+        render_table(session(args).get(f"/api/v1/{path}")[path], ["id", "state", "entrypoint", "slots"], args.json)
+    return f
+
+
+def cmd_kill(path: str):
+    def f(args):
+        session(args).post(f"/api/v1/{path}/{args.task_id}/kill")
+    return f
+
+
+def workspace_list(args):
+    render_table(session(args).get("/api/v1/workspaces")["workspaces"], ["id", "name", "num_projects", "archived"], args.json)
+
+
+def workspace_create(args):
+    w = session(args).post("/api/v1/workspaces", {"name": args.name})["workspace"]
+    print(f"Created workspace {w['name']} (id {w['id']})")
+
+
+def workspace_delete(args):
+    s = session(args)
+    w = [x for x in s.get("/api/v1/workspaces")["workspaces"] if x["name"] == args.name][0]
+    s.delete(f"/api/v1/workspaces/{w['id']}")
+
+
+def project_list(args):
+    s = session(args)
+    w = [x for x in s.get("/api/v1/workspaces")["workspaces"] if x["name"] == args.workspace][0]
+    render_table(s.get(f"/api/v1/workspaces/{w['id']}/projects")["projects"], ["id", "name", "num_experiments"], args.json)
+
+
+def project_create(args):
+    s = session(args)
+    w = [x for x in s.get("/api/v1/workspaces")["workspaces"] if x["name"] == args.workspace][0]
+    p = s.post(f"/api/v1/workspaces/{w['id']}/projects", {"name": args.name})["project"]
+    print(f"Created project {p['name']} (id {p['id']})")
+
+
+def deploy_local(args):
+    from determined_clone_amd.deploy import local
+
+    {"cluster-up": local.cluster_up, "cluster-down": local.cluster_down,
+     "master-up": local.master_up, "agent-up": local.agent_up}[args.deploy_cmd](args)
+
+
+# ---------------------------------------------------------------------------- parser
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="det", description="determined_clone_amd CLI")
+    p.add_argument("-m", "--master", default=os.environ.get("DET_MASTER", "http://127.0.0.1:8080"))
+    p.add_argument("-u", "--user", default=os.environ.get("DET_USER"))
+    p.add_argument("--json", action="store_true", help="JSON output")
+    sub = p.add_subparsers(dest="cmd")
+
+    def cmd(parent, names, fn, help_=""):
+        name, *aliases = names.split()
+        sp = parent.add_parser(name, aliases=aliases, help=help_)
+        sp.set_defaults(func=fn)
+        return sp
+
+    def group(names, help_=""):
+        name, *aliases = names.split()
+        g = sub.add_parser(name, aliases=aliases, help=help_)
+        return g.add_subparsers(dest="subcmd")
+
+    cmd(sub, "version", version)
+    u = group("user u")
+    sp = cmd(u, "login", user_login); sp.add_argument("username", nargs="?", default="admin"); sp.add_argument("--password")
+    cmd(u, "logout", user_logout)
+    cmd(u, "whoami", user_whoami)
+    cmd(u, "list ls", user_list)
+    sp = cmd(u, "create", user_create); sp.add_argument("username"); sp.add_argument("--admin", action="store_true"); sp.add_argument("--password")
+    sp = cmd(u, "activate", user_set_active(True)); sp.add_argument("username")
+    sp = cmd(u, "deactivate", user_set_active(False)); sp.add_argument("username")
+    sp = cmd(u, "change-password", user_change_password); sp.add_argument("target_user", nargs="?"); sp.add_argument("--password", required=True)
+
+    m = group("master")
+    cmd(m, "info", master_info)
+    cmd(m, "config", master_config)
+
+    e = group("experiment e")
+    sp = cmd(e, "create", experiment_create)
+    sp.add_argument("config_file"); sp.add_argument("model_def", nargs="?")
+    sp.add_argument("--paused", action="store_true"); sp.add_argument("--test", "--test-mode", dest="test", action="store_true")
+    sp.add_argument("--template"); sp.add_argument("--project-id", type=int)
+    sp.add_argument("--config", action="append", help="override: key.path=value")
+    sp.add_argument("-f", "--follow-first-trial", action="store_true")
+    sp = cmd(e, "list ls", experiment_list); sp.add_argument("--all", "-a", action="store_true")
+    for name, fn in (("describe", experiment_describe), ("config", experiment_config),
+                     ("list-trials lt", experiment_list_trials), ("delete", experiment_delete),
+                     ("activate", experiment_action("activate")), ("pause", experiment_action("pause")),
+                     ("cancel", experiment_action("cancel")), ("kill", experiment_action("kill")),
+                     ("archive", experiment_action("archive")), ("unarchive", experiment_action("unarchive"))):
+        sp = cmd(e, name, fn); sp.add_argument("experiment_id", type=int)
+    sp = cmd(e, "list-checkpoints lc", experiment_list_checkpoints); sp.add_argument("experiment_id", type=int); sp.add_argument("--best", type=int)
+    sp = cmd(e, "wait", experiment_wait); sp.add_argument("experiment_id", type=int); sp.add_argument("--polling-interval", type=float, default=5)
+    sp = cmd(e, "download", experiment_download); sp.add_argument("experiment_id", type=int); sp.add_argument("--top-n", type=int, default=1); sp.add_argument("--output-dir", default="checkpoints")
+    sp = cmd(e, "preview-search", preview_search); sp.add_argument("config_file")
+    for field in ("description", "name"):
+        sp = cmd(e, f"set-{field}", experiment_set(field)); sp.add_argument("experiment_id", type=int); sp.add_argument("value")
+    lab = e.add_parser("label").add_subparsers(dest="labelcmd")
+    for name, add in (("add", True), ("remove", False)):
+        sp = cmd(lab, name, experiment_label(add)); sp.add_argument("experiment_id", type=int); sp.add_argument("label")
+
+    t = group("trial t")
+    sp = cmd(t, "describe", trial_describe); sp.add_argument("trial_id", type=int); sp.add_argument("--metrics", action="store_true")
+    sp = cmd(t, "logs", trial_logs); sp.add_argument("trial_id", type=int); sp.add_argument("-f", "--follow", action="store_true"); sp.add_argument("--tail", type=int)
+    sp = cmd(t, "kill", trial_kill); sp.add_argument("trial_id", type=int)
+
+    c = group("checkpoint")
+    sp = cmd(c, "describe", checkpoint_describe); sp.add_argument("uuid")
+    sp = cmd(c, "download", checkpoint_download); sp.add_argument("uuid"); sp.add_argument("--output-dir", "-o")
+    sp = cmd(c, "delete", checkpoint_delete); sp.add_argument("uuids", nargs="+")
+
+    mo = group("model")
+    sp = cmd(mo, "create", model_create); sp.add_argument("name"); sp.add_argument("--description")
+    cmd(mo, "list ls", model_list)
+    sp = cmd(mo, "describe", model_describe); sp.add_argument("name")
+    sp = cmd(mo, "register-version", model_register); sp.add_argument("name"); sp.add_argument("uuid")
+    sp = cmd(mo, "delete", model_delete); sp.add_argument("name")
+
+    tp = group("template tpl")
+    cmd(tp, "list ls", template_list)
+    sp = cmd(tp, "describe", template_describe); sp.add_argument("name")
+    sp = cmd(tp, "set", template_set); sp.add_argument("name"); sp.add_argument("template_file")
+    sp = cmd(tp, "remove rm", template_remove); sp.add_argument("name")
+
+    a = group("agent a")
+    cmd(a, "list ls", agent_list)
+    sp = cmd(a, "enable", agent_enable(True)); sp.add_argument("agent_id")
+    sp = cmd(a, "disable", agent_enable(False)); sp.add_argument("agent_id"); sp.add_argument("--drain", action="store_true")
+    sl = group("slot s")
+    cmd(sl, "list ls", slot_list)
+    sp = cmd(sl, "enable", slot_enable(True)); sp.add_argument("agent_id"); sp.add_argument("slot_id", type=int)
+    sp = cmd(sl, "disable", slot_enable(False)); sp.add_argument("agent_id"); sp.add_argument("slot_id", type=int)
+    rp = group("resource-pool rp")
+    cmd(rp, "list ls", resource_pool_list)
+    j = group("job")
+    cmd(j, "list ls", job_list)
+    sp = cmd(j, "update", job_update); sp.add_argument("job_id"); sp.add_argument("--priority", type=int); sp.add_argument("--weight", type=float)
+    tk = group("task")
+    cmd(tk, "list ls", task_list)
+    sp = cmd(tk, "logs", task_logs); sp.add_argument("task_id"); sp.add_argument("-f", "--follow", action="store_true")
+
+    for kind, names, path in (("COMMAND", "command cmd", "commands"), ("SHELL", "shell", "shells"),
+                              ("NOTEBOOK", "notebook", "notebooks"), ("TENSORBOARD", "tensorboard", "tensorboards")):
+        g = group(names)
+        sp = cmd(g, "run" if kind == "COMMAND" else "start", cmd_run(kind, path))
+        sp.add_argument("--slots", type=int, default=0)
+        sp.add_argument("--context", "-c")
+        if kind == "COMMAND":
+            sp.add_argument("entrypoint", nargs=argparse.REMAINDER)
+            sp.add_argument("-d", "--detach", action="store_true")
+        if kind == "TENSORBOARD":
+            sp.add_argument("experiment_ids", nargs="*", type=int)
+        cmd(g, "list ls", cmd_list(path))
+        sp = cmd(g, "kill", cmd_kill(path)); sp.add_argument("task_id")
+
+    w = group("workspace")
+    cmd(w, "list ls", workspace_list)
+    sp = cmd(w, "create", workspace_create); sp.add_argument("name")
+    sp = cmd(w, "delete", workspace_delete); sp.add_argument("name")
+    pr = group("project")
+    sp = cmd(pr, "list ls", project_list); sp.add_argument("workspace")
+    sp = cmd(pr, "create", project_create); sp.add_argument("workspace"); sp.add_argument("name")
+
+    d = group("deploy")
+    lo = d.add_parser("local").add_subparsers(dest="deploy_cmd")
+    for name in ("cluster-up", "cluster-down", "master-up", "agent-up"):
+        sp = lo.add_parser(name)
+        sp.set_defaults(func=deploy_local)
+        sp.add_argument("--master-port", type=int, default=8080)
+        sp.add_argument("--agents", type=int, default=1)
+        sp.add_argument("--artificial-slots", type=int, default=0)
+        sp.add_argument("--storage-path", default=None)
+        sp.add_argument("--state-dir", default=os.path.join(os.path.expanduser("~"), ".det-clone"))
+    return p
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    p = build_parser()
+    args = p.parse_args(argv)
+    if not getattr(args, "func", None):
+        p.print_help()
+        return 1
+    try:
+        args.func(args)
+    except APIException as e:
+        print(f"Error: {e}", file=sys.stderr)
+        return 1
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -143,3 +143,32 @@ def test_invalid_config_rejected(cluster):
 
     with pytest.raises(APIException):
         _create(s, ctx, "entrypoint: x:y\nsearcher: {name: single}\n")
+
+
+def test_cli_against_cluster(cluster, tmp_path, capsys, monkeypatch):
+    from determined_clone_amd.cli import cli
+
+    m, s, ctx, _ = cluster
+    monkeypatch.setattr(cli, "AUTH_FILE", tmp_path / "auth.json")
+    cfgf = tmp_path / "c.yaml"
+    cfgf.write_text(BASE + "searcher: {name: grid, metric: val_loss, max_length: {batches: 4}}\n"
+                    .replace("grid", "grid") + "")
+    base = ["-m", m.master_url]
+    assert cli.main(base + ["user", "login", "admin", "--password", ""]) == 0
+    assert cli.main(base + ["experiment", "create", str(cfgf), ctx]) == 0
+    out = capsys.readouterr().out
+    eid = int(out.strip().split()[-1])
+    with pytest.raises(SystemExit) as ex:
+        cli.main(base + ["experiment", "wait", str(eid), "--polling-interval", "0.5"])
+    assert ex.value.code == 0
+    assert cli.main(base + ["experiment", "list"]) == 0
+    assert cli.main(base + ["experiment", "describe", str(eid)]) == 0
+    assert cli.main(base + ["agent", "list"]) == 0
+    assert cli.main(base + ["slot", "list"]) == 0
+    assert cli.main(base + ["experiment", "preview-search", str(cfgf)]) == 0
+    assert cli.main(base + ["model", "create", "mymodel"]) == 0
+    cks = s.get(f"/api/v1/experiments/{eid}/checkpoints")["checkpoints"]
+    assert cli.main(base + ["model", "register-version", "mymodel", cks[0]["uuid"]]) == 0
+    assert cli.main(base + ["model", "describe", "mymodel"]) == 0
+    out = capsys.readouterr().out
+    assert "mymodel" in out and cks[0]["uuid"] in out
