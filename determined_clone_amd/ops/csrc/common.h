@@ -100,6 +100,33 @@ template <> struct Vec8<F32> {
   static constexpr int bytes = 4;
 };
 
+// Scalar element access (for gather-style kernels; bulk paths use Vec8).
+template <typename T> struct Elem;
+template <> struct Elem<BF16> {
+  __device__ __forceinline__ static float get(const void* p, int64_t i) {
+    return __uint_as_float(static_cast<uint32_t>(reinterpret_cast<const uint16_t*>(p)[i]) << 16);
+  }
+  __device__ __forceinline__ static void put(void* p, int64_t i, float v) {
+    reinterpret_cast<uint16_t*>(p)[i] = static_cast<uint16_t>(f2bf_bits(v));
+  }
+};
+template <> struct Elem<F16> {
+  __device__ __forceinline__ static float get(const void* p, int64_t i) {
+    return h2f(reinterpret_cast<const uint16_t*>(p)[i]);
+  }
+  __device__ __forceinline__ static void put(void* p, int64_t i, float v) {
+    reinterpret_cast<uint16_t*>(p)[i] = f2h(v);
+  }
+};
+template <> struct Elem<F32> {
+  __device__ __forceinline__ static float get(const void* p, int64_t i) {
+    return reinterpret_cast<const float*>(p)[i];
+  }
+  __device__ __forceinline__ static void put(void* p, int64_t i, float v) {
+    reinterpret_cast<float*>(p)[i] = v;
+  }
+};
+
 // ---------------------------------------------------------------- reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -1,0 +1,381 @@
+// Transformer-block memory-bound kernels for MI355X: fused residual-add + LayerNorm (fwd/bwd),
+// fused bias + GELU(tanh) (fwd/bwd), rotary position embedding (fwd/bwd).
+//
+// Used by the GPT-2 / GPT-NeoX DeepSpeedTrial (reference: examples/deepspeed/gpt_neox, which
+// relies on DeepSpeed/apex CUDA kernels for these ops).
+//
+// Layout: activations are row-major [rows][D] bf16/fp32, D % 8 == 0. One wave64 owns a row (LN) so
+// row statistics are pure in-register wave reductions (no LDS, no __syncthreads); every lane moves
+// 16 B per access. Parameter gradients (dgamma/dbeta/dbias) are reduced deterministically:
+// each block accumulates its rows in registers, writes one partial row, and a column-reduce kernel
+// sums the partials.
+#include "common.h"
+
+#include <type_traits>
+
+namespace dca {
+
+enum class TDtype : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+namespace {
+
+constexpr int kWaves = 4;             // rows (LN) handled concurrently per block
+constexpr int kBlock = kWaves * 64;
+
+template <typename T, int NV>
+__global__ __launch_bounds__(kBlock) void ln_fwd_kernel(
+    const void* __restrict__ x, const void* __restrict__ res, void* __restrict__ sum_out,
+    void* __restrict__ y, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int64_t rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nvec = D / 8;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wid; row < rows;
+       row += static_cast<int64_t>(gridDim.x) * kWaves) {
+    const int64_t base = row * D;
+    float v[NV][8];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nvec) {
+        Vec8<T>::load(reinterpret_cast<const char*>(x) + (base + vi * 8) * Vec8<T>::bytes, v[i]);
+        if (res) {
+          float r[8];
+          Vec8<T>::load(reinterpret_cast<const char*>(res) + (base + vi * 8) * Vec8<T>::bytes, r);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[i][k] += r[k];
+          if (sum_out) Vec8<T>::store(reinterpret_cast<char*>(sum_out) + (base + vi * 8) * Vec8<T>::bytes, v[i]);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += v[i][k];
+      }
+    }
+    const float mean = wave_sum(s) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if (lane + i * 64 < nvec) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float d = v[i][k] - mean;
+          q = fmaf(d, d, q);
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / D + eps);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nvec) {
+        const int c = vi * 8;
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float g = gamma ? gamma[c + k] : 1.f;
+          const float b = beta ? beta[c + k] : 0.f;
+          o[k] = fmaf((v[i][k] - mean) * rstd, g, b);
+        }
+        Vec8<T>::store(reinterpret_cast<char*>(y) + (base + c) * Vec8<T>::bytes, o);
+      }
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) [+ dres passthrough handled by caller]
+// Per-block partial dgamma/dbeta: partial[blockIdx.x][2][D] (fp32).
+template <typename T, int NV>
+__global__ __launch_bounds__(kBlock) void ln_bwd_kernel(
+    const void* __restrict__ dy, const void* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const void* __restrict__ dsum, void* __restrict__ dx, float* __restrict__ partial,
+    int64_t rows, int D) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nvec = D / 8;
+  float dg[NV][8], db[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { dg[i][k] = 0.f; db[i][k] = 0.f; }
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wid; row < rows;
+       row += static_cast<int64_t>(gridDim.x) * kWaves) {
+    const int64_t base = row * D;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NV][8], g[NV][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nvec) {
+        const int c = vi * 8;
+        float xv[8];
+        Vec8<T>::load(reinterpret_cast<const char*>(x) + (base + c) * Vec8<T>::bytes, xv);
+        Vec8<T>::load(reinterpret_cast<const char*>(dy) + (base + c) * Vec8<T>::bytes, g[i]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xh[i][k] = (xv[k] - mean) * rstd;
+          dg[i][k] = fmaf(g[i][k], xh[i][k], dg[i][k]);
+          db[i][k] += g[i][k];
+          const float gg = g[i][k] * (gamma ? gamma[c + k] : 1.f);
+          g[i][k] = gg;
+          s1 += gg;
+          s2 = fmaf(gg, xh[i][k], s2);
+        }
+      }
+    }
+    const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nvec) {
+        const int c = vi * 8;
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = rstd * (g[i][k] - m1 - xh[i][k] * m2);
+        if (dsum) {
+          float r[8];
+          Vec8<T>::load(reinterpret_cast<const char*>(dsum) + (base + c) * Vec8<T>::bytes, r);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] += r[k];
+        }
+        Vec8<T>::store(reinterpret_cast<char*>(dx) + (base + c) * Vec8<T>::bytes, o);
+      }
+    }
+  }
+  // block-level combine of the kWaves waves' column partials through LDS
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [kWaves][2][D]
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = lane + i * 64;
+    if (vi < nvec)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        lds[(wid * 2 + 0) * D + vi * 8 + k] = dg[i][k];
+        lds[(wid * 2 + 1) * D + vi * 8 + k] = db[i][k];
+      }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += kBlock) {
+    const int which = c / D, col = c % D;
+    float a = 0.f;
+    for (int w = 0; w < kWaves; ++w) a += lds[(w * 2 + which) * D + col];
+    partial[(static_cast<int64_t>(blockIdx.x) * 2 + which) * D + col] = a;
+  }
+}
+
+// out[j] = sum_b partial[b][j] for j < ncols (fp32, coalesced across j).
+__global__ __launch_bounds__(256) void column_reduce_kernel(const float* __restrict__ partial,
+                                                            int nparts, int64_t ncols,
+                                                            float* __restrict__ out) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= ncols) return;
+  float a = 0.f;
+  for (int b = 0; b < nparts; ++b) a += partial[static_cast<int64_t>(b) * ncols + j];
+  out[j] = a;
+}
+
+// ------------------------------------------------------------------ bias + GELU(tanh)
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * fmaf(k1 * x * x, x, x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float u = k0 * fmaf(k1 * x2, x, x);
+  const float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const void* __restrict__ x,
+                                                            const float* __restrict__ bias,
+                                                            void* __restrict__ y, int64_t rows,
+                                                            int N) {
+  const int n8 = N / 8;
+  const int64_t total = rows * n8;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < total;
+       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(v % n8) * 8;
+    float a[8];
+    Vec8<T>::load(reinterpret_cast<const char*>(x) + v * 8 * Vec8<T>::bytes, a);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = gelu_tanh(a[k] + (bias ? bias[c + k] : 0.f));
+    Vec8<T>::store(reinterpret_cast<char*>(y) + v * 8 * Vec8<T>::bytes, a);
+  }
+}
+
+// Block = 256 threads covering 2048 columns (8 per thread) x a slab of rows; dbias partials
+// [gridDim.y][N] reduced by column_reduce_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
+    const void* __restrict__ dy, const void* __restrict__ x, const float* __restrict__ bias,
+    void* __restrict__ dx, float* __restrict__ partial, int64_t rows, int N) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= N) return;
+  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) b[k] = bias ? bias[c + k] : 0.f;
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    const int64_t off = (r * N + c) * Vec8<T>::bytes;
+    float g[8], a[8];
+    Vec8<T>::load(reinterpret_cast<const char*>(dy) + off, g);
+    Vec8<T>::load(reinterpret_cast<const char*>(x) + off, a);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      g[k] *= gelu_tanh_grad(a[k] + b[k]);
+      bsum[k] += g[k];
+    }
+    Vec8<T>::store(reinterpret_cast<char*>(dx) + off, g);
+  }
+  if (partial)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) partial[static_cast<int64_t>(blockIdx.y) * N + c + k] = bsum[k];
+}
+
+// ------------------------------------------------------------------ rotary embedding
+// x: [rows = B*S*H][D] (head-major inner layout [.., S, H, D] flattened so row -> position
+// pos = (row / H) % S). Rotates the first rot_dim features as pairs (i, i + rot_dim/2)
+// (GPT-NeoX "rotate_half" convention); cos/sin tables [S][rot_dim/2] fp32. backward = forward
+// with -sin.
+template <typename T>
+__global__ __launch_bounds__(256) void rope_kernel(const void* __restrict__ x, void* __restrict__ y,
+                                                   const float* __restrict__ cosT,
+                                                   const float* __restrict__ sinT, int64_t rows,
+                                                   int H, int S, int D, int rot, float sign) {
+  const int half = rot / 2;
+  const int per_row = D / 2;  // threads per row: each handles one (i, i+half) pair or 2 passthrough
+  const int64_t total = rows * per_row;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t row = t / per_row;
+    const int i = static_cast<int>(t % per_row);
+    const int pos = static_cast<int>((row / H) % S);
+    if (i < half) {
+      const float cs = cosT[pos * half + i], sn = sinT[pos * half + i] * sign;
+      const float a = Elem<T>::get(x, row * D + i), b = Elem<T>::get(x, row * D + i + half);
+      Elem<T>::put(y, row * D + i, a * cs - b * sn);
+      Elem<T>::put(y, row * D + i + half, b * cs + a * sn);
+    } else {
+      // pass-through features beyond rot_dim: two per thread
+      const int j = rot + 2 * (i - half);
+      if (j < D) {
+        Elem<T>::put(y, row * D + j, Elem<T>::get(x, row * D + j));
+        if (j + 1 < D) Elem<T>::put(y, row * D + j + 1, Elem<T>::get(x, row * D + j + 1));
+      }
+    }
+  }
+}
+
+template <int NV>
+struct NVTag {
+  static constexpr int value = NV;
+};
+
+template <typename T, typename F>
+void dispatch_nv(int D, F&& f) {
+  const int nv = (D / 8 + 63) / 64;
+  if (nv <= 1) f(NVTag<1>{});
+  else if (nv <= 2) f(NVTag<2>{});
+  else if (nv <= 4) f(NVTag<4>{});
+  else if (nv <= 8) f(NVTag<8>{});
+  else f(NVTag<16>{});
+}
+
+template <typename F>
+void dispatch_t(TDtype dt, F&& f) {
+  switch (dt) {
+    case TDtype::kBF16: f(BF16{}); break;
+    case TDtype::kF16: f(F16{}); break;
+    default: f(F32{}); break;
+  }
+}
+
+inline int ln_grid(int64_t rows) {
+  int64_t g = (rows + kWaves - 1) / kWaves;
+  return static_cast<int>(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+}
+
+}  // namespace
+
+int ln_bwd_blocks(int64_t rows) {
+  int64_t g = (rows + kWaves - 1) / kWaves;
+  return static_cast<int>(g < 512 ? (g < 1 ? 1 : g) : 512);
+}
+
+void layernorm_fwd(TDtype dt, const void* x, const void* res, void* sum_out, void* y,
+                   const float* gamma, const float* beta, float* mean, float* rstd, int64_t rows,
+                   int D, float eps, hipStream_t st) {
+  dispatch_t(dt, [&](auto t) {
+    using T = decltype(t);
+    dispatch_nv<T>(D, [&](auto nvt) {
+      constexpr int NV = decltype(nvt)::value;
+      hipLaunchKernelGGL((ln_fwd_kernel<T, NV>), dim3(ln_grid(rows)), dim3(kBlock), 0, st, x, res,
+                         sum_out, y, gamma, beta, mean, rstd, rows, D, eps);
+    });
+  });
+}
+
+void layernorm_bwd(TDtype dt, const void* dy, const void* x, const float* gamma, const float* mean,
+                   const float* rstd, const void* dsum, void* dx, float* partial, float* dgamma_dbeta,
+                   int64_t rows, int D, hipStream_t st) {
+  const int blocks = ln_bwd_blocks(rows);
+  dispatch_t(dt, [&](auto t) {
+    using T = decltype(t);
+    dispatch_nv<T>(D, [&](auto nvt) {
+      constexpr int NV = decltype(nvt)::value;
+      const size_t lds = static_cast<size_t>(kWaves) * 2 * D * sizeof(float);
+      hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3(blocks), dim3(kBlock), lds, st, dy, x, gamma,
+                         mean, rstd, dsum, dx, partial, rows, D);
+    });
+  });
+  if (dgamma_dbeta) {
+    const int64_t ncols = 2 * static_cast<int64_t>(D);
+    hipLaunchKernelGGL(column_reduce_kernel, dim3((ncols + 255) / 256), dim3(256), 0, st, partial,
+                       blocks, ncols, dgamma_dbeta);
+  }
+}
+
+void bias_gelu_fwd(TDtype dt, const void* x, const float* bias, void* y, int64_t rows, int N,
+                   hipStream_t st) {
+  const int grid = stream_grid(rows * N / 8, 256);
+  dispatch_t(dt, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(bias_gelu_fwd_kernel<T>, dim3(grid), dim3(256), 0, st, x, bias, y, rows, N);
+  });
+}
+
+int bias_gelu_bwd_row_blocks(int64_t rows) { return static_cast<int>(rows < 256 ? (rows < 1 ? 1 : rows) : 256); }
+
+void bias_gelu_bwd(TDtype dt, const void* dy, const void* x, const float* bias, void* dx,
+                   float* partial, float* dbias, int64_t rows, int N, hipStream_t st) {
+  const int rb = bias_gelu_bwd_row_blocks(rows);
+  dim3 grid((N / 8 + 255) / 256, rb);
+  dispatch_t(dt, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(bias_gelu_bwd_kernel<T>, grid, dim3(256), 0, st, dy, x, bias, dx,
+                       dbias ? partial : nullptr, rows, N);
+  });
+  if (dbias)
+    hipLaunchKernelGGL(column_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, st, partial, rb,
+                       static_cast<int64_t>(N), dbias);
+}
+
+void rope(TDtype dt, const void* x, void* y, const float* cosT, const float* sinT, int64_t rows,
+          int H, int S, int D, int rot, bool backward, hipStream_t st) {
+  const int grid = stream_grid(rows * (D / 2), 256);
+  dispatch_t(dt, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(rope_kernel<T>, dim3(grid), dim3(256), 0, st, x, y, cosT, sinT, rows, H, S, D,
+                       rot, backward ? -1.f : 1.f);
+  });
+}
+
+}  // namespace dca

@@ -1,5 +1,202 @@
-// Bindings for the transformer kernel family (LayerNorm, GELU, RoPE, attention) — filled in by
-// transformer.hip; kept in its own translation unit so bindings.cpp stays small.
+// Bindings for the transformer kernel family (transformer.hip, attention.hip).
 #include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
 
-void register_transformer_ops(pybind11::module& m) { (void)m; }
+#include <hip/hip_runtime.h>
+
+namespace dca {
+enum class TDtype : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+int ln_bwd_blocks(int64_t rows);
+void layernorm_fwd(TDtype dt, const void* x, const void* res, void* sum_out, void* y,
+                   const float* gamma, const float* beta, float* mean, float* rstd, int64_t rows,
+                   int D, float eps, hipStream_t st);
+void layernorm_bwd(TDtype dt, const void* dy, const void* x, const float* gamma, const float* mean,
+                   const float* rstd, const void* dsum, void* dx, float* partial, float* dgamma_dbeta,
+                   int64_t rows, int D, hipStream_t st);
+void bias_gelu_fwd(TDtype dt, const void* x, const float* bias, void* y, int64_t rows, int N,
+                   hipStream_t st);
+int bias_gelu_bwd_row_blocks(int64_t rows);
+void bias_gelu_bwd(TDtype dt, const void* dy, const void* x, const float* bias, void* dx,
+                   float* partial, float* dbias, int64_t rows, int N, hipStream_t st);
+void rope(TDtype dt, const void* x, void* y, const float* cosT, const float* sinT, int64_t rows,
+          int H, int S, int D, int rot, bool backward, hipStream_t st);
+void attention_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H,
+                   int Sq, int Sk, int D, const int64_t* qs, const int64_t* ks, const int64_t* vs,
+                   const int64_t* os, float scale, bool causal, hipStream_t st);
+void attention_bwd(const void* q, const void* k, const void* v, const void* o, const void* dO,
+                   const float* lse, float* delta, float* dq_acc, void* dq, void* dk, void* dv,
+                   int B, int H, int Sq, int Sk, int D, const int64_t* st_q, const int64_t* st_k,
+                   const int64_t* st_v, const int64_t* st_o, const int64_t* st_do,
+                   const int64_t* st_dq, const int64_t* st_dk, const int64_t* st_dv, float scale,
+                   bool causal, hipStream_t stream);
+}  // namespace dca
+
+namespace {
+using torch::Tensor;
+using OptT = c10::optional<Tensor>;
+
+hipStream_t stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+dca::TDtype tdt(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kBFloat16: return dca::TDtype::kBF16;
+    case at::kHalf: return dca::TDtype::kF16;
+    case at::kFloat: return dca::TDtype::kF32;
+    default: TORCH_CHECK(false, "unsupported dtype ", t.scalar_type());
+  }
+}
+const void* vp(const OptT& t) { return t.has_value() && t->defined() ? t->data_ptr() : nullptr; }
+const float* fp(const OptT& t) {
+  if (!(t.has_value() && t->defined())) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "params must be contiguous fp32");
+  return t->data_ptr<float>();
+}
+
+std::vector<Tensor> ln_fwd(const Tensor& x, const OptT& res, const OptT& gamma, const OptT& beta,
+                           double eps, bool want_sum) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "ln_fwd: contiguous GPU input required");
+  const c10::DeviceGuard g(x.device());
+  const int D = static_cast<int>(x.size(-1));
+  TORCH_CHECK(D % 8 == 0 && D <= 8192, "ln_fwd: D must be a multiple of 8 and <= 8192");
+  const int64_t rows = x.numel() / D;
+  if (res.has_value()) TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous(), "residual shape");
+  Tensor y = torch::empty_like(x);
+  Tensor sum = (res.has_value() && want_sum) ? torch::empty_like(x) : Tensor();
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor mean = torch::empty({rows}, fo), rstd = torch::empty({rows}, fo);
+  dca::layernorm_fwd(tdt(x), x.data_ptr(), vp(res), sum.defined() ? sum.data_ptr() : nullptr,
+                     y.data_ptr(), fp(gamma), fp(beta), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), rows, D, static_cast<float>(eps), stream());
+  return {y, sum, mean, rstd};
+}
+
+std::vector<Tensor> ln_bwd(const Tensor& dy_in, const Tensor& x, const OptT& gamma,
+                           const Tensor& mean, const Tensor& rstd, const OptT& dsum,
+                           bool need_param_grads) {
+  const c10::DeviceGuard g(x.device());
+  Tensor dy = dy_in.contiguous();
+  const int D = static_cast<int>(x.size(-1));
+  const int64_t rows = x.numel() / D;
+  Tensor dx = torch::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  const int blocks = dca::ln_bwd_blocks(rows);
+  Tensor partial = torch::empty({static_cast<int64_t>(blocks) * 2 * D}, fo);
+  Tensor dgb = need_param_grads ? torch::empty({2, D}, fo) : Tensor();
+  Tensor ds = dsum.has_value() && dsum->defined() ? dsum->contiguous() : Tensor();
+  dca::layernorm_bwd(tdt(x), dy.data_ptr(), x.data_ptr(), fp(gamma), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), ds.defined() ? ds.data_ptr() : nullptr, dx.data_ptr(),
+                     partial.data_ptr<float>(), need_param_grads ? dgb.data_ptr<float>() : nullptr,
+                     rows, D, stream());
+  if (!need_param_grads) return {dx, Tensor(), Tensor()};
+  return {dx, dgb[0], dgb[1]};
+}
+
+Tensor bias_gelu(const Tensor& x, const OptT& bias) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "bias_gelu: contiguous GPU input required");
+  const c10::DeviceGuard g(x.device());
+  const int N = static_cast<int>(x.size(-1));
+  TORCH_CHECK(N % 8 == 0, "bias_gelu: last dim must be a multiple of 8");
+  Tensor y = torch::empty_like(x);
+  dca::bias_gelu_fwd(tdt(x), x.data_ptr(), fp(bias), y.data_ptr(), x.numel() / N, N, stream());
+  return y;
+}
+
+std::vector<Tensor> bias_gelu_bwd(const Tensor& dy_in, const Tensor& x, const OptT& bias) {
+  const c10::DeviceGuard g(x.device());
+  Tensor dy = dy_in.contiguous();
+  const int N = static_cast<int>(x.size(-1));
+  const int64_t rows = x.numel() / N;
+  Tensor dx = torch::empty_like(x);
+  const bool want_db = bias.has_value() && bias->defined();
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor partial = want_db ? torch::empty({static_cast<int64_t>(dca::bias_gelu_bwd_row_blocks(rows)) * N}, fo) : Tensor();
+  Tensor db = want_db ? torch::empty({N}, fo) : Tensor();
+  dca::bias_gelu_bwd(tdt(x), dy.data_ptr(), x.data_ptr(), fp(bias), dx.data_ptr(),
+                     want_db ? partial.data_ptr<float>() : nullptr,
+                     want_db ? db.data_ptr<float>() : nullptr, rows, N, stream());
+  return {dx, db};
+}
+
+Tensor rope_apply(const Tensor& x, const Tensor& cosT, const Tensor& sinT, int64_t H, int64_t S,
+                  int64_t rot, bool backward) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "rope: contiguous GPU input [B, S, H, D] required");
+  const c10::DeviceGuard g(x.device());
+  const int D = static_cast<int>(x.size(-1));
+  TORCH_CHECK(rot % 2 == 0 && rot <= D, "rope: rot_dim must be even and <= head dim");
+  Tensor y = torch::empty_like(x);
+  dca::rope(tdt(x), x.data_ptr(), y.data_ptr(), cosT.data_ptr<float>(), sinT.data_ptr<float>(),
+            x.numel() / D, static_cast<int>(H), static_cast<int>(S), D, static_cast<int>(rot),
+            backward, stream());
+  return y;
+}
+
+// q/k/v/o are [B, S, H, D] tensors (any strides with the last dim contiguous). The kernels take
+// (batch, head, seq) strides, so both [B,S,H,D] and [B,H,S,D] layouts (and slices of a fused QKV
+// projection) work without copies.
+struct AttnStrides {
+  int64_t v[3];
+};
+AttnStrides bshd_strides(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 4, "attention: ", name, " must be [B, S, H, D]");
+  TORCH_CHECK(t.stride(3) == 1, "attention: ", name, " last dim must be contiguous");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "attention: ", name, " must be bf16");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && t.stride(1) % 8 == 0 &&
+                  t.stride(2) % 8 == 0 && t.stride(0) % 8 == 0,
+              "attention: ", name, " must be 16-byte aligned per row");
+  return {{t.stride(0), t.stride(2), t.stride(1)}};
+}
+
+std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, double scale,
+                             bool causal) {
+  TORCH_CHECK(q.is_cuda(), "attention: GPU tensors required");
+  const c10::DeviceGuard g(q.device());
+  const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
+  const int Sk = k.size(1);
+  TORCH_CHECK(D == 64 || D == 128, "attention: head dim must be 64 or 128");
+  TORCH_CHECK(k.size(0) == B && k.size(2) == H && k.size(3) == D && v.sizes() == k.sizes(),
+              "attention: k/v shape mismatch");
+  TORCH_CHECK(!causal || Sq == Sk, "attention: causal requires Sq == Sk");
+  auto qs = bshd_strides(q, "q"), ks = bshd_strides(k, "k"), vs = bshd_strides(v, "v");
+  Tensor o = torch::empty({B, Sq, H, D}, q.options());
+  Tensor lse = torch::empty({B, H, Sq}, q.options().dtype(at::kFloat));
+  auto os = bshd_strides(o, "o");
+  dca::attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                     B, H, Sq, Sk, D, qs.v, ks.v, vs.v, os.v, static_cast<float>(scale), causal,
+                     stream());
+  return {o, lse};
+}
+
+std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
+                             const Tensor& o, const Tensor& lse, double scale, bool causal) {
+  const c10::DeviceGuard g(q.device());
+  const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
+  const int Sk = k.size(1);
+  Tensor dO = dout.stride(3) == 1 ? dout : dout.contiguous();
+  auto qs = bshd_strides(q, "q"), ks = bshd_strides(k, "k"), vs = bshd_strides(v, "v");
+  auto os = bshd_strides(o, "o"), dos = bshd_strides(dO, "dout");
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() == static_cast<int64_t>(B) * H * Sq, "attention: lse");
+  Tensor dq = torch::empty({B, Sq, H, D}, q.options());
+  Tensor dk = torch::empty({B, Sk, H, D}, q.options());
+  Tensor dv = torch::empty({B, Sk, H, D}, q.options());
+  auto fo = q.options().dtype(at::kFloat);
+  Tensor delta = torch::empty({B, H, Sq}, fo);
+  Tensor dq_acc = torch::empty({B, H, Sq, D}, fo);
+  auto dqs = bshd_strides(dq, "dq"), dks = bshd_strides(dk, "dk"), dvs = bshd_strides(dv, "dv");
+  dca::attention_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dO.data_ptr(),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), dq_acc.data_ptr<float>(),
+                     dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, H, Sq, Sk, D, qs.v, ks.v, vs.v,
+                     os.v, dos.v, dqs.v, dks.v, dvs.v, static_cast<float>(scale), causal, stream());
+  return {dq, dk, dv};
+}
+}  // namespace
+
+void register_transformer_ops(pybind11::module& m) {
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("bias_gelu", &bias_gelu);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("rope", &rope_apply);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+}

@@ -1,0 +1,218 @@
+"""Transformer hot ops: fused residual-add + LayerNorm, bias + GELU, rotary embedding, flash
+attention.
+
+GPU path: `ops/csrc/transformer.hip` and `ops/csrc/attention.hip` (MFMA 16x16x32 bf16). CPU path
+(and fp32 oracle for the GPU numerics tests): plain PyTorch.
+
+These replace the fused kernels the reference's GPT-NeoX DeepSpeedTrial example gets from
+DeepSpeed / apex (reference: examples/deepspeed/gpt_neox/gpt2_trial.py, which builds the
+NeoX model with `fused_softmax`, `scaled_upper_triang_masked_softmax` and apex FusedLayerNorm).
+Layouts are the ones the model produces without copies: activations [..., D] row-major,
+attention operands [B, S, H, Dh] (slices of the fused QKV projection are accepted as-is).
+"""
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from determined_clone_amd.ops import _ext
+
+# ----------------------------------------------------------------------------- references
+
+
+def reference_layer_norm(x, weight, bias, eps=1e-5, residual=None):
+    s = x if residual is None else x + residual
+    y = F.layer_norm(s.float(), (s.shape[-1],), None if weight is None else weight.float(),
+                     None if bias is None else bias.float(), eps).to(x.dtype)
+    return y if residual is None else (y, s)
+
+
+def reference_bias_gelu(x, bias):
+    h = x.float() if bias is None else x.float() + bias.float()
+    return F.gelu(h, approximate="tanh").to(x.dtype)
+
+
+def rope_tables(seq_len: int, rot_dim: int, base: float = 10000.0, device=None):
+    """cos/sin tables [S, rot_dim/2] (fp32) for the rotate-half convention."""
+    inv = 1.0 / (base ** (torch.arange(0, rot_dim, 2, dtype=torch.float64) / rot_dim))
+    t = torch.arange(seq_len, dtype=torch.float64)
+    fr = torch.outer(t, inv)
+    return fr.cos().float().to(device), fr.sin().float().to(device)
+
+
+def reference_rope(x, cos, sin, rot_dim: Optional[int] = None):
+    """x: [B, S, H, D]."""
+    D = x.shape[-1]
+    rot = rot_dim or D
+    half = rot // 2
+    xf = x.float()
+    c = cos[: x.shape[1], :half].to(x.device)[None, :, None, :]
+    s = sin[: x.shape[1], :half].to(x.device)[None, :, None, :]
+    a, b, rest = xf[..., :half], xf[..., half:rot], xf[..., rot:]
+    out = torch.cat([a * c - b * s, b * c + a * s, rest], dim=-1)
+    return out.to(x.dtype)
+
+
+def reference_attention(q, k, v, causal=True, scale=None):
+    """q/k/v [B, S, H, D] -> [B, S, H, D] (fp32 math)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        S = s.shape[-1]
+        mask = torch.ones(s.shape[-2], S, dtype=torch.bool, device=s.device).triu(1)
+        s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    return torch.matmul(p, vf).transpose(1, 2).to(q.dtype)
+
+
+# ----------------------------------------------------------------------------- autograd
+
+
+def _gpu_ok(x: torch.Tensor, div: int = 8) -> bool:
+    return x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32) and x.shape[-1] % div == 0
+
+
+def _f32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if t is None:
+        return None
+    return t if t.dtype == torch.float32 and t.is_contiguous() else t.float().contiguous()
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, eps):
+        C = _ext.load()
+        x = x.contiguous()
+        res = residual.contiguous() if residual is not None else None
+        if res is not None and res.dtype != x.dtype:
+            res = res.to(x.dtype)
+        y, s, mean, rstd = C.ln_fwd(x, res, _f32(weight), _f32(bias), eps, res is not None)
+        # Backward needs the normalised input: the residual sum when fused, else x.
+        ctx.save_for_backward(s if res is not None else x, weight, mean, rstd)
+        ctx.has_res = res is not None
+        ctx.w_dtype = weight.dtype if weight is not None else None
+        if res is not None:
+            return y, s
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, dsum=None):
+        xin, weight, mean, rstd = ctx.saved_tensors
+        need_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        dx, dg, db = _ext.load().ln_bwd(dy, xin, _f32(weight), mean, rstd,
+                                        dsum if ctx.has_res else None, need_w)
+        if need_w:
+            dg = dg.to(ctx.w_dtype)
+            db = db.to(ctx.w_dtype)
+        return (dx, dx if ctx.has_res else None, dg if need_w else None, db if need_w else None,
+                None)
+
+
+def layer_norm(x: torch.Tensor, weight: Optional[torch.Tensor], bias: Optional[torch.Tensor],
+               eps: float = 1e-5, residual: Optional[torch.Tensor] = None):
+    """LayerNorm over the last dim. With ``residual`` returns ``(LN(x + residual), x + residual)``
+    from one HBM pass (pre-LN transformer block pattern)."""
+    if not _gpu_ok(x) or x.shape[-1] > 8192:
+        return reference_layer_norm(x, weight, bias, eps, residual)
+    return _LayerNorm.apply(x, residual, weight, bias, eps)
+
+
+class _BiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias):
+        x = x.contiguous()
+        y = _ext.load().bias_gelu(x, _f32(bias))
+        ctx.save_for_backward(x, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, bias = ctx.saved_tensors
+        dx, db = _ext.load().bias_gelu_bwd(dy, x, _f32(bias))
+        if bias is not None and ctx.needs_input_grad[1]:
+            db = db.to(bias.dtype)
+        else:
+            db = None
+        return dx, db
+
+
+def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:
+    """``gelu_tanh(x + bias)`` with the bias broadcast over the last dim."""
+    if not _gpu_ok(x):
+        return reference_bias_gelu(x, bias)
+    return _BiasGelu.apply(x, bias)
+
+
+class _Rope(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cos, sin, rot):
+        B, S, H, D = x.shape
+        x = x.contiguous()
+        ctx.save_for_backward(cos, sin)
+        ctx.meta = (H, S, rot)
+        return _ext.load().rope(x, cos, sin, H, S, rot, False)
+
+    @staticmethod
+    def backward(ctx, dy):
+        cos, sin = ctx.saved_tensors
+        H, S, rot = ctx.meta
+        return _ext.load().rope(dy.contiguous(), cos, sin, H, S, rot, True), None, None, None
+
+
+def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
+         rot_dim: Optional[int] = None) -> torch.Tensor:
+    """Rotary embedding (rotate-half convention) on the first ``rot_dim`` features of
+    ``x`` [B, S, H, D]; ``cos``/``sin`` are [>=S, rot_dim/2] fp32 tables."""
+    rot = rot_dim or x.shape[-1]
+    if not _gpu_ok(x, 2):
+        return reference_rope(x, cos, sin, rot)
+    S = x.shape[1]
+    half = rot // 2
+    cos = cos[:S, :half].contiguous()
+    sin = sin[:S, :half].contiguous()
+    if cos.dtype != torch.float32:
+        cos, sin = cos.float(), sin.float()
+    return _Rope.apply(x, cos, sin, rot)
+
+
+class _FlashAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale):
+        o, lse = _ext.load().attn_fwd(q, k, v, scale, causal)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        dq, dk, dv = _ext.load().attn_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal)
+        return dq, dk, dv, None, None
+
+
+def _attn_gpu_ok(q, k, v) -> bool:
+    if not (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128)):
+        return False
+    for t in (q, k, v):
+        if t.stride(-1) != 1 or any(s % 8 for s in t.stride()[:3]) or t.data_ptr() % 16:
+            return False
+    return True
+
+
+def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True,
+                    scale: Optional[float] = None) -> torch.Tensor:
+    """softmax(q k^T * scale [+ causal mask]) v for [B, S, H, Dh] operands (Dh in {64, 128},
+    bf16 on GPU). Never materialises the S x S score matrix."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if not q.is_cuda:
+        return reference_attention(q, k, v, causal, scale)
+    if not _attn_gpu_ok(q, k, v):
+        raise ValueError("flash_attention: GPU path needs bf16 [B,S,H,D] with D in {64,128} and "
+                         "16-byte aligned rows")
+    return _FlashAttention.apply(q, k, v, causal, float(scale))
+
+
+__all__ = ["layer_norm", "bias_gelu", "rope", "rope_tables", "flash_attention",
+           "reference_layer_norm", "reference_bias_gelu", "reference_rope", "reference_attention"]

@@ -1,0 +1,146 @@
+"""Numerics of the transformer HIP kernels (LayerNorm, bias+GELU, RoPE, MFMA flash attention)
+against plain PyTorch fp32 references (run on an MI355X)."""
+import math
+
+import pytest
+import torch
+
+from determined_clone_amd.ops import _ext
+from determined_clone_amd.ops import transformer as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _C():
+    C = _ext.load()
+    assert C.__file__.endswith("_C.so")
+    return C
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("D", [64, 1024, 1000 - 1000 % 8, 4096])
+@pytest.mark.parametrize("res", [False, True])
+def test_layer_norm(dtype, D, res):
+    _C()
+    torch.manual_seed(0)
+    rows = 333
+    x = (torch.randn(rows, D, device="cuda") * 3 + 1).to(dtype)
+    r = torch.randn(rows, D, device="cuda").to(dtype) if res else None
+    w = torch.rand(D, device="cuda") + 0.5
+    b = torch.randn(D, device="cuda")
+    xs = [t.clone().requires_grad_(True) if t is not None else None for t in (x, r, w, b)]
+    xr = [t.float().clone().requires_grad_(True) if t is not None else None for t in (x, r, w, b)]
+    out = T.layer_norm(xs[0], xs[2], xs[3], 1e-5, residual=xs[1])
+    ref = T.reference_layer_norm(xr[0], xr[2], xr[3], 1e-5, residual=xr[1])
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    if res:
+        y, s = out
+        y2, s2 = ref
+        torch.testing.assert_close(s.float(), s2, atol=tol, rtol=tol)
+        gy, gs = torch.randn_like(y2), torch.randn_like(s2)
+        torch.autograd.backward([y, s], [gy.to(dtype), gs.to(dtype)])
+        torch.autograd.backward([y2, s2], [gy, gs])
+    else:
+        y, y2 = out, ref
+        gy = torch.randn_like(y2)
+        y.backward(gy.to(dtype))
+        y2.backward(gy)
+    torch.testing.assert_close(y.float(), y2, atol=tol * 4, rtol=tol)
+    assert _rel(xs[0].grad, xr[0].grad) < (2e-2 if dtype == torch.bfloat16 else 1e-4)
+    if res:
+        assert _rel(xs[1].grad, xr[1].grad) < (2e-2 if dtype == torch.bfloat16 else 1e-4)
+    assert _rel(xs[2].grad, xr[2].grad) < 1e-2
+    assert _rel(xs[3].grad, xr[3].grad) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N", [64, 4096, 1032])
+def test_bias_gelu(dtype, N):
+    _C()
+    torch.manual_seed(1)
+    x = torch.randn(257, N, device="cuda").to(dtype)
+    b = torch.randn(N, device="cuda") * 0.5
+    x1, b1 = x.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    x2, b2 = x.float().clone().requires_grad_(True), b.clone().requires_grad_(True)
+    y = T.bias_gelu(x1, b1)
+    y2 = T.reference_bias_gelu(x2, b2)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(y.float(), y2, atol=tol, rtol=tol)
+    g = torch.randn_like(y2)
+    y.backward(g.to(dtype))
+    y2.backward(g)
+    assert _rel(x1.grad, x2.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-5)
+    assert _rel(b1.grad, b2.grad) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rot", [64, 16])
+def test_rope(dtype, rot):
+    _C()
+    torch.manual_seed(2)
+    B, S, H, D = 2, 37, 4, 64
+    cos, sin = T.rope_tables(64, rot, device="cuda")
+    x = torch.randn(B, S, H, D, device="cuda").to(dtype)
+    x1 = x.clone().requires_grad_(True)
+    x2 = x.float().clone().requires_grad_(True)
+    y = T.rope(x1, cos, sin, rot)
+    y2 = T.reference_rope(x2, cos, sin, rot)
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(y.float(), y2, atol=tol, rtol=tol)
+    g = torch.randn_like(y2)
+    y.backward(g.to(dtype))
+    y2.backward(g)
+    torch.testing.assert_close(x1.grad.float(), x2.grad, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("S", [64, 200, 512])
+def test_flash_attention(D, causal, S):
+    _C()
+    torch.manual_seed(3)
+    B, H = 2, 3
+    q, k, v = (torch.randn(B, S, H, D, device="cuda").bfloat16() for _ in range(3))
+    qs = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    qr = [t.float().clone().requires_grad_(True) for t in (q, k, v)]
+    o = T.flash_attention(*qs, causal=causal)
+    o2 = T.reference_attention(*qr, causal=causal)
+    assert _rel(o, o2) < 1e-2, _rel(o, o2)
+    g = torch.randn_like(o2)
+    o.backward(g.bfloat16())
+    o2.backward(g)
+    for a, b in zip(qs, qr):
+        assert _rel(a.grad, b.grad) < 2e-2, _rel(a.grad, b.grad)
+
+
+def test_flash_attention_strided_qkv_slices():
+    """Operands sliced from a fused QKV projection output [B, S, 3, H, D] need no copies."""
+    _C()
+    torch.manual_seed(4)
+    B, S, H, D = 2, 128, 4, 64
+    qkv = torch.randn(B, S, 3, H, D, device="cuda").bfloat16().requires_grad_(True)
+    q, k, v = qkv.unbind(2)
+    o = T.flash_attention(q, k, v, causal=True)
+    qkv2 = qkv.detach().float().requires_grad_(True)
+    o2 = T.reference_attention(*qkv2.unbind(2), causal=True)
+    assert _rel(o, o2) < 1e-2
+    g = torch.randn_like(o2)
+    o.backward(g.bfloat16())
+    o2.backward(g)
+    assert _rel(qkv.grad, qkv2.grad) < 2e-2
+
+
+def test_flash_attention_matches_sdpa_speed_sanity():
+    """Not a benchmark: runs a GPT-2-medium-shaped attention to make sure big grids execute."""
+    _C()
+    B, S, H, D = 8, 1024, 16, 64
+    q, k, v = (torch.randn(B, S, H, D, device="cuda").bfloat16() for _ in range(3))
+    o = T.flash_attention(q, k, v, causal=True)
+    ref = torch.nn.functional.scaled_dot_product_attention(
+        q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=True).transpose(1, 2)
+    assert _rel(o, ref) < 1e-2
+    assert math.isfinite(o.float().abs().max().item())
