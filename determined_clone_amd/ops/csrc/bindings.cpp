@@ -198,6 +198,42 @@ Tensor grad_norm_scale(const std::vector<Tensor>& grads, const OptT& loss_scale,
   return out;
 }
 
+// ZeRO path: per-rank sum-of-squares partials over the owned gradient shard (the caller sums them,
+// all-reduces the scalar and then calls norm_finalize on it).
+Tensor sumsq_partials(const std::vector<Tensor>& grads) {
+  TORCH_CHECK(!grads.empty(), "sumsq_partials: no gradients");
+  const c10::DeviceGuard guard(grads[0].device());
+  std::vector<int> blocks;
+  int total = 0;
+  for (auto& g : grads) {
+    CHECK_DEV(g);
+    TORCH_CHECK(g.is_contiguous(), "sumsq_partials: contiguous gradient slices required");
+    blocks.push_back(dca::sumsq_partial_blocks(g.numel()));
+    total += blocks.back();
+  }
+  Tensor partial = torch::empty({total}, grads[0].options().dtype(at::kFloat));
+  int off = 0;
+  for (size_t i = 0; i < grads.size(); ++i) {
+    dca::sumsq_partial(opt_dtype(grads[i]), grads[i].data_ptr(), grads[i].numel(),
+                       partial.data_ptr<float>() + off, blocks[i], cur_stream());
+    off += blocks[i];
+  }
+  return partial;
+}
+
+Tensor norm_finalize_t(const Tensor& partial, const OptT& loss_scale, double extra_scale,
+                       double max_norm) {
+  CHECK_DEV(partial);
+  CHECK_F32(partial);
+  TORCH_CHECK(partial.is_contiguous(), "norm_finalize: contiguous partials required");
+  const c10::DeviceGuard guard(partial.device());
+  Tensor out = torch::empty({3}, partial.options());
+  dca::norm_finalize(partial.data_ptr<float>(), static_cast<int>(partial.numel()),
+                     ptr_or_null<float>(loss_scale), static_cast<float>(extra_scale),
+                     static_cast<float>(max_norm), out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
 void check_flat(const Tensor& master, const Tensor& grad, const OptT& model) {
   CHECK_DEV(master);
   CHECK_F32(master);
@@ -294,6 +330,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd_affine", &bn_fwd_affine);
   m.def("bn_bwd_train", &bn_bwd_train);
   m.def("grad_norm_scale", &grad_norm_scale);
+  m.def("sumsq_partials", &sumsq_partials);
+  m.def("norm_finalize", &norm_finalize_t);
   m.def("sgd", &sgd);
   m.def("adam", &adam);
   m.def("lamb", &lamb);

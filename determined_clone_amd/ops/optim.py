@@ -43,10 +43,9 @@ class FusedOptimizerBase(torch.optim.Optimizer):
 
     def __init__(self, params: Any, defaults: Dict[str, Any]) -> None:
         super().__init__(params, defaults)
-        self.space = FlatParamSpace([g["params"] for g in self.param_groups])
-        self.flat: Dict[torch.dtype, _FlatState] = {
-            dt: _FlatState(buf, self.state_names) for dt, buf in self.space.buffers.items()
-        }
+        self.space = FlatParamSpace([g["params"] for g in self.param_groups],
+                                    pad_multiple=self._pad_multiple())
+        self.flat: Dict[torch.dtype, _FlatState] = self._build_flat_states()
         self._step = 0
         # Device-side [grad multiplier, found_inf, grad norm] produced by clip/unscale; None when
         # the step needs neither.
@@ -54,6 +53,12 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         # Host-side multiplier folded into every kernel (e.g. 1/world_size for summed all-reduce).
         self.grad_multiplier = 1.0
         self.last_grad_norm: Optional[torch.Tensor] = None
+
+    def _pad_multiple(self) -> int:
+        return 1
+
+    def _build_flat_states(self) -> Dict[torch.dtype, "_FlatState"]:
+        return {dt: _FlatState(buf, self.state_names) for dt, buf in self.space.buffers.items()}
 
     # ------------------------------------------------------------------ grad preprocessing
     def prepare_grads(self, max_norm: float = 0.0, loss_scale: Optional[torch.Tensor] = None) -> None:
@@ -181,10 +186,13 @@ class FusedSGD(FusedOptimizerBase):
         super().__init__(params, defaults)
 
     def _step_range(self, st, group, start, end, dev_scale) -> None:
-        master = st.master[start:end]
-        grad = st.buf.grad[start:end]
-        mom = st.state["momentum_buffer"][start:end]
-        model = self._slice(st.model, start, end)
+        self._update(st.master[start:end], self._slice(st.model, start, end),
+                     st.buf.grad[start:end], {n: v[start:end] for n, v in st.state.items()},
+                     group, dev_scale)
+
+    def _update(self, master, model, grad, states, group, dev_scale) -> None:
+        """One fused SGD pass over matching slices (flat range or ZeRO shard piece)."""
+        mom = states["momentum_buffer"]
         first = self._step == 1
         if master.is_cuda:
             _ext.load().sgd(master, model, grad, mom, group["lr"], group["momentum"],
@@ -219,11 +227,13 @@ class FusedAdam(FusedOptimizerBase):
         super().__init__(params, defaults)
 
     def _step_range(self, st, group, start, end, dev_scale) -> None:
-        master = st.master[start:end]
-        grad = st.buf.grad[start:end]
-        m = st.state["exp_avg"][start:end]
-        v = st.state["exp_avg_sq"][start:end]
-        model = self._slice(st.model, start, end)
+        self._update(st.master[start:end], self._slice(st.model, start, end),
+                     st.buf.grad[start:end], {n: v[start:end] for n, v in st.state.items()},
+                     group, dev_scale)
+
+    def _update(self, master, model, grad, states, group, dev_scale) -> None:
+        """One fused Adam/AdamW pass over matching slices (flat range or ZeRO shard piece)."""
+        m, v = states["exp_avg"], states["exp_avg_sq"]
         b1, b2 = group["betas"]
         if master.is_cuda:
             _ext.load().adam(master, model, grad, m, v, group["lr"], b1, b2, group["eps"],

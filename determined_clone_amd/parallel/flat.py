@@ -10,7 +10,8 @@ views into them:
   (`ops/csrc/optim.hip`), not a loop over ~160 tensors;
 * DDP buckets (`parallel/ddp.py`) are contiguous slices of the gradient buffer, all-reduced in
   place by RCCL with zero packing copies;
-* ZeRO shards (`parallel/zero.py`) are contiguous ranges of the same buffers.
+* ZeRO shards (`parallel/zero.py`) are per-bucket contiguous ranges of the same buffers
+  (``pad_multiple`` pads each buffer to a whole number of world_size x ALIGN units).
 
 Layout: params are grouped by dtype, then by optimizer param-group, and inside a group in REVERSE
 registration order (the order autograd produces gradients), each segment padded to ``ALIGN``
@@ -68,7 +69,8 @@ class FlatBuffer:
 class FlatParamSpace:
     """Flattens ``groups`` (list of param lists, one per optimizer param group)."""
 
-    def __init__(self, groups: Sequence[Sequence[torch.nn.Parameter]], reverse: bool = True) -> None:
+    def __init__(self, groups: Sequence[Sequence[torch.nn.Parameter]], reverse: bool = True,
+                 pad_multiple: int = 1) -> None:
         self.buffers: Dict[torch.dtype, FlatBuffer] = {}
         self.param_index: Dict[int, Tuple[torch.dtype, Segment]] = {}
         index = 0
@@ -101,6 +103,8 @@ class FlatParamSpace:
                     self.param_index[id(p)] = (dtype, seg)
                     off += _round_up(p.numel(), ALIGN)
                 buf.group_ranges[gi] = (start, off)
+            # ZeRO partitions each buffer into world_size * ALIGN-element units: pad the tail.
+            off = _round_up(off, max(1, pad_multiple))
             buf.numel = off
             buf.data = torch.zeros(off, dtype=dtype, device=device)
             buf.grad = torch.zeros(off, dtype=dtype, device=device)

@@ -2,6 +2,10 @@
 shapes). Prints one line per op: ours ms, torch ms, and achieved TFLOP/s or GB/s."""
 import argparse
 import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 import torch.nn.functional as F
