@@ -1,0 +1,236 @@
+"""GPT-2 / GPT-NeoX-style decoder-only transformer built on the MI355X transformer ops.
+
+Stands in for the GPT-NeoX model the reference's DeepSpeedTrial example trains
+(reference: `examples/deepspeed/gpt_neox/gpt2_trial.py`, which builds Megatron/NeoX GPT-2 with
+DeepSpeed; BASELINE config "GPT-2-medium DeepSpeedTrial ZeRO-2").
+
+MI355X layout decisions:
+* pre-LN blocks where each residual add is fused into the NEXT LayerNorm
+  (``ops.transformer.layer_norm(x, residual=delta)`` returns ``(LN(x + delta), x + delta)`` in one
+  HBM pass), so a block costs 2 fused add+LN kernels instead of 2 adds + 2 LNs;
+* the fused QKV projection output [B, S, 3, H, Dh] is consumed by the MFMA flash-attention kernel
+  through strided views (no q/k/v copies, no [S, S] score matrix);
+* MLP up-projection runs without bias in hipBLASLt and the bias + tanh-GELU are one fused kernel;
+* GEMM weights are bf16; LayerNorm affine parameters stay fp32 (they are read by the LN kernels as
+  fp32 and keep their own flat fp32 buffer in the optimizer);
+* position encoding: learned absolute (GPT-2) or rotary on the first ``rotary_pct`` of each head
+  (GPT-NeoX, rotate-half convention, fused RoPE kernel).
+"""
+import math
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from determined_clone_amd.ops import transformer as T
+
+
+@dataclass
+class GPTConfig:
+    vocab_size: int = 50257
+    n_layer: int = 24
+    n_head: int = 16
+    d_model: int = 1024
+    max_seq_len: int = 1024
+    mlp_ratio: int = 4
+    pos_emb: str = "learned"  # "learned" (GPT-2) | "rotary" (GPT-NeoX)
+    rotary_pct: float = 0.25
+    rotary_base: float = 10000.0
+    ln_eps: float = 1e-5
+    tie_embeddings: bool = True
+    dropout: float = 0.0
+    init_std: float = 0.02
+    pad_vocab_multiple: int = 128
+    extra: Dict = field(default_factory=dict)
+
+    @property
+    def head_dim(self) -> int:
+        return self.d_model // self.n_head
+
+    @property
+    def padded_vocab(self) -> int:
+        m = self.pad_vocab_multiple
+        return (self.vocab_size + m - 1) // m * m
+
+
+PRESETS = {
+    "gpt2-small": dict(n_layer=12, n_head=12, d_model=768),
+    "gpt2-medium": dict(n_layer=24, n_head=16, d_model=1024),
+    "gpt2-large": dict(n_layer=36, n_head=20, d_model=1280),
+    "gpt2-xl": dict(n_layer=48, n_head=25, d_model=1600),
+    "neox-125m": dict(n_layer=12, n_head=12, d_model=768, pos_emb="rotary"),
+    "neox-350m": dict(n_layer=24, n_head=16, d_model=1024, pos_emb="rotary"),
+    "tiny": dict(n_layer=2, n_head=2, d_model=128, vocab_size=512, max_seq_len=128),
+}
+
+
+def config_for(name: str, **overrides) -> GPTConfig:
+    kw = dict(PRESETS[name])
+    kw.update(overrides)
+    return GPTConfig(**kw)
+
+
+class FusedLayerNorm(nn.Module):
+    """LayerNorm whose forward optionally fuses the preceding residual add."""
+
+    keep_fp32 = True  # engines keep these parameters fp32 when casting the model to bf16
+
+    def __init__(self, dim: int, eps: float = 1e-5) -> None:
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(dim))
+        self.bias = nn.Parameter(torch.zeros(dim))
+        self.eps = eps
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None):
+        return T.layer_norm(x, self.weight, self.bias, self.eps, residual=residual)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: GPTConfig) -> None:
+        super().__init__()
+        self.cfg = cfg
+        E = cfg.d_model
+        self.qkv = nn.Linear(E, 3 * E)
+        self.proj = nn.Linear(E, E)
+        self.rot = 0
+        if cfg.pos_emb == "rotary":
+            rot = int(cfg.head_dim * cfg.rotary_pct)
+            self.rot = rot - rot % 2
+        if cfg.head_dim not in (64, 128):
+            raise ValueError("head_dim must be 64 or 128 for the MFMA attention kernel")
+
+    def forward(self, x: torch.Tensor, rope_cache=None) -> torch.Tensor:
+        B, S, E = x.shape
+        H, D = self.cfg.n_head, self.cfg.head_dim
+        qkv = self.qkv(x).view(B, S, 3, H, D)
+        q, k, v = qkv.unbind(2)
+        if self.rot:
+            cos, sin = rope_cache
+            q = T.rope(q, cos, sin, self.rot)
+            k = T.rope(k, cos, sin, self.rot)
+        o = T.flash_attention(q, k, v, causal=True)
+        if self.cfg.dropout and self.training:
+            o = F.dropout(o, self.cfg.dropout)
+        return self.proj(o.reshape(B, S, E))
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: GPTConfig) -> None:
+        super().__init__()
+        E = cfg.d_model
+        self.fc = nn.Linear(E, cfg.mlp_ratio * E)
+        self.proj = nn.Linear(cfg.mlp_ratio * E, E)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h = T.bias_gelu(F.linear(x, self.fc.weight), self.fc.bias)
+        return self.proj(h)
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: GPTConfig) -> None:
+        super().__init__()
+        self.ln1 = FusedLayerNorm(cfg.d_model, cfg.ln_eps)
+        self.attn = Attention(cfg)
+        self.ln2 = FusedLayerNorm(cfg.d_model, cfg.ln_eps)
+        self.mlp = MLP(cfg)
+        self.dropout = cfg.dropout
+
+    def forward(self, resid: torch.Tensor, delta: Optional[torch.Tensor], rope_cache=None):
+        """Returns the new (residual stream, pending delta); the delta is added by the next
+        fused LayerNorm."""
+        if delta is None:
+            h = self.ln1(resid)
+        else:
+            h, resid = self.ln1(resid, residual=delta)
+        a = self.attn(h, rope_cache)
+        h, resid = self.ln2(resid, residual=a)
+        m = self.mlp(h)
+        if self.dropout and self.training:
+            m = F.dropout(m, self.dropout)
+        return resid, m
+
+
+class GPT(nn.Module):
+    def __init__(self, cfg: GPTConfig) -> None:
+        super().__init__()
+        self.cfg = cfg
+        V, E = cfg.padded_vocab, cfg.d_model
+        self.wte = nn.Embedding(V, E)
+        self.wpe = nn.Embedding(cfg.max_seq_len, E) if cfg.pos_emb == "learned" else None
+        self.blocks = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
+        self.ln_f = FusedLayerNorm(E, cfg.ln_eps)
+        self.lm_head = None if cfg.tie_embeddings else nn.Linear(E, V, bias=False)
+        self._rope = None
+        if cfg.pos_emb == "rotary":
+            rot = self.blocks[0].attn.rot
+            cos, sin = T.rope_tables(cfg.max_seq_len, rot, cfg.rotary_base)
+            self.register_buffer("rope_cos", cos, persistent=False)
+            self.register_buffer("rope_sin", sin, persistent=False)
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        std = self.cfg.init_std
+        proj_std = std / math.sqrt(2 * self.cfg.n_layer)
+        for name, p in self.named_parameters():
+            if p.dim() < 2:
+                if name.endswith("weight"):  # LayerNorm gains
+                    nn.init.ones_(p)
+                else:
+                    nn.init.zeros_(p)
+            elif name.endswith("proj.weight"):
+                nn.init.normal_(p, 0.0, proj_std)
+            else:
+                nn.init.normal_(p, 0.0, std)
+
+    def num_params(self, non_embedding: bool = True) -> int:
+        n = sum(p.numel() for p in self.parameters())
+        if non_embedding:
+            n -= self.wte.weight.numel()
+            if self.wpe is not None:
+                n -= self.wpe.weight.numel()
+        return n
+
+    def flops_per_token(self, seq_len: Optional[int] = None) -> float:
+        """Training FLOPs per token (fwd + bwd = 3x fwd), incl. causal attention (half of S^2)."""
+        cfg = self.cfg
+        S = seq_len or cfg.max_seq_len
+        N = self.num_params(non_embedding=True)
+        dense = 6 * N + 6 * cfg.d_model * cfg.padded_vocab
+        attn = 6 * cfg.n_layer * cfg.d_model * S  # 12*L*E*S/2 for the causal half
+        return float(dense + attn)
+
+    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None):
+        B, S = idx.shape
+        x = self.wte(idx)
+        if self.wpe is not None:
+            x = x + self.wpe.weight[:S].unsqueeze(0)
+        rope = (self.rope_cos, self.rope_sin) if self.cfg.pos_emb == "rotary" else None
+        resid, delta = x, None
+        for blk in self.blocks:
+            resid, delta = blk(resid, delta, rope)
+        h, _ = self.ln_f(resid, residual=delta)
+        w = self.wte.weight if self.lm_head is None else self.lm_head.weight
+        logits = F.linear(h, w)
+        if targets is None:
+            return logits
+        loss = F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.reshape(-1),
+                               ignore_index=-100)
+        return logits, loss
+
+
+def cast_for_mi355x(model: nn.Module, dtype: torch.dtype = torch.bfloat16) -> nn.Module:
+    """GEMM / embedding weights -> ``dtype``; modules marked ``keep_fp32`` (LayerNorm, BatchNorm)
+    keep fp32 parameters (the fused kernels read them as fp32)."""
+    for m in model.modules():
+        keep = getattr(m, "keep_fp32", False) or isinstance(m, (nn.LayerNorm, nn.GroupNorm,
+                                                                 nn.modules.batchnorm._BatchNorm))
+        for name, p in list(m.named_parameters(recurse=False)):
+            if p.is_floating_point() and not keep:
+                p.data = p.data.to(dtype)
+    return model
+
+
+def gpt2(name: str = "gpt2-medium", **overrides) -> GPT:
+    return GPT(config_for(name, **overrides))

@@ -128,8 +128,8 @@ class _PyTorchTrialController:
                  checkpoint_policy: str, step_zero_validation: bool,
                  max_length: Optional[TrainUnit], global_batch_size: Optional[int],
                  profiler: Any = None) -> None:
-        if not isinstance(trial_inst, PyTorchTrial):
-            raise TypeError("PyTorchTrialController requires a PyTorchTrial.")
+        if not isinstance(trial_inst, self._trial_base()):
+            raise TypeError(f"{type(self).__name__} requires a {self._trial_base().__name__}.")
         self.trial = trial_inst
         self.context = context
         self.core_context = context._core
@@ -164,6 +164,17 @@ class _PyTorchTrialController:
         if self.searcher_unit == core.Unit.RECORDS and self.global_batch_size is None:
             raise ValueError("global_batch_size required for searcher unit RECORDS.")
         self.callbacks: Dict[str, PyTorchCallback] = self.trial.build_callbacks()
+        self._check_trial()
+        self.last_step_time_s: float = 0.0
+        self.samples_per_second: List[float] = []
+
+    def _trial_base(self) -> type:
+        return PyTorchTrial
+
+    # Checkpoints written by every rank into one storage id (ZeRO shards); chief-only otherwise.
+    _sharded_checkpoint = False
+
+    def _check_trial(self) -> None:
         if len(self.context.models) == 0:
             raise errors.InvalidExperimentException(
                 "Must have at least one model. This might be caused by not wrapping your model "
@@ -175,8 +186,6 @@ class _PyTorchTrialController:
         if self._evaluate_batch_defined() == self._evaluate_full_dataset_defined():
             raise errors.InvalidExperimentException(
                 "Please define exactly one of: `evaluate_batch()` or `evaluate_full_dataset()`.")
-        self.last_step_time_s: float = 0.0
-        self.samples_per_second: List[float] = []
 
     # ------------------------------------------------------------------ helpers
     def _evaluate_batch_defined(self) -> bool:
@@ -453,42 +462,7 @@ class _PyTorchTrialController:
         t0 = time.time()
         for cb in self.callbacks.values():
             cb.on_validation_start()
-        metrics: Dict[str, Any] = {}
-        if self._evaluate_batch_defined():
-            keys = None
-            batch_metrics: List[Dict[str, Any]] = []
-            if len(self.validation_loader) == 0:
-                raise RuntimeError("validation_loader is empty.")
-            for cb in self.callbacks.values():
-                cb.on_validation_epoch_start()
-            idx = -1
-            for idx, batch in enumerate(iter(self.validation_loader)):
-                if self.context.experimental._auto_to_device:
-                    batch = self.context.to_device(batch)
-                if util.has_param(self.trial.evaluate_batch, "batch_idx", 2):
-                    vm = self.trial.evaluate_batch(batch=batch, batch_idx=idx)
-                else:
-                    vm = self.trial.evaluate_batch(batch=batch)
-                if not isinstance(vm, dict):
-                    raise TypeError(f"evaluate_batch() must return a dict, got {type(vm).__name__}")
-                if keys is None:
-                    keys = vm.keys()
-                elif keys != vm.keys():
-                    raise ValueError(f"Validation metric names must match across all batches: "
-                                     f"{keys} != {vm.keys()}")
-                batch_metrics.append({k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in vm.items()})
-                if self.test_mode:
-                    break
-            for cb in self.callbacks.values():
-                cb.on_validation_epoch_end(batch_metrics)
-            metrics = _reducer.reduce_validation_metrics(
-                self.context.distributed, batch_metrics, keys,
-                _reducer._prepare_metrics_reducers(self.trial.evaluation_reducer(), keys=keys or []))
-        else:
-            if self.is_chief:
-                metrics = self.trial.evaluate_full_dataset(data_loader=self.validation_loader)
-                if not isinstance(metrics, dict):
-                    raise TypeError(f"evaluate_full_dataset() must return a dict, got {type(metrics).__name__}")
+        metrics = self._compute_validation_metrics()
         metrics.update(self.context.reduce_metrics(for_training=False))
         metrics = {k: util.to_python(v) for k, v in metrics.items()}
         if self.context.distributed.size > 1:
@@ -527,6 +501,45 @@ class _PyTorchTrialController:
             self._checkpoint(already_exiting=False)
         return metrics
 
+    def _compute_validation_metrics(self) -> Dict[str, Any]:
+        metrics: Dict[str, Any] = {}
+        if self._evaluate_batch_defined():
+            keys = None
+            batch_metrics: List[Dict[str, Any]] = []
+            if len(self.validation_loader) == 0:
+                raise RuntimeError("validation_loader is empty.")
+            for cb in self.callbacks.values():
+                cb.on_validation_epoch_start()
+            idx = -1
+            for idx, batch in enumerate(iter(self.validation_loader)):
+                if self.context.experimental._auto_to_device:
+                    batch = self.context.to_device(batch)
+                if util.has_param(self.trial.evaluate_batch, "batch_idx", 2):
+                    vm = self.trial.evaluate_batch(batch=batch, batch_idx=idx)
+                else:
+                    vm = self.trial.evaluate_batch(batch=batch)
+                if not isinstance(vm, dict):
+                    raise TypeError(f"evaluate_batch() must return a dict, got {type(vm).__name__}")
+                if keys is None:
+                    keys = vm.keys()
+                elif keys != vm.keys():
+                    raise ValueError(f"Validation metric names must match across all batches: "
+                                     f"{keys} != {vm.keys()}")
+                batch_metrics.append({k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in vm.items()})
+                if self.test_mode:
+                    break
+            for cb in self.callbacks.values():
+                cb.on_validation_epoch_end(batch_metrics)
+            metrics = _reducer.reduce_validation_metrics(
+                self.context.distributed, batch_metrics, keys,
+                _reducer._prepare_metrics_reducers(self.trial.evaluation_reducer(), keys=keys or []))
+        else:
+            if self.is_chief:
+                metrics = self.trial.evaluate_full_dataset(data_loader=self.validation_loader)
+                if not isinstance(metrics, dict):
+                    raise TypeError(f"evaluate_full_dataset() must return a dict, got {type(metrics).__name__}")
+        return metrics
+
     # ------------------------------------------------------------------ checkpoint
     def _checkpoint(self, already_exiting: bool) -> None:
         if self.is_chief:
@@ -535,12 +548,16 @@ class _PyTorchTrialController:
         self.context._sync_buffers()
         try:
             uuid = ""
-            if self.is_chief:
-                from determined_clone_amd import __version__
+            from determined_clone_amd import __version__
 
-                md = {"determined_version": __version__,
-                      "steps_completed": self.state.batches_trained,
-                      "framework": f"torch-{torch.__version__}", "format": "pickle"}
+            md = {"determined_version": __version__,
+                  "steps_completed": self.state.batches_trained,
+                  "framework": f"torch-{torch.__version__}", "format": "pickle"}
+            if self._sharded_checkpoint:
+                with self.core_context.checkpoint.store_path(md if self.is_chief else {}, shard=True) as (path, storage_id):
+                    self._save(path)
+                    uuid = storage_id
+            elif self.is_chief:
                 with self.core_context.checkpoint.store_path(md) as (path, storage_id):
                     self._save(path)
                     uuid = storage_id

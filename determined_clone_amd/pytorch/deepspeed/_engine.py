@@ -1,0 +1,540 @@
+"""DeepSpeed-compatible training engine on the MI355X stack (no DeepSpeed dependency).
+
+The reference's DeepSpeedTrial drives a ``deepspeed.DeepSpeedEngine`` built by
+``deepspeed.initialize`` from a DeepSpeed JSON config (reference:
+`harness/determined/pytorch/deepspeed/_deepspeed_context.py:178` wrap_model_engine,
+`_deepspeed_trial.py:366` _train_for_step, `examples/deepspeed/gpt_neox`). This module provides the
+same engine surface -- ``initialize()``, ``engine(batch)``, ``engine.backward(loss)``,
+``engine.step()``, micro-batch / gradient-accumulation bookkeeping, ``save_checkpoint`` /
+``load_checkpoint`` -- implemented with:
+
+* ZeRO stage 1/2: :mod:`determined_clone_amd.parallel.zero` (bucketed in-place RCCL
+  reduce-scatter / all-gather on flat buffers, fused HIP Adam/SGD on the owned shard);
+* stage 0: flat fused optimizer + bucketed all-reduce overlapped with backward
+  (:mod:`determined_clone_amd.parallel.ddp`);
+* bf16: GEMM weights cast to bf16, norm parameters kept fp32, fp32 master weights in the
+  optimizer; fp16: the device-resident dynamic loss scaler (no host sync per step);
+* gradient clipping: device-side global norm folded into the optimizer kernel.
+
+Supported config keys: train_batch_size, train_micro_batch_size_per_gpu,
+gradient_accumulation_steps, optimizer {type: Adam|AdamW|SGD|Lamb, params}, scheduler
+{type: WarmupLR|WarmupDecayLR|WarmupCosineLR, params}, gradient_clipping, bf16.enabled,
+fp16 {enabled, loss_scale, initial_scale_power, loss_scale_window, min_loss_scale},
+zero_optimization {stage (0-2), reduce_bucket_size, allgather_bucket_size, overlap_comm},
+steps_per_print. Unknown keys are accepted and ignored (with a debug log), like DeepSpeed's
+permissive parsing of e.g. ``wall_clock_breakdown``.
+"""
+import json
+import logging
+import math
+import os
+import pathlib
+from typing import Any, Dict, Iterable, List, Optional, Tuple, Union
+
+import torch
+import torch.distributed as dist
+
+from determined_clone_amd.ops import optim as fopt
+from determined_clone_amd.parallel import ddp, zero
+
+logger = logging.getLogger("determined_clone_amd.pytorch.deepspeed")
+
+
+# ---------------------------------------------------------------------------------- config
+class DeepSpeedConfig:
+    def __init__(self, config: Union[str, Dict[str, Any]], world_size: int) -> None:
+        if isinstance(config, (str, os.PathLike)):
+            with open(config) as f:
+                config = json.load(f)
+        self.raw: Dict[str, Any] = dict(config)
+        c = self.raw
+        tbs = c.get("train_batch_size")
+        mbs = c.get("train_micro_batch_size_per_gpu")
+        gas = c.get("gradient_accumulation_steps")
+        W = world_size
+        if tbs is not None and mbs is not None and gas is None:
+            gas = tbs // (mbs * W)
+        elif tbs is not None and gas is not None and mbs is None:
+            mbs = tbs // (gas * W)
+        elif tbs is None and mbs is not None:
+            gas = gas or 1
+            tbs = mbs * gas * W
+        elif tbs is not None and mbs is None and gas is None:
+            gas = 1
+            mbs = tbs // W
+        if tbs is None or mbs is None or gas is None:
+            raise ValueError("DeepSpeed config needs train_batch_size or "
+                             "train_micro_batch_size_per_gpu")
+        if tbs != mbs * gas * W or mbs <= 0 or gas <= 0:
+            raise ValueError(f"Check batch related parameters. train_batch_size ({tbs}) is not equal "
+                             f"to micro_batch_per_gpu ({mbs}) * gradient_acc_step ({gas}) * "
+                             f"world_size ({W})")
+        self.train_batch_size = int(tbs)
+        self.micro_batch = int(mbs)
+        self.grad_accum = int(gas)
+        self.optimizer = c.get("optimizer")
+        self.scheduler = c.get("scheduler")
+        self.gradient_clipping = float(c.get("gradient_clipping", 0.0) or 0.0)
+        fp16 = c.get("fp16") or {}
+        bf16 = c.get("bf16") or c.get("bfloat16") or {}
+        self.fp16 = bool(fp16.get("enabled", False))
+        self.bf16 = bool(bf16.get("enabled", False))
+        if self.fp16 and self.bf16:
+            raise ValueError("fp16 and bf16 cannot both be enabled")
+        self.loss_scale = float(fp16.get("loss_scale", 0.0) or 0.0)
+        self.initial_scale_power = int(fp16.get("initial_scale_power", 16))
+        self.loss_scale_window = int(fp16.get("loss_scale_window", 1000))
+        self.min_loss_scale = float(fp16.get("min_loss_scale", 1.0))
+        z = c.get("zero_optimization") or {}
+        if isinstance(z, bool):
+            z = {"stage": 1 if z else 0}
+        self.zero_stage = int(z.get("stage", 0))
+        if self.zero_stage > 2:
+            raise ValueError("ZeRO stage 3 (parameter partitioning) is not implemented; use stage "
+                             "<= 2 (a 288 GB MI355X holds GPT-2 XL-class parameters unpartitioned)")
+        self.reduce_bucket_size = int(z.get("reduce_bucket_size", 32 * 2 ** 20))  # elements
+        self.allgather_bucket_size = int(z.get("allgather_bucket_size", 32 * 2 ** 20))
+        self.overlap_comm = bool(z.get("overlap_comm", True))
+        self.steps_per_print = int(c.get("steps_per_print", 10))
+
+
+# ---------------------------------------------------------------------------------- schedulers
+class _DSScheduler:
+    def __init__(self, optimizer: torch.optim.Optimizer, last_batch_iteration: int = -1) -> None:
+        self.optimizer = optimizer
+        self.last_batch_iteration = last_batch_iteration
+        self.step(last_batch_iteration + 1)
+
+    def get_lr(self) -> List[float]:
+        raise NotImplementedError
+
+    def get_last_lr(self) -> List[float]:
+        return self._last_lr
+
+    def step(self, last_batch_iteration: Optional[int] = None) -> None:
+        if last_batch_iteration is None:
+            last_batch_iteration = self.last_batch_iteration + 1
+        self.last_batch_iteration = last_batch_iteration
+        lrs = self.get_lr()
+        for g, lr in zip(self.optimizer.param_groups, lrs):
+            g["lr"] = lr
+        self._last_lr = lrs
+
+    def state_dict(self) -> Dict[str, Any]:
+        return {"last_batch_iteration": self.last_batch_iteration}
+
+    def load_state_dict(self, sd: Dict[str, Any]) -> None:
+        self.last_batch_iteration = sd["last_batch_iteration"]
+        self.step(self.last_batch_iteration)
+
+
+class WarmupLR(_DSScheduler):
+    def __init__(self, optimizer, warmup_min_lr: float = 0.0, warmup_max_lr: float = 0.001,
+                 warmup_num_steps: int = 1000, warmup_type: str = "log",
+                 last_batch_iteration: int = -1) -> None:
+        n = len(optimizer.param_groups)
+        self.min_lrs = [warmup_min_lr] * n
+        self.max_lrs = [warmup_max_lr] * n
+        self.warmup_num_steps = max(2, warmup_num_steps)
+        self.warmup_type = warmup_type
+        self.inverse_log_warm_up = 1.0 / math.log(self.warmup_num_steps)
+        super().__init__(optimizer, last_batch_iteration)
+
+    def _gamma(self) -> float:
+        it = self.last_batch_iteration
+        if it < self.warmup_num_steps:
+            if self.warmup_type == "log":
+                return self.inverse_log_warm_up * math.log(it + 1)
+            return it / self.warmup_num_steps
+        return 1.0
+
+    def get_lr(self) -> List[float]:
+        if self.last_batch_iteration < 0:
+            return list(self.min_lrs)
+        g = self._gamma()
+        return [lo + (hi - lo) * g for lo, hi in zip(self.min_lrs, self.max_lrs)]
+
+
+class WarmupDecayLR(WarmupLR):
+    def __init__(self, optimizer, total_num_steps: int, warmup_min_lr: float = 0.0,
+                 warmup_max_lr: float = 0.001, warmup_num_steps: int = 1000,
+                 warmup_type: str = "log", last_batch_iteration: int = -1) -> None:
+        self.total_num_steps = total_num_steps
+        super().__init__(optimizer, warmup_min_lr, warmup_max_lr, warmup_num_steps, warmup_type,
+                         last_batch_iteration)
+
+    def _gamma(self) -> float:
+        it = self.last_batch_iteration
+        if it < self.warmup_num_steps:
+            return super()._gamma()
+        return max(0.0, float(self.total_num_steps - it) /
+                   float(max(1.0, self.total_num_steps - self.warmup_num_steps)))
+
+
+class WarmupCosineLR(_DSScheduler):
+    def __init__(self, optimizer, total_num_steps: int, warmup_min_ratio: float = 0.0,
+                 warmup_num_steps: int = 1000, cos_min_ratio: float = 0.0001,
+                 warmup_type: str = "log", last_batch_iteration: int = -1) -> None:
+        self.total_num_steps = total_num_steps
+        self.warmup_min_ratio = warmup_min_ratio
+        self.warmup_num_steps = max(2, warmup_num_steps)
+        self.cos_min_ratio = cos_min_ratio
+        self.warmup_type = warmup_type
+        self.org_lrs = [g["lr"] for g in optimizer.param_groups]
+        super().__init__(optimizer, last_batch_iteration)
+
+    def get_lr(self) -> List[float]:
+        it = max(self.last_batch_iteration, 0)
+        if it < self.warmup_num_steps:
+            if self.warmup_type == "log":
+                r = math.log(it + 1) / math.log(self.warmup_num_steps)
+            else:
+                r = it / self.warmup_num_steps
+            ratio = self.warmup_min_ratio + (1 - self.warmup_min_ratio) * r
+        else:
+            p = (it - self.warmup_num_steps) / max(1, self.total_num_steps - self.warmup_num_steps)
+            ratio = self.cos_min_ratio + (1 - self.cos_min_ratio) * 0.5 * (1 + math.cos(math.pi * min(p, 1.0)))
+        return [lr * ratio for lr in self.org_lrs]
+
+
+_SCHEDULERS = {"WarmupLR": WarmupLR, "WarmupDecayLR": WarmupDecayLR, "WarmupCosineLR": WarmupCosineLR}
+
+
+# ---------------------------------------------------------------------------------- engine
+def _keep_fp32(m: torch.nn.Module) -> bool:
+    return bool(getattr(m, "keep_fp32", False)) or isinstance(
+        m, (torch.nn.LayerNorm, torch.nn.GroupNorm, torch.nn.modules.batchnorm._BatchNorm))
+
+
+def _cast_module(model: torch.nn.Module, dtype: torch.dtype) -> None:
+    for m in model.modules():
+        if _keep_fp32(m):
+            continue
+        for p in m.parameters(recurse=False):
+            if p.is_floating_point():
+                p.data = p.data.to(dtype)
+
+
+class DeepSpeedEngine(torch.nn.Module):
+    def __init__(self, model: torch.nn.Module, config: Union[str, Dict[str, Any]],
+                 optimizer: Optional[torch.optim.Optimizer] = None,
+                 model_parameters: Optional[Iterable[Any]] = None,
+                 lr_scheduler: Any = None, group: Any = None,
+                 device: Optional[torch.device] = None) -> None:
+        super().__init__()
+        self.group = group
+        self.world_size = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.global_rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.config = DeepSpeedConfig(config, self.world_size)
+        cfg = self.config
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+                else torch.device("cpu")
+        self.device = device
+        self.module = model
+        if cfg.bf16:
+            _cast_module(model, torch.bfloat16)
+        elif cfg.fp16:
+            _cast_module(model, torch.float16)
+        model.to(device)
+        if model_parameters is not None and not isinstance(model_parameters, list):
+            model_parameters = list(model_parameters)
+        if self.world_size > 1:
+            ddp.broadcast_module_state(model, group)
+        self.optimizer = self._build_optimizer(optimizer, model_parameters)
+        self.basic_optimizer = self.optimizer
+        self.lr_scheduler = self._build_scheduler(lr_scheduler)
+        self.scaler: Optional[fopt.DeviceGradScaler] = None
+        self._static_scale: Optional[torch.Tensor] = None
+        if cfg.fp16:
+            if cfg.loss_scale > 0:
+                self._static_scale = torch.tensor([cfg.loss_scale], device=device)
+            else:
+                self.scaler = fopt.DeviceGradScaler(init_scale=2.0 ** cfg.initial_scale_power,
+                                                    growth_interval=cfg.loss_scale_window,
+                                                    device=device)
+        self.micro_steps = 0
+        self.global_steps = 0
+        self.global_samples = 0
+        self.skipped_steps = 0
+        self._last_grad_norm: Optional[torch.Tensor] = None
+
+    # ------------------------------------------------------------------ construction
+    def _param_groups(self, model_parameters: Optional[List[Any]]) -> List[Dict[str, Any]]:
+        params = model_parameters if model_parameters is not None else \
+            [p for p in self.module.parameters() if p.requires_grad]
+        if params and isinstance(params[0], dict):
+            return [dict(g, params=list(g["params"])) for g in params]
+        return [{"params": list(params)}]
+
+    def _build_optimizer(self, optimizer: Optional[torch.optim.Optimizer],
+                         model_parameters: Optional[List[Any]]) -> fopt.FusedOptimizerBase:
+        cfg = self.config
+        stage = cfg.zero_stage
+        if optimizer is not None:
+            groups = [dict(g) for g in optimizer.param_groups]
+            if isinstance(optimizer, torch.optim.AdamW):
+                kind, kw = "adamw", {}
+            elif isinstance(optimizer, torch.optim.Adam):
+                kind, kw = "adam", {}
+            elif isinstance(optimizer, torch.optim.SGD):
+                kind, kw = "sgd", {}
+            elif isinstance(optimizer, fopt.FusedOptimizerBase) and stage == 0:
+                opt = optimizer
+                self._setup_dp(opt)
+                return opt
+            else:
+                raise ValueError(f"unsupported client optimizer {type(optimizer).__name__}")
+            base = {k: v for k, v in groups[0].items() if k != "params"}
+            defaults = _filter_defaults(kind, base)
+        else:
+            if not cfg.optimizer:
+                raise ValueError("no optimizer: pass one to initialize() or set config['optimizer']")
+            t = cfg.optimizer["type"].lower()
+            p = dict(cfg.optimizer.get("params") or {})
+            if t in ("adam", "fusedadam"):
+                # DeepSpeed's Adam defaults to decoupled weight decay (adam_w_mode=True)
+                kind = "adamw" if p.pop("adam_w_mode", True) else "adam"
+                p.pop("torch_adam", None)
+            elif t == "adamw":
+                kind = "adamw"
+            elif t == "sgd":
+                kind = "sgd"
+            elif t in ("lamb", "fusedlamb"):
+                kind = "lamb"
+            else:
+                raise ValueError(f"unsupported DeepSpeed optimizer type {cfg.optimizer['type']}")
+            defaults = _filter_defaults(kind, p)
+            groups = self._param_groups(model_parameters)
+        if stage >= 1:
+            cls = zero.zero_optimizer_for(kind)
+            esz = 2 if (cfg.bf16 or cfg.fp16) else 4
+            opt = cls(groups, stage=stage, group=self.group, overlap_comm=cfg.overlap_comm,
+                      bucket_mb=max(1.0, cfg.reduce_bucket_size * esz / 2 ** 20), **defaults)
+            return opt
+        cls = {"adam": fopt.FusedAdam, "adamw": fopt.FusedAdamW, "sgd": fopt.FusedSGD,
+               "lamb": fopt.FusedLAMB}[kind]
+        opt = cls(groups, **defaults)
+        self._setup_dp(opt)
+        return opt
+
+    def _setup_dp(self, opt: fopt.FusedOptimizerBase) -> None:
+        self._sync: Optional[ddp.GradientSync] = None
+        if self.world_size > 1:
+            self._sync = ddp.GradientSync(opt.space, group=self.group)
+            self._sync.fold_average = True
+            opt.grad_multiplier = 1.0 / self.world_size
+
+    def _build_scheduler(self, lr_scheduler: Any) -> Any:
+        if lr_scheduler is not None:
+            if callable(lr_scheduler) and not hasattr(lr_scheduler, "step"):
+                return lr_scheduler(self.optimizer)
+            return lr_scheduler
+        s = self.config.scheduler
+        if not s:
+            return None
+        cls = _SCHEDULERS.get(s["type"])
+        if cls is None:
+            raise ValueError(f"unsupported DeepSpeed scheduler {s['type']}")
+        return cls(self.optimizer, **(s.get("params") or {}))
+
+    # ------------------------------------------------------------------ batch-size info
+    def train_batch_size(self) -> int:
+        return self.config.train_batch_size
+
+    def train_micro_batch_size_per_gpu(self) -> int:
+        return self.config.micro_batch
+
+    def gradient_accumulation_steps(self) -> int:
+        return self.config.grad_accum
+
+    def is_gradient_accumulation_boundary(self) -> bool:
+        return (self.micro_steps + 1) % self.config.grad_accum == 0
+
+    @property
+    def zero_optimization_stage(self) -> int:
+        return self.config.zero_stage
+
+    def get_lr(self) -> List[float]:
+        return [g["lr"] for g in self.optimizer.param_groups]
+
+    def get_global_grad_norm(self) -> Optional[float]:
+        return None if self._last_grad_norm is None else float(self._last_grad_norm)
+
+    @property
+    def cur_scale(self) -> float:
+        if self.scaler is not None:
+            return self.scaler.get_scale()
+        return float(self._static_scale) if self._static_scale is not None else 1.0
+
+    # ------------------------------------------------------------------ training
+    def forward(self, *args: Any, **kwargs: Any) -> Any:
+        return self.module(*args, **kwargs)
+
+    def _set_sync(self, enabled: bool) -> None:
+        if isinstance(self.optimizer, zero.ZeroShardMixin):
+            self.optimizer.sync_enabled = enabled
+        elif getattr(self, "_sync", None) is not None:
+            self._sync.enabled = enabled
+
+    def backward(self, loss: torch.Tensor, retain_graph: bool = False) -> torch.Tensor:
+        self._set_sync(self.is_gradient_accumulation_boundary())
+        scaled = loss
+        if self.config.grad_accum > 1:
+            scaled = scaled / self.config.grad_accum
+        if self.scaler is not None:
+            scaled = self.scaler.scale(scaled)
+        elif self._static_scale is not None:
+            scaled = scaled * self._static_scale.to(scaled.dtype)
+        scaled.backward(retain_graph=retain_graph)
+        return loss
+
+    def step(self, lr_kwargs: Optional[Dict[str, Any]] = None) -> None:
+        if self.is_gradient_accumulation_boundary():
+            self._take_model_step(lr_kwargs)
+        self.micro_steps += 1
+        self.global_samples += self.config.micro_batch * self.world_size
+
+    def _take_model_step(self, lr_kwargs: Optional[Dict[str, Any]]) -> None:
+        opt = self.optimizer
+        if isinstance(opt, zero.ZeroShardMixin):
+            opt.finish_grad_sync()
+        elif getattr(self, "_sync", None) is not None:
+            self._sync.finish()
+        clip = self.config.gradient_clipping
+        ls = None
+        if self.scaler is not None:
+            ls = self.scaler.state[0:1]
+        elif self._static_scale is not None:
+            ls = self._static_scale
+        if clip > 0 or ls is not None:
+            opt.prepare_grads(max_norm=clip, loss_scale=ls)
+            self._last_grad_norm = opt.last_grad_norm
+        if self.scaler is not None:
+            self.scaler._last_dev_scale = opt._dev_scale
+        opt.step()
+        if self.scaler is not None:
+            self.scaler.update()
+        if self.lr_scheduler is not None:
+            self.lr_scheduler.step(**(lr_kwargs or {}))
+        opt.zero_grad()
+        self.global_steps += 1
+
+    def zero_grad(self) -> None:
+        self.optimizer.zero_grad()
+
+    # ------------------------------------------------------------------ checkpoint
+    def _ckpt_dir(self, save_dir: Union[str, pathlib.Path], tag: Optional[str]) -> pathlib.Path:
+        return pathlib.Path(save_dir) / str(tag)
+
+    def save_checkpoint(self, save_dir: Union[str, pathlib.Path], tag: Optional[str] = None,
+                        client_state: Optional[Dict[str, Any]] = None,
+                        save_latest: bool = True) -> bool:
+        """Layout (DeepSpeed-like): ``<dir>/<tag>/mp_rank_00_model_states.pt`` (rank 0: module,
+        scheduler, counters, client state, stage-0 optimizer) and
+        ``<dir>/<tag>/zero_pp_rank_<r>_mp_rank_00_optim_states.pt`` (every rank's ZeRO shard)."""
+        tag = tag or f"global_step{self.global_steps}"
+        d = self._ckpt_dir(save_dir, tag)
+        d.mkdir(parents=True, exist_ok=True)
+        if self.global_rank == 0:
+            state = {
+                "module": self.module.state_dict(),
+                "lr_scheduler": self.lr_scheduler.state_dict() if self.lr_scheduler is not None else None,
+                "global_steps": self.global_steps, "global_samples": self.global_samples,
+                "micro_steps": self.micro_steps, "skipped_steps": self.skipped_steps,
+                "dp_world_size": self.world_size, "zero_stage": self.config.zero_stage,
+                "scaler": self.scaler.state_dict() if self.scaler is not None else None,
+                "client_state": client_state or {},
+            }
+            if self.config.zero_stage == 0:
+                state["optimizer"] = self.optimizer.state_dict()
+            torch.save(state, d / "mp_rank_00_model_states.pt")
+            if save_latest:
+                (pathlib.Path(save_dir) / "latest").write_text(str(tag))
+        if self.config.zero_stage >= 1:
+            torch.save({"optimizer_state_dict": self.optimizer.state_dict()},
+                       d / f"zero_pp_rank_{self.global_rank}_mp_rank_00_optim_states.pt")
+        return True
+
+    def load_checkpoint(self, load_dir: Union[str, pathlib.Path], tag: Optional[str] = None,
+                        load_module_strict: bool = True, load_optimizer_states: bool = True,
+                        load_lr_scheduler_states: bool = True
+                        ) -> Tuple[Optional[str], Optional[Dict[str, Any]]]:
+        load_dir = pathlib.Path(load_dir)
+        if tag is None:
+            latest = load_dir / "latest"
+            if not latest.exists():
+                logger.warning(f"no 'latest' file under {load_dir}; nothing loaded")
+                return None, None
+            tag = latest.read_text().strip()
+        d = self._ckpt_dir(load_dir, tag)
+        path = d / "mp_rank_00_model_states.pt"
+        if not path.exists():
+            raise FileNotFoundError(f"DeepSpeed-format checkpoint not found at {path}")
+        state = torch.load(path, map_location="cpu", weights_only=True)
+        self.module.load_state_dict(state["module"], strict=load_module_strict)
+        self.global_steps = int(state.get("global_steps", 0))
+        self.global_samples = int(state.get("global_samples", 0))
+        self.micro_steps = int(state.get("micro_steps", 0))
+        self.skipped_steps = int(state.get("skipped_steps", 0))
+        if load_lr_scheduler_states and self.lr_scheduler is not None and state.get("lr_scheduler"):
+            self.lr_scheduler.load_state_dict(state["lr_scheduler"])
+        if self.scaler is not None and state.get("scaler"):
+            self.scaler.load_state_dict(state["scaler"])
+        if load_optimizer_states:
+            if isinstance(self.optimizer, zero.ZeroShardMixin):
+                saved_world = int(state.get("dp_world_size", self.world_size))
+                own = d / f"zero_pp_rank_{self.global_rank}_mp_rank_00_optim_states.pt"
+                if saved_world == self.world_size and own.exists():
+                    shards = [torch.load(own, map_location="cpu", weights_only=True)["optimizer_state_dict"]]
+                else:
+                    shards = [torch.load(d / f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt",
+                                         map_location="cpu", weights_only=True)["optimizer_state_dict"]
+                              for r in range(saved_world)]
+                self.optimizer.load_shard_state_dicts(shards)
+            elif state.get("optimizer") is not None:
+                self.optimizer.load_state_dict(state["optimizer"])
+                if not any("master_param" in s for s in state["optimizer"]["state"].values()):
+                    self.optimizer.sync_master_from_model()
+            else:
+                self.optimizer.sync_master_from_model()
+        else:
+            self.optimizer.sync_master_from_model()
+        return str(d), state.get("client_state", {})
+
+
+def _filter_defaults(kind: str, p: Dict[str, Any]) -> Dict[str, Any]:
+    allowed = {
+        "adam": {"lr", "betas", "eps", "weight_decay"},
+        "adamw": {"lr", "betas", "eps", "weight_decay"},
+        "sgd": {"lr", "momentum", "dampening", "weight_decay", "nesterov"},
+        "lamb": {"lr", "betas", "eps", "weight_decay"},
+    }[kind]
+    out = {k: v for k, v in p.items() if k in allowed}
+    if "betas" in out:
+        out["betas"] = tuple(out["betas"])
+    dropped = set(p) - allowed - {"params", "amsgrad", "foreach", "maximize", "capturable",
+                                  "differentiable", "fused", "initial_lr", "decoupled_weight_decay"}
+    if dropped:
+        logger.debug(f"ignoring optimizer params {sorted(dropped)}")
+    return out
+
+
+def initialize(args: Any = None, model: Optional[torch.nn.Module] = None,
+               optimizer: Optional[torch.optim.Optimizer] = None,
+               model_parameters: Optional[Iterable[Any]] = None, training_data: Any = None,
+               lr_scheduler: Any = None, mpu: Any = None, dist_init_required: Optional[bool] = None,
+               collate_fn: Any = None, config: Any = None, config_params: Any = None,
+               group: Any = None) -> Tuple[DeepSpeedEngine, Any, Any, Any]:
+    """``deepspeed.initialize`` equivalent: returns ``(engine, optimizer, None, lr_scheduler)``.
+    The config comes from ``config`` / ``config_params`` or ``args.deepspeed_config``."""
+    if model is None:
+        raise ValueError("initialize() requires a model")
+    cfg = config if config is not None else config_params
+    if cfg is None and args is not None:
+        cfg = getattr(args, "deepspeed_config", None) or getattr(args, "deepscale_config", None)
+    if cfg is None:
+        raise ValueError("initialize() requires a DeepSpeed config")
+    engine = DeepSpeedEngine(model, cfg, optimizer=optimizer, model_parameters=model_parameters,
+                             lr_scheduler=lr_scheduler, group=group)
+    return engine, engine.optimizer, None, engine.lr_scheduler
