@@ -168,15 +168,34 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_kernel(
   }
 }
 
-// out[j] = sum_b partial[b][j] for j < ncols (fp32, coalesced across j).
-__global__ __launch_bounds__(256) void column_reduce_kernel(const float* __restrict__ partial,
-                                                            int nparts, int64_t ncols,
-                                                            float* __restrict__ out) {
-  const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j >= ncols) return;
-  float a = 0.f;
-  for (int b = 0; b < nparts; ++b) a += partial[static_cast<int64_t>(b) * ncols + j];
-  out[j] = a;
+// out[j] = sum_b partial[b][j] for j < ncols (fp32). Block = 16 waves x 64 columns: lane -> column
+// (coalesced 256-B rows), wave -> every 16th partial row with 4 independent loads in flight, then an
+// LDS tree over the 16 waves. Deterministic (fixed order).
+constexpr int kColWaves = 16;
+__global__ __launch_bounds__(kColWaves * 64) void column_reduce_kernel(const float* __restrict__ partial,
+                                                                      int nparts, int64_t ncols,
+                                                                      float* __restrict__ out) {
+  __shared__ float red[kColWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (j < ncols) {
+    int b = w;
+    for (; b + 3 * kColWaves < nparts; b += 4 * kColWaves) {
+      a0 += partial[static_cast<int64_t>(b) * ncols + j];
+      a1 += partial[static_cast<int64_t>(b + kColWaves) * ncols + j];
+      a2 += partial[static_cast<int64_t>(b + 2 * kColWaves) * ncols + j];
+      a3 += partial[static_cast<int64_t>(b + 3 * kColWaves) * ncols + j];
+    }
+    for (; b < nparts; b += kColWaves) a0 += partial[static_cast<int64_t>(b) * ncols + j];
+  }
+  red[w][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  for (int s = kColWaves / 2; s > 0; s >>= 1) {
+    if (w < s) red[w][lane] += red[w + s][lane];
+    __syncthreads();
+  }
+  if (w == 0 && j < ncols) out[j] = red[0][lane];
 }
 
 // ------------------------------------------------------------------ bias + GELU(tanh)
@@ -338,8 +357,8 @@ void layernorm_bwd(TDtype dt, const void* dy, const void* x, const float* gamma,
   });
   if (dgamma_dbeta) {
     const int64_t ncols = 2 * static_cast<int64_t>(D);
-    hipLaunchKernelGGL(column_reduce_kernel, dim3((ncols + 255) / 256), dim3(256), 0, st, partial,
-                       blocks, ncols, dgamma_dbeta);
+    hipLaunchKernelGGL(column_reduce_kernel, dim3((ncols + 63) / 64), dim3(kColWaves * 64), 0, st,
+                       partial, blocks, ncols, dgamma_dbeta);
   }
 }
 
@@ -364,8 +383,8 @@ void bias_gelu_bwd(TDtype dt, const void* dy, const void* x, const float* bias, 
                        dbias ? partial : nullptr, rows, N);
   });
   if (dbias)
-    hipLaunchKernelGGL(column_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, st, partial, rb,
-                       static_cast<int64_t>(N), dbias);
+    hipLaunchKernelGGL(column_reduce_kernel, dim3((N + 63) / 64), dim3(kColWaves * 64), 0, st,
+                       partial, rb, static_cast<int64_t>(N), dbias);
 }
 
 void rope(TDtype dt, const void* x, void* y, const float* cosT, const float* sinT, int64_t rows,
