@@ -42,6 +42,44 @@ __device__ __forceinline__ bf16x8 zero8() {
 __device__ __forceinline__ uint16_t to_bf16(float f) { return static_cast<uint16_t>(f2bf_bits(f)); }
 __device__ __forceinline__ float from_bf16(uint16_t h) { return __uint_as_float(static_cast<uint32_t>(h) << 16); }
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q / columns 4p..4p+3 of a 4x16
+// block; lane i receives column i (4 rows) -- a transposed fragment read straight from a row-major
+// LDS tile. Needs all 64 lanes active.
+__device__ __forceinline__ s16x4 tr_read(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(p));
+}
+
+__device__ __forceinline__ bf16x8 cat8(s16x4 a, s16x4 b) {
+  const s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// 8 consecutive accumulator registers [base, base+8) -> bf16 MFMA fragment.
+__device__ __forceinline__ bf16x8 pack8(const f32x16& x, int base) {
+  uint4 u;
+  u.x = pack_bf16x2(x[base + 0], x[base + 1]);
+  u.y = pack_bf16x2(x[base + 2], x[base + 3]);
+  u.z = pack_bf16x2(x[base + 4], x[base + 5]);
+  u.w = pack_bf16x2(x[base + 6], x[base + 7]);
+  return __builtin_bit_cast(bf16x8, u);
+}
+
 struct Strides {
   int64_t b, h, s;  // element strides; d stride is 1
 };
@@ -67,291 +105,379 @@ __device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ src, Str
   }
 }
 
+// Stage ROWS consecutive rows (from r0, zero-filled beyond n_rows) row-major into LDS.
+template <int D, int ROWS>
+__device__ __forceinline__ void stage_rows(const uint16_t* __restrict__ src, Strides st, int r0,
+                                           int n_rows, uint16_t* dst) {
+  constexpr int cpr = D / 8;
+  for (int c = threadIdx.x; c < ROWS * cpr; c += blockDim.x) {
+    const int rr = c / cpr, d0 = (c % cpr) * 8;
+    uint4 val = make_uint4(0, 0, 0, 0);
+    if (r0 + rr < n_rows) val = *reinterpret_cast<const uint4*>(src + static_cast<int64_t>(r0 + rr) * st.s + d0);
+    *reinterpret_cast<uint4*>(dst + rr * (D + kPad) + d0) = val;
+  }
+}
+
 // ------------------------------------------------------------------------------------ forward
+// One workgroup = 4 waves x 32 queries = 128 query rows of one (batch, head). Per 64-key LDS tile,
+// each wave computes S^T = K Q^T as 32x32 tiles with v_mfma_f32_32x32x16_bf16 so that the KEY is in
+// the registers and the QUERY on the lane: the softmax row statistics are lane-local (16 registers
+// + one exchange with lane^32), and P^T -- still in registers -- is directly the B operand of
+// O^T += V^T P^T (no LDS round trip for P). V^T fragments come from the row-major V tile through
+// ds_read_b64_tr_b16 (hardware transpose), so K and V are staged exactly as they arrive from HBM.
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
     Strides ks, Strides vs, Strides os, float scale_log2) {
+  constexpr int KT = 64;       // keys per LDS tile
+  constexpr int QB = 128;      // queries per workgroup
+  constexpr int RS = D + kPad; // LDS row stride (elements)
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Ks = smem;                                 // [64][D + pad]
-  uint16_t* Vt = Ks + kTile * (D + kPad);              // [D][64 + pad]
-  uint16_t* Ps = Vt + D * (kTile + kPad);              // [4][16][64 + pad]
+  uint16_t* Ks = smem;           // [KT][RS]
+  uint16_t* Vs = Ks + KT * RS;   // [KT][RS]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int lr = lane & 15, lg = lane >> 4;
+  const int r = lane & 31, hf = lane >> 5;
   const int b = blockIdx.z, h = blockIdx.y;
-  const int q_blk = blockIdx.x * kTile;
-  const int q0 = q_blk + w * 16;
+  // heaviest (largest causal extent) query blocks first
+  const int q_blk = (CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * QB;
+  const int q0 = q_blk + w * 32;
+  const int my_q = q0 + r;
   const uint16_t* qb = q + b * qs.b + h * qs.h;
   const uint16_t* kb = k + b * ks.b + h * ks.h;
   const uint16_t* vb = v + b * vs.b + h * vs.h;
-  uint16_t* ob = o + b * os.b + h * os.h;
-  uint16_t* Pw = Ps + w * 16 * (kTile + kPad);
 
-  bf16x8 qa[D / 32];
+  bf16x8 qf[D / 16];
 #pragma unroll
-  for (int s = 0; s < D / 32; ++s) {
-    const int row = q0 + lr;
-    qa[s] = row < Sq ? load8(qb + static_cast<int64_t>(row) * qs.s + 32 * s + 8 * lg) : zero8();
-  }
-  f32x4 oacc[D / 16];
+  for (int s = 0; s < D / 16; ++s)
+    qf[s] = my_q < Sq ? load8(qb + static_cast<int64_t>(my_q) * qs.s + 16 * s + 8 * hf) : zero8();
+  f32x16 oacc[D / 32];
 #pragma unroll
-  for (int n = 0; n < D / 16; ++n) oacc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[4], l[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { m[i] = -INFINITY; l[i] = 0.f; }
-
-  const int k_end = CAUSAL ? min(Sk, q_blk + kTile) : Sk;
-  for (int kt = 0; kt < k_end; kt += kTile) {
+  for (int n = 0; n < D / 32; ++n) oacc[n] = zero16();
+  float m = -INFINITY, l = 0.f;
+  const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
+  // tr-read lane address pieces (see T10: lane 4q+p of a 16-lane group -> row q, cols 4p..4p+3)
+  const int tr_row = (r & 15) >> 2;
+  const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
+  for (int kt = 0; kt < k_end; kt += KT) {
     __syncthreads();
     stage_tile<D>(kb, ks, kt, Sk, Ks, nullptr);
-    stage_tile<D>(vb, vs, kt, Sk, nullptr, Vt);
+    stage_tile<D>(vb, vs, kt, Sk, Vs, nullptr);
     __syncthreads();
-    f32x4 sacc[4];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb0 = kt + 32 * sub;
+      if (kb0 >= k_end) break;
+      if (CAUSAL && kb0 > q0 + 31) break;  // wave-uniform: the rest of this tile is masked
+      f32x16 sc = zero16();
 #pragma unroll
-      for (int s = 0; s < D / 32; ++s)
-        acc = mfma(qa[s], load8(Ks + (16 * n + lr) * (D + kPad) + 32 * s + 8 * lg), acc);
-      sacc[n] = acc;
-    }
-    float mx[4];
+      for (int s = 0; s < D / 16; ++s)
+        sc = mfma32(load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf), qf[s], sc);
+      // sc[i]: key = kb0 + (i&3) + 8(i>>2) + 4hf, query = my_q
+      const bool need_mask = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0);
+      float mx = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = q0 + lg * 4 + i;
-      float t = -INFINITY;
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int key = kt + 16 * n + lr;
-        float sv = sacc[n][i] * scale_log2;
-        if (key >= Sk || (CAUSAL && key > row)) sv = -INFINITY;
-        sacc[n][i] = sv;
-        t = fmaxf(t, sv);
+      for (int i = 0; i < 16; ++i) {
+        float x = sc[i] * scale_log2;
+        if (need_mask) {
+          const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          if (key >= Sk || (CAUSAL && key > my_q)) x = -INFINITY;
+        }
+        sc[i] = x;
+        mx = fmaxf(mx, x);
       }
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) t = fmaxf(t, __shfl_xor(t, off, 64));
-      mx[i] = t;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float mnew = fmaxf(m[i], mx[i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
       const float mref = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = exp2f(m[i] - mref);
+      const float alpha = exp2f(m - mref);
       float rs = 0.f;
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const float p = exp2f(sacc[n][i] - mref);
-        sacc[n][i] = p;
+      for (int i = 0; i < 16; ++i) {
+        const float p = exp2f(sc[i] - mref);
+        sc[i] = p;
         rs += p;
       }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mnew;
 #pragma unroll
-      for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off, 64);
-      l[i] = l[i] * alpha + rs;
-      m[i] = mnew;
+      for (int n = 0; n < D / 32; ++n) oacc[n] *= alpha;
+      const bf16x8 p0 = pack8(sc, 0), p1 = pack8(sc, 8);
 #pragma unroll
-      for (int n = 0; n < D / 16; ++n) oacc[n][i] *= alpha;
-    }
+      for (int n = 0; n < D / 32; ++n) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Pw[(lg * 4 + i) * (kTile + kPad) + 16 * n + lr] = to_bf16(sacc[n][i]);
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 pa = load8(Pw + lr * (kTile + kPad) + 32 * s + 8 * lg);
-#pragma unroll
-      for (int n = 0; n < D / 16; ++n)
-        oacc[n] = mfma(pa, load8(Vt + (16 * n + lr) * (kTile + kPad) + 32 * s + 8 * lg), oacc[n]);
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
+          oacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RS)), s2 ? p1 : p0, oacc[n]);
+        }
+      }
     }
   }
+  if (my_q < Sq) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    uint16_t* orow = o + b * os.b + h * os.h + static_cast<int64_t>(my_q) * os.s;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = q0 + lg * 4 + i;
-    if (row >= Sq) continue;
-    const float inv = l[i] > 0.f ? 1.f / l[i] : 0.f;
+    for (int n = 0; n < D / 32; ++n)
 #pragma unroll
-    for (int n = 0; n < D / 16; ++n)
-      ob[static_cast<int64_t>(row) * os.s + 16 * n + lr] = to_bf16(oacc[n][i] * inv);
-    if (lr == 0)
-      lse[(static_cast<int64_t>(b) * H + h) * Sq + row] = l[i] > 0.f ? m[i] + log2f(l[i]) : INFINITY;
+      for (int g = 0; g < 4; ++g) {
+        uint2 pk;
+        pk.x = pack_bf16x2(oacc[n][4 * g] * inv, oacc[n][4 * g + 1] * inv);
+        pk.y = pack_bf16x2(oacc[n][4 * g + 2] * inv, oacc[n][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + 32 * n + 8 * g + 4 * hf) = pk;
+      }
+    if (hf == 0)
+      lse[(static_cast<int64_t>(b) * H + h) * Sq + my_q] = l > 0.f ? m + log2f(l) : INFINITY;
   }
-}
-
-// delta[b,h,q] = sum_d dO * O  (one wave per row)
-template <int D>
-__global__ __launch_bounds__(256) void attn_delta_kernel(const uint16_t* __restrict__ o,
-                                                         const uint16_t* __restrict__ dO,
-                                                         float* __restrict__ delta, int B, int H,
-                                                         int Sq, Strides os, Strides ds) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (row >= static_cast<int64_t>(B) * H * Sq) return;
-  const int s = static_cast<int>(row % Sq);
-  const int h = static_cast<int>((row / Sq) % H);
-  const int b = static_cast<int>(row / (static_cast<int64_t>(Sq) * H));
-  const uint16_t* op = o + b * os.b + h * os.h + static_cast<int64_t>(s) * os.s;
-  const uint16_t* dp = dO + b * ds.b + h * ds.h + static_cast<int64_t>(s) * ds.s;
-  float acc = 0.f;
-  for (int d = lane; d < D; d += 64) acc = fmaf(from_bf16(op[d]), from_bf16(dp[d]), acc);
-  acc = wave_sum(acc);
-  if (lane == 0) delta[row] = acc;
 }
 
 // ------------------------------------------------------------------------------------ backward
+// Two kernels, no atomics (FlashAttention-2 style split, MI355X layouts):
+//  * attn_bwd_dq_kernel: one workgroup = 128 queries (4 waves x 32). Computes delta = rowsum(dO*O)
+//    in its prologue (written for the dK/dV kernel), then sweeps key tiles like the forward:
+//    S^T = K Q^T and dP^T = V dO^T with the key in registers / query on the lane, dS^T lane-local,
+//    dQ^T += K^T dS^T with K^T fragments from ds_read_b64_tr_b16 -> dQ written once, in bf16.
+//  * attn_bwd_dkdv_kernel: one workgroup = 128 keys (4 waves x 32); dK^T / dV^T accumulate in
+//    registers while the workgroup sweeps 32-query tiles (double-buffered through registers so the
+//    next tile's HBM loads overlap the current tile's MFMAs). S and dP have the key on the lane, so
+//    P and dS are directly the B operands of dV^T += dO^T P and dK^T += Q^T dS (A operands by
+//    transposed LDS reads of the row-major Q / dO tiles).
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
-    const uint16_t* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
-    float* __restrict__ dq_acc, uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int Sq,
-    int Sk, int H, Strides qs, Strides ks, Strides vs, Strides dos, Strides dks, Strides dvs,
-    float scale_log2, float scale) {
+    const uint16_t* __restrict__ o, const uint16_t* __restrict__ dO, const float* __restrict__ lse,
+    float* __restrict__ delta, uint16_t* __restrict__ dq, int Sq, int Sk, int H, Strides qs,
+    Strides ks, Strides vs, Strides os, Strides dos, Strides dqs, float scale_log2, float scale) {
+  constexpr int KT = 64;
+  constexpr int QB = 128;
+  constexpr int RS = D + kPad;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  constexpr int RS = D + kPad;      // row-major tile stride
-  constexpr int TS = kTile + kPad;  // transposed tile stride
-  uint16_t* Qs = smem;              // [64 q][D]
-  uint16_t* Qt = Qs + kTile * RS;   // [D][64 q]
-  uint16_t* dOs = Qt + D * TS;      // [64 q][D]
-  uint16_t* dOt = dOs + kTile * RS; // [D][64 q]
-  uint16_t* Kt = dOt + D * TS;      // [D][64 keys]
-  uint16_t* Pw_all = Kt + D * TS;   // [4][16 keys][64 q]   P^T
-  uint16_t* Sw_all = Pw_all + 4 * 16 * TS;  // [4][16 keys][64 q]  dS^T
-  uint16_t* dSq = Sw_all + 4 * 16 * TS;     // [64 q][64 keys]    dS
+  uint16_t* Ks = smem;
+  uint16_t* Vs = Ks + KT * RS;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int lr = lane & 15, lg = lane >> 4;
+  const int r = lane & 31, hf = lane >> 5;
   const int b = blockIdx.z, h = blockIdx.y;
-  const int kb0 = blockIdx.x * kTile;
-  const int key0 = kb0 + w * 16;
-  const uint16_t* qb = q + b * qs.b + h * qs.h;
+  const int q_blk = (CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * QB;
+  const int q0 = q_blk + w * 32;
+  const int my_q = q0 + r;
+  const bool q_ok = my_q < Sq;
   const uint16_t* kb = k + b * ks.b + h * ks.h;
   const uint16_t* vb = v + b * vs.b + h * vs.h;
+  const int64_t bh = static_cast<int64_t>(b) * H + h;
+
+  bf16x8 qf[D / 16], dof[D / 16];
+  float dsum = 0.f;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    const int d0 = 16 * s + 8 * hf;
+    qf[s] = q_ok ? load8(q + b * qs.b + h * qs.h + static_cast<int64_t>(my_q) * qs.s + d0) : zero8();
+    dof[s] = q_ok ? load8(dO + b * dos.b + h * dos.h + static_cast<int64_t>(my_q) * dos.s + d0) : zero8();
+    if (q_ok) {
+      const bf16x8 of = load8(o + b * os.b + h * os.h + static_cast<int64_t>(my_q) * os.s + d0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += static_cast<float>(of[j]) * static_cast<float>(dof[s][j]);
+    }
+  }
+  dsum += __shfl_xor(dsum, 32, 64);
+  if (q_ok && hf == 0) delta[bh * Sq + my_q] = dsum;
+  const float lq = q_ok ? lse[bh * Sq + my_q] : INFINITY;
+  f32x16 dqacc[D / 32];
+#pragma unroll
+  for (int n = 0; n < D / 32; ++n) dqacc[n] = zero16();
+  const int tr_row = (r & 15) >> 2;
+  const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
+  const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
+  for (int kt = 0; kt < k_end; kt += KT) {
+    __syncthreads();
+    stage_tile<D>(kb, ks, kt, Sk, Ks, nullptr);
+    stage_tile<D>(vb, vs, kt, Sk, Vs, nullptr);
+    __syncthreads();
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb0 = kt + 32 * sub;
+      if (kb0 >= k_end) break;
+      if (CAUSAL && kb0 > q0 + 31) break;
+      f32x16 sc = zero16(), dp = zero16();
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        sc = mfma32(load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf), qf[s], sc);
+        dp = mfma32(load8(Vs + (32 * sub + r) * RS + 16 * s + 8 * hf), dof[s], dp);
+      }
+      const bool need_mask = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = exp2f(sc[i] * scale_log2 - lq);
+        if (need_mask) {
+          const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          if (key >= Sk || (CAUSAL && key > my_q)) p = 0.f;
+        }
+        dp[i] = p * (dp[i] - dsum) * scale;
+      }
+      const bf16x8 s0 = pack8(dp, 0), s1 = pack8(dp, 8);
+#pragma unroll
+      for (int n = 0; n < D / 32; ++n)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const uint16_t* base = Ks + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
+          dqacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RS)), s2 ? s1 : s0, dqacc[n]);
+        }
+    }
+  }
+  if (q_ok) {
+    uint16_t* row = dq + b * dqs.b + h * dqs.h + static_cast<int64_t>(my_q) * dqs.s;
+#pragma unroll
+    for (int n = 0; n < D / 32; ++n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 pk;
+        pk.x = pack_bf16x2(dqacc[n][4 * g], dqacc[n][4 * g + 1]);
+        pk.y = pack_bf16x2(dqacc[n][4 * g + 2], dqacc[n][4 * g + 3]);
+        *reinterpret_cast<uint2*>(row + 32 * n + 8 * g + 4 * hf) = pk;
+      }
+  }
+}
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
+    const uint16_t* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
+    uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int Sq, int Sk, int H, Strides qs,
+    Strides ks, Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale) {
+  constexpr int KB = 128;
+  constexpr int QT = 32;
+  constexpr int RS = D + kPad;
+  constexpr int CPR = D / 8;                 // 16-byte chunks per row
+  constexpr int NPF = 2 * QT * CPR / 256;    // prefetched chunks per thread (Q and dO tiles)
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Qs = smem;            // [QT][RS]
+  uint16_t* dOs = Qs + QT * RS;   // [QT][RS]
+  float* lse_s = reinterpret_cast<float*>(dOs + QT * RS);
+  float* del_s = lse_s + QT;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 31, hf = lane >> 5;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int k_blk = blockIdx.x * KB;
+  const int kw0 = k_blk + 32 * w;
+  const int my_key = kw0 + r;
+  const uint16_t* qb = q + b * qs.b + h * qs.h;
   const uint16_t* dob = dO + b * dos.b + h * dos.h;
-  const float* lseb = lse + (static_cast<int64_t>(b) * H + h) * Sq;
-  const float* delb = delta + (static_cast<int64_t>(b) * H + h) * Sq;
-  float* dqb = dq_acc + (static_cast<int64_t>(b) * H + h) * Sq * D;
-  uint16_t* Pw = Pw_all + w * 16 * TS;
-  uint16_t* Sw = Sw_all + w * 16 * TS;
+  const int64_t bh = static_cast<int64_t>(b) * H + h;
 
-  bf16x8 ka[D / 32], va[D / 32];
+  bf16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
-  for (int s = 0; s < D / 32; ++s) {
-    const int key = key0 + lr;
-    ka[s] = key < Sk ? load8(kb + static_cast<int64_t>(key) * ks.s + 32 * s + 8 * lg) : zero8();
-    va[s] = key < Sk ? load8(vb + static_cast<int64_t>(key) * vs.s + 32 * s + 8 * lg) : zero8();
+  for (int s = 0; s < D / 16; ++s) {
+    const bool ok = my_key < Sk;
+    kf[s] = ok ? load8(k + b * ks.b + h * ks.h + static_cast<int64_t>(my_key) * ks.s + 16 * s + 8 * hf) : zero8();
+    vf[s] = ok ? load8(v + b * vs.b + h * vs.h + static_cast<int64_t>(my_key) * vs.s + 16 * s + 8 * hf) : zero8();
   }
-  stage_tile<D>(kb, ks, kb0, Sk, nullptr, Kt);
-  f32x4 dkacc[D / 16], dvacc[D / 16];
+  f32x16 dkacc[D / 32], dvacc[D / 32];
 #pragma unroll
-  for (int n = 0; n < D / 16; ++n) {
-    dkacc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    dvacc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int n = 0; n < D / 32; ++n) {
+    dkacc[n] = zero16();
+    dvacc[n] = zero16();
   }
-  const int q_start = CAUSAL ? (kb0 / kTile) * kTile : 0;
-  for (int qt = q_start; qt < Sq; qt += kTile) {
-    __syncthreads();
-    stage_tile<D>(qb, qs, qt, Sq, Qs, Qt);
-    stage_tile<D>(dob, dos, qt, Sq, dOs, dOt);
-    __syncthreads();
-    f32x4 pt[4], dpt[4];
+  // register double buffer for the next query tile
+  uint4 pf[NPF];
+  float pl = 0.f, pd = 0.f;
+  auto fetch = [&](int qt) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      f32x4 a = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < D / 32; ++s) {
-        a = mfma(ka[s], load8(Qs + (16 * n + lr) * RS + 32 * s + 8 * lg), a);
-        c = mfma(va[s], load8(dOs + (16 * n + lr) * RS + 32 * s + 8 * lg), c);
-      }
-      pt[n] = a;
-      dpt[n] = c;
-    }
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int qi = qt + 16 * n + lr;
-      const float lq = qi < Sq ? lseb[qi] : INFINITY;
-      const float dl = qi < Sq ? delb[qi] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = key0 + lg * 4 + i;
-        float p = exp2f(pt[n][i] * scale_log2 - lq);
-        if (qi >= Sq || key >= Sk || (CAUSAL && key > qi)) p = 0.f;
-        const float ds = p * (dpt[n][i] - dl) * scale;
-        Pw[(lg * 4 + i) * TS + 16 * n + lr] = to_bf16(p);
-        const uint16_t dsb = to_bf16(ds);
-        Sw[(lg * 4 + i) * TS + 16 * n + lr] = dsb;
-        dSq[(16 * n + lr) * TS + w * 16 + lg * 4 + i] = dsb;
+    for (int j = 0; j < NPF; ++j) {
+      const int c = threadIdx.x + 256 * j;
+      const int which = c / (QT * CPR);  // 0: Q, 1: dO
+      const int cc = c % (QT * CPR);
+      const int rr = cc / CPR, d0 = (cc % CPR) * 8;
+      pf[j] = make_uint4(0, 0, 0, 0);
+      if (qt + rr < Sq) {
+        const uint16_t* src = which ? dob + static_cast<int64_t>(qt + rr) * dos.s
+                                    : qb + static_cast<int64_t>(qt + rr) * qs.s;
+        pf[j] = *reinterpret_cast<const uint4*>(src + d0);
       }
     }
+    if (threadIdx.x < QT) {
+      const int qi = qt + threadIdx.x;
+      pl = qi < Sq ? lse[bh * Sq + qi] : INFINITY;
+      pd = qi < Sq ? delta[bh * Sq + qi] : 0.f;
+    }
+  };
+  const int tr_row = (r & 15) >> 2;
+  const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
+  const int q_start = CAUSAL ? (k_blk / QT) * QT : 0;
+  if (q_start < Sq) fetch(q_start);
+  for (int qt = q_start; qt < Sq; qt += QT) {
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 pa = load8(Pw + lr * TS + 32 * s + 8 * lg);
-      const bf16x8 sa = load8(Sw + lr * TS + 32 * s + 8 * lg);
+    for (int j = 0; j < NPF; ++j) {
+      const int c = threadIdx.x + 256 * j;
+      const int which = c / (QT * CPR);
+      const int cc = c % (QT * CPR);
+      *reinterpret_cast<uint4*>((which ? dOs : Qs) + (cc / CPR) * RS + (cc % CPR) * 8) = pf[j];
+    }
+    if (threadIdx.x < QT) {
+      lse_s[threadIdx.x] = pl;
+      del_s[threadIdx.x] = pd;
+    }
+    __syncthreads();
+    if (qt + QT < Sq) fetch(qt + QT);
+    const bool active = !(CAUSAL && kw0 > qt + QT - 1) && kw0 < Sk;  // wave-uniform
+    if (!active) continue;
+    f32x16 sacc = zero16(), dpacc = zero16();
 #pragma unroll
-      for (int n = 0; n < D / 16; ++n) {
-        dvacc[n] = mfma(pa, load8(dOt + (16 * n + lr) * TS + 32 * s + 8 * lg), dvacc[n]);
-        dkacc[n] = mfma(sa, load8(Qt + (16 * n + lr) * TS + 32 * s + 8 * lg), dkacc[n]);
+    for (int s = 0; s < D / 16; ++s) {
+      sacc = mfma32(load8(Qs + r * RS + 16 * s + 8 * hf), kf[s], sacc);
+      dpacc = mfma32(load8(dOs + r * RS + 16 * s + 8 * hf), vf[s], dpacc);
+    }
+    const bool need_mask = (qt + QT > Sq) || (my_key >= Sk) || (CAUSAL && kw0 + 31 > qt);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ql = (i & 3) + 8 * (i >> 2) + 4 * hf;
+      float p = exp2f(sacc[i] * scale_log2 - lse_s[ql]);
+      if (need_mask) {
+        const int qi = qt + ql;
+        if (qi >= Sq || my_key >= Sk || (CAUSAL && my_key > qi)) p = 0.f;
+      }
+      sacc[i] = p;
+      dpacc[i] = p * (dpacc[i] - del_s[ql]) * scale;
+    }
+    const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8);
+    const bf16x8 s0 = pack8(dpacc, 0), s1 = pack8(dpacc, 8);
+#pragma unroll
+    for (int n = 0; n < D / 32; ++n) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int off = (16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
+        dvacc[n] = mfma32(cat8(tr_read(dOs + off), tr_read(dOs + off + 8 * RS)), s2 ? p1 : p0, dvacc[n]);
+        dkacc[n] = mfma32(cat8(tr_read(Qs + off), tr_read(Qs + off + 8 * RS)), s2 ? s1 : s0, dkacc[n]);
       }
     }
-    // dQ rows 16w.. of this query tile: dS[q][keys 0..63] . K[keys][D]
-    f32x4 dqacc[D / 16];
-#pragma unroll
-    for (int n = 0; n < D / 16; ++n) dqacc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 a = load8(dSq + (16 * w + lr) * TS + 32 * s + 8 * lg);
-#pragma unroll
-      for (int n = 0; n < D / 16; ++n)
-        dqacc[n] = mfma(a, load8(Kt + (16 * n + lr) * TS + 32 * s + 8 * lg), dqacc[n]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int qi = qt + 16 * w + lg * 4 + i;
-      if (qi >= Sq) continue;
-#pragma unroll
-      for (int n = 0; n < D / 16; ++n)
-        atomicAdd(dqb + static_cast<int64_t>(qi) * D + 16 * n + lr, dqacc[n][i]);
-    }
   }
+  if (my_key < Sk) {
+    uint16_t* dkrow = dk + b * dks.b + h * dks.h + static_cast<int64_t>(my_key) * dks.s;
+    uint16_t* dvrow = dv + b * dvs.b + h * dvs.h + static_cast<int64_t>(my_key) * dvs.s;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int key = key0 + lg * 4 + i;
-    if (key >= Sk) continue;
+    for (int n = 0; n < D / 32; ++n)
 #pragma unroll
-    for (int n = 0; n < D / 16; ++n) {
-      dk[b * dks.b + h * dks.h + static_cast<int64_t>(key) * dks.s + 16 * n + lr] = to_bf16(dkacc[n][i]);
-      dv[b * dvs.b + h * dvs.h + static_cast<int64_t>(key) * dvs.s + 16 * n + lr] = to_bf16(dvacc[n][i]);
-    }
+      for (int g = 0; g < 4; ++g) {
+        uint2 pk;
+        pk.x = pack_bf16x2(dkacc[n][4 * g], dkacc[n][4 * g + 1]);
+        pk.y = pack_bf16x2(dkacc[n][4 * g + 2], dkacc[n][4 * g + 3]);
+        *reinterpret_cast<uint2*>(dkrow + 32 * n + 8 * g + 4 * hf) = pk;
+        pk.x = pack_bf16x2(dvacc[n][4 * g], dvacc[n][4 * g + 1]);
+        pk.y = pack_bf16x2(dvacc[n][4 * g + 2], dvacc[n][4 * g + 3]);
+        *reinterpret_cast<uint2*>(dvrow + 32 * n + 8 * g + 4 * hf) = pk;
+      }
   }
 }
 
-// dq (strided bf16) <- dq_acc (contiguous fp32 [B, H, S, D])
-__global__ __launch_bounds__(256) void attn_dq_convert_kernel(const float* __restrict__ acc,
-                                                              uint16_t* __restrict__ dq, int B,
-                                                              int H, int Sq, int D, Strides st) {
-  const int64_t total = static_cast<int64_t>(B) * H * Sq * D;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int d = static_cast<int>(i % D);
-    const int s = static_cast<int>((i / D) % Sq);
-    const int h = static_cast<int>((i / (static_cast<int64_t>(D) * Sq)) % H);
-    const int b = static_cast<int>(i / (static_cast<int64_t>(D) * Sq * H));
-    dq[b * st.b + h * st.h + static_cast<int64_t>(s) * st.s + d] = to_bf16(acc[i]);
-  }
-}
-
-size_t fwd_lds(int D) { return (static_cast<size_t>(kTile) * (D + kPad) + D * (kTile + kPad) + 4 * 16 * (kTile + kPad)) * 2; }
-size_t bwd_lds(int D) {
-  return (2 * static_cast<size_t>(kTile) * (D + kPad) + 3 * static_cast<size_t>(D) * (kTile + kPad) +
-          2 * 4 * 16 * (kTile + kPad) + kTile * (kTile + kPad)) * 2;
-}
+size_t fwd_lds(int D) { return 2 * static_cast<size_t>(64) * (D + kPad) * 2; }
+size_t bwd_dq_lds(int D) { return fwd_lds(D); }
+size_t bwd_dkdv_lds(int D) { return 2 * 32 * static_cast<size_t>(D + kPad) * 2 + 2 * 32 * sizeof(float); }
 
 template <int D, bool C>
 void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse,
                 int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs, Strides os,
                 float scale_log2, hipStream_t st) {
-  dim3 grid((Sq + kTile - 1) / kTile, H, B);
+  dim3 grid((Sq + 127) / 128, H, B);
   const size_t lds = fwd_lds(D);
-  hipFuncSetAttribute(reinterpret_cast<const void*>(attn_fwd_kernel<D, C>),
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_fwd_kernel<D, C>),
                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
   hipLaunchKernelGGL((attn_fwd_kernel<D, C>), grid, dim3(256), lds, st, q, k, v, o, lse, Sq, Sk, H,
                      qs, ks, vs, os, scale_log2);
@@ -359,22 +485,20 @@ void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
 
 template <int D, bool C>
 void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o,
-                const uint16_t* dO, const float* lse, float* delta, float* dq_acc, uint16_t* dq,
-                uint16_t* dk, uint16_t* dv, int B, int H, int Sq, int Sk, Strides qs, Strides ks,
-                Strides vs, Strides os, Strides dos, Strides dqs, Strides dks, Strides dvs,
-                float scale_log2, float scale, hipStream_t st) {
-  const int64_t rows = static_cast<int64_t>(B) * H * Sq;
-  hipLaunchKernelGGL(attn_delta_kernel<D>, dim3((rows + 3) / 4), dim3(256), 0, st, o, dO, delta, B,
-                     H, Sq, os, dos);
-  hipMemsetAsync(dq_acc, 0, rows * D * sizeof(float), st);
-  dim3 grid((Sk + kTile - 1) / kTile, H, B);
-  const size_t lds = bwd_lds(D);
-  hipFuncSetAttribute(reinterpret_cast<const void*>(attn_bwd_kernel<D, C>),
-                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-  hipLaunchKernelGGL((attn_bwd_kernel<D, C>), grid, dim3(256), lds, st, q, k, v, dO, lse, delta,
-                     dq_acc, dk, dv, Sq, Sk, H, qs, ks, vs, dos, dks, dvs, scale_log2, scale);
-  hipLaunchKernelGGL(attn_dq_convert_kernel, dim3(stream_grid(rows * D, 256)), dim3(256), 0, st,
-                     dq_acc, dq, B, H, Sq, D, dqs);
+                const uint16_t* dO, const float* lse, float* delta, uint16_t* dq, uint16_t* dk,
+                uint16_t* dv, int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs,
+                Strides os, Strides dos, Strides dqs, Strides dks, Strides dvs, float scale_log2,
+                float scale, hipStream_t st) {
+  const size_t l1 = bwd_dq_lds(D);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_bwd_dq_kernel<D, C>),
+                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l1));
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C>), dim3((Sq + 127) / 128, H, B), dim3(256), l1, st, q,
+                     k, v, o, dO, lse, delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2,
+                     scale);
+  const size_t l2 = bwd_dkdv_lds(D);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C>), dim3((Sk + 127) / 128, H, B), dim3(256), l2, st,
+                     q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks, vs, dos, dks, dvs,
+                     scale_log2, scale);
 }
 
 }  // namespace
@@ -408,11 +532,11 @@ void attention_bwd(const void* q, const void* k, const void* v, const void* o, c
   auto c16 = [](const void* p) { return static_cast<const uint16_t*>(p); };
   auto m16 = [](void* p) { return static_cast<uint16_t*>(p); };
   if (D == 64) {
-    if (causal) launch_bwd<64, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, dq_acc, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
-    else launch_bwd<64, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, dq_acc, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
+    if (causal) launch_bwd<64, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
+    else launch_bwd<64, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
   } else {
-    if (causal) launch_bwd<128, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, dq_acc, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
-    else launch_bwd<128, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, dq_acc, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
+    if (causal) launch_bwd<128, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
+    else launch_bwd<128, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
   }
 }
 

@@ -181,10 +181,9 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   Tensor dv = torch::empty({B, Sk, H, D}, q.options());
   auto fo = q.options().dtype(at::kFloat);
   Tensor delta = torch::empty({B, H, Sq}, fo);
-  Tensor dq_acc = torch::empty({B, H, Sq, D}, fo);
   auto dqs = bshd_strides(dq, "dq"), dks = bshd_strides(dk, "dk"), dvs = bshd_strides(dv, "dv");
   dca::attention_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dO.data_ptr(),
-                     lse.data_ptr<float>(), delta.data_ptr<float>(), dq_acc.data_ptr<float>(),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), nullptr,
                      dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, H, Sq, Sk, D, qs.v, ks.v, vs.v,
                      os.v, dos.v, dqs.v, dks.v, dvs.v, static_cast<float>(scale), causal, stream());
   return {dq, dk, dv};
