@@ -105,12 +105,14 @@ class Attention(nn.Module):
         B, S, E = x.shape
         H, D = self.cfg.n_head, self.cfg.head_dim
         qkv = self.qkv(x).view(B, S, 3, H, D)
-        q, k, v = qkv.unbind(2)
         if self.rot:
+            q, k, v = qkv.unbind(2)
             cos, sin = rope_cache
             q = T.rope(q, cos, sin, self.rot)
             k = T.rope(k, cos, sin, self.rot)
-        o = T.flash_attention(q, k, v, causal=True)
+            o = T.flash_attention(q, k, v, causal=True)
+        else:
+            o = T.flash_attention_qkvpacked(qkv, causal=True)
         if self.cfg.dropout and self.training:
             o = F.dropout(o, self.cfg.dropout)
         return self.proj(o.reshape(B, S, E))
@@ -215,8 +217,7 @@ class GPT(nn.Module):
         logits = F.linear(h, w)
         if targets is None:
             return logits
-        loss = F.cross_entropy(logits.float().view(-1, logits.shape[-1]), targets.reshape(-1),
-                               ignore_index=-100)
+        loss = T.cross_entropy(logits, targets, ignore_index=-100)
         return logits, loss
 
 

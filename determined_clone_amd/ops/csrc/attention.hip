@@ -80,6 +80,9 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int base) {
   return __builtin_bit_cast(bf16x8, u);
 }
 
+// v_exp_f32 directly (inputs are finite or -inf; no denormal range fix-up needed)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 struct Strides {
   int64_t b, h, s;  // element strides; d stride is 1
 };
@@ -117,6 +120,41 @@ __device__ __forceinline__ void stage_rows(const uint16_t* __restrict__ src, Str
     *reinterpret_cast<uint4*>(dst + rr * (D + kPad) + d0) = val;
   }
 }
+
+// Register double buffer for a pair of [64 rows][D] tiles (K and V): fetch() issues the HBM loads of
+// the NEXT tile before the current tile's MFMAs, store() writes them to LDS after the barrier.
+template <int D>
+struct KVPrefetch {
+  static constexpr int CPR = D / 8;
+  static constexpr int N = 2 * 64 * CPR / 256;
+  uint4 reg[N];
+  __device__ __forceinline__ void fetch(const uint16_t* __restrict__ kb, Strides ks,
+                                        const uint16_t* __restrict__ vb, Strides vs, int r0,
+                                        int n_rows) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const int c = threadIdx.x + 256 * j;
+      const int which = c / (64 * CPR);
+      const int cc = c % (64 * CPR);
+      const int rr = cc / CPR, d0 = (cc % CPR) * 8;
+      reg[j] = make_uint4(0, 0, 0, 0);
+      if (r0 + rr < n_rows) {
+        const uint16_t* src = which ? vb + static_cast<int64_t>(r0 + rr) * vs.s
+                                    : kb + static_cast<int64_t>(r0 + rr) * ks.s;
+        reg[j] = *reinterpret_cast<const uint4*>(src + d0);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* Ks, uint16_t* Vs) const {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const int c = threadIdx.x + 256 * j;
+      const int which = c / (64 * CPR);
+      const int cc = c % (64 * CPR);
+      *reinterpret_cast<uint4*>((which ? Vs : Ks) + (cc / CPR) * (D + kPad) + (cc % CPR) * 8) = reg[j];
+    }
+  }
+};
 
 // ------------------------------------------------------------------------------------ forward
 // One workgroup = 4 waves x 32 queries = 128 query rows of one (batch, head). Per 64-key LDS tile,
@@ -159,11 +197,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   // tr-read lane address pieces (see T10: lane 4q+p of a 16-lane group -> row q, cols 4p..4p+3)
   const int tr_row = (r & 15) >> 2;
   const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
+  KVPrefetch<D> pf;
+  pf.fetch(kb, ks, vb, vs, 0, Sk);
   for (int kt = 0; kt < k_end; kt += KT) {
     __syncthreads();
-    stage_tile<D>(kb, ks, kt, Sk, Ks, nullptr);
-    stage_tile<D>(vb, vs, kt, Sk, Vs, nullptr);
+    pf.store(Ks, Vs);
     __syncthreads();
+    if (kt + KT < k_end) pf.fetch(kb, ks, vb, vs, kt + KT, Sk);
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const int kb0 = kt + 32 * sub;
@@ -189,11 +229,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m, mx);
       const float mref = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = exp2f(m - mref);
+      const float alpha = fast_exp2(m - mref);
       float rs = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = exp2f(sc[i] - mref);
+        const float p = fast_exp2(sc[i] - mref);
         sc[i] = p;
         rs += p;
       }
@@ -286,11 +326,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   const int tr_row = (r & 15) >> 2;
   const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
   const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
+  KVPrefetch<D> pf;
+  pf.fetch(kb, ks, vb, vs, 0, Sk);
   for (int kt = 0; kt < k_end; kt += KT) {
     __syncthreads();
-    stage_tile<D>(kb, ks, kt, Sk, Ks, nullptr);
-    stage_tile<D>(vb, vs, kt, Sk, Vs, nullptr);
+    pf.store(Ks, Vs);
     __syncthreads();
+    if (kt + KT < k_end) pf.fetch(kb, ks, vb, vs, kt + KT, Sk);
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const int kb0 = kt + 32 * sub;
@@ -305,7 +347,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
       const bool need_mask = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float p = exp2f(sc[i] * scale_log2 - lq);
+        float p = fast_exp2(sc[i] * scale_log2 - lq);
         if (need_mask) {
           const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
           if (key >= Sk || (CAUSAL && key > my_q)) p = 0.f;
@@ -429,7 +471,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ql = (i & 3) + 8 * (i >> 2) + 4 * hf;
-      float p = exp2f(sacc[i] * scale_log2 - lse_s[ql]);
+      float p = fast_exp2(sacc[i] * scale_log2 - lse_s[ql]);
       if (need_mask) {
         const int qi = qt + ql;
         if (qi >= Sq || my_key >= Sk || (CAUSAL && my_key > qi)) p = 0.f;

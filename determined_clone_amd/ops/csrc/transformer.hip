@@ -397,4 +397,101 @@ void rope(TDtype dt, const void* x, void* y, const float* cosT, const float* sin
   });
 }
 
+// ------------------------------------------------------------------ fused softmax cross-entropy
+// logits [rows][V] (bf16/f16/f32) -> per-row lse (fp32) and loss = lse - logit[target]
+// (0 for ignore_index rows) in ONE read of the logits (online max/sum per thread, then a
+// wave/LDS combine). Backward recomputes softmax from the saved lse:
+// dlogits = (exp(x - lse) - onehot) * grad / n_valid, with grad and n_valid read from device
+// memory (no host sync). Replaces the reference GPT trial's fp32 upcast + log_softmax + nll.
+template <typename T>
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const void* __restrict__ logits,
+                                                     const int64_t* __restrict__ target,
+                                                     float* __restrict__ lse_out,
+                                                     float* __restrict__ loss_out, int V,
+                                                     int64_t ignore_index) {
+  __shared__ float sm[8], ss[8];
+  const int64_t row = blockIdx.x;
+  const char* base = reinterpret_cast<const char*>(logits) + row * V * Vec8<T>::bytes;
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x * 8; c < V; c += blockDim.x * 8) {
+    float v[8];
+    Vec8<T>::load(base + static_cast<int64_t>(c) * Vec8<T>::bytes, v);
+    float mx = v[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) mx = fmaxf(mx, v[k]);
+    const float nm = fmaxf(m, mx);
+    float acc = s * __expf(m - nm);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += __expf(v[k] - nm);
+    m = nm;
+    s = acc;
+  }
+  // combine (m, s) across the wave, then across waves
+  for (int off = 32; off > 0; off >>= 1) {
+    const float om = __shfl_xor(m, off, 64), os = __shfl_xor(s, off, 64);
+    const float nm = fmaxf(m, om);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+    m = nm;
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { sm[w] = m; ss[w] = s; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], S = ss[0];
+    for (int i = 1; i < static_cast<int>(blockDim.x >> 6); ++i) {
+      const float nm = fmaxf(M, sm[i]);
+      S = S * __expf(M - nm) + ss[i] * __expf(sm[i] - nm);
+      M = nm;
+    }
+    const float l = M + __logf(S);
+    lse_out[row] = l;
+    const int64_t t = target[row];
+    float loss = 0.f;
+    if (t != ignore_index && t >= 0 && t < V) loss = l - Elem<T>::get(logits, row * V + t);
+    loss_out[row] = loss;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const void* __restrict__ logits,
+                                                     const int64_t* __restrict__ target,
+                                                     const float* __restrict__ lse,
+                                                     const float* __restrict__ gscale,
+                                                     void* __restrict__ dlogits, int V,
+                                                     int64_t ignore_index) {
+  const int64_t row = blockIdx.x;
+  const int64_t t = target[row];
+  const bool valid = t != ignore_index;
+  // gscale = [grad_output, n_valid]
+  const float g = valid ? gscale[0] / fmaxf(gscale[1], 1.f) : 0.f;
+  const float l = lse[row];
+  const int64_t off = row * V;
+  for (int c = threadIdx.x * 8; c < V; c += blockDim.x * 8) {
+    float v[8];
+    Vec8<T>::load(reinterpret_cast<const char*>(logits) + (off + c) * Vec8<T>::bytes, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (__expf(v[k] - l) - ((c + k) == t ? 1.f : 0.f)) * g;
+    Vec8<T>::store(reinterpret_cast<char*>(dlogits) + (off + c) * Vec8<T>::bytes, v);
+  }
+}
+
+void cross_entropy_fwd(TDtype dt, const void* logits, const int64_t* target, float* lse,
+                       float* loss, int64_t rows, int V, int64_t ignore_index, hipStream_t st) {
+  dispatch_t(dt, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(ce_fwd_kernel<T>, dim3(rows), dim3(256), 0, st, logits, target, lse, loss, V,
+                       ignore_index);
+  });
+}
+
+void cross_entropy_bwd(TDtype dt, const void* logits, const int64_t* target, const float* lse,
+                       const float* gscale, void* dlogits, int64_t rows, int V,
+                       int64_t ignore_index, hipStream_t st) {
+  dispatch_t(dt, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(ce_bwd_kernel<T>, dim3(rows), dim3(256), 0, st, logits, target, lse, gscale,
+                       dlogits, V, ignore_index);
+  });
+}
+
 }  // namespace dca

@@ -30,6 +30,11 @@ void attention_bwd(const void* q, const void* k, const void* v, const void* o, c
                    const int64_t* st_v, const int64_t* st_o, const int64_t* st_do,
                    const int64_t* st_dq, const int64_t* st_dk, const int64_t* st_dv, float scale,
                    bool causal, hipStream_t stream);
+void cross_entropy_fwd(TDtype dt, const void* logits, const int64_t* target, float* lse,
+                       float* loss, int64_t rows, int V, int64_t ignore_index, hipStream_t st);
+void cross_entropy_bwd(TDtype dt, const void* logits, const int64_t* target, const float* lse,
+                       const float* gscale, void* dlogits, int64_t rows, int V,
+                       int64_t ignore_index, hipStream_t st);
 }  // namespace dca
 
 namespace {
@@ -168,7 +173,8 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
 }
 
 std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
-                             const Tensor& o, const Tensor& lse, double scale, bool causal) {
+                             const Tensor& o, const Tensor& lse, double scale, bool causal,
+                             const OptT& dq_out, const OptT& dk_out, const OptT& dv_out) {
   const c10::DeviceGuard g(q.device());
   const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
   const int Sk = k.size(1);
@@ -176,9 +182,12 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   auto qs = bshd_strides(q, "q"), ks = bshd_strides(k, "k"), vs = bshd_strides(v, "v");
   auto os = bshd_strides(o, "o"), dos = bshd_strides(dO, "dout");
   TORCH_CHECK(lse.is_contiguous() && lse.numel() == static_cast<int64_t>(B) * H * Sq, "attention: lse");
-  Tensor dq = torch::empty({B, Sq, H, D}, q.options());
-  Tensor dk = torch::empty({B, Sk, H, D}, q.options());
-  Tensor dv = torch::empty({B, Sk, H, D}, q.options());
+  // optional preallocated outputs (e.g. views into one packed dQKV buffer)
+  Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({B, Sq, H, D}, q.options());
+  Tensor dk = dk_out.has_value() ? *dk_out : torch::empty({B, Sk, H, D}, q.options());
+  Tensor dv = dv_out.has_value() ? *dv_out : torch::empty({B, Sk, H, D}, q.options());
+  TORCH_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(),
+              "attention: gradient output shape mismatch");
   auto fo = q.options().dtype(at::kFloat);
   Tensor delta = torch::empty({B, H, Sq}, fo);
   auto dqs = bshd_strides(dq, "dq"), dks = bshd_strides(dk, "dk"), dvs = bshd_strides(dv, "dv");
@@ -187,6 +196,33 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
                      dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, H, Sq, Sk, D, qs.v, ks.v, vs.v,
                      os.v, dos.v, dqs.v, dks.v, dvs.v, static_cast<float>(scale), causal, stream());
   return {dq, dk, dv};
+}
+// logits [N, V] contiguous, target [N] int64 -> (lse [N], per-row loss [N])
+std::vector<Tensor> ce_fwd(const Tensor& logits, const Tensor& target, int64_t ignore_index) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2, "ce_fwd: [N, V] GPU logits");
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.is_contiguous() && target.numel() == logits.size(0),
+              "ce_fwd: int64 targets [N]");
+  const int V = static_cast<int>(logits.size(1));
+  TORCH_CHECK(V % 8 == 0, "ce_fwd: vocab must be a multiple of 8 (pad it)");
+  const c10::DeviceGuard g(logits.device());
+  auto fo = logits.options().dtype(at::kFloat);
+  Tensor lse = torch::empty({logits.size(0)}, fo), loss = torch::empty({logits.size(0)}, fo);
+  dca::cross_entropy_fwd(tdt(logits), logits.data_ptr(), target.data_ptr<int64_t>(),
+                         lse.data_ptr<float>(), loss.data_ptr<float>(), logits.size(0), V,
+                         ignore_index, stream());
+  return {lse, loss};
+}
+
+// gscale = [grad_output, n_valid] (fp32, device)
+Tensor ce_bwd(const Tensor& logits, const Tensor& target, const Tensor& lse, const Tensor& gscale,
+              int64_t ignore_index) {
+  const c10::DeviceGuard g(logits.device());
+  TORCH_CHECK(gscale.scalar_type() == at::kFloat && gscale.numel() == 2 && gscale.is_contiguous(), "ce_bwd: gscale");
+  Tensor d = torch::empty_like(logits);
+  dca::cross_entropy_bwd(tdt(logits), logits.data_ptr(), target.data_ptr<int64_t>(),
+                         lse.data_ptr<float>(), gscale.data_ptr<float>(), d.data_ptr(),
+                         logits.size(0), static_cast<int>(logits.size(1)), ignore_index, stream());
+  return d;
 }
 }  // namespace
 
@@ -197,5 +233,10 @@ void register_transformer_ops(pybind11::module& m) {
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("rope", &rope_apply);
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("attn_bwd", &attn_bwd, pybind11::arg("dout"), pybind11::arg("q"), pybind11::arg("k"),
+        pybind11::arg("v"), pybind11::arg("o"), pybind11::arg("lse"), pybind11::arg("scale"),
+        pybind11::arg("causal"), pybind11::arg("dq_out") = pybind11::none(),
+        pybind11::arg("dk_out") = pybind11::none(), pybind11::arg("dv_out") = pybind11::none());
 }

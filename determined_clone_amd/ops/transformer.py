@@ -192,6 +192,71 @@ class _FlashAttention(torch.autograd.Function):
         return dq, dk, dv, None, None
 
 
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index):
+        C = _ext.load()
+        lse, loss_rows = C.ce_fwd(logits, target, ignore_index)
+        n_valid = (target != ignore_index).sum().float()
+        ctx.save_for_backward(logits, target, lse, n_valid)
+        ctx.ignore_index = ignore_index
+        return loss_rows.sum() / n_valid.clamp_min(1.0)
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, target, lse, n_valid = ctx.saved_tensors
+        gscale = torch.stack([g.float().reshape(()), n_valid]).contiguous()
+        d = _ext.load().ce_bwd(logits, target, lse, gscale, ctx.ignore_index)
+        return d, None, None
+
+
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100) -> torch.Tensor:
+    """Mean softmax cross-entropy over rows of ``logits`` [..., V] without materialising fp32
+    logits or log-probabilities: one read forward, one read + one write backward."""
+    V = logits.shape[-1]
+    l2 = logits.reshape(-1, V)
+    t = target.reshape(-1)
+    if not (logits.is_cuda and V % 8 == 0 and logits.dtype in (torch.bfloat16, torch.float16, torch.float32)):
+        return F.cross_entropy(l2.float(), t, ignore_index=ignore_index)
+    return _CrossEntropy.apply(l2.contiguous(), t.contiguous().long(), ignore_index)
+
+
+class _FlashAttentionQKVPacked(torch.autograd.Function):
+    """Attention on a fused QKV projection output [B, S, 3, H, D]: q/k/v are strided views and the
+    backward writes dQ/dK/dV straight into one packed gradient (no stack/cat)."""
+
+    @staticmethod
+    def forward(ctx, qkv, causal, scale):
+        q, k, v = qkv.unbind(2)
+        o, lse = _ext.load().attn_fwd(q, k, v, scale, causal)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        q, k, v = qkv.unbind(2)
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = dqkv.unbind(2)
+        _ext.load().attn_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal, dq, dk, dv)
+        return dqkv, None, None
+
+
+def flash_attention_qkvpacked(qkv: torch.Tensor, causal: bool = True,
+                              scale: Optional[float] = None) -> torch.Tensor:
+    """``flash_attention`` for a packed [B, S, 3, H, D] QKV tensor -> [B, S, H, D]."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(qkv.shape[-1])
+    if not qkv.is_cuda:
+        q, k, v = qkv.unbind(2)
+        return reference_attention(q, k, v, causal, scale)
+    q, k, v = qkv.unbind(2)
+    if not _attn_gpu_ok(q, k, v):
+        raise ValueError("flash_attention_qkvpacked: GPU path needs bf16 [B,S,3,H,D] with D in "
+                         "{64,128} and 16-byte aligned rows")
+    return _FlashAttentionQKVPacked.apply(qkv, causal, float(scale))
+
+
 def _attn_gpu_ok(q, k, v) -> bool:
     if not (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128)):
         return False
@@ -215,4 +280,5 @@ def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: b
 
 
 __all__ = ["layer_norm", "bias_gelu", "rope", "rope_tables", "flash_attention",
+           "flash_attention_qkvpacked", "cross_entropy",
            "reference_layer_norm", "reference_bias_gelu", "reference_rope", "reference_attention"]

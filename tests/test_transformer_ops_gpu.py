@@ -144,3 +144,36 @@ def test_flash_attention_matches_sdpa_speed_sanity():
         q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), is_causal=True).transpose(1, 2)
     assert _rel(o, ref) < 1e-2
     assert math.isfinite(o.float().abs().max().item())
+
+
+def test_flash_attention_qkvpacked_matches_unpacked():
+    _C()
+    torch.manual_seed(5)
+    B, S, H, D = 2, 192, 4, 64
+    qkv = torch.randn(B, S, 3, H, D, device="cuda").bfloat16().requires_grad_(True)
+    o = T.flash_attention_qkvpacked(qkv, causal=True)
+    qkv2 = qkv.detach().clone().requires_grad_(True)
+    o2 = T.flash_attention(*qkv2.unbind(2), causal=True)
+    torch.testing.assert_close(o, o2)
+    g = torch.randn_like(o)
+    o.backward(g)
+    o2.backward(g)
+    torch.testing.assert_close(qkv.grad, qkv2.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_fused_cross_entropy(dtype):
+    _C()
+    torch.manual_seed(6)
+    N, V = 300, 50304
+    logits = (torch.randn(N, V, device="cuda") * 3).to(dtype)
+    t = torch.randint(0, 50257, (N,), device="cuda")
+    t[::7] = -100
+    a = logits.clone().requires_grad_(True)
+    b = logits.float().clone().requires_grad_(True)
+    la = T.cross_entropy(a, t)
+    lb = torch.nn.functional.cross_entropy(b, t, ignore_index=-100)
+    torch.testing.assert_close(la, lb, atol=1e-3, rtol=1e-4)
+    (la * 3.0).backward()
+    (lb * 3.0).backward()
+    assert _rel(a.grad, b.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-5)
