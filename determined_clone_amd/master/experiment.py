@@ -20,8 +20,9 @@ from typing import Any, Dict, List, Optional
 
 from determined_clone_amd.master.db import DB, dec, now
 from determined_clone_amd.master.rm import AllocationRequest
-from determined_clone_amd.searcher import (Close, Create, ExitedReason, Searcher, Shutdown,
-                                           ValidateAfter, make_search_method)
+from determined_clone_amd.searcher import Searcher
+from determined_clone_amd.searcher.methods import (Close, Create, ExitedReason, Shutdown,
+                                                   ValidateAfter, make_search_method)
 
 logger = logging.getLogger("determined_clone_amd.master")
 
