@@ -52,3 +52,7 @@ class ForbiddenException(APIException):
 class UnauthenticatedException(APIException):
     def __init__(self, message: str = "unauthenticated") -> None:
         super().__init__(401, message)
+
+
+class DeterminedError(Exception):
+    """Generic client-side error (reference: det.common.api.errors.DeterminedError-style)."""
