@@ -1,0 +1,2 @@
+"""Hugging Face Trainer integration (reference: `harness/determined/transformers`)."""
+from determined_clone_amd.transformers._hf_callback import DetCallback, metric_kind
