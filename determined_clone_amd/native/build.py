@@ -10,6 +10,20 @@ import sysconfig
 HERE = pathlib.Path(__file__).resolve().parent
 SOURCES = [HERE / "scheduler.cpp"]
 TARGET = HERE / ("_native" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+PIDWATCH_SRC = HERE / "pidwatch.cpp"
+PIDWATCH = HERE / "bin" / "dca-pidwatch"
+
+
+def build_pidwatch(force: bool = False) -> pathlib.Path:
+    """Standalone launcher-side failure detector (no Python, no GPU)."""
+    if not force and PIDWATCH.exists() and PIDWATCH.stat().st_mtime >= PIDWATCH_SRC.stat().st_mtime:
+        return PIDWATCH
+    PIDWATCH.parent.mkdir(exist_ok=True)
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", str(PIDWATCH_SRC), "-o", str(PIDWATCH)]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("pidwatch build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return PIDWATCH
 
 
 def build(force: bool = False) -> pathlib.Path:
@@ -29,3 +43,4 @@ def build(force: bool = False) -> pathlib.Path:
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv))
+    print(build_pidwatch(force="--force" in sys.argv))
