@@ -7,12 +7,16 @@ from determined_clone_amd._info import ClusterInfo, RendezvousInfo, TrialInfo, g
 from determined_clone_amd.errors import InvalidHP
 from determined_clone_amd import errors, util
 
+# Log format whose level prefix the master's log viewer filters on (reference: det.LOG_FORMAT).
+LOG_FORMAT = "%(levelname)s: [%(process)s] %(name)s: %(message)s"
+
 
 def __getattr__(name: str):
     # Lazy subpackages so `import determined_clone_amd` stays light (CLI, master).
     import importlib
 
     if name in ("core", "pytorch", "searcher", "experimental", "tensorboard", "profiler",
-                "launch", "ops", "parallel", "models", "master", "agent", "cli", "config"):
+                "launch", "ops", "parallel", "models", "master", "agent", "cli", "config",
+                "transformers", "exec", "native", "common"):
         return importlib.import_module(f"determined_clone_amd.{name}")
     raise AttributeError(name)

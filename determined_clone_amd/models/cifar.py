@@ -1,0 +1,47 @@
+"""CIFAR-10 CNN used for the adaptive_asha search config (reference: the CIFAR-10 PyTorch example
+of the e2e fixtures / docs: 4 conv layers + dropout + 2 FC). NHWC bf16-friendly: the conv stack runs
+channels_last, BatchNorm+ReLU uses the fused HIP kernel on the GPU. Offline synthetic data."""
+from typing import Any, Dict
+
+import numpy as np
+import torch
+from torch import nn
+
+from determined_clone_amd.models.resnet import BatchNormAct2d
+
+
+class CifarCNN(nn.Module):
+    def __init__(self, hparams: Dict[str, Any]) -> None:
+        super().__init__()
+        w = int(hparams.get("width", 32))
+        d = float(hparams.get("dropout", 0.25))
+        self.features = nn.Sequential(
+            nn.Conv2d(3, w, 3, padding=1, bias=False), BatchNormAct2d(w),
+            nn.Conv2d(w, w, 3, padding=1, bias=False), BatchNormAct2d(w),
+            nn.MaxPool2d(2), nn.Dropout(d),
+            nn.Conv2d(w, 2 * w, 3, padding=1, bias=False), BatchNormAct2d(2 * w),
+            nn.Conv2d(2 * w, 2 * w, 3, padding=1, bias=False), BatchNormAct2d(2 * w),
+            nn.MaxPool2d(2), nn.Dropout(d),
+        )
+        self.head = nn.Sequential(nn.Flatten(), nn.Linear(2 * w * 8 * 8, int(hparams.get("hidden", 512))),
+                                  nn.ReLU(), nn.Dropout(float(hparams.get("dropout2", 0.5))),
+                                  nn.Linear(int(hparams.get("hidden", 512)), 10))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.head(self.features(x))
+
+
+class SyntheticCIFAR10(torch.utils.data.Dataset):
+    """Deterministic 32x32x3 class-conditional data (learnable)."""
+
+    def __init__(self, n: int, seed: int) -> None:
+        g = np.random.RandomState(seed)
+        proto = np.random.RandomState(99).randn(10, 3, 32, 32).astype(np.float32)
+        self.y = g.randint(0, 10, size=n).astype(np.int64)
+        self.x = proto[self.y] + g.randn(n, 3, 32, 32).astype(np.float32)
+
+    def __len__(self) -> int:
+        return len(self.y)
+
+    def __getitem__(self, i: int):
+        return torch.from_numpy(self.x[i]), int(self.y[i])

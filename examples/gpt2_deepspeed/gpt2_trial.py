@@ -1,0 +1,61 @@
+"""GPT-2 DeepSpeedTrial on the native ZeRO engine (reference: examples/deepspeed/gpt_neox/
+gpt2_trial.py, which drives GPT-NeoX through DeepSpeed; here ``det_ds.initialize`` builds the
+MI355X engine: ZeRO-1/2 over RCCL, fused HIP AdamW, MFMA flash attention, fused LN / GELU / CE).
+
+The DeepSpeed JSON config is ``ds_config.json`` overlaid with ``hyperparameters.overwrite_deepspeed_args``
+(same convention as the reference's ``overwrite_deepspeed_config``). Synthetic token data."""
+import json
+import os
+
+import torch
+
+from determined_clone_amd import pytorch
+from determined_clone_amd.models import gpt2
+from determined_clone_amd.pytorch import deepspeed as det_ds
+
+
+class TokenData(torch.utils.data.Dataset):
+    def __init__(self, n: int, seq: int, vocab: int, seed: int) -> None:
+        self.n, self.seq, self.vocab, self.seed = n, seq, vocab, seed
+
+    def __len__(self) -> int:
+        return self.n
+
+    def __getitem__(self, i: int):
+        g = torch.Generator().manual_seed(self.seed * 1000003 + i)
+        t = torch.randint(0, self.vocab, (self.seq + 1,), generator=g)
+        return t[:-1], t[1:]
+
+
+class GPT2Trial(det_ds.DeepSpeedTrial):
+    def __init__(self, context: det_ds.DeepSpeedTrialContext) -> None:
+        self.context = context
+        hp = context.get_hparams()
+        self.seq = int(hp.get("seq_len", 1024))
+        model = gpt2.gpt2(hp.get("model", "gpt2-medium"), max_seq_len=self.seq)
+        base = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "ds_config.json")))
+        ds_config = det_ds.overwrite_deepspeed_config(base, hp.get("overwrite_deepspeed_args", {}))
+        engine, _, _, _ = det_ds.initialize(model=model, config=ds_config)
+        self.engine = context.wrap_model_engine(engine)
+        self.vocab = model.cfg.vocab_size
+
+    def train_batch(self, it, epoch_idx, batch_idx):
+        x, y = self.context.to_device(next(it))
+        _, loss = self.engine(x, y)
+        self.engine.backward(loss)
+        self.engine.step()
+        return {"loss": loss}
+
+    def evaluate_batch(self, it, batch_idx):
+        x, y = self.context.to_device(next(it))
+        with torch.no_grad():
+            _, loss = self.engine(x, y)
+        return {"lm_loss": loss}
+
+    def build_training_data_loader(self):
+        return pytorch.DataLoader(TokenData(1 << 20, self.seq, self.vocab, 0),
+                                  batch_size=self.context.train_micro_batch_size_per_gpu)
+
+    def build_validation_data_loader(self):
+        return pytorch.DataLoader(TokenData(64, self.seq, self.vocab, 1),
+                                  batch_size=self.context.train_micro_batch_size_per_gpu)
