@@ -1,0 +1,3 @@
+"""Experimental PyTorch APIs (reference: `harness/determined/pytorch/experimental`)."""
+from determined_clone_amd.pytorch.experimental._torch_batch_process import (
+    TorchBatchProcessor, TorchBatchProcessorContext, get_default_device, torch_batch_process)
