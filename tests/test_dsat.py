@@ -1,0 +1,108 @@
+"""DeepSpeed autotune (dsat): binary search over (ZeRO stage, micro batch) against an in-process
+master + CPU agent; a fake OOM above micro batch 8 exercises the failure path."""
+import os
+import shutil
+import tempfile
+
+import pytest
+import yaml
+
+from determined_clone_amd.agent import Agent
+from determined_clone_amd.common.api import Session
+from determined_clone_amd.master import Master, MasterServer
+from determined_clone_amd.pytorch.dsat import DSATSearchMethod
+from determined_clone_amd.pytorch.dsat import __main__ as dsat_main
+
+MODEL_DEF = '''
+import torch
+from determined_clone_amd import pytorch
+from determined_clone_amd.pytorch import deepspeed as det_ds
+
+class Data(torch.utils.data.Dataset):
+    def __len__(self):
+        return 4096
+    def __getitem__(self, i):
+        return torch.randn(8), torch.randn(1)
+
+class DSTrial(det_ds.DeepSpeedTrial):
+    def __init__(self, context):
+        self.context = context
+        cfg = det_ds.overwrite_deepspeed_config(
+            {"train_micro_batch_size_per_gpu": 1, "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}},
+            context.get_hparams().get("overwrite_deepspeed_args", {}))
+        engine, _, _, _ = det_ds.initialize(model=torch.nn.Linear(8, 1), config=cfg)
+        self.engine = context.wrap_model_engine(engine)
+    def train_batch(self, it, epoch_idx, batch_idx):
+        if self.context.train_micro_batch_size_per_gpu > 8:
+            raise torch.cuda.OutOfMemoryError("fake OOM")
+        x, y = next(it)
+        loss = torch.nn.functional.mse_loss(self.engine(x), y)
+        self.engine.backward(loss)
+        self.engine.step()
+        return {"loss": loss}
+    def evaluate_batch(self, it, batch_idx):
+        x, y = next(it)
+        return {"val_loss": torch.nn.functional.mse_loss(self.engine(x), y)}
+    def build_training_data_loader(self):
+        return pytorch.DataLoader(Data(), batch_size=self.context.train_micro_batch_size_per_gpu)
+    def build_validation_data_loader(self):
+        return pytorch.DataLoader(Data(), batch_size=4)
+'''
+
+
+def test_binary_search_space_logic():
+    m = DSATSearchMethod({}, "binary", zero_stages=(1,), max_trials=20, max_concurrent_trials=1, max_mbs=64)
+    proposals = []
+    # simulate: mbs <= 12 fits
+    import uuid
+
+    ops = m.initial_operations(None)
+    while ops:
+        creates = [o for o in ops if o.kind == "Create"]
+        nxt = []
+        for c in creates:
+            mbs = c.hparams["overwrite_deepspeed_args"]["train_micro_batch_size_per_gpu"]
+            proposals.append(mbs)
+            rid = uuid.UUID(str(c.request_id))
+            if mbs <= 12:
+                nxt += m.on_validation_completed(None, rid, float(mbs), 5)
+            else:
+                nxt += m.on_trial_exited_early(None, rid, "INVALID_HP")
+        ops = [o for o in nxt if o.kind == "Create"]
+    assert proposals[:5] == [1, 2, 4, 8, 16]
+    assert m.best()["train_micro_batch_size_per_gpu"] == 12
+
+
+@pytest.fixture()
+def cluster():
+    tmp = tempfile.mkdtemp(prefix="det-dsat-")
+    m = Master(os.path.join(tmp, "m.db"), checkpoint_storage={"type": "shared_fs", "host_path": os.path.join(tmp, "ckpt")})
+    srv = MasterServer(m, "127.0.0.1", 0).start()
+    agent = Agent(m.master_url, "agent-0", artificial_slots=2).start_background()
+    s = Session(m.master_url)
+    s.token = s.post("/api/v1/auth/login", {"username": "admin", "password": ""})["token"]
+    ctx = os.path.join(tmp, "ctx")
+    os.makedirs(ctx)
+    with open(os.path.join(ctx, "model_def.py"), "w") as f:
+        f.write(MODEL_DEF)
+    yield s, ctx, tmp
+    agent.stop()
+    srv.stop()
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_dsat_cli_on_cluster(cluster, capsys):
+    s, ctx, tmp = cluster
+    cfg_path = os.path.join(tmp, "cfg.yaml")
+    with open(cfg_path, "w") as f:
+        yaml.safe_dump({"name": "dsat", "entrypoint": "model_def:DSTrial", "hyperparameters": {},
+                        "max_restarts": 0}, f)
+    rc = dsat_main.main(["binary", cfg_path, ctx, "-z", "1", "-mt", "8", "-mct", "2",
+                         "--start-profile-step", "1", "--end-profile-step", "3", "--max-mbs", "32",
+                         "--searcher-dir", os.path.join(tmp, "dsat")], session=s)
+    assert rc == 0
+    import json
+
+    out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert out["best"]["train_micro_batch_size_per_gpu"] == 8
+    assert any(t["oom"] for t in out["trials"])
