@@ -12,7 +12,7 @@ import socket
 import struct
 import threading
 import time
-from typing import Any, Callable, Dict, Optional
+from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 
 # ----------------------------------------------------------------------------- CRC32C
 _CRC_TABLE = []
@@ -182,3 +182,83 @@ def build(cluster_id: str, experiment_id: str, trial_id: str, storage_config: Di
 
 def get_metric_writer(logdir: str) -> MetricWriter:
     return MetricWriter(logdir)
+
+
+# ------------------------------------------------------------------ reading (no TF/TB dependency)
+def _read_varint(buf: bytes, i: int) -> Tuple[int, int]:
+    shift = result = 0
+    while True:
+        b = buf[i]
+        i += 1
+        result |= (b & 0x7F) << shift
+        if not b & 0x80:
+            return result, i
+        shift += 7
+
+
+def _fields(buf: bytes) -> Iterator[Tuple[int, int, Any]]:
+    """(field number, wire type, value) of a protobuf message; length-delimited values are bytes."""
+    i = 0
+    while i < len(buf):
+        key, i = _read_varint(buf, i)
+        num, wire = key >> 3, key & 7
+        if wire == 0:
+            v, i = _read_varint(buf, i)
+        elif wire == 1:
+            v = buf[i:i + 8]
+            i += 8
+        elif wire == 2:
+            n, i = _read_varint(buf, i)
+            v = buf[i:i + n]
+            i += n
+        elif wire == 5:
+            v = buf[i:i + 4]
+            i += 4
+        else:
+            raise ValueError(f"unsupported wire type {wire}")
+        yield num, wire, v
+
+
+def decode_scalar_event(record: bytes) -> List[Tuple[str, int, float, float]]:
+    """Event{wall_time=1, step=2, summary=5{value=1{tag=1, simple_value=2}}} -> [(tag, step,
+    wall_time, value)]."""
+    wall, step, out = 0.0, 0, []
+    summaries = []
+    for num, wire, v in _fields(record):
+        if num == 1 and wire == 1:
+            (wall,) = struct.unpack("<d", v)
+        elif num == 2 and wire == 0:
+            step = v
+        elif num == 5 and wire == 2:
+            summaries.append(v)
+    for s in summaries:
+        for num, wire, v in _fields(s):
+            if num != 1 or wire != 2:
+                continue
+            tag, val = None, None
+            for n2, w2, v2 in _fields(v):
+                if n2 == 1 and w2 == 2:
+                    tag = v2.decode("utf-8", "replace")
+                elif n2 == 2 and w2 == 5:
+                    (val,) = struct.unpack("<f", v2)
+            if tag is not None and val is not None:
+                out.append((tag, int(step), float(wall), float(val)))
+    return out
+
+
+def read_scalars(logdir: str) -> Dict[str, Dict[str, List[Tuple[int, float, float]]]]:
+    """{run (relative dir): {tag: [(step, wall_time, value)]}} for every event file under logdir."""
+    runs: Dict[str, Dict[str, List[Tuple[int, float, float]]]] = {}
+    for root, _dirs, files in os.walk(logdir):
+        for fn in sorted(files):
+            if "tfevents" not in fn:
+                continue
+            run = os.path.relpath(root, logdir)
+            tags = runs.setdefault(run, {})
+            for rec in read_records(os.path.join(root, fn)):
+                for tag, step, wall, val in decode_scalar_event(rec):
+                    tags.setdefault(tag, []).append((step, wall, val))
+    for tags in runs.values():
+        for series in tags.values():
+            series.sort()
+    return runs
