@@ -33,7 +33,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
         super().__init__(num_features, eps=eps, momentum=momentum)
         self.relu = relu
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                fuse_residual_grad: bool = False) -> torch.Tensor:
         return bn_ops.batch_norm_act(
             x,
             self.weight,
@@ -46,6 +47,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
             eps=self.eps,
             relu=self.relu,
             num_batches_tracked=self.num_batches_tracked,
+            fuse_residual_grad=fuse_residual_grad,
         )
 
 
@@ -75,7 +77,9 @@ class Bottleneck(nn.Module):
         identity = x if self.downsample is None else self.downsample(x)
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), residual=identity)
+        # identity shortcut: x also feeds conv1, so its gradient can be summed inside the
+        # producer's BN backward (no separate autograd add)
+        return self.bn3(self.conv3(out), residual=identity, fuse_residual_grad=self.downsample is None)
 
 
 class ResNet(nn.Module):
@@ -109,7 +113,13 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn3.weight)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        # stem: conv -> fused BN + ReLU + 3x3/2 max-pool (the 112x112 pre-pool activation is never
+        # written; its gradient is gathered inside the BN backward)
+        bn = self.bn1
+        x = bn_ops.batch_norm_relu_maxpool(self.conv1(x), bn.weight, bn.bias, bn.running_mean,
+                                           bn.running_var, training=bn.training,
+                                           momentum=bn.momentum, eps=bn.eps,
+                                           num_batches_tracked=bn.num_batches_tracked)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

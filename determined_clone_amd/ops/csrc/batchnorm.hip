@@ -44,9 +44,9 @@ inline ReduceGeom reduce_geom(int C) {
 
 template <typename T, bool BWD>
 __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
-    const void* __restrict__ x, const void* __restrict__ dy, const uint8_t* __restrict__ mask,
-    const float* __restrict__ mean, int64_t M, int C, int tpr, int rpi, bool relu,
-    float* __restrict__ partial) {
+    const void* __restrict__ x, const void* __restrict__ dy, const void* __restrict__ dy2,
+    const uint8_t* __restrict__ mask, const float* __restrict__ mean, int64_t M, int C, int tpr,
+    int rpi, bool relu, float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][tpr*16]
   const int tid = threadIdx.x;
   const int lc = tid % tpr, r0 = tid / tpr;
@@ -62,7 +62,45 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
   }
   if (active) {
     const int64_t stride = static_cast<int64_t>(gridDim.x) * rpi;
-    for (int64_t r = static_cast<int64_t>(blockIdx.x) * rpi + r0; r < M; r += stride) {
+    int64_t r = static_cast<int64_t>(blockIdx.x) * rpi + r0;
+    // 4 rows in flight per thread (independent 16-B loads) before any accumulation, so each wave
+    // keeps several HBM requests outstanding instead of one load -> use -> load chain.
+    constexpr int U = BWD ? 2 : 4;
+    for (; r + (U - 1) * stride < M; r += U * stride) {
+      float xv[U][8];
+      float g[U][8];
+      uint32_t mk[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t off = (r + u * stride) * C + c;
+        Vec8<T>::load(reinterpret_cast<const char*>(x) + off * Vec8<T>::bytes, xv[u]);
+        if (BWD) {
+          Vec8<T>::load(reinterpret_cast<const char*>(dy) + off * Vec8<T>::bytes, g[u]);
+          if (dy2) {
+            float g2[8];
+            Vec8<T>::load(reinterpret_cast<const char*>(dy2) + off * Vec8<T>::bytes, g2);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) g[u][k] += g2[k];
+          }
+          mk[u] = relu ? mask[off >> 3] : 0xffu;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!BWD) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { s[k] += xv[u][k]; q[k] = fmaf(xv[u][k], xv[u][k], q[k]); }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float gk = ((mk[u] >> k) & 1u) ? g[u][k] : 0.f;
+            s[k] += gk;
+            q[k] = fmaf(gk, xv[u][k] - mu[k], q[k]);
+          }
+        }
+      }
+    }
+    for (; r < M; r += stride) {
       const int64_t off = r * C + c;
       float xv[8];
       Vec8<T>::load(reinterpret_cast<const char*>(x) + off * Vec8<T>::bytes, xv);
@@ -72,6 +110,12 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
       } else {
         float g[8];
         Vec8<T>::load(reinterpret_cast<const char*>(dy) + off * Vec8<T>::bytes, g);
+        if (dy2) {
+          float g2[8];
+          Vec8<T>::load(reinterpret_cast<const char*>(dy2) + off * Vec8<T>::bytes, g2);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[k] += g2[k];
+        }
         if (relu) {
           const uint32_t m = mask[off >> 3];  // one ReLU bit per element, 8 channels per byte
 #pragma unroll
@@ -107,10 +151,25 @@ __device__ __forceinline__ void combine_partials(const float* __restrict__ parti
   const int ch = blockIdx.x * 8 + cl;
   double s = 0.0, q = 0.0;
   if (ch < C) {
-    for (int b = sl; b < B; b += 32) {
-      s += partial[(static_cast<int64_t>(b) * 2) * C + ch];
-      q += partial[(static_cast<int64_t>(b) * 2 + 1) * C + ch];
+    // 4 independent partial rows in flight per thread (latency-bound otherwise)
+    float fs[4] = {0.f, 0.f, 0.f, 0.f}, fq[4] = {0.f, 0.f, 0.f, 0.f};
+    double ds[4] = {0.0, 0.0, 0.0, 0.0}, dq[4] = {0.0, 0.0, 0.0, 0.0};
+    int b = sl;
+    for (; b + 96 < B; b += 128) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        fs[u] = partial[(static_cast<int64_t>(b + 32 * u) * 2) * C + ch];
+        fq[u] = partial[(static_cast<int64_t>(b + 32 * u) * 2 + 1) * C + ch];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { ds[u] += fs[u]; dq[u] += fq[u]; }
     }
+    for (; b < B; b += 32) {
+      ds[0] += partial[(static_cast<int64_t>(b) * 2) * C + ch];
+      dq[0] += partial[(static_cast<int64_t>(b) * 2 + 1) * C + ch];
+    }
+    s = (ds[0] + ds[1]) + (ds[2] + ds[3]);
+    q = (dq[0] + dq[1]) + (dq[2] + dq[3]);
   }
   red[tid] = s;
   red[256 + tid] = q;
@@ -216,9 +275,9 @@ __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
-    const void* __restrict__ dy, const uint8_t* __restrict__ mask, const void* __restrict__ x,
-    const float* __restrict__ coef, void* __restrict__ dx, void* __restrict__ dres, int64_t nvec,
-    int c8, int C, bool relu) {
+    const void* __restrict__ dy, const void* __restrict__ dy2, const uint8_t* __restrict__ mask,
+    const void* __restrict__ x, const float* __restrict__ coef, void* __restrict__ dx,
+    void* __restrict__ dres, int64_t nvec, int c8, int C, bool relu) {
   // nvec < 2^31 is checked on the host: 32-bit index math (a 64-bit modulo is a long
   // software sequence on CDNA), 64-bit byte offsets.
   const uint32_t stride = gridDim.x * blockDim.x, n = static_cast<uint32_t>(nvec);
@@ -227,6 +286,12 @@ __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
     const int64_t off = static_cast<int64_t>(v) * 8 * Vec8<T>::bytes;
     float g[8], xv[8];
     Vec8<T>::load(reinterpret_cast<const char*>(dy) + off, g);
+    if (dy2) {
+      float g2[8];
+      Vec8<T>::load(reinterpret_cast<const char*>(dy2) + off, g2);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] += g2[k];
+    }
     if (relu) {
       const uint32_t m = mask[v];
 #pragma unroll
@@ -255,17 +320,168 @@ inline int reduce_blocks(int64_t M, int C, const ReduceGeom& g) {
 }
 
 template <typename T>
-void launch_reduce(bool bwd, const void* x, const void* dy, const uint8_t* y, const float* mean,
+void launch_reduce(bool bwd, const void* x, const void* dy, const void* dy2, const uint8_t* y,
+                   const float* mean,
                    int64_t M, int C, bool relu, float* partial, int B, const ReduceGeom& g,
                    hipStream_t st) {
   dim3 grid(B, g.cgroups);
   size_t lds = static_cast<size_t>(g.rpi) * g.tpr * 16 * sizeof(float);
   if (bwd)
-    hipLaunchKernelGGL((bn_reduce_kernel<T, true>), grid, dim3(kBlock), lds, st, x, dy, y, mean,
-                       M, C, g.tpr, g.rpi, relu, partial);
+    hipLaunchKernelGGL((bn_reduce_kernel<T, true>), grid, dim3(kBlock), lds, st, x, dy, dy2, y,
+                       mean, M, C, g.tpr, g.rpi, relu, partial);
   else
-    hipLaunchKernelGGL((bn_reduce_kernel<T, false>), grid, dim3(kBlock), lds, st, x, dy, y, mean,
-                       M, C, g.tpr, g.rpi, relu, partial);
+    hipLaunchKernelGGL((bn_reduce_kernel<T, false>), grid, dim3(kBlock), lds, st, x, dy, dy2, y,
+                       mean, M, C, g.tpr, g.rpi, relu, partial);
+}
+
+
+// ------------------------------------------------------------------ stem: BN + ReLU + MaxPool(3,2,1)
+// ResNet stem fusion: the pre-pool activation (N x 112 x 112 x 64 for ImageNet -- the largest
+// tensor of the network) is never written. Forward writes the pooled output and one byte per
+// pooled element: window slot (0..8) of the max | 0x10 if the max is > 0 (i.e. the ReLU passed).
+// Backward re-derives the pre-pool gradient on the fly by GATHER (each input position is covered
+// by at most 2x2 pooling windows) inside the BN-backward reduce/apply passes, instead of a zero-fill
+// + scatter max-pool backward followed by a full-size BN backward read.
+struct PoolGeom {
+  int H, W, Ho, Wo;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_relu_pool_fwd_kernel(
+    const void* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
+    void* __restrict__ y, uint8_t* __restrict__ idx, int64_t nout, int C, PoolGeom g) {
+  const int c8 = C / 8;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < nout;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(t % c8) * 8;
+    const int64_t o = t / c8;  // (n, ho, wo)
+    const int wo = static_cast<int>(o % g.Wo);
+    const int ho = static_cast<int>((o / g.Wo) % g.Ho);
+    const int64_t n = o / (static_cast<int64_t>(g.Wo) * g.Ho);
+    float a[8], b[8], best[8];
+    uint32_t slot[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { a[k] = scale[c + k]; b[k] = shift[c + k]; best[k] = 0.f; slot[k] = 0xff; }
+    for (int kh = 0; kh < 3; ++kh) {
+      const int h = 2 * ho - 1 + kh;
+      if (h < 0 || h >= g.H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int w = 2 * wo - 1 + kw;
+        if (w < 0 || w >= g.W) continue;
+        float v[8];
+        Vec8<T>::load(reinterpret_cast<const char*>(x) +
+                          (((n * g.H + h) * g.W + w) * C + c) * Vec8<T>::bytes, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float r = fmaxf(fmaf(v[k], a[k], b[k]), 0.f);
+          // first maximum wins (matches max_pool2d over the ReLU output)
+          if (slot[k] == 0xff || r > best[k]) { best[k] = r; slot[k] = kh * 3 + kw; }
+        }
+      }
+    }
+    Vec8<T>::store(reinterpret_cast<char*>(y) + t * 8 * Vec8<T>::bytes, best);
+    if (idx) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lo |= ((slot[k] | (best[k] > 0.f ? 0x10u : 0u)) & 0xffu) << (8 * k);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) hi |= ((slot[4 + k] | (best[4 + k] > 0.f ? 0x10u : 0u)) & 0xffu) << (8 * k);
+      *reinterpret_cast<uint2*>(idx + t * 8) = make_uint2(lo, hi);
+    }
+  }
+}
+
+// Pre-pool gradient of 8 channels at input position (n, h, w): sum of pooled gradients whose
+// argmax is this position and whose ReLU passed.
+template <typename T>
+__device__ __forceinline__ void gather_pool_grad(const void* __restrict__ dyp, const uint8_t* __restrict__ idx,
+                                                 int64_t n, int h, int w, int c, int C, const PoolGeom& g,
+                                                 float* out) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = 0.f;
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh) {
+    const int ho = (h + 1) / 2 - dh;
+    const int kh = h - 2 * ho + 1;
+    if (ho < 0 || ho >= g.Ho || kh > 2) continue;
+#pragma unroll
+    for (int dw = 0; dw < 2; ++dw) {
+      const int wo = (w + 1) / 2 - dw;
+      const int kw = w - 2 * wo + 1;
+      if (wo < 0 || wo >= g.Wo || kw > 2) continue;
+      const uint32_t want = static_cast<uint32_t>(kh * 3 + kw) | 0x10u;
+      const int64_t off = ((n * g.Ho + ho) * g.Wo + wo) * C + c;
+      const uint2 ib = *reinterpret_cast<const uint2*>(idx + off);
+      float d[8];
+      Vec8<T>::load(reinterpret_cast<const char*>(dyp) + off * Vec8<T>::bytes, d);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t byte = ((k < 4 ? ib.x : ib.y) >> (8 * (k & 3))) & 0xffu;
+        if (byte == want) out[k] += d[k];
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_pool_reduce_bwd_kernel(
+    const void* __restrict__ x, const void* __restrict__ dyp, const uint8_t* __restrict__ idx,
+    const float* __restrict__ mean, int64_t M, int C, int tpr, int rpi, PoolGeom g,
+    float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x;
+  const int lc = tid % tpr, r0 = tid / tpr;
+  const int c = (blockIdx.y * tpr + lc) * 8;
+  const bool active = c < C;
+  float s[8], q[8], mu[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; mu[k] = active ? mean[c + k] : 0.f; }
+  if (active) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * rpi;
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * rpi + r0; r < M; r += stride) {
+      const int w = static_cast<int>(r % g.W);
+      const int h = static_cast<int>((r / g.W) % g.H);
+      const int64_t n = r / (static_cast<int64_t>(g.W) * g.H);
+      float gr[8], xv[8];
+      gather_pool_grad<T>(dyp, idx, n, h, w, c, C, g, gr);
+      Vec8<T>::load(reinterpret_cast<const char*>(x) + (r * C + c) * Vec8<T>::bytes, xv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s[k] += gr[k]; q[k] = fmaf(gr[k], xv[k] - mu[k], q[k]); }
+    }
+  }
+  const int width = tpr * 16;
+  float* mine = lds + r0 * width + lc * 16;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { mine[k] = s[k]; mine[8 + k] = q[k]; }
+  __syncthreads();
+  for (int o = tid; o < width; o += kBlock) {
+    float acc = 0.f;
+    for (int r = 0; r < rpi; ++r) acc += lds[r * width + o];
+    const int lco = o / 16, k = o % 16;
+    const int ch = (blockIdx.y * tpr + lco) * 8 + (k & 7);
+    if (ch < C) partial[(static_cast<int64_t>(blockIdx.x) * 2 + (k >> 3)) * C + ch] = acc;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_pool_apply_bwd_kernel(
+    const void* __restrict__ x, const void* __restrict__ dyp, const uint8_t* __restrict__ idx,
+    const float* __restrict__ coef, void* __restrict__ dx, int64_t nvec, int C, PoolGeom g) {
+  const int c8 = C / 8;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
+       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(v % c8) * 8;
+    const int64_t r = v / c8;
+    const int w = static_cast<int>(r % g.W);
+    const int h = static_cast<int>((r / g.W) % g.H);
+    const int64_t n = r / (static_cast<int64_t>(g.W) * g.H);
+    float gr[8], xv[8], o[8];
+    gather_pool_grad<T>(dyp, idx, n, h, w, c, C, g, gr);
+    Vec8<T>::load(reinterpret_cast<const char*>(x) + v * 8 * Vec8<T>::bytes, xv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = fmaf(coef[c + k], gr[k], fmaf(coef[C + c + k], xv[k], coef[2 * C + c + k]));
+    Vec8<T>::store(reinterpret_cast<char*>(dx) + v * 8 * Vec8<T>::bytes, o);
+  }
 }
 
 }  // namespace
@@ -288,9 +504,9 @@ void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64
   float* scale = workspace + static_cast<int64_t>(B) * 2 * C;
   float* shift = scale + C;
   switch (dt) {
-    case BnDtype::kBF16: launch_reduce<BF16>(false, x, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
-    case BnDtype::kF16: launch_reduce<F16>(false, x, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
-    default: launch_reduce<F32>(false, x, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
+    case BnDtype::kBF16: launch_reduce<BF16>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
+    case BnDtype::kF16: launch_reduce<F16>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
+    default: launch_reduce<F32>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
   }
   hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
                      C, M, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
@@ -317,7 +533,8 @@ void bn_forward_affine(BnDtype dt, const void* x, const void* res, void* y, int6
   }
 }
 
-void bn_backward_train(BnDtype dt, const void* dy, const uint8_t* y, const void* x, int64_t M, int C,
+void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_t* y, const void* x,
+                       int64_t M, int C,
                        const float* gamma, const float* save_mean, const float* save_invstd,
                        bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
                        float* workspace, hipStream_t st) {
@@ -326,18 +543,81 @@ void bn_backward_train(BnDtype dt, const void* dy, const uint8_t* y, const void*
   float* partial = workspace;
   float* coef = workspace + static_cast<int64_t>(B) * 2 * C;  // [3][C]
   switch (dt) {
-    case BnDtype::kBF16: launch_reduce<BF16>(true, x, dy, y, save_mean, M, C, relu, partial, B, g, st); break;
-    case BnDtype::kF16: launch_reduce<F16>(true, x, dy, y, save_mean, M, C, relu, partial, B, g, st); break;
-    default: launch_reduce<F32>(true, x, dy, y, save_mean, M, C, relu, partial, B, g, st); break;
+    case BnDtype::kBF16: launch_reduce<BF16>(true, x, dy, dy2, y, save_mean, M, C, relu, partial, B, g, st); break;
+    case BnDtype::kF16: launch_reduce<F16>(true, x, dy, dy2, y, save_mean, M, C, relu, partial, B, g, st); break;
+    default: launch_reduce<F32>(true, x, dy, dy2, y, save_mean, M, C, relu, partial, B, g, st); break;
   }
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
                      C, M, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
   const int64_t nvec = M * C / 8;
   const int grid = stream_grid(nvec, kBlock);
   switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_bwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, dy, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
-    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_bwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, dy, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
-    default: hipLaunchKernelGGL(bn_apply_bwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, dy, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_bwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, dy, dy2, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_bwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, dy, dy2, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
+    default: hipLaunchKernelGGL(bn_apply_bwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, dy, dy2, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
+  }
+}
+
+void bn_relu_pool_forward(BnDtype dt, const void* x, void* y, uint8_t* idx, int N, int H, int W,
+                          int C, const float* gamma, const float* beta, float* running_mean,
+                          float* running_var, float momentum, float eps, float* save_mean,
+                          float* save_invstd, int64_t* num_batches, float* workspace,
+                          const float* affine_scale, const float* affine_shift, hipStream_t st) {
+  const PoolGeom g{H, W, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
+  const int64_t M = static_cast<int64_t>(N) * H * W;
+  const float* scale = affine_scale;
+  const float* shift = affine_shift;
+  if (scale == nullptr) {  // training: batch statistics
+    ReduceGeom rg = reduce_geom(C);
+    int B = reduce_blocks(M, C, rg);
+    float* partial = workspace;
+    float* sc = workspace + static_cast<int64_t>(B) * 2 * C;
+    float* sh = sc + C;
+    switch (dt) {
+      case BnDtype::kBF16: launch_reduce<BF16>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, rg, st); break;
+      case BnDtype::kF16: launch_reduce<F16>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, rg, st); break;
+      default: launch_reduce<F32>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, rg, st); break;
+    }
+    hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
+                       C, M, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
+                       save_invstd, sc, sh, num_batches);
+    scale = sc;
+    shift = sh;
+  }
+  const int64_t nout = static_cast<int64_t>(N) * g.Ho * g.Wo * C / 8;
+  const int grid = stream_grid(nout, kBlock);
+  switch (dt) {
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_relu_pool_fwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nout, C, g); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_relu_pool_fwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nout, C, g); break;
+    default: hipLaunchKernelGGL(bn_relu_pool_fwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nout, C, g); break;
+  }
+}
+
+void bn_relu_pool_backward(BnDtype dt, const void* dyp, const uint8_t* idx, const void* x, int N,
+                           int H, int W, int C, const float* gamma, const float* save_mean,
+                           const float* save_invstd, void* dx, float* dgamma, float* dbeta,
+                           float* workspace, hipStream_t st) {
+  const PoolGeom g{H, W, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
+  const int64_t M = static_cast<int64_t>(N) * H * W;
+  ReduceGeom rg = reduce_geom(C);
+  int B = reduce_blocks(M, C, rg);
+  float* partial = workspace;
+  float* coef = workspace + static_cast<int64_t>(B) * 2 * C;
+  dim3 grid(B, rg.cgroups);
+  size_t lds = static_cast<size_t>(rg.rpi) * rg.tpr * 16 * sizeof(float);
+  switch (dt) {
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_pool_reduce_bwd_kernel<BF16>, grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_pool_reduce_bwd_kernel<F16>, grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
+    default: hipLaunchKernelGGL(bn_pool_reduce_bwd_kernel<F32>, grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
+  }
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
+                     C, M, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+  const int64_t nvec = M * C / 8;
+  const int ag = stream_grid(nvec, kBlock);
+  switch (dt) {
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_pool_apply_bwd_kernel<BF16>, dim3(ag), dim3(kBlock), 0, st, x, dyp, idx, coef, dx, nvec, C, g); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_pool_apply_bwd_kernel<F16>, dim3(ag), dim3(kBlock), 0, st, x, dyp, idx, coef, dx, nvec, C, g); break;
+    default: hipLaunchKernelGGL(bn_pool_apply_bwd_kernel<F32>, dim3(ag), dim3(kBlock), 0, st, x, dyp, idx, coef, dx, nvec, C, g); break;
   }
 }
 

@@ -20,8 +20,17 @@ void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64
                       hipStream_t st);
 void bn_forward_affine(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
                        const float* scale, const float* shift, bool relu, hipStream_t st);
-void bn_backward_train(BnDtype dt, const void* dy, const uint8_t* mask, const void* x, int64_t M, int C,
-                       const float* gamma, const float* save_mean, const float* save_invstd,
+void bn_relu_pool_forward(BnDtype dt, const void* x, void* y, uint8_t* idx, int N, int H, int W,
+                          int C, const float* gamma, const float* beta, float* running_mean,
+                          float* running_var, float momentum, float eps, float* save_mean,
+                          float* save_invstd, int64_t* num_batches, float* workspace,
+                          const float* affine_scale, const float* affine_shift, hipStream_t st);
+void bn_relu_pool_backward(BnDtype dt, const void* dyp, const uint8_t* idx, const void* x, int N,
+                           int H, int W, int C, const float* gamma, const float* save_mean,
+                           const float* save_invstd, void* dx, float* dgamma, float* dbeta,
+                           float* workspace, hipStream_t st);
+void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_t* mask, const void* x,
+                       int64_t M, int C, const float* gamma, const float* save_mean, const float* save_invstd,
                        bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
                        float* workspace, hipStream_t st);
 
@@ -145,12 +154,18 @@ Tensor bn_fwd_affine(const Tensor& x, const OptT& residual, const Tensor& scale,
 std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const OptT& mask,
                                  const OptT& weight, const Tensor& save_mean,
                                  const Tensor& save_invstd, bool relu, bool need_dres,
-                                 bool need_dweight) {
+                                 bool need_dweight, const OptT& dy2_in) {
   CHECK_DEV(x);
   const c10::DeviceGuard guard(x.device());
   auto [M, C] = rows_channels(x);
   Tensor dy = dy_in.dim() == 4 ? dy_in.contiguous(at::MemoryFormat::ChannelsLast) : dy_in.contiguous();
   TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "batchnorm bwd: grad dtype mismatch");
+  // optional second upstream gradient (the residual branch of the consumer), summed in-kernel
+  Tensor dy2;
+  if (dy2_in.has_value() && dy2_in->defined()) {
+    dy2 = dy2_in->dim() == 4 ? dy2_in->contiguous(at::MemoryFormat::ChannelsLast) : dy2_in->contiguous();
+    TORCH_CHECK(dy2.sizes() == x.sizes() && dy2.scalar_type() == x.scalar_type(), "batchnorm bwd: dy2 mismatch");
+  }
   TORCH_CHECK(!relu || (mask.has_value() && mask->defined() && mask->numel() == M * C / 8),
               "batchnorm bwd: relu needs the forward's ReLU bitmask");
   auto fopt = x.options().dtype(at::kFloat);
@@ -159,7 +174,8 @@ std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const Opt
   Tensor dgamma = need_dweight ? torch::empty({C}, fopt) : Tensor();
   Tensor dbeta = need_dweight ? torch::empty({C}, fopt) : Tensor();
   Tensor ws = torch::empty({dca::bn_workspace_floats(M, C)}, fopt);
-  dca::bn_backward_train(bn_dtype(x), dy.data_ptr(), relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(),
+  dca::bn_backward_train(bn_dtype(x), dy.data_ptr(), dy2.defined() ? dy2.data_ptr() : nullptr,
+                         relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(),
                          M, C, ptr_or_null<float>(weight), save_mean.data_ptr<float>(),
                          save_invstd.data_ptr<float>(), relu, dx.data_ptr(),
                          need_dres ? dres.data_ptr() : nullptr,
@@ -167,6 +183,68 @@ std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const Opt
                          need_dweight ? dbeta.data_ptr<float>() : nullptr, ws.data_ptr<float>(),
                          cur_stream());
   return {dx, dgamma, dbeta, dres};
+}
+
+// Stem fusion: act(bn(x)) -> max_pool2d(3, 2, 1) without materialising the pre-pool tensor.
+// x: NHWC (channels_last) [N, C, H, W]. Returns (y_pool, save_mean, save_invstd, idx).
+std::vector<Tensor> bn_pool_fwd_train(const Tensor& x, const OptT& weight, const OptT& bias,
+                                      const OptT& running_mean, const OptT& running_var,
+                                      const OptT& num_batches, double momentum, double eps) {
+  CHECK_DEV(x);
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0,
+              "bn_pool: channels_last [N, C%8==0, H, W] input required");
+  const c10::DeviceGuard guard(x.device());
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor y = torch::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor idx = torch::empty({static_cast<int64_t>(N) * Ho * Wo * C}, x.options().dtype(at::kByte));
+  Tensor save_mean = torch::empty({C}, fopt), save_invstd = torch::empty({C}, fopt);
+  Tensor ws = torch::empty({dca::bn_workspace_floats(static_cast<int64_t>(N) * H * W, C)}, fopt);
+  dca::bn_relu_pool_forward(bn_dtype(x), x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), N, H, W, C,
+                            ptr_or_null<float>(weight), ptr_or_null<float>(bias),
+                            ptr_or_null<float>(running_mean), ptr_or_null<float>(running_var),
+                            static_cast<float>(momentum), static_cast<float>(eps),
+                            save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
+                            ptr_or_null<int64_t>(num_batches), ws.data_ptr<float>(), nullptr, nullptr,
+                            cur_stream());
+  return {y, save_mean, save_invstd, idx};
+}
+
+Tensor bn_pool_fwd_affine(const Tensor& x, const Tensor& scale, const Tensor& shift) {
+  CHECK_DEV(x);
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0,
+              "bn_pool: channels_last [N, C%8==0, H, W] input required");
+  const c10::DeviceGuard guard(x.device());
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  Tensor sc = scale.contiguous(), sh = shift.contiguous();
+  Tensor y = torch::empty({N, C, (H - 1) / 2 + 1, (W - 1) / 2 + 1},
+                          x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dca::bn_relu_pool_forward(bn_dtype(x), x.data_ptr(), y.data_ptr(), nullptr, N, H, W, C, nullptr,
+                            nullptr, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr,
+                            sc.data_ptr<float>(), sh.data_ptr<float>(), cur_stream());
+  return y;
+}
+
+std::vector<Tensor> bn_pool_bwd(const Tensor& dyp_in, const Tensor& x, const Tensor& idx,
+                                const OptT& weight, const Tensor& save_mean,
+                                const Tensor& save_invstd, bool need_dweight) {
+  const c10::DeviceGuard guard(x.device());
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  Tensor dyp = dyp_in.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(dyp.scalar_type() == x.scalar_type(), "bn_pool bwd: grad dtype mismatch");
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor dx = torch::empty_like(x);
+  Tensor dgamma = need_dweight ? torch::empty({C}, fopt) : Tensor();
+  Tensor dbeta = need_dweight ? torch::empty({C}, fopt) : Tensor();
+  Tensor ws = torch::empty({dca::bn_workspace_floats(static_cast<int64_t>(N) * H * W, C)}, fopt);
+  dca::bn_relu_pool_backward(bn_dtype(x), dyp.data_ptr(), idx.data_ptr<uint8_t>(), x.data_ptr(), N, H, W,
+                             C, ptr_or_null<float>(weight), save_mean.data_ptr<float>(),
+                             save_invstd.data_ptr<float>(), dx.data_ptr(),
+                             need_dweight ? dgamma.data_ptr<float>() : nullptr,
+                             need_dweight ? dbeta.data_ptr<float>() : nullptr, ws.data_ptr<float>(),
+                             cur_stream());
+  return {dx, dgamma, dbeta};
 }
 
 // Global gradient norm over one flat buffer: returns a 3-float device tensor
@@ -328,7 +406,13 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "determined_clone_amd MI355X (gfx950) HIP kernels";
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_fwd_affine", &bn_fwd_affine);
-  m.def("bn_bwd_train", &bn_bwd_train);
+  m.def("bn_bwd_train", &bn_bwd_train, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("mask"),
+        pybind11::arg("weight"), pybind11::arg("save_mean"), pybind11::arg("save_invstd"),
+        pybind11::arg("relu"), pybind11::arg("need_dres"), pybind11::arg("need_dweight"),
+        pybind11::arg("dy2") = pybind11::none());
+  m.def("bn_pool_fwd_train", &bn_pool_fwd_train);
+  m.def("bn_pool_fwd_affine", &bn_pool_fwd_affine);
+  m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("grad_norm_scale", &grad_norm_scale);
   m.def("sumsq_partials", &sumsq_partials);
   m.def("norm_finalize", &norm_finalize_t);

@@ -1,0 +1,10 @@
+set -o pipefail
+ROOT=$GRAFT_REPO_ROOT
+cd $ROOT
+mkdir -p gpurun_out
+timeout -k 10 400 python -m pytest tests/test_ops_gpu.py -q -m gpu -x > gpurun_out/r14_pytest.txt 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/r14_pytest.txt; exit 1; }
+tail -2 gpurun_out/r14_pytest.txt
+timeout -k 10 300 python bench.py --steps 30 --warmup 10 2>&1 | tee gpurun_out/r14_bench.txt | tail -1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $ROOT/gpurun_out/prof14 -o run --output-format csv -- python3 $ROOT/bench.py --steps 5 --warmup 3 > $ROOT/gpurun_out/r14_prof_stdout.txt 2>&1
+echo "prof rc=$?"
