@@ -9,6 +9,13 @@ grace period.
 
 Devices: KFD topology via the native module (`native/scheduler.cpp: detect_kfd_gpus`), falling
 back to ``rocm-smi --json``; CPU-only hosts expose ``--artificial-slots`` CPU slots.
+
+GPU sharing (``--slots-per-gpu K``, MI355X-specific): one MI355X has 256 CUs and 288 GB of HBM3E, far
+more than a small HP-search trial (e.g. the CIFAR-10 CNN of the adaptive_asha config) can use, so
+the agent may expose each physical GPU as K schedulable slots. Trials placed on slots of the same
+GPU run as separate processes on separate HIP queues of that device (time-sliced / co-resident
+waves), which is how 16 concurrent ASHA trials fit on 8 GPUs. Slot ``i`` maps to physical device
+``i // K``; ``HIP_VISIBLE_DEVICES`` lists the distinct physical devices of the task's slots.
 """
 import argparse
 import base64
@@ -33,7 +40,24 @@ logger = logging.getLogger("determined_clone_amd.agent")
 FRAMEWORK_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def detect_devices(artificial_slots: int = 0) -> List[Dict[str, Any]]:
+def share_devices(devs: List[Dict[str, Any]], slots_per_gpu: int) -> List[Dict[str, Any]]:
+    """Expose each ROCm device as ``slots_per_gpu`` slots (see module docstring)."""
+    out: List[Dict[str, Any]] = []
+    for d in devs:
+        d = dict(d, device_index=d["id"])
+        k = slots_per_gpu if d["type"] == "rocm" else 1
+        for j in range(max(1, k)):
+            out.append(dict(d, id=len(out), uuid=d["uuid"] if k <= 1 else f"{d['uuid']}/{j}",
+                            share=j, shares=k))
+    return out
+
+
+def detect_devices(artificial_slots: int = 0, slots_per_gpu: int = 1) -> List[Dict[str, Any]]:
+    devs = _detect_physical(artificial_slots)
+    return share_devices(devs, slots_per_gpu) if slots_per_gpu > 1 else devs
+
+
+def _detect_physical(artificial_slots: int = 0) -> List[Dict[str, Any]]:
     if artificial_slots > 0:
         return [{"id": i, "uuid": f"cpu-{i}", "type": "cpu", "brand": "artificial"} for i in range(artificial_slots)]
     devs: List[Dict[str, Any]] = []
@@ -77,7 +101,7 @@ class _Task:
 class Agent:
     def __init__(self, master_url: str, agent_id: Optional[str] = None, pool: str = "default",
                  artificial_slots: int = 0, label: str = "", username: str = "admin",
-                 password: str = "", workdir: Optional[str] = None) -> None:
+                 password: str = "", workdir: Optional[str] = None, slots_per_gpu: int = 1) -> None:
         self.session = Session(master_url)
         tok = self.session.post("/api/v1/auth/login", {"username": username, "password": password})["token"]
         self.session.token = tok
@@ -85,7 +109,7 @@ class Agent:
         self.id = agent_id or socket.gethostname()
         self.pool = pool
         self.label = label
-        self.devices = detect_devices(artificial_slots)
+        self.devices = detect_devices(artificial_slots, slots_per_gpu)
         self.tasks: Dict[str, _Task] = {}
         self.workdir = workdir or tempfile.mkdtemp(prefix="det-clone-agent-")
         self._stop = threading.Event()
@@ -114,8 +138,8 @@ class Agent:
         info = dict(spec["cluster_info"])
         info["agent_id"] = self.id
         info["slot_ids"] = list(spec.get("slots") or [])
-        info["gpu_uuids"] = [d["uuid"] for d in self.devices if d["id"] in set(spec.get("slots") or [])
-                             and d["type"] == "rocm"]
+        mine = [d for d in self.devices if d["id"] in set(spec.get("slots") or [])]
+        info["gpu_uuids"] = [d["uuid"] for d in mine if d["type"] == "rocm"]
         if spec.get("num_containers", 1) > 1:
             info["rendezvous"] = {"container_addrs": ["127.0.0.1"] * spec["num_containers"],
                                   "container_rank": spec.get("container_rank", 0)}
@@ -137,9 +161,19 @@ class Agent:
         env["PYTHONPATH"] = os.pathsep.join([ctx_dir, FRAMEWORK_ROOT] + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
         slots = spec.get("slots") or []
         if any(d["type"] == "rocm" for d in self.devices):
-            env["HIP_VISIBLE_DEVICES"] = ",".join(str(s) for s in slots) if slots else ""
+            phys = sorted({int(d.get("device_index", d["id"])) for d in mine})
+            if spec["kind"] == "TRIAL" and len(mine) > 1 and len(phys) < len(mine):
+                # RCCL needs one rank per device: a multi-slot trial must not land on two shares
+                # of the same GPU.
+                raise RuntimeError(f"task {task_id}: {len(mine)} slots map to only {len(phys)} "
+                                   "GPU(s); --slots-per-gpu > 1 supports single-slot trials only")
+            env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in phys)
         else:
             env["DET_SLOTS"] = str(max(len(slots), 1))
+            # CPU slots: give each task its share of the host's cores so concurrent trials do not
+            # oversubscribe the CPU with one full-size OpenMP pool each.
+            share = max(1, (os.cpu_count() or 1) * max(len(slots), 1) // max(len(self.devices), 1))
+            env.setdefault("OMP_NUM_THREADS", str(share))
         if spec["kind"] == "TRIAL":
             cmd = [sys.executable, "-m", "determined_clone_amd.exec.launch"]
         else:
@@ -261,9 +295,12 @@ def main() -> None:
     ap.add_argument("--resource-pool", default="default")
     ap.add_argument("--artificial-slots", type=int, default=0)
     ap.add_argument("--label", default="")
+    ap.add_argument("--slots-per-gpu", type=int, default=1,
+                    help="expose each MI355X as this many slots (HP-search trials sharing a GPU)")
     args = ap.parse_args()
     logging.basicConfig(level=logging.INFO)
-    Agent(args.master_url, args.agent_id, args.resource_pool, args.artificial_slots, args.label).run()
+    Agent(args.master_url, args.agent_id, args.resource_pool, args.artificial_slots, args.label,
+          slots_per_gpu=args.slots_per_gpu).run()
 
 
 if __name__ == "__main__":

@@ -156,8 +156,12 @@ class Master:
             from determined_clone_amd.util import merge_dicts
 
             raw = merge_dicts(dec(t["config"], {}), raw)
-        if raw.get("checkpoint_storage") is None:
+        cs = raw.get("checkpoint_storage")
+        if cs is None:
             raw["checkpoint_storage"] = dict(self.checkpoint_storage)
+        elif "type" not in cs:
+            # Experiment-level GC policy (save_*) over the cluster's storage backend.
+            raw["checkpoint_storage"] = {**self.checkpoint_storage, **cs}
         cfg = expconf.complete(raw)
         seed = cfg["reproducibility"].get("experiment_seed")
         if seed is None:

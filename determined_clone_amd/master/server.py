@@ -1146,11 +1146,14 @@ class _Handler(BaseHTTPRequestHandler):
 
     def _send(self, status: int, payload: Any) -> None:
         data = json.dumps(payload, default=str).encode()
-        self.send_response(status)
-        self.send_header("Content-Type", "application/json")
-        self.send_header("Content-Length", str(len(data)))
-        self.end_headers()
-        self.wfile.write(data)
+        try:
+            self.send_response(status)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+        except (BrokenPipeError, ConnectionResetError):  # client went away (long-poll cancelled)
+            self.close_connection = True
 
     def _dispatch(self, method: str) -> None:
         parsed = urllib.parse.urlparse(self.path)

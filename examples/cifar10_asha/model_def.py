@@ -44,9 +44,11 @@ class CIFARTrial(pytorch.PyTorchTrial):
                 "validation_error": (logits.argmax(1) != y).float().mean()}
 
     def build_training_data_loader(self):
-        return pytorch.DataLoader(cifar.SyntheticCIFAR10(50000, seed=0),
+        n = int(self.context.get_hparams().get("train_records", 50000))
+        return pytorch.DataLoader(cifar.SyntheticCIFAR10(n, seed=0),
                                   batch_size=self.context.get_per_slot_batch_size(), shuffle=True)
 
     def build_validation_data_loader(self):
-        return pytorch.DataLoader(cifar.SyntheticCIFAR10(10000, seed=1),
+        n = int(self.context.get_hparams().get("val_records", 10000))
+        return pytorch.DataLoader(cifar.SyntheticCIFAR10(n, seed=1),
                                   batch_size=self.context.get_per_slot_batch_size())

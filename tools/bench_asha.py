@@ -1,0 +1,127 @@
+"""ASHA search throughput: completed trials per hour of the CIFAR-10 adaptive_asha search.
+
+BASELINE.json's second metric ("ASHA trials/hr") on the config "CIFAR-10 adaptive_asha HP search,
+16 concurrent trials gang-scheduled across 8 MI355X". This runs the real platform end to end, all
+in one process tree on this node: an in-process master (searcher + native scheduler) and an agent
+that exposes every MI355X as ``--slots-per-gpu`` slots; the master schedules
+``max_concurrent_trials`` CIFAR-10 trials (``examples/cifar10_asha/model_def.py``: bf16 NHWC CNN,
+fused BN+ReLU HIP kernel, fused SGD) as separate trial processes; adaptive ASHA promotes / stops
+them. The value is COMPLETED trials / wall-clock hours from experiment creation to the searcher's
+shutdown (trial process start-up, validation and checkpointing included).
+
+Search length is scaled down from the example's 8 x 50k-image epochs (``--records-per-epoch``,
+``--epochs``) so a run fits a short GPU slot; the searcher config (adaptive_asha, standard mode,
+max_concurrent_trials) is the example's. Data: synthetic CIFAR-shaped tensors (no network).
+
+Usage: ``python tools/bench_asha.py [--slots-per-gpu 8 --max-trials 32 --max-concurrent 8]``;
+prints one JSON line.
+"""
+import argparse
+import base64
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+
+import yaml  # noqa: E402
+
+from determined_clone_amd.agent import Agent  # noqa: E402
+from determined_clone_amd.common.api import Session  # noqa: E402
+from determined_clone_amd.master import Master, MasterServer  # noqa: E402
+from determined_clone_amd.util import tar_directory  # noqa: E402
+
+
+def search_config(args: argparse.Namespace) -> dict:
+    with open(os.path.join(ROOT, "examples", "cifar10_asha", "adaptive.yaml")) as f:
+        cfg = yaml.safe_load(f)
+    cfg["name"] = "bench_asha"
+    cfg["records_per_epoch"] = args.records_per_epoch
+    # PyTorchTrial epochs follow the training loader's length: shrink the synthetic dataset.
+    cfg["hyperparameters"]["train_records"] = args.records_per_epoch
+    cfg["hyperparameters"]["val_records"] = max(args.batch, args.records_per_epoch // 5)
+    cfg["searcher"].update(max_trials=args.max_trials, max_concurrent_trials=args.max_concurrent,
+                           max_length={"epochs": args.epochs})
+    cfg["hyperparameters"]["global_batch_size"] = args.batch
+    cfg["checkpoint_storage"] = {"save_trial_latest": 1, "save_trial_best": 0, "save_experiment_best": 1}
+    cfg["max_restarts"] = 0
+    return cfg
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--slots-per-gpu", type=int, default=8)
+    ap.add_argument("--max-trials", type=int, default=32)
+    ap.add_argument("--max-concurrent", type=int, default=8)
+    ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--records-per-epoch", type=int, default=6400)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--timeout", type=float, default=1500.0)
+    ap.add_argument("--cpu", action="store_true", help="artificial CPU slots (plumbing check)")
+    args = ap.parse_args()
+
+    tmp = tempfile.mkdtemp(prefix="det-asha-bench-")
+    m = Master(os.path.join(tmp, "m.db"),
+               checkpoint_storage={"type": "shared_fs", "host_path": os.path.join(tmp, "ckpt")})
+    srv = MasterServer(m, "127.0.0.1", 0).start()
+    agent = Agent(m.master_url, "agent-0", artificial_slots=args.max_concurrent if args.cpu else 0,
+                  workdir=os.path.join(tmp, "agent"), slots_per_gpu=args.slots_per_gpu).start_background()
+    n_gpus = len({d.get("device_index", d["id"]) for d in agent.devices if d["type"] == "rocm"})
+    s = Session(m.master_url)
+    s.token = s.post("/api/v1/auth/login", {"username": "admin", "password": ""})["token"]
+    try:
+        body = {"config": search_config(args), "model_definition": base64.b64encode(
+            tar_directory(os.path.join(ROOT, "examples", "cifar10_asha"))).decode()}
+        t0 = time.time()
+        eid = s.post("/api/v1/experiments", body)["experiment"]["id"]
+        state, last_print = "", 0.0
+        while time.time() - t0 < args.timeout:
+            state = s.get(f"/api/v1/experiments/{eid}")["experiment"]["state"]
+            if state in ("COMPLETED", "CANCELED", "ERROR"):
+                break
+            if time.time() - last_print > 30:
+                trials = s.get(f"/api/v1/experiments/{eid}/trials")["trials"]
+                done = sum(t["state"] == "COMPLETED" for t in trials)
+                print(f"[bench_asha] t={time.time() - t0:.0f}s trials={len(trials)} completed={done}",
+                      file=sys.stderr, flush=True)
+                last_print = time.time()
+            time.sleep(0.5)
+        wall = time.time() - t0
+        trials = s.get(f"/api/v1/experiments/{eid}/trials")["trials"]
+        done = [t for t in trials if t["state"] == "COMPLETED"]
+        steps = sum(int(t.get("steps_completed") or 0) for t in done)
+        best = None
+        for t in done:
+            v = t.get("best_validation")
+            if v is not None and (best is None or v < best):
+                best = v
+        if state != "COMPLETED":
+            errs = [t["id"] for t in trials if t["state"] == "ERROR"]
+            print(f"[bench_asha] experiment ended {state!r}; errored trials {errs}", file=sys.stderr)
+            for tid in (errs or [t["id"] for t in trials if t["state"] == "RUNNING"])[:1]:
+                for line in s.get(f"/api/v1/trials/{tid}/logs")["logs"][-40:]:
+                    print("   ", line["log"], file=sys.stderr)
+        print(json.dumps({
+            "metric": "ASHA trials/hr", "value": round(len(done) / (wall / 3600.0), 1),
+            "unit": "trials/hr", "n_gpus": n_gpus, "higher_is_better": True,
+            "experiment_state": state, "trials_completed": len(done), "trials_created": len(trials),
+            "batches_trained": steps, "wall_s": round(wall, 1), "best_validation_error": best,
+            "dtype": "bf16" if not args.cpu else "fp32", "data": "synthetic CIFAR-10-shaped",
+            "config": {"model": "cifar10_cnn", "searcher": "adaptive_asha", "max_trials": args.max_trials,
+                       "max_concurrent_trials": args.max_concurrent, "slots_per_gpu": args.slots_per_gpu,
+                       "max_length_epochs": args.epochs, "records_per_epoch": args.records_per_epoch,
+                       "global_batch": args.batch}}), flush=True)
+    finally:
+        agent.stop()
+        srv.stop()
+        time.sleep(1.0)
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
