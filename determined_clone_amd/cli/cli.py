@@ -665,6 +665,7 @@ def build_parser() -> argparse.ArgumentParser:
         sp.add_argument("--master-port", type=int, default=8080)
         sp.add_argument("--agents", type=int, default=1)
         sp.add_argument("--artificial-slots", type=int, default=0)
+        sp.add_argument("--slots-per-gpu", type=int, default=1)
         sp.add_argument("--storage-path", default=None)
         sp.add_argument("--state-dir", default=os.path.join(os.path.expanduser("~"), ".det-clone"))
     return p

@@ -46,6 +46,8 @@ def agent_up(args) -> None:
                f"http://127.0.0.1:{args.master_port}", "--agent-id", f"agent-{i}"]
         if args.artificial_slots:
             cmd += ["--artificial-slots", str(args.artificial_slots)]
+        if getattr(args, "slots_per_gpu", 1) > 1:
+            cmd += ["--slots-per-gpu", str(args.slots_per_gpu)]
         _spawn(cmd, args.state_dir, f"agent-{i}")
     print(f"{args.agents} agent(s) started")
 

@@ -104,7 +104,7 @@ class Attention(nn.Module):
     def forward(self, x: torch.Tensor, rope_cache=None) -> torch.Tensor:
         B, S, E = x.shape
         H, D = self.cfg.n_head, self.cfg.head_dim
-        qkv = self.qkv(x).view(B, S, 3, H, D)
+        qkv = T.linear(x, self.qkv.weight, self.qkv.bias).view(B, S, 3, H, D)
         if self.rot:
             q, k, v = qkv.unbind(2)
             cos, sin = rope_cache
@@ -115,7 +115,7 @@ class Attention(nn.Module):
             o = T.flash_attention_qkvpacked(qkv, causal=True)
         if self.cfg.dropout and self.training:
             o = F.dropout(o, self.cfg.dropout)
-        return self.proj(o.reshape(B, S, E))
+        return T.linear(o.reshape(B, S, E), self.proj.weight, self.proj.bias)
 
 
 class MLP(nn.Module):
@@ -126,8 +126,8 @@ class MLP(nn.Module):
         self.proj = nn.Linear(cfg.mlp_ratio * E, E)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = T.bias_gelu(F.linear(x, self.fc.weight), self.fc.bias)
-        return self.proj(h)
+        h = T.bias_gelu(T.linear(x, self.fc.weight), self.fc.bias)
+        return T.linear(h, self.proj.weight, self.proj.bias)
 
 
 class Block(nn.Module):

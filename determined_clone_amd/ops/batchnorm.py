@@ -9,7 +9,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
-from determined_clone_amd.ops import _ext
+from determined_clone_amd.ops import _ext, _grad
 
 
 def reference_batch_norm_act(x, weight, bias, running_mean, running_var, residual=None,
@@ -50,6 +50,7 @@ class _BNActTrain(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.res_sink = res_sink      # where to deposit d(residual) (or None: return it)
         ctx.out_sink = out_sink      # extra upstream gradient of y deposited by a consumer
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
@@ -59,8 +60,11 @@ class _BNActTrain(torch.autograd.Function):
         dy2 = ctx.out_sink.grad if ctx.out_sink is not None else None
         if ctx.out_sink is not None:
             ctx.out_sink.grad = None
+        acc_w, acc_b = _direct_grad_targets(*ctx.params) if need_w else (None, None)
         dx, dgamma, dbeta, dres = _ext.load().bn_bwd_train(
-            dy, x, mask, weight, mean, invstd, ctx.relu, ctx.has_res, need_w, dy2)
+            dy, x, mask, weight, mean, invstd, ctx.relu, ctx.has_res, need_w, dy2, acc_w, acc_b)
+        if acc_w is not None:
+            need_w = False  # already accumulated into .grad by the finalize kernel
         dres_out = None
         if ctx.has_res:
             if ctx.res_sink is not None:
@@ -69,6 +73,15 @@ class _BNActTrain(torch.autograd.Function):
                 dres_out = dres
         return (dx, dgamma if need_w else None, dbeta if need_w else None, dres_out,
                 None, None, None, None, None, None, None, None)
+
+
+def _direct_grad_targets(weight: Optional[torch.Tensor], bias: Optional[torch.Tensor]):
+    """``(weight.grad, bias.grad)`` when the BN finalize kernel may accumulate dgamma/dbeta into
+    them directly (see ``ops._grad``), else ``(None, None)``."""
+    gw, gb = _grad.target(weight), _grad.target(bias)
+    if gw is None or gb is None or gw.dtype != torch.float32 or gb.dtype != torch.float32:
+        return None, None
+    return gw, gb
 
 
 def _hip_ok(x: torch.Tensor) -> bool:

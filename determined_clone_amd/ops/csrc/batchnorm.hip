@@ -16,6 +16,8 @@
 //   bn_finalize_bwd  : dgamma, dbeta and the affine form dx = k1*dy' + k2*x + k3
 //   bn_apply_bwd     : dx (and d_residual = dy' when the residual add was fused)
 // Every lane moves 8 channels (16 B of bf16) per access; reductions are deterministic.
+#include <cstdio>
+#include <cstdlib>
 #include "common.h"
 
 namespace dca {
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(kBlock) void bn_finalize_fwd_kernel(
 __global__ __launch_bounds__(kBlock) void bn_finalize_bwd_kernel(
     const float* __restrict__ partial, int B, int C, int64_t M, const float* __restrict__ gamma,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, float* __restrict__ coef /* [3][C] */) {
+    float* __restrict__ dbeta, bool accumulate, float* __restrict__ coef /* [3][C] */) {
   __shared__ double red[512];
   double s, q;
   int ch;
@@ -222,8 +224,10 @@ __global__ __launch_bounds__(kBlock) void bn_finalize_bwd_kernel(
     const float g = gamma ? gamma[ch] : 1.f;
     const float sdy = static_cast<float>(s);
     const float sdyx = static_cast<float>(q);  // sum dy' * (x - mean)
-    if (dgamma) dgamma[ch] = sdyx * is;
-    if (dbeta) dbeta[ch] = sdy;
+    // accumulate: dgamma/dbeta are the parameters' .grad (flat-buffer views) -- add in place so
+    // autograd never runs a separate AccumulateGrad add for them.
+    if (dgamma) dgamma[ch] = accumulate ? dgamma[ch] + sdyx * is : sdyx * is;
+    if (dbeta) dbeta[ch] = accumulate ? dbeta[ch] + sdy : sdy;
     const float invM = 1.f / static_cast<float>(M);
     const float k1 = g * is;
     const float k2 = -k1 * is * is * sdyx * invM;
@@ -307,12 +311,30 @@ __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
   }
 }
 
+struct ReduceTuning {
+  int64_t elems_per_block, min_blocks, max_blocks;
+};
+inline const ReduceTuning& reduce_tuning() {
+  // DCA_BN_REDUCE="elems,min,max" overrides the workgroup-count heuristic (tuning sweeps only).
+  static const ReduceTuning t = [] {
+    ReduceTuning r{65536, 256, 1024};
+    if (const char* e = std::getenv("DCA_BN_REDUCE")) {
+      long long a = 0, b = 0, c = 0;
+      if (std::sscanf(e, "%lld,%lld,%lld", &a, &b, &c) == 3 && a > 0 && b > 0 && c >= b) r = {a, b, c};
+    }
+    return r;
+  }();
+  return t;
+}
+
 inline int reduce_blocks(int64_t M, int C, const ReduceGeom& g) {
-  // Aim at ~64K elements per workgroup, 256..1024 workgroups in x (x cgroups in y).
+  // ~elems_per_block elements per workgroup, clamped to [min_blocks, max_blocks] in x (x cgroups
+  // in y).
+  const ReduceTuning& t = reduce_tuning();
   int64_t total = M * static_cast<int64_t>(C);
-  int64_t b = (total + 65535) / 65536;
-  if (b < 256) b = 256;
-  if (b > 1024) b = 1024;
+  int64_t b = (total + t.elems_per_block - 1) / t.elems_per_block;
+  if (b < t.min_blocks) b = t.min_blocks;
+  if (b > t.max_blocks) b = t.max_blocks;
   int64_t rows_iter = (M + g.rpi - 1) / g.rpi;
   if (b > rows_iter) b = rows_iter;
   if (b < 1) b = 1;
@@ -537,7 +559,7 @@ void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_
                        int64_t M, int C,
                        const float* gamma, const float* save_mean, const float* save_invstd,
                        bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
-                       float* workspace, hipStream_t st) {
+                       bool accumulate_dw, float* workspace, hipStream_t st) {
   ReduceGeom g = reduce_geom(C);
   int B = reduce_blocks(M, C, g);
   float* partial = workspace;
@@ -548,7 +570,7 @@ void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_
     default: launch_reduce<F32>(true, x, dy, dy2, y, save_mean, M, C, relu, partial, B, g, st); break;
   }
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
-                     C, M, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+                     C, M, gamma, save_mean, save_invstd, dgamma, dbeta, accumulate_dw, coef);
   const int64_t nvec = M * C / 8;
   const int grid = stream_grid(nvec, kBlock);
   switch (dt) {
@@ -611,7 +633,7 @@ void bn_relu_pool_backward(BnDtype dt, const void* dyp, const uint8_t* idx, cons
     default: hipLaunchKernelGGL(bn_pool_reduce_bwd_kernel<F32>, grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
   }
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
-                     C, M, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+                     C, M, gamma, save_mean, save_invstd, dgamma, dbeta, false, coef);
   const int64_t nvec = M * C / 8;
   const int ag = stream_grid(nvec, kBlock);
   switch (dt) {

@@ -32,7 +32,7 @@ void bn_relu_pool_backward(BnDtype dt, const void* dyp, const uint8_t* idx, cons
 void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_t* mask, const void* x,
                        int64_t M, int C, const float* gamma, const float* save_mean, const float* save_invstd,
                        bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
-                       float* workspace, hipStream_t st);
+                       bool accumulate_dw, float* workspace, hipStream_t st);
 
 int sumsq_partial_blocks(int64_t n);
 void sumsq_partial(OptDtype g, const void* grad, int64_t n, float* partial, int blocks,
@@ -154,7 +154,8 @@ Tensor bn_fwd_affine(const Tensor& x, const OptT& residual, const Tensor& scale,
 std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const OptT& mask,
                                  const OptT& weight, const Tensor& save_mean,
                                  const Tensor& save_invstd, bool relu, bool need_dres,
-                                 bool need_dweight, const OptT& dy2_in) {
+                                 bool need_dweight, const OptT& dy2_in, const OptT& dweight_acc,
+                                 const OptT& dbias_acc) {
   CHECK_DEV(x);
   const c10::DeviceGuard guard(x.device());
   auto [M, C] = rows_channels(x);
@@ -171,8 +172,17 @@ std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const Opt
   auto fopt = x.options().dtype(at::kFloat);
   Tensor dx = torch::empty_like(x);
   Tensor dres = need_dres ? torch::empty_like(x) : Tensor();
-  Tensor dgamma = need_dweight ? torch::empty({C}, fopt) : Tensor();
-  Tensor dbeta = need_dweight ? torch::empty({C}, fopt) : Tensor();
+  // dweight_acc / dbias_acc: accumulate the parameter gradients in place (into .grad) instead
+  // of returning fresh tensors.
+  const bool acc = need_dweight && dweight_acc.has_value() && dweight_acc->defined() &&
+                   dbias_acc.has_value() && dbias_acc->defined();
+  if (acc) {
+    for (const Tensor* t : {&*dweight_acc, &*dbias_acc})
+      TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C &&
+                  t->device() == x.device(), "batchnorm bwd: accumulation target must be fp32 [C]");
+  }
+  Tensor dgamma = acc ? *dweight_acc : need_dweight ? torch::empty({C}, fopt) : Tensor();
+  Tensor dbeta = acc ? *dbias_acc : need_dweight ? torch::empty({C}, fopt) : Tensor();
   Tensor ws = torch::empty({dca::bn_workspace_floats(M, C)}, fopt);
   dca::bn_backward_train(bn_dtype(x), dy.data_ptr(), dy2.defined() ? dy2.data_ptr() : nullptr,
                          relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(),
@@ -180,8 +190,9 @@ std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const Opt
                          save_invstd.data_ptr<float>(), relu, dx.data_ptr(),
                          need_dres ? dres.data_ptr() : nullptr,
                          need_dweight ? dgamma.data_ptr<float>() : nullptr,
-                         need_dweight ? dbeta.data_ptr<float>() : nullptr, ws.data_ptr<float>(),
-                         cur_stream());
+                         need_dweight ? dbeta.data_ptr<float>() : nullptr, acc,
+                         ws.data_ptr<float>(), cur_stream());
+  if (acc) return {dx, Tensor(), Tensor(), dres};
   return {dx, dgamma, dbeta, dres};
 }
 
@@ -409,7 +420,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_train", &bn_bwd_train, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("mask"),
         pybind11::arg("weight"), pybind11::arg("save_mean"), pybind11::arg("save_invstd"),
         pybind11::arg("relu"), pybind11::arg("need_dres"), pybind11::arg("need_dweight"),
-        pybind11::arg("dy2") = pybind11::none());
+        pybind11::arg("dy2") = pybind11::none(), pybind11::arg("dweight_acc") = pybind11::none(),
+        pybind11::arg("dbias_acc") = pybind11::none());
   m.def("bn_pool_fwd_train", &bn_pool_fwd_train);
   m.def("bn_pool_fwd_affine", &bn_pool_fwd_affine);
   m.def("bn_pool_bwd", &bn_pool_bwd);

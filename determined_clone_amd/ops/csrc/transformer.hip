@@ -10,12 +10,12 @@
 // each block accumulates its rows in registers, writes one partial row, and a column-reduce kernel
 // sums the partials.
 #include "common.h"
+#include "transformer_api.h"
 
 #include <type_traits>
 
 namespace dca {
 
-enum class TDtype : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
 namespace {
 
@@ -172,9 +172,22 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_kernel(
 // (coalesced 256-B rows), wave -> every 16th partial row with 4 independent loads in flight, then an
 // LDS tree over the 16 waves. Deterministic (fixed order).
 constexpr int kColWaves = 16;
+__device__ __forceinline__ void column_store(const ColumnOut& o, int64_t j, float v) {
+  char* base = static_cast<char*>(j < o.split ? o.p0 : o.p1);
+  const int64_t k = j < o.split ? j : j - o.split;
+  if (o.bf16) {
+    uint16_t* q = reinterpret_cast<uint16_t*>(base) + k;
+    if (o.accumulate) v += __uint_as_float(static_cast<uint32_t>(*q) << 16);
+    *q = static_cast<uint16_t>(f2bf_bits(v));
+  } else {
+    float* q = reinterpret_cast<float*>(base) + k;
+    *q = o.accumulate ? *q + v : v;
+  }
+}
+
 __global__ __launch_bounds__(kColWaves * 64) void column_reduce_kernel(const float* __restrict__ partial,
                                                                       int nparts, int64_t ncols,
-                                                                      float* __restrict__ out) {
+                                                                      ColumnOut out) {
   __shared__ float red[kColWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + lane;
@@ -195,7 +208,51 @@ __global__ __launch_bounds__(kColWaves * 64) void column_reduce_kernel(const flo
     if (w < s) red[w][lane] += red[w + s][lane];
     __syncthreads();
   }
-  if (w == 0 && j < ncols) out[j] = red[0][lane];
+  if (w == 0 && j < ncols) column_store(out, j, red[0][lane]);
+}
+
+// Per-block column partial sums of dy [rows][N] (bias gradient of a linear layer): block = 256
+// threads x 8 columns, rows strided by gridDim.y with 4 independent 16-B loads in flight.
+template <typename T>
+__global__ __launch_bounds__(256) void row_sum_kernel(const void* __restrict__ dy,
+                                                      float* __restrict__ partial, int64_t rows,
+                                                      int N) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= N) return;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t step = gridDim.y;
+  int64_t r = blockIdx.y;
+  for (; r + 3 * step < rows; r += 4 * step) {
+    float g[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      Vec8<T>::load(reinterpret_cast<const char*>(dy) + ((r + u * step) * N + c) * Vec8<T>::bytes, g[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += g[u][k];
+  }
+  for (; r < rows; r += step) {
+    float g[8];
+    Vec8<T>::load(reinterpret_cast<const char*>(dy) + (r * N + c) * Vec8<T>::bytes, g);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += g[k];
+  }
+  float4* out = reinterpret_cast<float4*>(partial + static_cast<int64_t>(blockIdx.y) * N + c);
+  out[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  out[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+
+// 8 bias values starting at column c, fp32 or bf16 storage (nullptr -> zeros).
+__device__ __forceinline__ void load_bias8(const void* bias, bool bf16, int c, float (&b)[8]) {
+  if (!bias) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b[k] = 0.f;
+  } else if (bf16) {
+    Vec8<BF16>::load(static_cast<const char*>(bias) + static_cast<int64_t>(c) * 2, b);
+  } else {
+    Vec8<F32>::load(static_cast<const char*>(bias) + static_cast<int64_t>(c) * 4, b);
+  }
 }
 
 // ------------------------------------------------------------------ bias + GELU(tanh)
@@ -214,7 +271,8 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
 
 template <typename T>
 __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const void* __restrict__ x,
-                                                            const float* __restrict__ bias,
+                                                            const void* __restrict__ bias,
+                                                            bool bias_bf16,
                                                             void* __restrict__ y, int64_t rows,
                                                             int N) {
   const int n8 = N / 8;
@@ -224,8 +282,10 @@ __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const void* __restri
     const int c = static_cast<int>(v % n8) * 8;
     float a[8];
     Vec8<T>::load(reinterpret_cast<const char*>(x) + v * 8 * Vec8<T>::bytes, a);
+    float b[8];
+    load_bias8(bias, bias_bf16, c, b);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] = gelu_tanh(a[k] + (bias ? bias[c + k] : 0.f));
+    for (int k = 0; k < 8; ++k) a[k] = gelu_tanh(a[k] + b[k]);
     Vec8<T>::store(reinterpret_cast<char*>(y) + v * 8 * Vec8<T>::bytes, a);
   }
 }
@@ -234,14 +294,13 @@ __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const void* __restri
 // [gridDim.y][N] reduced by column_reduce_kernel.
 template <typename T>
 __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
-    const void* __restrict__ dy, const void* __restrict__ x, const float* __restrict__ bias,
-    void* __restrict__ dx, float* __restrict__ partial, int64_t rows, int N) {
+    const void* __restrict__ dy, const void* __restrict__ x, const void* __restrict__ bias,
+    bool bias_bf16, void* __restrict__ dx, float* __restrict__ partial, int64_t rows, int N) {
   const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (c >= N) return;
   float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float b[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) b[k] = bias ? bias[c + k] : 0.f;
+  load_bias8(bias, bias_bf16, c, b);
   for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
     const int64_t off = (r * N + c) * Vec8<T>::bytes;
     float g[8], a[8];
@@ -343,8 +402,8 @@ void layernorm_fwd(TDtype dt, const void* x, const void* res, void* sum_out, voi
 }
 
 void layernorm_bwd(TDtype dt, const void* dy, const void* x, const float* gamma, const float* mean,
-                   const float* rstd, const void* dsum, void* dx, float* partial, float* dgamma_dbeta,
-                   int64_t rows, int D, hipStream_t st) {
+                   const float* rstd, const void* dsum, void* dx, float* partial,
+                   const ColumnOut* dgamma_dbeta, int64_t rows, int D, hipStream_t st) {
   const int blocks = ln_bwd_blocks(rows);
   dispatch_t(dt, [&](auto t) {
     using T = decltype(t);
@@ -358,33 +417,53 @@ void layernorm_bwd(TDtype dt, const void* dy, const void* x, const float* gamma,
   if (dgamma_dbeta) {
     const int64_t ncols = 2 * static_cast<int64_t>(D);
     hipLaunchKernelGGL(column_reduce_kernel, dim3((ncols + 63) / 64), dim3(kColWaves * 64), 0, st,
-                       partial, blocks, ncols, dgamma_dbeta);
+                       partial, blocks, ncols, *dgamma_dbeta);
   }
 }
 
-void bias_gelu_fwd(TDtype dt, const void* x, const float* bias, void* y, int64_t rows, int N,
-                   hipStream_t st) {
+void bias_gelu_fwd(TDtype dt, const void* x, const void* bias, bool bias_bf16, void* y,
+                   int64_t rows, int N, hipStream_t st) {
   const int grid = stream_grid(rows * N / 8, 256);
   dispatch_t(dt, [&](auto t) {
     using T = decltype(t);
-    hipLaunchKernelGGL(bias_gelu_fwd_kernel<T>, dim3(grid), dim3(256), 0, st, x, bias, y, rows, N);
+    hipLaunchKernelGGL(bias_gelu_fwd_kernel<T>, dim3(grid), dim3(256), 0, st, x, bias, bias_bf16, y,
+                       rows, N);
   });
 }
 
 int bias_gelu_bwd_row_blocks(int64_t rows) { return static_cast<int>(rows < 256 ? (rows < 1 ? 1 : rows) : 256); }
 
-void bias_gelu_bwd(TDtype dt, const void* dy, const void* x, const float* bias, void* dx,
-                   float* partial, float* dbias, int64_t rows, int N, hipStream_t st) {
+void bias_gelu_bwd(TDtype dt, const void* dy, const void* x, const void* bias, bool bias_bf16,
+                   void* dx, float* partial, const ColumnOut* dbias, int64_t rows, int N,
+                   hipStream_t st) {
   const int rb = bias_gelu_bwd_row_blocks(rows);
   dim3 grid((N / 8 + 255) / 256, rb);
   dispatch_t(dt, [&](auto t) {
     using T = decltype(t);
-    hipLaunchKernelGGL(bias_gelu_bwd_kernel<T>, grid, dim3(256), 0, st, dy, x, bias, dx,
+    hipLaunchKernelGGL(bias_gelu_bwd_kernel<T>, grid, dim3(256), 0, st, dy, x, bias, bias_bf16, dx,
                        dbias ? partial : nullptr, rows, N);
   });
   if (dbias)
     hipLaunchKernelGGL(column_reduce_kernel, dim3((N + 63) / 64), dim3(kColWaves * 64), 0, st,
-                       partial, rb, static_cast<int64_t>(N), dbias);
+                       partial, rb, static_cast<int64_t>(N), *dbias);
+}
+
+int row_sum_blocks(int64_t rows) {
+  // ~64 rows per block-row, at most 256 slabs (partials stay small for the column pass).
+  int64_t b = (rows + 63) / 64;
+  return static_cast<int>(b < 1 ? 1 : (b > 256 ? 256 : b));
+}
+
+void row_sum(TDtype dt, const void* dy, float* partial, const ColumnOut& out, int64_t rows, int N,
+             hipStream_t st) {
+  const int rb = row_sum_blocks(rows);
+  dim3 grid((N / 8 + 255) / 256, rb);
+  dispatch_t(dt, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(row_sum_kernel<T>, grid, dim3(256), 0, st, dy, partial, rows, N);
+  });
+  hipLaunchKernelGGL(column_reduce_kernel, dim3((N + 63) / 64), dim3(kColWaves * 64), 0, st,
+                     partial, rb, static_cast<int64_t>(N), out);
 }
 
 void rope(TDtype dt, const void* x, void* y, const float* cosT, const float* sinT, int64_t rows,

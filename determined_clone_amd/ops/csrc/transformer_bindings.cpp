@@ -5,37 +5,8 @@
 
 #include <hip/hip_runtime.h>
 
-namespace dca {
-enum class TDtype : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
-int ln_bwd_blocks(int64_t rows);
-void layernorm_fwd(TDtype dt, const void* x, const void* res, void* sum_out, void* y,
-                   const float* gamma, const float* beta, float* mean, float* rstd, int64_t rows,
-                   int D, float eps, hipStream_t st);
-void layernorm_bwd(TDtype dt, const void* dy, const void* x, const float* gamma, const float* mean,
-                   const float* rstd, const void* dsum, void* dx, float* partial, float* dgamma_dbeta,
-                   int64_t rows, int D, hipStream_t st);
-void bias_gelu_fwd(TDtype dt, const void* x, const float* bias, void* y, int64_t rows, int N,
-                   hipStream_t st);
-int bias_gelu_bwd_row_blocks(int64_t rows);
-void bias_gelu_bwd(TDtype dt, const void* dy, const void* x, const float* bias, void* dx,
-                   float* partial, float* dbias, int64_t rows, int N, hipStream_t st);
-void rope(TDtype dt, const void* x, void* y, const float* cosT, const float* sinT, int64_t rows,
-          int H, int S, int D, int rot, bool backward, hipStream_t st);
-void attention_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H,
-                   int Sq, int Sk, int D, const int64_t* qs, const int64_t* ks, const int64_t* vs,
-                   const int64_t* os, float scale, bool causal, hipStream_t st);
-void attention_bwd(const void* q, const void* k, const void* v, const void* o, const void* dO,
-                   const float* lse, float* delta, float* dq_acc, void* dq, void* dk, void* dv,
-                   int B, int H, int Sq, int Sk, int D, const int64_t* st_q, const int64_t* st_k,
-                   const int64_t* st_v, const int64_t* st_o, const int64_t* st_do,
-                   const int64_t* st_dq, const int64_t* st_dk, const int64_t* st_dv, float scale,
-                   bool causal, hipStream_t stream);
-void cross_entropy_fwd(TDtype dt, const void* logits, const int64_t* target, float* lse,
-                       float* loss, int64_t rows, int V, int64_t ignore_index, hipStream_t st);
-void cross_entropy_bwd(TDtype dt, const void* logits, const int64_t* target, const float* lse,
-                       const float* gscale, void* dlogits, int64_t rows, int V,
-                       int64_t ignore_index, hipStream_t st);
-}  // namespace dca
+#include "transformer_api.h"
+
 
 namespace {
 using torch::Tensor;
@@ -76,9 +47,18 @@ std::vector<Tensor> ln_fwd(const Tensor& x, const OptT& res, const OptT& gamma, 
   return {y, sum, mean, rstd};
 }
 
+// Where a column reduction lands: accumulate into a parameter's .grad (fp32 or bf16, contiguous,
+// `n` elements) or -- when `acc` is absent -- a fresh fp32 tensor returned to autograd.
+bool want_acc(const OptT& acc) { return acc.has_value() && acc->defined(); }
+void check_acc(const Tensor& t, int64_t n, const Tensor& like, const char* what) {
+  TORCH_CHECK(t.is_contiguous() && t.numel() == n && t.device() == like.device() &&
+                  (t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16),
+              what, ": accumulation target must be a contiguous fp32/bf16 tensor of ", n, " elements");
+}
+
 std::vector<Tensor> ln_bwd(const Tensor& dy_in, const Tensor& x, const OptT& gamma,
                            const Tensor& mean, const Tensor& rstd, const OptT& dsum,
-                           bool need_param_grads) {
+                           bool need_param_grads, const OptT& dgamma_acc, const OptT& dbeta_acc) {
   const c10::DeviceGuard g(x.device());
   Tensor dy = dy_in.contiguous();
   const int D = static_cast<int>(x.size(-1));
@@ -87,14 +67,34 @@ std::vector<Tensor> ln_bwd(const Tensor& dy_in, const Tensor& x, const OptT& gam
   auto fo = x.options().dtype(at::kFloat);
   const int blocks = dca::ln_bwd_blocks(rows);
   Tensor partial = torch::empty({static_cast<int64_t>(blocks) * 2 * D}, fo);
-  Tensor dgb = need_param_grads ? torch::empty({2, D}, fo) : Tensor();
+  const bool acc = need_param_grads && want_acc(dgamma_acc) && want_acc(dbeta_acc);
+  Tensor dgb;
+  dca::ColumnOut out;
+  if (acc) {
+    check_acc(*dgamma_acc, D, x, "ln_bwd");
+    check_acc(*dbeta_acc, D, x, "ln_bwd");
+    TORCH_CHECK(dgamma_acc->scalar_type() == dbeta_acc->scalar_type(), "ln_bwd: gamma/beta grad dtypes differ");
+    out = {dgamma_acc->data_ptr(), dbeta_acc->data_ptr(), D,
+           dgamma_acc->scalar_type() == at::kBFloat16, true};
+  } else if (need_param_grads) {
+    dgb = torch::empty({2, D}, fo);
+    out = {dgb.data_ptr(), nullptr, 2 * static_cast<int64_t>(D), false, false};
+  }
   Tensor ds = dsum.has_value() && dsum->defined() ? dsum->contiguous() : Tensor();
   dca::layernorm_bwd(tdt(x), dy.data_ptr(), x.data_ptr(), fp(gamma), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), ds.defined() ? ds.data_ptr() : nullptr, dx.data_ptr(),
-                     partial.data_ptr<float>(), need_param_grads ? dgb.data_ptr<float>() : nullptr,
-                     rows, D, stream());
-  if (!need_param_grads) return {dx, Tensor(), Tensor()};
+                     partial.data_ptr<float>(), need_param_grads ? &out : nullptr, rows, D, stream());
+  if (!need_param_grads || acc) return {dx, Tensor(), Tensor()};
   return {dx, dgb[0], dgb[1]};
+}
+
+// bias: fp32 or bf16 [N] (read directly -- no cast kernel for bf16 models).
+std::pair<const void*, bool> bias_arg(const OptT& bias, int64_t N) {
+  if (!bias.has_value() || !bias->defined()) return {nullptr, false};
+  TORCH_CHECK(bias->is_contiguous() && bias->numel() == N &&
+                  (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16),
+              "bias_gelu: bias must be a contiguous fp32/bf16 [N] tensor");
+  return {bias->data_ptr(), bias->scalar_type() == at::kBFloat16};
 }
 
 Tensor bias_gelu(const Tensor& x, const OptT& bias) {
@@ -103,24 +103,59 @@ Tensor bias_gelu(const Tensor& x, const OptT& bias) {
   const int N = static_cast<int>(x.size(-1));
   TORCH_CHECK(N % 8 == 0, "bias_gelu: last dim must be a multiple of 8");
   Tensor y = torch::empty_like(x);
-  dca::bias_gelu_fwd(tdt(x), x.data_ptr(), fp(bias), y.data_ptr(), x.numel() / N, N, stream());
+  auto [bp, bbf] = bias_arg(bias, N);
+  dca::bias_gelu_fwd(tdt(x), x.data_ptr(), bp, bbf, y.data_ptr(), x.numel() / N, N, stream());
   return y;
 }
 
-std::vector<Tensor> bias_gelu_bwd(const Tensor& dy_in, const Tensor& x, const OptT& bias) {
+std::vector<Tensor> bias_gelu_bwd(const Tensor& dy_in, const Tensor& x, const OptT& bias,
+                                  bool need_db, const OptT& dbias_acc) {
   const c10::DeviceGuard g(x.device());
   Tensor dy = dy_in.contiguous();
   const int N = static_cast<int>(x.size(-1));
   const int64_t rows = x.numel() / N;
   Tensor dx = torch::empty_like(x);
-  const bool want_db = bias.has_value() && bias->defined();
+  auto [bp, bbf] = bias_arg(bias, N);
+  const bool want_db = need_db && bp != nullptr;
+  const bool acc = want_db && want_acc(dbias_acc);
   auto fo = x.options().dtype(at::kFloat);
   Tensor partial = want_db ? torch::empty({static_cast<int64_t>(dca::bias_gelu_bwd_row_blocks(rows)) * N}, fo) : Tensor();
-  Tensor db = want_db ? torch::empty({N}, fo) : Tensor();
-  dca::bias_gelu_bwd(tdt(x), dy.data_ptr(), x.data_ptr(), fp(bias), dx.data_ptr(),
-                     want_db ? partial.data_ptr<float>() : nullptr,
-                     want_db ? db.data_ptr<float>() : nullptr, rows, N, stream());
+  Tensor db;
+  dca::ColumnOut out;
+  if (acc) {
+    check_acc(*dbias_acc, N, x, "bias_gelu_bwd");
+    out = {dbias_acc->data_ptr(), nullptr, N, dbias_acc->scalar_type() == at::kBFloat16, true};
+  } else if (want_db) {
+    db = torch::empty({N}, fo);
+    out = {db.data_ptr(), nullptr, N, false, false};
+  }
+  dca::bias_gelu_bwd(tdt(x), dy.data_ptr(), x.data_ptr(), bp, bbf, dx.data_ptr(),
+                     want_db ? partial.data_ptr<float>() : nullptr, want_db ? &out : nullptr, rows,
+                     N, stream());
   return {dx, db};
+}
+
+// Bias gradient of a linear layer: sum of dy [.., N] over all leading dims. Accumulates into
+// `acc` (the bias .grad) when given and returns an undefined tensor; else returns fp32 [N].
+Tensor bias_grad(const Tensor& dy_in, const OptT& acc) {
+  const c10::DeviceGuard g(dy_in.device());
+  Tensor dy = dy_in.contiguous();
+  const int N = static_cast<int>(dy.size(-1));
+  TORCH_CHECK(N % 8 == 0, "bias_grad: last dim must be a multiple of 8");
+  const int64_t rows = dy.numel() / N;
+  auto fo = dy.options().dtype(at::kFloat);
+  Tensor partial = torch::empty({static_cast<int64_t>(dca::row_sum_blocks(rows)) * N}, fo);
+  Tensor db;
+  dca::ColumnOut out;
+  if (want_acc(acc)) {
+    check_acc(*acc, N, dy, "bias_grad");
+    out = {acc->data_ptr(), nullptr, N, acc->scalar_type() == at::kBFloat16, true};
+  } else {
+    db = torch::empty({N}, fo);
+    out = {db.data_ptr(), nullptr, N, false, false};
+  }
+  dca::row_sum(tdt(dy), dy.data_ptr(), partial.data_ptr<float>(), out, rows, N, stream());
+  return db;
 }
 
 Tensor rope_apply(const Tensor& x, const Tensor& cosT, const Tensor& sinT, int64_t H, int64_t S,
@@ -228,9 +263,15 @@ Tensor ce_bwd(const Tensor& logits, const Tensor& target, const Tensor& lse, con
 
 void register_transformer_ops(pybind11::module& m) {
   m.def("ln_fwd", &ln_fwd);
-  m.def("ln_bwd", &ln_bwd);
+  m.def("ln_bwd", &ln_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("gamma"),
+        pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("dsum"),
+        pybind11::arg("need_param_grads"), pybind11::arg("dgamma_acc") = pybind11::none(),
+        pybind11::arg("dbeta_acc") = pybind11::none());
+  m.def("bias_grad", &bias_grad, pybind11::arg("dy"), pybind11::arg("acc") = pybind11::none());
   m.def("bias_gelu", &bias_gelu);
-  m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd, pybind11::arg("dy"), pybind11::arg("x"),
+        pybind11::arg("bias"), pybind11::arg("need_db") = true,
+        pybind11::arg("dbias_acc") = pybind11::none());
   m.def("rope", &rope_apply);
   m.def("attn_fwd", &attn_fwd);
   m.def("ce_fwd", &ce_fwd);

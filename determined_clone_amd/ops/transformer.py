@@ -16,7 +16,7 @@ from typing import Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from determined_clone_amd.ops import _ext
+from determined_clone_amd.ops import _ext, _grad
 
 # ----------------------------------------------------------------------------- references
 
@@ -93,6 +93,7 @@ class _LayerNorm(torch.autograd.Function):
         ctx.save_for_backward(s if res is not None else x, weight, mean, rstd)
         ctx.has_res = res is not None
         ctx.w_dtype = weight.dtype if weight is not None else None
+        ctx.params = (weight, bias)
         if res is not None:
             return y, s
         return y
@@ -101,8 +102,13 @@ class _LayerNorm(torch.autograd.Function):
     def backward(ctx, dy, dsum=None):
         xin, weight, mean, rstd = ctx.saved_tensors
         need_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        acc_g, acc_b = (_grad.target(ctx.params[0]), _grad.target(ctx.params[1])) if need_w else (None, None)
+        if acc_g is None or acc_b is None or acc_g.dtype != acc_b.dtype:
+            acc_g = acc_b = None
         dx, dg, db = _ext.load().ln_bwd(dy, xin, _f32(weight), mean, rstd,
-                                        dsum if ctx.has_res else None, need_w)
+                                        dsum if ctx.has_res else None, need_w, acc_g, acc_b)
+        if acc_g is not None:
+            need_w = False  # accumulated into .grad in-kernel
         if need_w:
             dg = dg.to(ctx.w_dtype)
             db = db.to(ctx.w_dtype)
@@ -119,23 +125,78 @@ def layer_norm(x: torch.Tensor, weight: Optional[torch.Tensor], bias: Optional[t
     return _LayerNorm.apply(x, residual, weight, bias, eps)
 
 
+def _bias_arg(bias: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    # the kernels read fp32 or bf16 biases directly; anything else is cast once
+    if bias is None or (bias.dtype in (torch.float32, torch.bfloat16) and bias.is_contiguous()):
+        return bias
+    return bias.float().contiguous()
+
+
 class _BiasGelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, bias):
         x = x.contiguous()
-        y = _ext.load().bias_gelu(x, _f32(bias))
-        ctx.save_for_backward(x, bias)
+        b = _bias_arg(bias)
+        y = _ext.load().bias_gelu(x, b)
+        ctx.save_for_backward(x, b)
+        ctx.bias = bias
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, bias = ctx.saved_tensors
-        dx, db = _ext.load().bias_gelu_bwd(dy, x, _f32(bias))
-        if bias is not None and ctx.needs_input_grad[1]:
-            db = db.to(bias.dtype)
-        else:
-            db = None
-        return dx, db
+        x, b = ctx.saved_tensors
+        need_db = b is not None and ctx.needs_input_grad[1]
+        acc = _grad.target(ctx.bias) if need_db else None
+        dx, db = _ext.load().bias_gelu_bwd(dy, x, b, need_db, acc)
+        if not need_db or acc is not None:
+            return dx, None
+        return dx, db.to(ctx.bias.dtype)
+
+
+class _Linear(torch.autograd.Function):
+    """``y = x @ w.T + b`` whose backward accumulates straight into the parameters' flat
+    ``.grad`` views: dW by a GEMM with beta = 1 (``grad.addmm_``), db by the fused column
+    reduction (``bias_grad``) -- no AccumulateGrad adds, no torch reduce kernel (see
+    ``ops._grad``). Falls back to returning gradients when the parameters have no persistent
+    ``.grad``."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.params = (weight, bias)
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        w_param, b_param = ctx.params
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, x.shape[-1])
+            acc = _grad.target(w_param)
+            if acc is not None:
+                acc.addmm_(dy2.t(), x2)
+            else:
+                dw = dy2.t() @ x2
+        if b_param is not None and ctx.needs_input_grad[2]:
+            acc = _grad.target(b_param)
+            if dy2.shape[-1] % 8 == 0 and dy2.is_cuda:
+                out = _ext.load().bias_grad(dy2, acc)
+                db = None if acc is not None else out.to(b_param.dtype)
+            else:
+                db = dy2.sum(0).to(b_param.dtype)
+        return dx, dw, db
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.linear`` with fused gradient accumulation into flat ``.grad`` buffers on the GPU."""
+    if not x.is_cuda or x.dtype != weight.dtype or (bias is not None and bias.dtype != x.dtype) or \
+            torch.is_autocast_enabled():
+        return F.linear(x, weight, bias)
+    return _Linear.apply(x, weight, bias)
 
 
 def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor]) -> torch.Tensor:

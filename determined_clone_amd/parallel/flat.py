@@ -120,6 +120,9 @@ class FlatParamSpace:
                     if p.grad is not None:
                         g.copy_(p.grad)
                     p.grad = g
+                    # fused kernels may accumulate straight into this persistent .grad view
+                    # (see ops.batchnorm._direct_grad_targets)
+                    p._dca_direct_grad = True
             self.buffers[dtype] = buf
 
     # ------------------------------------------------------------------ helpers
@@ -138,6 +141,12 @@ class FlatParamSpace:
         for buf in self.buffers.values():
             for seg in buf.segments:
                 yield seg.param
+
+    def release_direct_grad(self) -> None:
+        """Stop fused kernels from accumulating into these parameters' ``.grad`` (needed before
+        driving backward with ``torch.autograd.grad`` over them; see ``ops._grad``)."""
+        for p in self.params():
+            p._dca_direct_grad = False
 
     def zero_grad(self) -> None:
         for buf in self.buffers.values():

@@ -213,3 +213,36 @@ def test_bn_relu_maxpool_stem(dtype, hw):
     y3 = batchnorm.batch_norm_relu_maxpool(x, w, b, rm, rv, training=False, eps=1e-5)
     y4 = batchnorm.reference_bn_relu_maxpool(x.float(), w, b, rm, rv, False, 0.1, 1e-5)
     torch.testing.assert_close(y3.float(), y4, atol=tol * 4, rtol=tol)
+
+
+def test_bn_direct_grad_accumulation_into_flat_buffer():
+    """BN weight/bias grads accumulated in-kernel into FlatParamSpace .grad views equal autograd's
+    AccumulateGrad path over two backward passes, and post-accumulate hooks (DDP/ZeRO triggers)
+    still fire once per backward."""
+    _ext_loaded()
+    from determined_clone_amd.parallel.flat import FlatParamSpace
+
+    torch.manual_seed(0)
+    C = 64
+    x = torch.randn(8, C, 10, 10, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(8, C, 10, 10, device="cuda")
+    w1 = torch.nn.Parameter(torch.rand(C, device="cuda") + 0.5)
+    b1 = torch.nn.Parameter(torch.randn(C, device="cuda"))
+    w2 = torch.nn.Parameter(w1.detach().clone())
+    b2 = torch.nn.Parameter(b1.detach().clone())
+    space = FlatParamSpace([[w1, b1]])
+    assert w1._dca_direct_grad and w1.grad is not None
+    calls = []
+    w1.register_post_accumulate_grad_hook(lambda p: calls.append("w"))
+    b1.register_post_accumulate_grad_hook(lambda p: calls.append("b"))
+    ptr = w1.grad.data_ptr()
+    for w, b in ((w1, b1), (w2, b2)):
+        for _ in range(2):
+            rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+            y = batchnorm.batch_norm_act(x, w, b, rm, rv)
+            (y.float() * g).sum().backward()
+    assert w1.grad.data_ptr() == ptr  # still the flat view
+    assert sorted(calls) == ["b", "b", "w", "w"]
+    torch.testing.assert_close(w1.grad, w2.grad, atol=1e-3, rtol=1e-4)
+    torch.testing.assert_close(b1.grad, b2.grad, atol=1e-3, rtol=1e-4)
+    assert space.grads_are_views()

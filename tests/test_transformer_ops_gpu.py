@@ -177,3 +177,79 @@ def test_fused_cross_entropy(dtype):
     (la * 3.0).backward()
     (lb * 3.0).backward()
     assert _rel(a.grad, b.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,N", [(1, 8), (333, 1024), (8192, 3072), (4097, 4096)])
+def test_bias_grad_column_sum(dtype, rows, N):
+    C = _C()
+    torch.manual_seed(0)
+    dy = torch.randn(rows, N, device="cuda").to(dtype)
+    ref = dy.float().sum(0)
+    out = C.bias_grad(dy)
+    assert out.dtype == torch.float32
+    torch.testing.assert_close(out, ref, atol=1e-3 * math.sqrt(rows), rtol=1e-4)
+    acc = torch.randn(N, device="cuda").to(dtype)
+    want = (acc.float() + ref).to(dtype)
+    assert C.bias_grad(dy, acc) is None
+    torch.testing.assert_close(acc.float(), want.float(), atol=1e-3 * math.sqrt(rows) + (0.02 if dtype == torch.bfloat16 else 0), rtol=1e-2)
+
+
+def _flat(params):
+    from determined_clone_amd.parallel.flat import FlatParamSpace
+
+    space = FlatParamSpace([params])
+    calls = []
+    for p in params:
+        p.register_post_accumulate_grad_hook(lambda q, calls=calls: calls.append(id(q)))
+    return space, calls
+
+
+@pytest.mark.parametrize("bias", [True, False])
+def test_linear_direct_grad_accumulation(bias):
+    """T.linear accumulates dW (GEMM beta=1) and db (fused column sum) into flat .grad views;
+    equals autograd's F.linear over two backward passes; post-accumulate hooks fire."""
+    _C()
+    torch.manual_seed(0)
+    x = torch.randn(4, 96, 256, device="cuda").bfloat16()
+    g = torch.randn(4, 96, 512, device="cuda").bfloat16()
+    w1 = torch.nn.Parameter(torch.randn(512, 256, device="cuda").bfloat16() * 0.05)
+    b1 = torch.nn.Parameter(torch.randn(512, device="cuda").bfloat16()) if bias else None
+    w2 = torch.nn.Parameter(w1.detach().clone())
+    b2 = torch.nn.Parameter(b1.detach().clone()) if bias else None
+    params = [p for p in (w1, b1) if p is not None]
+    space, calls = _flat(params)
+    ptrs = [p.grad.data_ptr() for p in params]
+    xs = [x.clone().requires_grad_(True) for _ in range(2)]
+    for _ in range(2):
+        (T.linear(xs[0], w1, b1) * g).float().sum().backward()
+        (torch.nn.functional.linear(xs[1], w2, b2) * g).float().sum().backward()
+    assert [p.grad.data_ptr() for p in params] == ptrs
+    assert len(calls) == 2 * len(params)
+    assert _rel(w1.grad, w2.grad) < 1e-2
+    if bias:
+        assert _rel(b1.grad, b2.grad) < 1e-2
+    assert _rel(xs[0].grad, xs[1].grad) < 1e-2
+
+
+def test_layer_norm_and_bias_gelu_direct_grad_accumulation():
+    _C()
+    torch.manual_seed(0)
+    D, N = 256, 1024
+    x = torch.randn(8, 64, D, device="cuda").bfloat16()
+    r = torch.randn(8, 64, D, device="cuda").bfloat16()
+    h = torch.randn(8, 64, N, device="cuda").bfloat16()
+    lw1 = torch.nn.Parameter(torch.rand(D, device="cuda") + 0.5)
+    lb1 = torch.nn.Parameter(torch.randn(D, device="cuda"))
+    gb1 = torch.nn.Parameter(torch.randn(N, device="cuda").bfloat16())
+    lw2, lb2, gb2 = (torch.nn.Parameter(p.detach().clone()) for p in (lw1, lb1, gb1))
+    space, calls = _flat([lw1, lb1, gb1])
+    for _ in range(2):
+        for lw, lb, gb in ((lw1, lb1, gb1), (lw2, lb2, gb2)):
+            y, s = T.layer_norm(x, lw, lb, 1e-5, residual=r)
+            z = T.bias_gelu(h, gb)
+            (y.float().square().sum() + s.float().sum() + z.float().sum()).backward()
+    assert len(calls) == 6
+    assert _rel(lw1.grad, lw2.grad) < 1e-4
+    assert _rel(lb1.grad, lb2.grad) < 1e-4
+    assert _rel(gb1.grad, gb2.grad) < 1e-2
