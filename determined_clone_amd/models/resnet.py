@@ -10,7 +10,10 @@ architecture is defined here. It is laid out for MI355X rather than copied:
   GPU runs the hand-written NHWC HIP kernels in ``ops/csrc/batchnorm.hip`` (stats + apply + add +
   ReLU in two passes over HBM instead of four separate PyTorch ops); BN affine params and running
   stats stay fp32 while activations are bf16;
-* the stem max-pool and the classifier are plain PyTorch ops (they are <2 % of step time).
+* 1x1/stride-1 convolutions go through ``ops.conv.pointwise_conv``: MIOpen by default (measured
+  faster), or with ``DCA_CONV1X1=1`` hand-written MFMA GEMM kernels (``ops/csrc/conv1x1.hip``)
+  whose forward epilogue also reduces the next BatchNorm's statistics;
+* the classifier is a plain PyTorch op (<2 % of step time).
 """
 from typing import List, Optional, Type
 
@@ -19,6 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from determined_clone_amd.ops import batchnorm as bn_ops
+from determined_clone_amd.ops.conv import pointwise_conv
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -74,12 +78,19 @@ class Bottleneck(nn.Module):
             )
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
+        # 1x1/stride-1 convolutions: ops/conv.py (MIOpen, or opt-in MFMA kernels whose forward
+        # epilogue also reduces the following BatchNorm's statistics)
+        if self.downsample is None:
+            identity = x
+        else:
+            ds_conv, ds_bn = self.downsample
+            identity = ds_bn(pointwise_conv(ds_conv, x, ds_bn.training))
+        out = self.bn1(pointwise_conv(self.conv1, x, self.bn1.training))
         out = self.bn2(self.conv2(out))
         # identity shortcut: x also feeds conv1, so its gradient can be summed inside the
         # producer's BN backward (no separate autograd add)
-        return self.bn3(self.conv3(out), residual=identity, fuse_residual_grad=self.downsample is None)
+        return self.bn3(pointwise_conv(self.conv3, out, self.bn3.training), residual=identity,
+                        fuse_residual_grad=self.downsample is None)
 
 
 class ResNet(nn.Module):

@@ -40,10 +40,11 @@ class ResidualGradSink:
 class _BNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, num_batches, momentum,
-                eps, relu, res_sink, out_sink):
+                eps, relu, res_sink, out_sink, partials):
         C = _ext.load()
         y, mean, invstd, mask = C.bn_fwd_train(x, residual, weight, bias, running_mean,
-                                               running_var, num_batches, momentum, eps, relu)
+                                               running_var, num_batches, momentum, eps, relu,
+                                               partials)
         # The ReLU decision is kept as a bitmask (1/16 of y) instead of y itself.
         ctx.save_for_backward(x, mask if relu else None, weight, mean, invstd)
         ctx.relu = relu
@@ -72,7 +73,7 @@ class _BNActTrain(torch.autograd.Function):
             else:
                 dres_out = dres
         return (dx, dgamma if need_w else None, dbeta if need_w else None, dres_out,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None)
 
 
 def _direct_grad_targets(weight: Optional[torch.Tensor], bias: Optional[torch.Tensor]):
@@ -113,6 +114,8 @@ def batch_norm_act(x: torch.Tensor, weight: Optional[torch.Tensor], bias: Option
         return reference_batch_norm_act(x, weight, bias, running_mean, running_var, residual,
                                         training, momentum if momentum is not None else 0.0, eps,
                                         relu)
+    # per-block (sum, sum^2) of x already reduced by its producer (ops.conv.pointwise_conv)
+    partials = getattr(x, "_dca_bn_partials", None)
     if x.dim() == 4:
         x = x.contiguous(memory_format=torch.channels_last)
         if residual is not None:
@@ -136,7 +139,7 @@ def batch_norm_act(x: torch.Tensor, weight: Optional[torch.Tensor], bias: Option
                                  running_mean if training else None,
                                  running_var if training else None,
                                  num_batches_tracked if training else None, float(momentum),
-                                 float(eps), relu, res_sink, out_sink)
+                                 float(eps), relu, res_sink, out_sink, partials)
         if out_sink is not None:
             y._dca_grad_sink = out_sink
         return y

@@ -1,0 +1,93 @@
+"""Pointwise (1x1, stride 1) NHWC convolution on the MFMA GEMM kernels of ``csrc/conv1x1.hip``.
+
+GPU path: forward GEMM (optionally emitting the per-block (sum, sum^2) statistics the following
+fused BatchNorm consumes instead of re-reading the output), dgrad GEMM and split-m wgrad, the
+weight gradient accumulated straight into the parameter's persistent ``.grad`` view when the
+optimizer's flat buffers own it (``ops/_grad.py``).
+CPU / unsupported shapes: ``torch.nn.functional.conv2d`` (also the fp32 oracle of the GPU tests).
+
+The partial statistics ride on the output tensor as ``y._dca_bn_partials`` and
+``ops.batchnorm.batch_norm_act`` picks them up when it normalises exactly that tensor.
+
+Status: OPT-IN (``DCA_CONV1X1=1``). Measured on MI355X at ResNet-50 bs256 shapes
+(``tools/bench_pointwise.py``, ``profiles/r8_pointwise_conv_study.txt``), MIOpen's NHWC 1x1
+kernels already stream the memory-bound layer1/layer2 shapes at ~5-6 TB/s and reach 500-650
+TFLOP/s on layer3/layer4; these kernels win only the layer3/4 weight gradients (6-25 %), lose the
+forward/dgrad by 1.3-2.4x, so the end-to-end step is slower (7.8k vs 9.2k img/s) even with the
+BatchNorm statistics pass removed. The model therefore keeps MIOpen by default.
+"""
+import os
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from determined_clone_amd.ops import _ext, _grad
+
+ENABLED = os.environ.get("DCA_CONV1X1", "0") == "1"
+
+
+class _Conv1x1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stats):
+        y, partial = _ext.load().conv1x1_fwd(x, weight, stats)
+        ctx.save_for_backward(x, weight)
+        if partial is not None:
+            ctx.mark_non_differentiable(partial)
+        return y, partial
+
+    @staticmethod
+    def backward(ctx, dy, _dpartial):
+        x, w = ctx.saved_tensors
+        C = _ext.load()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = C.conv1x1_dgrad(dy, w)
+        if ctx.needs_input_grad[1]:
+            acc = _grad.target(w)
+            dw = C.conv1x1_wgrad(dy, x, w, acc)
+            if acc is not None:
+                dw = None  # already accumulated into w.grad
+        return dx, dw, None
+
+
+def supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """True when ``conv(x)`` can run on the HIP pointwise kernels."""
+    if not (ENABLED and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16):
+        return False
+    if conv.kernel_size != (1, 1) or conv.stride != (1, 1) or conv.padding != (0, 0):
+        return False
+    if conv.groups != 1 or conv.dilation != (1, 1) or conv.bias is not None:
+        return False
+    w = conv.weight
+    if w.dtype != torch.bfloat16 or conv.in_channels % 64 or conv.out_channels % 64:
+        return False
+    return w.stride(0) == conv.in_channels and w.stride(1) == 1
+
+
+def pointwise_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> torch.Tensor:
+    """``conv(x)`` for a 1x1/stride-1 convolution in NHWC bf16; with ``bn_stats`` the output
+    carries the partial BatchNorm statistics of the forward epilogue (training only)."""
+    if not supported(conv, x):
+        return conv(x)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y, partial = _Conv1x1.apply(x, conv.weight, bool(bn_stats))
+    if partial is not None:
+        y._dca_bn_partials = partial
+    return y
+
+
+def take_bn_partials(x: torch.Tensor) -> Optional[torch.Tensor]:
+    """The fused statistics attached to ``x`` by :func:`pointwise_conv` (consumed once)."""
+    p = getattr(x, "_dca_bn_partials", None)
+    if p is not None:
+        x._dca_bn_partials = None
+    return p
+
+
+def reference_conv1x1(x: torch.Tensor, weight: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp32 oracle: ``(y, per-channel [sum, sum^2])`` of the convolution output."""
+    y = F.conv2d(x.float(), weight.float())
+    yc = y.permute(0, 2, 3, 1).reshape(-1, y.shape[1])
+    return y, torch.stack([yc.sum(0), (yc * yc).sum(0)])

@@ -519,17 +519,25 @@ void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64
                       const float* gamma, const float* beta, float* running_mean,
                       float* running_var, float momentum, float eps, bool relu, float* save_mean,
                       float* save_invstd, int64_t* num_batches, uint8_t* mask, float* workspace,
-                      hipStream_t st) {
-  ReduceGeom g = reduce_geom(C);
-  int B = reduce_blocks(M, C, g);
-  float* partial = workspace;
-  float* scale = workspace + static_cast<int64_t>(B) * 2 * C;
-  float* shift = scale + C;
-  switch (dt) {
-    case BnDtype::kBF16: launch_reduce<BF16>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
-    case BnDtype::kF16: launch_reduce<F16>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
-    default: launch_reduce<F32>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, g, st); break;
+                      const float* given_partials, int given_blocks, hipStream_t st) {
+  const float* partial = given_partials;
+  int B = given_blocks;
+  float* scale = workspace;
+  if (given_partials == nullptr) {
+    // statistics pass over x; with given_partials the producer (e.g. the pointwise-convolution
+    // GEMM epilogue, conv1x1.hip) already reduced them in the same [B][2][C] layout
+    ReduceGeom g = reduce_geom(C);
+    B = reduce_blocks(M, C, g);
+    float* part = workspace;
+    scale = workspace + static_cast<int64_t>(B) * 2 * C;
+    switch (dt) {
+      case BnDtype::kBF16: launch_reduce<BF16>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, part, B, g, st); break;
+      case BnDtype::kF16: launch_reduce<F16>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, part, B, g, st); break;
+      default: launch_reduce<F32>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, part, B, g, st); break;
+    }
+    partial = part;
   }
+  float* shift = scale + C;
   hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
                      C, M, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
                      save_invstd, scale, shift, num_batches);

@@ -17,7 +17,7 @@ void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64
                       const float* gamma, const float* beta, float* running_mean,
                       float* running_var, float momentum, float eps, bool relu, float* save_mean,
                       float* save_invstd, int64_t* num_batches, uint8_t* mask, float* workspace,
-                      hipStream_t st);
+                      const float* given_partials, int given_blocks, hipStream_t st);
 void bn_forward_affine(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
                        const float* scale, const float* shift, bool relu, hipStream_t st);
 void bn_relu_pool_forward(BnDtype dt, const void* x, void* y, uint8_t* idx, int N, int H, int W,
@@ -112,7 +112,7 @@ std::pair<int64_t, int> rows_channels(const Tensor& x) {
 std::vector<Tensor> bn_fwd_train(const Tensor& x, const OptT& residual, const OptT& weight,
                                  const OptT& bias, const OptT& running_mean,
                                  const OptT& running_var, const OptT& num_batches, double momentum,
-                                 double eps, bool relu) {
+                                 double eps, bool relu, const OptT& partials) {
   CHECK_DEV(x);
   const c10::DeviceGuard guard(x.device());
   auto [M, C] = rows_channels(x);
@@ -124,7 +124,14 @@ std::vector<Tensor> bn_fwd_train(const Tensor& x, const OptT& residual, const Op
   auto fopt = x.options().dtype(at::kFloat);
   Tensor y = torch::empty_like(x);
   Tensor save_mean = torch::empty({C}, fopt), save_invstd = torch::empty({C}, fopt);
-  Tensor ws = torch::empty({dca::bn_workspace_floats(M, C)}, fopt);
+  const bool given = partials.has_value() && partials->defined();
+  if (given) {
+    TORCH_CHECK(partials->scalar_type() == at::kFloat && partials->is_contiguous() &&
+                    partials->dim() == 3 && partials->size(1) == 2 && partials->size(2) == C &&
+                    partials->device() == x.device(),
+                "batchnorm: partial statistics must be contiguous fp32 [blocks, 2, C]");
+  }
+  Tensor ws = torch::empty({given ? 2 * C : dca::bn_workspace_floats(M, C)}, fopt);
   Tensor mask = relu ? torch::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
   dca::bn_forward_train(bn_dtype(x), x.data_ptr(), vptr_or_null(residual), y.data_ptr(), M, C,
                         ptr_or_null<float>(weight), ptr_or_null<float>(bias),
@@ -133,7 +140,8 @@ std::vector<Tensor> bn_fwd_train(const Tensor& x, const OptT& residual, const Op
                         save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
                         ptr_or_null<int64_t>(num_batches),
                         relu ? mask.data_ptr<uint8_t>() : nullptr, ws.data_ptr<float>(),
-                        cur_stream());
+                        given ? partials->data_ptr<float>() : nullptr,
+                        given ? static_cast<int>(partials->size(0)) : 0, cur_stream());
   return {y, save_mean, save_invstd, mask};
 }
 
@@ -412,10 +420,14 @@ void scale_(const Tensor& x, double s, const OptT& dev_scale) {
 
 // Extra kernel families register themselves from their own translation units.
 void register_transformer_ops(pybind11::module& m);
+void register_conv_ops(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "determined_clone_amd MI355X (gfx950) HIP kernels";
-  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_fwd_train", &bn_fwd_train, pybind11::arg("x"), pybind11::arg("residual"),
+        pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
+        pybind11::arg("running_var"), pybind11::arg("num_batches"), pybind11::arg("momentum"),
+        pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("partials") = pybind11::none());
   m.def("bn_fwd_affine", &bn_fwd_affine);
   m.def("bn_bwd_train", &bn_bwd_train, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("mask"),
         pybind11::arg("weight"), pybind11::arg("save_mean"), pybind11::arg("save_invstd"),
@@ -434,4 +446,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("amp_scaler_update", &amp_scaler_update);
   m.def("scale_", &scale_);
   register_transformer_ops(m);
+  register_conv_ops(m);
 }

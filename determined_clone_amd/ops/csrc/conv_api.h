@@ -1,0 +1,21 @@
+// Host API of the pointwise-convolution family (conv1x1.hip), shared by the kernels' translation
+// unit and the PyTorch bindings (conv_bindings.cpp). Activations are NHWC bf16 viewed as
+// [M = N*H*W][C] row-major matrices; weights are bf16 [Cout][Cin]. Channel counts are multiples of
+// 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dca {
+// Number of row blocks of the forward GEMM = first dimension of its BatchNorm partial-statistics
+// output ([blocks][2][Cout] fp32: per-block sum and sum of squares of the bf16 outputs).
+int conv1x1_fwd_row_blocks(int64_t M, int Cout);
+void conv1x1_fwd(const void* x, const void* w, void* y, float* partial, int64_t M, int Cin,
+                 int Cout, hipStream_t st);
+// wt: Cin*Cout bf16 scratch for the transposed weight.
+void conv1x1_dgrad(const void* dy, const void* w, void* wt, void* dx, int64_t M, int Cin, int Cout,
+                   hipStream_t st);
+int64_t conv1x1_wgrad_ws_floats(int64_t M, int Cin, int Cout);
+void conv1x1_wgrad(const void* dy, const void* x, float* ws, void* dw, bool dw_f32,
+                   bool accumulate, int64_t M, int Cin, int Cout, hipStream_t st);
+}  // namespace dca

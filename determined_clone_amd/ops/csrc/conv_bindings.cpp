@@ -1,0 +1,107 @@
+// Bindings for the pointwise-convolution family (conv1x1.hip).
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+
+#include <hip/hip_runtime.h>
+
+#include "conv_api.h"
+
+namespace {
+using torch::Tensor;
+using OptT = c10::optional<Tensor>;
+
+hipStream_t stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+// NHWC activation [N, C, H, W] (channels_last) viewed as a row-major [N*H*W][C] matrix.
+int64_t nhwc_rows(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4, what,
+              ": bf16 4-D GPU tensor required");
+  TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), what, ": channels_last layout required");
+  TORCH_CHECK(t.size(1) % 64 == 0, what, ": channels must be a multiple of 64");
+  const int64_t M = t.size(0) * t.size(2) * t.size(3);
+  TORCH_CHECK(M < (int64_t{1} << 31), what, ": too many rows");
+  return M;
+}
+
+void check_weight(const Tensor& w, int64_t cout, int64_t cin) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(0) == cout &&
+                  w.size(1) == cin && w.size(2) == 1 && w.size(3) == 1,
+              "conv1x1: weight must be bf16 [Cout, Cin, 1, 1]");
+  TORCH_CHECK(w.stride(0) == cin && w.stride(1) == 1, "conv1x1: weight must be dense [Cout][Cin]");
+}
+
+Tensor nhwc_empty(const Tensor& like, int64_t c) {
+  return torch::empty({like.size(0), c, like.size(2), like.size(3)},
+                      like.options().memory_format(at::MemoryFormat::ChannelsLast));
+}
+
+std::vector<Tensor> conv1x1_fwd(const Tensor& x, const Tensor& w, bool stats) {
+  const c10::DeviceGuard g(x.device());
+  const int64_t M = nhwc_rows(x, "conv1x1_fwd");
+  const int64_t cin = x.size(1), cout = w.size(0);
+  check_weight(w, cout, cin);
+  TORCH_CHECK(cout % 64 == 0, "conv1x1_fwd: Cout must be a multiple of 64");
+  Tensor y = nhwc_empty(x, cout);
+  Tensor partial;
+  if (stats) {
+    const int B = dca::conv1x1_fwd_row_blocks(M, static_cast<int>(cout));
+    partial = torch::empty({B, 2, cout}, x.options().dtype(at::kFloat));
+  }
+  dca::conv1x1_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                   stats ? partial.data_ptr<float>() : nullptr, M, static_cast<int>(cin),
+                   static_cast<int>(cout), stream());
+  return {y, partial};
+}
+
+Tensor conv1x1_dgrad(const Tensor& dy_in, const Tensor& w) {
+  const Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const c10::DeviceGuard g(dy.device());
+  const int64_t M = nhwc_rows(dy, "conv1x1_dgrad");
+  const int64_t cout = dy.size(1), cin = w.size(1);
+  check_weight(w, cout, cin);
+  TORCH_CHECK(cin % 64 == 0, "conv1x1_dgrad: Cin must be a multiple of 64");
+  Tensor wt = torch::empty({cin, cout}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  Tensor dx = nhwc_empty(dy, cin);
+  dca::conv1x1_dgrad(dy.data_ptr(), w.data_ptr(), wt.data_ptr(), dx.data_ptr(), M,
+                     static_cast<int>(cin), static_cast<int>(cout), stream());
+  return dx;
+}
+
+// Returns the weight gradient; with `acc` (the parameter's persistent .grad view) the result is
+// added into it in place and `acc` is returned.
+Tensor conv1x1_wgrad(const Tensor& dy_in, const Tensor& x, const Tensor& w, const OptT& acc) {
+  const Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const c10::DeviceGuard g(dy.device());
+  const int64_t M = nhwc_rows(dy, "conv1x1_wgrad");
+  TORCH_CHECK(nhwc_rows(x, "conv1x1_wgrad") == M, "conv1x1_wgrad: dy / x row mismatch");
+  const int64_t cout = dy.size(1), cin = x.size(1);
+  check_weight(w, cout, cin);
+  Tensor ws = torch::empty({dca::conv1x1_wgrad_ws_floats(M, static_cast<int>(cin), static_cast<int>(cout))},
+                           dy.options().dtype(at::kFloat));
+  Tensor out;
+  bool accumulate = false;
+  if (acc.has_value() && acc->defined()) {
+    out = *acc;
+    TORCH_CHECK(out.numel() == cout * cin && out.device() == dy.device() && out.dim() == 4 &&
+                    (out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16) &&
+                    out.stride(0) == cin && out.stride(1) == 1,
+                "conv1x1_wgrad: accumulation target must be a dense fp32/bf16 [Cout, Cin, 1, 1]");
+    accumulate = true;
+  } else {
+    out = torch::empty({cout, cin, 1, 1}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  }
+  dca::conv1x1_wgrad(dy.data_ptr(), x.data_ptr(), ws.data_ptr<float>(), out.data_ptr(),
+                     out.scalar_type() == at::kFloat, accumulate, M, static_cast<int>(cin),
+                     static_cast<int>(cout), stream());
+  return out;
+}
+
+}  // namespace
+
+void register_conv_ops(pybind11::module& m) {
+  m.def("conv1x1_fwd", &conv1x1_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stats"));
+  m.def("conv1x1_dgrad", &conv1x1_dgrad);
+  m.def("conv1x1_wgrad", &conv1x1_wgrad, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"),
+        pybind11::arg("acc") = pybind11::none());
+}
