@@ -657,6 +657,10 @@ def build_parser() -> argparse.ArgumentParser:
     sp = cmd(pr, "list ls", project_list); sp.add_argument("workspace")
     sp = cmd(pr, "create", project_create); sp.add_argument("workspace"); sp.add_argument("name")
 
+    from determined_clone_amd.cli import rbac as rbac_cli
+
+    rbac_cli.register(cmd, group)
+
     d = group("deploy")
     lo = d.add_parser("local").add_subparsers(dest="deploy_cmd")
     for name in ("cluster-up", "cluster-down", "master-up", "agent-up"):

@@ -19,6 +19,8 @@ def main() -> None:
     ap.add_argument("--scheduler", default=None, choices=[None, "priority", "fair_share", "round_robin"])
     ap.add_argument("--fit", default=None, choices=[None, "best", "worst"])
     ap.add_argument("--checkpoint-dir", default=None)
+    ap.add_argument("--authz", default=None, choices=[None, "basic", "rbac"],
+                    help="security.authz.type: basic (admin-only cluster administration) or rbac")
     args = ap.parse_args()
     cfg = {}
     if args.config_file:
@@ -32,7 +34,8 @@ def main() -> None:
     m = Master(args.db, scheduler=args.scheduler or sched.get("type", "priority"),
                fit=args.fit or sched.get("fitting_policy", "best"),
                preemption=bool(sched.get("preemption", True)), checkpoint_storage=cs,
-               cluster_name=cfg.get("cluster_name", "default"))
+               cluster_name=cfg.get("cluster_name", "default"),
+               authz=args.authz or ((cfg.get("security") or {}).get("authz") or {}).get("type", "basic"))
     srv = MasterServer(m, args.host, int(cfg.get("port", args.port))).start()
     logging.info(f"master listening on {m.master_url}")
     stop = threading.Event()

@@ -15,6 +15,7 @@ import uuid
 from typing import Any, Dict, List, Optional, Tuple
 
 from determined_clone_amd.config import expconf
+from determined_clone_amd.master.rbac import Authz
 from determined_clone_amd.master.db import DB, dec, now
 from determined_clone_amd.master.experiment import (ACTIVE, PAUSED, TERMINAL, Experiment, Trial,
                                                     experiment_row_to_api, trial_row_to_api)
@@ -89,8 +90,10 @@ class Webhooks:
 class Master:
     def __init__(self, db_path: str = ":memory:", scheduler: str = "priority", fit: str = "best",
                  preemption: bool = True, checkpoint_storage: Optional[Dict[str, Any]] = None,
-                 cluster_name: str = "default", master_url: str = "http://127.0.0.1:8080") -> None:
+                 cluster_name: str = "default", master_url: str = "http://127.0.0.1:8080",
+                 authz: str = "basic") -> None:
         self.db = DB(db_path)
+        self.authz = Authz(self.db, authz)
         self.cluster_id = self.db.kv_get("cluster_id") or str(uuid.uuid4())
         self.db.kv_set("cluster_id", self.cluster_id)
         self.cluster_name = cluster_name
