@@ -35,7 +35,7 @@ class Context:
                  searcher: Optional[SearcherContext] = None,
                  info: Optional[_info.ClusterInfo] = None, experimental: Any = None,
                  _tensorboard_manager: Any = None, _heartbeat: Optional[_Heartbeat] = None,
-                 _session: Any = None) -> None:
+                 _session: Any = None, _log_shipper: Any = None) -> None:
         self.checkpoint = checkpoint
         self.distributed = distributed or DummyDistributedContext()
         self.preempt = preempt or DummyPreemptContext(self.distributed)
@@ -49,8 +49,11 @@ class Context:
         self._tensorboard_manager = _tensorboard_manager
         self._heartbeat = _heartbeat
         self._session = _session
+        self._log_shipper = _log_shipper
 
     def start(self) -> None:
+        if self._log_shipper is not None:
+            self._log_shipper.start()
         self.preempt.start()
         if self._tensorboard_manager is not None:
             self._tensorboard_manager.start()
@@ -69,6 +72,8 @@ class Context:
             self._tensorboard_manager.close()
         if self._heartbeat is not None:
             self._heartbeat.close(exc_type, exc_val, exc_tb)
+        if self._log_shipper is not None:
+            self._log_shipper.close(exc_type, exc_val, exc_tb)
 
     def __exit__(self, exc_type: Optional[type], exc_val: Optional[BaseException],
                  exc_tb: Optional[types.TracebackType]) -> None:

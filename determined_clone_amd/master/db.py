@@ -28,14 +28,14 @@ CREATE TABLE IF NOT EXISTS experiments (
   id INTEGER PRIMARY KEY AUTOINCREMENT, config TEXT, original_config TEXT, model_definition BLOB,
   state TEXT, progress REAL DEFAULT 0, start_time REAL, end_time REAL, archived INTEGER DEFAULT 0,
   parent_id INTEGER, owner_id INTEGER, project_id INTEGER, job_id TEXT, searcher_snapshot TEXT,
-  notes TEXT DEFAULT '', unmanaged INTEGER DEFAULT 0);
+  notes TEXT DEFAULT '', unmanaged INTEGER DEFAULT 0, external_experiment_id TEXT);
 CREATE TABLE IF NOT EXISTS trials (
   id INTEGER PRIMARY KEY AUTOINCREMENT, experiment_id INTEGER, request_id TEXT, hparams TEXT,
   state TEXT, start_time REAL, end_time REAL, seed INTEGER, restarts INTEGER DEFAULT 0,
   run_id INTEGER DEFAULT 0, steps_completed INTEGER DEFAULT 0, latest_checkpoint TEXT,
   warm_start_checkpoint TEXT, searcher_state TEXT DEFAULT '{}', summary_metrics TEXT DEFAULT '{}',
   best_validation REAL, latest_validation_steps INTEGER, runner_state TEXT DEFAULT '',
-  task_id TEXT, progress REAL DEFAULT 0, tags TEXT DEFAULT '{}');
+  task_id TEXT, progress REAL DEFAULT 0, tags TEXT DEFAULT '{}', external_trial_id TEXT);
 CREATE INDEX IF NOT EXISTS trials_exp ON trials(experiment_id);
 CREATE TABLE IF NOT EXISTS metrics (
   id INTEGER PRIMARY KEY AUTOINCREMENT, trial_id INTEGER, trial_run_id INTEGER, grp TEXT,
@@ -74,6 +74,12 @@ CREATE TABLE IF NOT EXISTS kv (key TEXT PRIMARY KEY, value TEXT);
 """
 
 
+MIGRATIONS = [
+    ("experiments", "external_experiment_id", "TEXT"),
+    ("trials", "external_trial_id", "TEXT"),
+]
+
+
 class DB:
     def __init__(self, path: str = ":memory:") -> None:
         self.path = path
@@ -84,6 +90,14 @@ class DB:
             if path != ":memory:":
                 self._conn.execute("PRAGMA journal_mode=WAL")
             self._conn.executescript(SCHEMA)
+            self._migrate()
+
+    def _migrate(self) -> None:
+        """Columns added after a table first shipped (CREATE TABLE IF NOT EXISTS keeps old tables)."""
+        for table, col, decl in MIGRATIONS:
+            cols = {r[1] for r in self._conn.execute(f"PRAGMA table_info({table})").fetchall()}
+            if col not in cols:
+                self._conn.execute(f"ALTER TABLE {table} ADD COLUMN {col} {decl}")
 
     # ------------------------------------------------------------------ primitives
     def execute(self, sql: str, args: Iterable[Any] = ()) -> sqlite3.Cursor:

@@ -155,6 +155,40 @@ class Experiment:
         self._process(self.searcher.trial_created(op.request_id))
         self.master.webhooks.trial_event(self, t, "ACTIVE")
 
+    # ------------------------------------------------------------------ unmanaged trials
+    def add_unmanaged_trial(self, hparams: Optional[Dict[str, Any]] = None,
+                            external_id: Optional[str] = None) -> Trial:
+        """A trial whose process runs outside the cluster (Core API v2 ``unmanaged`` mode): no
+        searcher operation and no allocation; it reports metrics / checkpoints / heartbeats
+        itself. ``external_id`` makes the call idempotent (resume of the same external trial)."""
+        with self.lock:
+            if external_id is not None:
+                row = self.master.db.one("SELECT request_id FROM trials WHERE experiment_id=? AND "
+                                         "external_trial_id=?", [self.id, str(external_id)])
+                if row is not None and row["request_id"] in self.trials:
+                    return self.trials[row["request_id"]]
+            rid = str(uuid.uuid4())
+            tid = self.master.db.insert("trials", {
+                "experiment_id": self.id, "request_id": rid, "hparams": hparams or {},
+                "state": ACTIVE, "start_time": now(), "seed": 0, "task_id": f"{self.id}.{rid}",
+                "external_trial_id": None if external_id is None else str(external_id)})
+            t = Trial(self, tid, rid, hparams or {}, 0)
+            self.trials[rid] = t
+            return t
+
+    def unmanaged_heartbeat(self, t: Trial, state: str) -> None:
+        """RUNNING keeps the trial alive; COMPLETED / ERROR / CANCELED end it, and the
+        experiment ends with its last trial."""
+        with self.lock:
+            if state not in TERMINAL or t.state in TERMINAL:
+                return
+            t.state = state
+            self.master.db.update("trials", "id", t.id, {"state": state, "end_time": now()})
+            if all(x.state in TERMINAL for x in self.trials.values()):
+                final = COMPLETED if all(x.state == COMPLETED for x in self.trials.values()) else ERROR
+                self._set_state(final)
+                self.master.db.update("experiments", "id", self.id, {"end_time": now()})
+
     def _ensure_running(self, t: Trial) -> None:
         if self.state != ACTIVE or t.allocation_id is not None or t.state in TERMINAL:
             return

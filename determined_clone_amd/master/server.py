@@ -591,6 +591,8 @@ def runner_metadata(r: Req) -> Any:
 
 @route("POST", "/api/v1/trials/{tid}/heartbeat")
 def trial_heartbeat(r: Req) -> Any:
+    t = _trial(r)
+    t.exp.unmanaged_heartbeat(t, str(r.body.get("state", "RUNNING")))
     return {}
 
 
@@ -1261,4 +1263,4 @@ class MasterServer:
 
 
 # routes that live in their own modules register on import
-from determined_clone_amd.master import rbac_api  # noqa: E402,F401
+from determined_clone_amd.master import rbac_api, unmanaged_api  # noqa: E402,F401

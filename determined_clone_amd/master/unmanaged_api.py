@@ -1,0 +1,90 @@
+"""Routes for unmanaged experiments and trials -- training processes that run outside the cluster
+and only report to the master (Core API v2, ``experimental.core_v2``).
+
+Reference: ``api.proto`` PutExperiment (``PUT /api/v1/experiments/{external_experiment_id}``),
+CreateTrial (``POST /api/v1/trials``), PutTrial (``PUT /api/v1/trials``), StartTrial
+(``POST /api/v1/trials/{trial_id}/start``); ``master/internal/api_trials.go``,
+``api_experiment.go`` (unmanaged paths). Imported by ``server`` to register them."""
+from typing import Any, Dict, Optional
+
+from determined_clone_amd.errors import InvalidConfigurationException
+from determined_clone_amd.master.server import (HTTPError, Req, _int, _project_workspace, require,
+                                                route)
+
+
+def _unmanaged_experiment(r: Req, eid: int) -> Any:
+    e = r.m.experiments.get(eid)
+    row = r.m.db.one("SELECT unmanaged FROM experiments WHERE id=?", [eid])
+    if e is None or row is None:
+        raise HTTPError(404, f"experiment {eid} not found")
+    if not row["unmanaged"]:
+        raise HTTPError(400, f"experiment {eid} is managed by the cluster")
+    return e
+
+
+@route("PUT", "/api/v1/experiments/{external_id}")
+def put_experiment(r: Req) -> Any:
+    """Get-or-create an unmanaged experiment keyed by an external id."""
+    ext = r.p["external_id"]
+    row = r.m.db.one("SELECT id FROM experiments WHERE external_experiment_id=?", [ext])
+    if row is None:
+        require(r, "CREATE_EXPERIMENT", _project_workspace(r.m, r.body.get("project_id")))
+        try:
+            e = r.m.create_experiment(r.body["config"], None, activate=True,
+                                      project_id=r.body.get("project_id"), owner_id=r.user["id"],
+                                      unmanaged=True)
+        except InvalidConfigurationException as ex:
+            raise HTTPError(400, str(ex))
+        r.m.db.update("experiments", "id", e.id, {"external_experiment_id": ext})
+        eid = e.id
+    else:
+        eid = row["id"]
+    return {"experiment": r.m.experiment_api(eid), "config": r.m.experiments[eid].config}
+
+
+def _trial_out(r: Req, t: Any) -> Dict[str, Any]:
+    d = r.m.trial_api(t.id)
+    d["taskId"] = t.task_id
+    return {"trial": d}
+
+
+def _create(r: Req, body: Dict[str, Any], external_id: Optional[str]) -> Any:
+    eid = _int(body.get("experiment_id", body.get("experimentId")))
+    e = _unmanaged_experiment(r, eid)
+    t = e.add_unmanaged_trial(body.get("hparams") or {}, external_id)
+    return _trial_out(r, t)
+
+
+@route("POST", "/api/v1/trials")
+def create_trial(r: Req) -> Any:
+    if not r.body.get("unmanaged", True):
+        raise HTTPError(400, "only unmanaged trials can be created directly")
+    return _create(r, r.body, None)
+
+
+@route("PUT", "/api/v1/trials")
+def put_trial(r: Req) -> Any:
+    body = r.body.get("create_trial_request") or r.body.get("createTrialRequest") or {}
+    ext = r.body.get("external_trial_id") or r.body.get("externalTrialId")
+    if ext is None:
+        raise HTTPError(400, "external_trial_id required")
+    return _create(r, body, str(ext))
+
+
+@route("POST", "/api/v1/trials/{tid}/start")
+def start_trial(r: Req) -> Any:
+    """Begin (or resume) a run of an unmanaged trial: a new run id, and the progress and latest
+    checkpoint to resume from."""
+    try:
+        t = r.m.trial_by_id(_int(r.p["tid"]))
+    except KeyError as ex:
+        raise HTTPError(404, str(ex))
+    _unmanaged_experiment(r, t.exp.id)
+    with t.exp.lock:
+        t.run_id += 1
+        r.m.db.update("trials", "id", t.id, {"run_id": t.run_id})
+        row = r.m.db.one("SELECT steps_completed, latest_checkpoint FROM trials WHERE id=?", [t.id])
+    resume = bool(r.body.get("resume", True))
+    return {"trial_run_id": t.run_id,
+            "steps_completed": int(row["steps_completed"] or 0) if resume else 0,
+            "latest_checkpoint": row["latest_checkpoint"] if resume else None}
