@@ -68,6 +68,7 @@ def test_unmanaged_resume_by_external_ids(master):
     assert (tid1, eid1) == (tid2, eid2)
     assert run2 == run1 + 1
     assert start2 == 2 and latest2 == ck1  # resumed from the first run's checkpoint
+    assert master.db.one("SELECT state FROM trials WHERE id=?", [tid1])["state"] == "COMPLETED"
     # a second external trial id groups a new trial into the same experiment
     tid3, eid3, *_ = _run(d, defaults, core_v2.UnmanagedConfig(external_experiment_id="ext-exp-1",
                                                                   external_trial_id="ext-trial-2"), steps=(1,))
