@@ -1,8 +1,9 @@
 """Checkpoint storage managers (reference: `harness/determined/common/storage/*`).
 
 ``shared_fs`` and ``directory`` write straight into the target directory (no staging copy — on a
-single MI355X node the checkpoint directory IS the storage). Cloud backends (s3/gcs/azure) are
-implemented against their SDKs and raise a clear error when the SDK is not importable.
+single MI355X node the checkpoint directory IS the storage). Cloud backends (s3/gcs/azure) speak
+their REST protocols directly (``_cloud.py``: SigV4, Azure SharedKey/SAS, GCS JSON API) -- no
+vendor SDK is needed.
 """
 import contextlib
 import os
@@ -145,76 +146,33 @@ class DirectoryStorageManager(SharedFSStorageManager):
     """``type: directory`` — a path already mounted in the task (container_path)."""
 
 
-class _CloudStorageManager(StorageManager):
-    sdk = ""
-
-    def __init__(self, base_path: str, **kw: Any) -> None:
-        super().__init__(base_path)
-        self._kw = kw
-        self._client = self._make_client()
-
-    def _make_client(self) -> Any:
-        raise RuntimeError(f"{type(self).__name__} needs the '{self.sdk}' package, which is not "
-                           "installed in this environment")
+from determined_clone_amd.common.storage._cloud import (AzureBlobStore, GCSStore,  # noqa: E402
+                                                        ObjectStorageManager, S3Store)
 
 
-class S3StorageManager(_CloudStorageManager):
-    sdk = "boto3"
+class S3StorageManager(ObjectStorageManager):
+    """``type: s3`` (AWS or any S3-compatible endpoint), SigV4 over HTTP."""
 
-    def _make_client(self) -> Any:
-        try:
-            import boto3  # type: ignore
-        except ImportError:
-            return super()._make_client()
-        return boto3.client("s3", endpoint_url=self._kw.get("endpoint_url"),
-                            aws_access_key_id=self._kw.get("access_key"),
-                            aws_secret_access_key=self._kw.get("secret_key"))
-
-    def _key(self, *parts: str) -> str:
-        prefix = (self._kw.get("prefix") or "").strip("/")
-        return "/".join(p for p in [prefix, *parts] if p)
-
-    def upload(self, src, dst, paths=None) -> None:
-        src = pathlib.Path(src)
-        files = paths if paths is not None else [str(p.relative_to(src)) for p in src.rglob("*") if p.is_file()]
-        for rel in files:
-            if (src / rel).is_file():
-                self._client.upload_file(str(src / rel), self._base_path, self._key(dst, rel))
-
-    def download(self, src, dst, selector=None) -> None:
-        pag = self._client.get_paginator("list_objects_v2")
-        for page in pag.paginate(Bucket=self._base_path, Prefix=self._key(src) + "/"):
-            for obj in page.get("Contents", []):
-                rel = obj["Key"][len(self._key(src)) + 1:]
-                if selector is not None and not selector(rel):
-                    continue
-                d = pathlib.Path(dst) / rel
-                d.parent.mkdir(parents=True, exist_ok=True)
-                self._client.download_file(self._base_path, obj["Key"], str(d))
-
-    def delete(self, storage_id, globs=None) -> Dict[str, int]:
-        pag = self._client.get_paginator("list_objects_v2")
-        for page in pag.paginate(Bucket=self._base_path, Prefix=self._key(storage_id) + "/"):
-            keys = [{"Key": o["Key"]} for o in page.get("Contents", [])]
-            if keys:
-                self._client.delete_objects(Bucket=self._base_path, Delete={"Objects": keys})
-        return {}
-
-    def list_files(self, storage_id: str) -> Dict[str, int]:
-        out: Dict[str, int] = {}
-        pag = self._client.get_paginator("list_objects_v2")
-        for page in pag.paginate(Bucket=self._base_path, Prefix=self._key(storage_id) + "/"):
-            for o in page.get("Contents", []):
-                out[o["Key"][len(self._key(storage_id)) + 1:]] = o["Size"]
-        return out
+    def __init__(self, bucket: str, access_key: Optional[str] = None, secret_key: Optional[str] = None,
+                 endpoint_url: Optional[str] = None, prefix: Optional[str] = None,
+                 region: Optional[str] = None) -> None:
+        super().__init__(S3Store(bucket, access_key, secret_key, endpoint_url, region), prefix)
 
 
-class GCSStorageManager(_CloudStorageManager):
-    sdk = "google-cloud-storage"
+class GCSStorageManager(ObjectStorageManager):
+    """``type: gcs``, GCS JSON API with an OAuth bearer token."""
+
+    def __init__(self, bucket: str, prefix: Optional[str] = None, endpoint_url: Optional[str] = None) -> None:
+        super().__init__(GCSStore(bucket, endpoint_url), prefix)
 
 
-class AzureStorageManager(_CloudStorageManager):
-    sdk = "azure-storage-blob"
+class AzureStorageManager(ObjectStorageManager):
+    """``type: azure``, Blob REST with SharedKey or SAS."""
+
+    def __init__(self, container: str, connection_string: Optional[str] = None,
+                 account_url: Optional[str] = None, credential: Optional[str] = None,
+                 prefix: Optional[str] = None) -> None:
+        super().__init__(AzureBlobStore(container, connection_string, account_url, credential), prefix)
 
 
 def build(cfg: Dict[str, Any], container_path: Optional[str] = None) -> StorageManager:
@@ -232,9 +190,11 @@ def build(cfg: Dict[str, Any], container_path: Optional[str] = None) -> StorageM
     if t == "s3":
         return S3StorageManager(cfg["bucket"], **{k: cfg.get(k) for k in ("access_key", "secret_key", "endpoint_url", "prefix")})
     if t == "gcs":
-        return GCSStorageManager(cfg["bucket"], prefix=cfg.get("prefix"))
+        return GCSStorageManager(cfg["bucket"], prefix=cfg.get("prefix"), endpoint_url=cfg.get("endpoint_url"))
     if t == "azure":
-        return AzureStorageManager(cfg["container"], connection_string=cfg.get("connection_string"))
+        return AzureStorageManager(cfg["container"], connection_string=cfg.get("connection_string"),
+                                   account_url=cfg.get("account_url"), credential=cfg.get("credential"),
+                                   prefix=cfg.get("prefix"))
     raise ValueError(f"unknown checkpoint storage type: {t}")
 
 
