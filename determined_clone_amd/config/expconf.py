@@ -63,6 +63,9 @@ OPTIMIZATIONS = {
     "average_training_metrics": ((bool,), True),
     "gradient_compression": ((bool,), False),
     "grad_updates_size_file": ((str,), None),
+    # MI355X extension: capture the training step as a HIP graph after N eager warm-up steps
+    "hip_graph": ((bool,), False),
+    "hip_graph_warmup_steps": ((int,), 3),
     "mixed_precision": ((str,), "O0"),
     "tensor_fusion_cycle_time": ((int,), 1),
     "tensor_fusion_threshold": ((int,), 64),

@@ -282,6 +282,8 @@ class Experiment:
 
     # ------------------------------------------------------------------ user actions
     def _set_state(self, state: str) -> None:
+        if state != self.state:
+            logger.info(f"experiment {self.id}: {self.state} -> {state}")
         self.state = state
         self.master.db.update("experiments", "id", self.id, {"state": state})
         self.master.webhooks.experiment_event(self, state)
@@ -318,6 +320,38 @@ class Experiment:
                 elif t.state not in TERMINAL:
                     self._end_trial(t, CANCELED)
             self._maybe_finish()
+
+    def continue_with(self, cfg: Dict[str, Any]) -> None:
+        """ContinueExperiment (reference: ``api_experiment.go`` ContinueExperiment,
+        ``e2e_tests/tests/cluster/test_exp_continue.py``): re-open a terminal single-trial
+        experiment (COMPLETED, CANCELED or ERROR) with a merged config -- new constant
+        hyperparameters, a longer ``searcher.max_length`` -- and resume its trial from its latest
+        checkpoint under a fresh searcher whose operations are re-keyed to the existing trial."""
+        with self.lock:
+            if self.state not in TERMINAL:
+                raise ValueError("only a terminal experiment can be continued")
+            if len(self.trials) != 1 or cfg["searcher"]["name"] != "single":
+                raise ValueError("only single-trial (searcher: single) experiments can be continued")
+            (t,) = self.trials.values()
+            self.config = cfg
+            self.searcher = Searcher(self.seed, make_search_method(cfg["searcher"]), cfg["hyperparameters"])
+            self.smaller_is_better = bool(cfg["searcher"].get("smaller_is_better", True))
+            ops = self.searcher.initial_operations()
+            for op in ops:
+                if isinstance(op, Create):
+                    t.hparams = op.hparams
+                op.request_id = t.request_id
+            ops = [op for op in ops if not isinstance(op, Create)]
+            ops += self.searcher.trial_created(t.request_id)
+            self.shutdown = False
+            t.state, t.closed, t.op, t.op_complete = ACTIVE, False, None, True
+            t.killed, t.exited_early, t.restarts = False, False, 0
+            self.master.db.update("trials", "id", t.id, {"state": ACTIVE, "end_time": None, "restarts": 0,
+                                                         "hparams": t.hparams})
+            self.master.db.update("experiments", "id", self.id, {"config": cfg, "end_time": None})
+            self._set_state(ACTIVE)
+            self._process(ops)
+            self._persist()
 
     def kill_trial(self, t: Trial) -> None:
         with self.lock:

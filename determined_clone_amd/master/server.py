@@ -174,6 +174,14 @@ def master_info(r: Req) -> Any:
             "product": "determined_clone_amd", "uptime_s": time.time() - r.m.start_time}
 
 
+@route("GET", "/api/v1/master/logs")
+def master_logs(r: Req) -> Any:
+    """MasterLogs: the master's own log records (ring buffer), after ``after_id`` or the last
+    ``tail`` entries."""
+    require(r, "VIEW_MASTER_LOGS")
+    return {"logs": r.m.log_buffer.entries(_int(r.qget("after_id", 0)), _int(r.qget("tail", 0)))}
+
+
 @route("GET", "/api/v1/master/config")
 def master_config(r: Req) -> Any:
     require(r, "VIEW_MASTER_CONFIG")
@@ -329,6 +337,28 @@ def _exp(r: Req, perm: Optional[str] = None):
     return e
 
 
+@route("POST", "/api/v1/experiments/continue")
+def continue_experiment(r: Req) -> Any:
+    """ContinueExperiment: merge ``override_config`` (YAML text or a mapping) into a terminal
+    single-trial experiment's config and resume its trial."""
+    import yaml
+
+    from determined_clone_amd.config import expconf
+    from determined_clone_amd.util import merge_dicts
+
+    r.p["eid"] = str(r.body.get("id"))
+    e = _exp(r, "UPDATE_EXPERIMENT")
+    ov = r.body.get("override_config") or {}
+    if isinstance(ov, str):
+        ov = yaml.safe_load(ov) or {}
+    try:
+        cfg = expconf.complete(merge_dicts(e.config, expconf.parse(ov) if ov else {}))
+        e.continue_with(cfg)
+    except (InvalidConfigurationException, ValueError) as ex:
+        raise HTTPError(400, str(ex))
+    return {"experiment": r.m.experiment_api(e.id), "config": e.config}
+
+
 @route("POST", "/api/v1/experiments/{eid}/activate")
 def exp_activate(r: Req) -> Any:
     _exp(r, "UPDATE_EXPERIMENT").activate()
@@ -379,6 +409,12 @@ def exp_patch(r: Req) -> Any:
     fields: Dict[str, Any] = {"config": cfg}
     if "notes" in r.body:
         fields["notes"] = r.body["notes"]
+    if "checkpoint_storage" in r.body:  # GC policy (save_*) only; the storage backend is fixed
+        gc = {k: int(v) for k, v in (r.body["checkpoint_storage"] or {}).items()
+              if k in ("save_experiment_best", "save_trial_best", "save_trial_latest")}
+        cfg["checkpoint_storage"] = dict(cfg.get("checkpoint_storage") or {}, **gc)
+        e.config = cfg
+        fields["config"] = cfg
     if "resources" in r.body:
         res = r.body["resources"] or {}
         if "priority" in res or "weight" in res:

@@ -41,10 +41,10 @@ void norm_finalize(const float* partial, int nparts, const float* loss_scale, fl
                    float max_norm, float* out, hipStream_t st);
 void sgd_step(OptDtype gdt, OptDtype pdt, float* master, void* model, const void* grad, float* mom,
               int64_t n, float lr, float momentum, float dampening, float wd, bool nesterov,
-              bool first_step, float gscale, const float* dev_scale, hipStream_t st);
+              bool first_step, float gscale, const float* dev_scale, const float* dyn, hipStream_t st);
 void adam_step(OptDtype gdt, OptDtype pdt, float* master, void* model, const void* grad, float* m,
                float* v, int64_t n, float lr, float beta1, float beta2, float eps, float wd,
-               bool adamw, float bc1, float bc2, float gscale, const float* dev_scale,
+               bool adamw, float bc1, float bc2, float gscale, const float* dev_scale, const float* dyn,
                hipStream_t st);
 void lamb_step(OptDtype gdt, OptDtype pdt, float* master, void* model, const void* grad, float* m,
                float* v, float* ubuf, const int64_t* cstart, const int* clen, const int* cseg,
@@ -340,11 +340,21 @@ void check_flat(const Tensor& master, const Tensor& grad, const OptT& model) {
     TORCH_CHECK(model->numel() == master.numel() && model->is_contiguous(), "model buffer mismatch");
 }
 
+// Optional device-resident step hyper-parameters read by the optimizer kernels instead of their
+// scalar arguments (a HIP graph replays the launch with the values current at replay time).
+void check_dyn(const OptT& dyn, int64_t n) {
+  if (dyn.has_value() && dyn->defined())
+    TORCH_CHECK(dyn->is_cuda() && dyn->scalar_type() == at::kFloat && dyn->is_contiguous() &&
+                    dyn->numel() >= n,
+                "optimizer hyper-parameter buffer must be a contiguous fp32 GPU tensor of >= ", n);
+}
+
 void sgd(const Tensor& master, const OptT& model, const Tensor& grad, const OptT& mom, double lr,
          double momentum, double dampening, double wd, bool nesterov, bool first_step,
-         double gscale, const OptT& dev_scale) {
+         double gscale, const OptT& dev_scale, const OptT& dyn) {
   check_flat(master, grad, model);
   const c10::DeviceGuard guard(master.device());
+  check_dyn(dyn, 2);
   TORCH_CHECK(momentum == 0.0 || (mom.has_value() && mom->numel() == master.numel()),
               "sgd: momentum buffer required");
   dca::sgd_step(opt_dtype(grad),
@@ -353,14 +363,15 @@ void sgd(const Tensor& master, const OptT& model, const Tensor& grad, const OptT
                 grad.data_ptr(), ptr_or_null<float>(mom), master.numel(), static_cast<float>(lr),
                 static_cast<float>(momentum), static_cast<float>(dampening), static_cast<float>(wd),
                 nesterov, first_step, static_cast<float>(gscale), ptr_or_null<float>(dev_scale),
-                cur_stream());
+                ptr_or_null<float>(dyn), cur_stream());
 }
 
 void adam(const Tensor& master, const OptT& model, const Tensor& grad, const Tensor& m,
           const Tensor& v, double lr, double beta1, double beta2, double eps, double wd, bool adamw,
-          int64_t step, double gscale, const OptT& dev_scale) {
+          int64_t step, double gscale, const OptT& dev_scale, const OptT& dyn) {
   check_flat(master, grad, model);
   const c10::DeviceGuard guard(master.device());
+  check_dyn(dyn, 3);
   const double bc1 = 1.0 - std::pow(beta1, static_cast<double>(step));
   const double bc2 = 1.0 - std::pow(beta2, static_cast<double>(step));
   dca::adam_step(opt_dtype(grad),
@@ -370,7 +381,7 @@ void adam(const Tensor& master, const OptT& model, const Tensor& grad, const Ten
                  static_cast<float>(lr), static_cast<float>(beta1), static_cast<float>(beta2),
                  static_cast<float>(eps), static_cast<float>(wd), adamw, static_cast<float>(bc1),
                  static_cast<float>(bc2), static_cast<float>(gscale), ptr_or_null<float>(dev_scale),
-                 cur_stream());
+                 ptr_or_null<float>(dyn), cur_stream());
 }
 
 // chunks: int64 [3][nchunks] = (start, len, seg) on device; seg_begin: int32 [nseg+1] on device.
@@ -440,8 +451,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_norm_scale", &grad_norm_scale);
   m.def("sumsq_partials", &sumsq_partials);
   m.def("norm_finalize", &norm_finalize_t);
-  m.def("sgd", &sgd);
-  m.def("adam", &adam);
+  m.def("sgd", &sgd, pybind11::arg("master"), pybind11::arg("model"), pybind11::arg("grad"),
+        pybind11::arg("mom"), pybind11::arg("lr"), pybind11::arg("momentum"),
+        pybind11::arg("dampening"), pybind11::arg("wd"), pybind11::arg("nesterov"),
+        pybind11::arg("first_step"), pybind11::arg("gscale"), pybind11::arg("dev_scale"),
+        pybind11::arg("dyn") = pybind11::none());
+  m.def("adam", &adam, pybind11::arg("master"), pybind11::arg("model"), pybind11::arg("grad"),
+        pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("lr"), pybind11::arg("beta1"),
+        pybind11::arg("beta2"), pybind11::arg("eps"), pybind11::arg("wd"), pybind11::arg("adamw"),
+        pybind11::arg("step"), pybind11::arg("gscale"), pybind11::arg("dev_scale"),
+        pybind11::arg("dyn") = pybind11::none());
   m.def("lamb", &lamb);
   m.def("amp_scaler_update", &amp_scaler_update);
   m.def("scale_", &scale_);

@@ -132,8 +132,11 @@ template <typename G, typename P>
 __global__ __launch_bounds__(kBlock) void sgd_kernel(
     float* __restrict__ master, void* __restrict__ model, const void* __restrict__ grad,
     float* __restrict__ mom, int64_t n, float lr, float momentum, float dampening, float wd,
-    bool nesterov, bool first_step, float gscale, const float* __restrict__ dev_scale) {
+    bool nesterov, bool first_step, float gscale, const float* __restrict__ dev_scale,
+    const float* __restrict__ dyn) {
   if (dev_scale && dev_scale[1] != 0.f) return;  // found_inf: skip the step
+  // Device-resident step hyper-parameters (HIP-graph replay: refreshed before each launch).
+  if (dyn) { lr = dyn[0]; first_step = dyn[1] != 0.f; }
   const float gs = gscale * (dev_scale ? dev_scale[0] : 1.f);
   const int64_t n4 = n / 4;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
@@ -171,8 +174,9 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(
     float* __restrict__ master, void* __restrict__ model, const void* __restrict__ grad,
     float* __restrict__ m, float* __restrict__ v, int64_t n, float lr, float beta1, float beta2,
     float eps, float wd, bool adamw, float bc1, float bc2, float gscale,
-    const float* __restrict__ dev_scale) {
+    const float* __restrict__ dev_scale, const float* __restrict__ dyn) {
   if (dev_scale && dev_scale[1] != 0.f) return;
+  if (dyn) { lr = dyn[0]; bc1 = dyn[1]; bc2 = dyn[2]; }
   const float gs = gscale * (dev_scale ? dev_scale[0] : 1.f);
   const float step_size = lr / bc1;
   const float inv_sqrt_bc2 = rsqrtf(bc2);
@@ -347,19 +351,20 @@ void norm_finalize(const float* partial, int nparts, const float* loss_scale, fl
 
 void sgd_step(OptDtype gdt, OptDtype pdt, float* master, void* model, const void* grad, float* mom,
               int64_t n, float lr, float momentum, float dampening, float wd, bool nesterov,
-              bool first_step, float gscale, const float* dev_scale, hipStream_t st) {
+              bool first_step, float gscale, const float* dev_scale, const float* dyn,
+              hipStream_t st) {
   const int grid = stream_grid((n + 3) / 4, kBlock);
   DCA_DISPATCH_GP(gdt, pdt, sgd_kernel, grid, master, model, grad, mom, n, lr, momentum,
-                  dampening, wd, nesterov, first_step, gscale, dev_scale);
+                  dampening, wd, nesterov, first_step, gscale, dev_scale, dyn);
 }
 
 void adam_step(OptDtype gdt, OptDtype pdt, float* master, void* model, const void* grad, float* m,
                float* v, int64_t n, float lr, float beta1, float beta2, float eps, float wd,
                bool adamw, float bc1, float bc2, float gscale, const float* dev_scale,
-               hipStream_t st) {
+               const float* dyn, hipStream_t st) {
   const int grid = stream_grid((n + 3) / 4, kBlock);
   DCA_DISPATCH_GP(gdt, pdt, adam_kernel, grid, master, model, grad, m, v, n, lr, beta1, beta2,
-                  eps, wd, adamw, bc1, bc2, gscale, dev_scale);
+                  eps, wd, adamw, bc1, bc2, gscale, dev_scale, dyn);
 }
 
 void lamb_step(OptDtype gdt, OptDtype pdt, float* master, void* model, const void* grad, float* m,

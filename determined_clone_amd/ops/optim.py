@@ -53,6 +53,10 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         # Host-side multiplier folded into every kernel (e.g. 1/world_size for summed all-reduce).
         self.grad_multiplier = 1.0
         self.last_grad_norm: Optional[torch.Tensor] = None
+        # Device-resident per-group step hyper-parameters (lr, step-dependent terms) read by the
+        # kernels instead of scalar launch arguments: a captured HIP graph then replays each step
+        # with the current LR schedule (see pytorch/_graph.py). None = scalar arguments.
+        self._dyn: Optional[torch.Tensor] = None
 
     def _pad_multiple(self) -> int:
         return 1
@@ -90,12 +94,44 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         # Flat gradients are zeroed in one memset per dtype; views stay installed.
         self.space.zero_grad()
 
+    # ------------------------------------------------------------------ HIP-graph support
+    graph_capturable = True
+
+    def _dyn_row(self, group: Dict[str, Any], step: int) -> List[float]:
+        """Per-group values the kernels read from the device buffer for optimizer step ``step``."""
+        return [float(group["lr"]), 0.0, 0.0, 0.0]
+
+    def enable_device_hparams(self) -> None:
+        dev = next(iter(self.flat.values())).master.device if self.flat else torch.device("cpu")
+        if dev.type != "cuda":
+            return
+        self._dyn = torch.zeros(len(self.param_groups), 4, dtype=torch.float32, device=dev)
+
+    def refresh_device_hparams(self, step: Optional[int] = None) -> None:
+        """Upload this step's lr / bias-correction terms (an async H2D copy from pinned memory,
+        issued OUTSIDE any captured graph)."""
+        if self._dyn is None:
+            return
+        step = self._step if step is None else step
+        rows = [self._dyn_row(g, step) for g in self.param_groups]
+        self._dyn.copy_(torch.tensor(rows, dtype=torch.float32).pin_memory(), non_blocking=True)
+
+    def _dyn_of(self, group: Dict[str, Any]) -> Optional[torch.Tensor]:
+        if self._dyn is None:
+            return None
+        for i, g in enumerate(self.param_groups):
+            if g is group:
+                return self._dyn[i]
+        return None
+
     # ------------------------------------------------------------------ step
     @torch.no_grad()
     def step(self, closure: Optional[Callable] = None) -> Any:  # type: ignore[override]
         loss = closure() if closure is not None else None
         self.space.ensure_views()
         self._step += 1
+        if self._dyn is not None and not torch.cuda.is_current_stream_capturing():
+            self.refresh_device_hparams()
         dev_scale = self._dev_scale
         for st in self.flat.values():
             for gi, (start, end) in st.buf.group_ranges.items():
@@ -179,6 +215,9 @@ class FusedOptimizerBase(torch.optim.Optimizer):
 class FusedSGD(FusedOptimizerBase):
     state_names = ["momentum_buffer"]
 
+    def _dyn_row(self, group: Dict[str, Any], step: int) -> List[float]:
+        return [float(group["lr"]), 1.0 if step == 1 else 0.0, 0.0, 0.0]
+
     def __init__(self, params: Any, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
                  weight_decay: float = 0.0, nesterov: bool = False) -> None:
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
@@ -197,7 +236,8 @@ class FusedSGD(FusedOptimizerBase):
         if master.is_cuda:
             _ext.load().sgd(master, model, grad, mom, group["lr"], group["momentum"],
                             group["dampening"], group["weight_decay"], group["nesterov"], first,
-                            self.grad_multiplier if dev_scale is None else 1.0, dev_scale)
+                            self.grad_multiplier if dev_scale is None else 1.0, dev_scale,
+                            self._dyn_of(group))
             return
         if dev_scale is not None and float(dev_scale[1]) != 0.0:
             return
@@ -220,6 +260,10 @@ class FusedSGD(FusedOptimizerBase):
 class FusedAdam(FusedOptimizerBase):
     state_names = ["exp_avg", "exp_avg_sq"]
 
+    def _dyn_row(self, group: Dict[str, Any], step: int) -> List[float]:
+        b1, b2 = group["betas"]
+        return [float(group["lr"]), 1.0 - b1 ** step, 1.0 - b2 ** step, 0.0]
+
     def __init__(self, params: Any, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, adamw: bool = False) -> None:
         defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay)
@@ -238,7 +282,8 @@ class FusedAdam(FusedOptimizerBase):
         if master.is_cuda:
             _ext.load().adam(master, model, grad, m, v, group["lr"], b1, b2, group["eps"],
                              group["weight_decay"], self.adamw, self._step,
-                             self.grad_multiplier if dev_scale is None else 1.0, dev_scale)
+                             self.grad_multiplier if dev_scale is None else 1.0, dev_scale,
+                             self._dyn_of(group))
             return
         if dev_scale is not None and float(dev_scale[1]) != 0.0:
             return
@@ -269,6 +314,7 @@ class FusedLAMB(FusedOptimizerBase):
     """LAMB (You et al. 2019): Adam update + decoupled decay, scaled per tensor by
     ||w|| / ||update||. Per-tensor norms come from a chunk table over the flat buffer."""
 
+    graph_capturable = False  # scalar-argument path only
     state_names = ["exp_avg", "exp_avg_sq"]
     CHUNK = 65536
 

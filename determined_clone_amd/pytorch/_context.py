@@ -65,6 +65,12 @@ class _Experimental:
         for i, m in enumerate(self._ctx.models):
             self._ctx.models[i] = self._ctx.autocast_forward_pass(m)
 
+    def use_hip_graph(self, warmup_steps: int = 3) -> None:
+        """Capture ``train_batch`` as a HIP graph after ``warmup_steps`` eager steps and replay it
+        (same as ``optimizations.hip_graph: true``; see ``pytorch/_graph.py`` for requirements)."""
+        self._ctx._hip_graph = True
+        self._ctx._hip_graph_warmup = int(warmup_steps)
+
     def disable_auto_to_device(self) -> None:
         self._auto_to_device = False
 
@@ -96,6 +102,8 @@ class PyTorchTrialContext(_PyTorchReducerContext):
         self._average_aggregated_gradients = bool(opts.get("average_aggregated_gradients", True))
         self._gradient_compression = bool(opts.get("gradient_compression", False))
         self._average_training_metrics = bool(opts.get("average_training_metrics", True))
+        self._hip_graph = bool(opts.get("hip_graph", False))
+        self._hip_graph_warmup = int(opts.get("hip_graph_warmup_steps", 3) or 3)
         fusion_mb = opts.get("tensor_fusion_threshold")
         self._bucket_mb = float(fusion_mb) if fusion_mb and fusion_mb != 64 else 32.0
 

@@ -411,6 +411,22 @@ class _PyTorchTrialController:
                 if (e + 1) % sched._frequency == 0:
                     sched.step()
 
+    def _graph_step(self) -> Any:
+        """The HIP-graph runner when ``optimizations.hip_graph`` is on and supported."""
+        if not getattr(self.context, "_hip_graph", False):
+            return None
+        if getattr(self, "_graphed", None) is None:
+            from determined_clone_amd.pytorch import _graph
+
+            reason = _graph.unsupported_reason(self.context)
+            if reason is not None:
+                logger.warning(f"optimizations.hip_graph disabled: {reason}")
+                self.context._hip_graph = False
+                return None
+            self._graphed = _graph.GraphedTrainStep(self.context, self.trial.train_batch,
+                                                    self.context._hip_graph_warmup)
+        return self._graphed
+
     def _train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, Any]:
         self.context._loss_ids = {}
         t0 = time.time()
@@ -420,6 +436,8 @@ class _PyTorchTrialController:
             with self.context.profiler:
                 out = self.trial.train_batch(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
                 self.context.profiler.step()
+        elif self._graph_step() is not None:
+            out = self._graphed(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
         else:
             out = self.trial.train_batch(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
         if self.context._scaler is not None and self.context.experimental._auto_amp \

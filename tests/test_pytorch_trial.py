@@ -102,3 +102,23 @@ def test_trainunit_semantics():
     assert pytorch.Batch([3, 7]).should_stop(7)
     assert pytorch.Batch(0).should_stop(1)
     assert pytorch.TrainUnit._from_searcher_unit(100, core.Unit.RECORDS, 32).value == 3
+
+
+def test_hip_graph_option_falls_back_to_eager_on_cpu(tmp_path, caplog):
+    """optimizations.hip_graph is accepted by expconf; off-GPU the controller logs why it is
+    disabled and trains eagerly (the GPU replay path is tests/test_graph_gpu.py)."""
+    from determined_clone_amd.config import expconf
+
+    cfg = expconf.complete({"entrypoint": "x:y", "searcher": {"name": "single", "metric": "m",
+                                                              "max_length": {"batches": 1}},
+                            "optimizations": {"hip_graph": True, "hip_graph_warmup_steps": 2}})
+    assert cfg["optimizations"]["hip_graph"] is True
+    storage = str(tmp_path / "ckpts")
+    with pytorch.init(hparams={"batch_size": 4}, exp_conf={"optimizations": {"hip_graph": True}}) as ctx:
+        ctx._core.checkpoint._storage_manager = __import__(
+            "determined_clone_amd.common.storage", fromlist=["x"]).SharedFSStorageManager(storage)
+        trial = OneVarTrial(ctx)
+        with caplog.at_level("WARNING"):
+            ctrl = pytorch.Trainer(trial, ctx).fit(max_length=pytorch.Batch(4))
+    assert "hip_graph disabled: not on a GPU" in caplog.text
+    assert getattr(ctrl, "_graphed", None) is None
