@@ -87,7 +87,7 @@ class TinyLMTrial(hf.BaseTransformerTrial):
 
     def train_batch(self, batch, epoch_idx, batch_idx):
         loss = super().train_batch(batch, epoch_idx, batch_idx)
-        self.losses.append(float(loss))
+        self.losses.append(float(loss.detach()))
         return loss
 
     def evaluate_batch(self, batch, batch_idx):
