@@ -221,6 +221,104 @@ class GPT(nn.Module):
         return logits, loss
 
 
+# ---------------------------------------------------------------------------------- pipeline form
+def _init_like_gpt(module: nn.Module, cfg: GPTConfig) -> None:
+    """GPT.reset_parameters' rules applied to one pipeline layer (same parameter names)."""
+    std = cfg.init_std
+    proj_std = std / math.sqrt(2 * cfg.n_layer)
+    for name, p in module.named_parameters():
+        if p.dim() < 2:
+            nn.init.ones_(p) if name.endswith("weight") else nn.init.zeros_(p)
+        elif name.endswith("proj.weight"):
+            nn.init.normal_(p, 0.0, proj_std)
+        else:
+            nn.init.normal_(p, 0.0, std)
+
+
+class EmbeddingPipe(nn.Module):
+    """Token (+ learned position) embedding; tokens -> residual stream."""
+
+    def __init__(self, cfg: GPTConfig) -> None:
+        super().__init__()
+        self.cfg = cfg
+        self.wte = nn.Embedding(cfg.padded_vocab, cfg.d_model)
+        self.wpe = nn.Embedding(cfg.max_seq_len, cfg.d_model) if cfg.pos_emb == "learned" else None
+        _init_like_gpt(self, cfg)
+
+    def forward(self, idx: torch.Tensor) -> torch.Tensor:
+        x = self.wte(idx)
+        if self.wpe is not None:
+            x = x + self.wpe.weight[:idx.shape[1]].unsqueeze(0)
+        return x
+
+
+class BlockPipe(Block):
+    """Transformer block on a pipeline activation: the residual stream, or (residual, pending
+    delta) -- the delta is folded into the next fused LayerNorm, across stage boundaries too."""
+
+    def __init__(self, cfg: GPTConfig) -> None:
+        super().__init__(cfg)
+        self.rotary = cfg.pos_emb == "rotary"
+        if self.rotary:
+            cos, sin = T.rope_tables(cfg.max_seq_len, self.attn.rot, cfg.rotary_base)
+            self.register_buffer("rope_cos", cos, persistent=False)
+            self.register_buffer("rope_sin", sin, persistent=False)
+        _init_like_gpt(self, cfg)
+
+    def forward(self, x):  # type: ignore[override]
+        resid, delta = (x, None) if isinstance(x, torch.Tensor) else x
+        rope = (self.rope_cos, self.rope_sin) if self.rotary else None
+        return super().forward(resid, delta, rope)
+
+
+class FinalNormPipe(nn.Module):
+    def __init__(self, cfg: GPTConfig) -> None:
+        super().__init__()
+        self.ln_f = FusedLayerNorm(cfg.d_model, cfg.ln_eps)
+
+    def forward(self, x) -> torch.Tensor:
+        if isinstance(x, torch.Tensor):
+            return self.ln_f(x)
+        h, _ = self.ln_f(x[0], residual=x[1])
+        return h
+
+
+class LMHeadPipe(nn.Module):
+    def __init__(self, cfg: GPTConfig) -> None:
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(cfg.padded_vocab, cfg.d_model))
+        nn.init.normal_(self.weight, 0.0, cfg.init_std)
+
+    def forward(self, h: torch.Tensor) -> torch.Tensor:
+        return F.linear(h, self.weight)
+
+
+def _tied_head(module: nn.Module, h: torch.Tensor) -> torch.Tensor:
+    return F.linear(h, module.wte.weight)
+
+
+def pipeline_loss(logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+    return T.cross_entropy(logits, targets, ignore_index=-100)
+
+
+def pipeline_specs(cfg: GPTConfig) -> list:
+    """GPT as a layer list for :class:`~determined_clone_amd.parallel.pipeline.PipelineModule`
+    (the GPT-NeoX pipe form the reference's gpt_neox example trains with pipe_parallel_size=2):
+    embedding, blocks, final LayerNorm, LM head (tied to the embedding table when
+    ``cfg.tie_embeddings``: a TiedLayerSpec whose gradient is summed across the first and last
+    stage)."""
+    from determined_clone_amd.parallel.pipeline import LayerSpec, TiedLayerSpec
+
+    if cfg.tie_embeddings:
+        embed = TiedLayerSpec("embed", EmbeddingPipe, cfg, tied_weight_attr="wte.weight")
+        head = TiedLayerSpec("embed", EmbeddingPipe, cfg, forward_fn=_tied_head,
+                             tied_weight_attr="wte.weight")
+    else:
+        embed, head = LayerSpec(EmbeddingPipe, cfg), LayerSpec(LMHeadPipe, cfg)
+    return [embed] + [LayerSpec(BlockPipe, cfg) for _ in range(cfg.n_layer)] + \
+        [LayerSpec(FinalNormPipe, cfg), head]
+
+
 def cast_for_mi355x(model: nn.Module, dtype: torch.dtype = torch.bfloat16) -> nn.Module:
     """GEMM / embedding weights -> ``dtype``; modules marked ``keep_fp32`` (LayerNorm, BatchNorm)
     keep fp32 parameters (the fused kernels read them as fp32)."""

@@ -57,6 +57,11 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         # kernels instead of scalar launch arguments: a captured HIP graph then replays each step
         # with the current LR schedule (see pytorch/_graph.py). None = scalar arguments.
         self._dyn: Optional[torch.Tensor] = None
+        # Pipeline parallelism (parallel/pipeline.py): the clip norm spans every stage, so the
+        # squared norm is also summed over ``norm_group``; ``norm_exclude`` params (tied-weight
+        # copies on non-owner stages) are left out so each tied weight is counted once.
+        self.norm_group: Any = None
+        self.norm_exclude: List[torch.Tensor] = []
 
     def _pad_multiple(self) -> int:
         return 1
@@ -69,6 +74,12 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         """Compute (on device) the global grad norm, found_inf and the combined multiplier
         ``grad_multiplier / loss_scale * clip_coef`` consumed by the next :meth:`step`."""
         self.space.ensure_views()
+        if self.norm_group is not None or self.norm_exclude:
+            slices = [st.buf.grad[a:b] for st in self.flat.values()
+                      for a, b in self._norm_ranges(st.buf, [(0, st.buf.grad.numel())])]
+            groups = [self.norm_group] if self.norm_group is not None else []
+            self._finish_norm(self._sumsq(slices), max_norm, loss_scale, groups)
+            return
         grads = [st.buf.grad for st in self.flat.values()]
         if grads and grads[0].is_cuda:
             self._dev_scale = _ext.load().grad_norm_scale(grads, loss_scale, self.grad_multiplier,
@@ -84,6 +95,58 @@ class FusedOptimizerBase(torch.optim.Optimizer):
             inf = 0.0 if math.isfinite(sq) else 1.0
             dev = grads[0].device if grads else "cpu"
             self._dev_scale = torch.tensor([mult * coef, inf, norm], dtype=torch.float32, device=dev)
+        self.last_grad_norm = self._dev_scale[2:3]
+
+    def _norm_ranges(self, buf: FlatBuffer, ranges: List[Any]) -> List[Any]:
+        """``ranges`` ([start, end) of ``buf``) minus the segments of ``norm_exclude`` params."""
+        if not self.norm_exclude:
+            return [(a, b) for a, b in ranges if b > a]
+        ex = sorted((seg.offset, seg.offset + seg.numel) for p in self.norm_exclude
+                    if self.space.buffer_of(p) is buf for seg in [self.space.segment(p)])
+        out = []
+        for a, b in ranges:
+            cur = a
+            for s, e in ex:
+                if e <= cur or s >= b:
+                    continue
+                if s > cur:
+                    out.append((cur, s))
+                cur = max(cur, e)
+            if cur < b:
+                out.append((cur, b))
+        return out
+
+    def _sumsq(self, slices: List[torch.Tensor]) -> torch.Tensor:
+        """Sum of squares of ``slices`` as a 1-element tensor (fp32 on GPU, fp64 on CPU)."""
+        dev = next(iter(self.flat.values())).buf.grad.device if self.flat else torch.device("cpu")
+        if dev.type == "cuda":
+            if not slices:
+                return torch.zeros(1, dtype=torch.float32, device=dev)
+            return _ext.load().sumsq_partials(slices).sum().reshape(1)
+        sq = torch.zeros(1, dtype=torch.float64)
+        for s in slices:
+            sq += s.double().pow(2).sum()
+        return sq
+
+    def _finish_norm(self, sq: torch.Tensor, max_norm: float, loss_scale: Optional[torch.Tensor],
+                     groups: List[Any]) -> None:
+        """All-reduce the squared norm over ``groups`` and derive ``_dev_scale``."""
+        import torch.distributed as dist
+
+        for g in groups:
+            dist.all_reduce(sq, group=g)
+        if sq.is_cuda:
+            self._dev_scale = _ext.load().norm_finalize(sq, loss_scale, self.grad_multiplier,
+                                                        float(max_norm))
+        else:
+            tot = float(sq)
+            inv_ls = 1.0 / float(loss_scale[0]) if loss_scale is not None else 1.0
+            mult = inv_ls * self.grad_multiplier
+            finite = math.isfinite(tot)
+            norm = math.sqrt(tot) * mult if finite else float("inf")
+            coef = min(1.0, max_norm / (norm + 1e-6)) if max_norm > 0 and finite else 1.0
+            self._dev_scale = torch.tensor([mult * coef, 0.0 if finite else 1.0, norm],
+                                           dtype=torch.float32)
         self.last_grad_norm = self._dev_scale[2:3]
 
     @property

@@ -220,29 +220,12 @@ class ZeroShardMixin:
     # ------------------------------------------------------------------ clip / overflow
     def prepare_grads(self, max_norm: float = 0.0, loss_scale: Optional[torch.Tensor] = None) -> None:
         self.space.ensure_views()
-        slices = [st.buf.grad[a0:a1] for st in self._order for a0, a1, _ in st.owned if a1 > a0]
-        dev = slices[0].device if slices else torch.device("cpu")
-        if dev.type == "cuda":
-            C = _ext.load()
-            sq = C.sumsq_partials(slices).sum().reshape(1)
-            if self.world > 1:
-                dist.all_reduce(sq, group=self.pg)
-            self._dev_scale = C.norm_finalize(sq, loss_scale, self.grad_multiplier, float(max_norm))
-        else:
-            sq = torch.zeros(1, dtype=torch.float64)
-            for s in slices:
-                sq += s.double().pow(2).sum()
-            if self.world > 1:
-                dist.all_reduce(sq, group=self.pg)
-            tot = float(sq)
-            inv_ls = 1.0 / float(loss_scale[0]) if loss_scale is not None else 1.0
-            mult = inv_ls * self.grad_multiplier
-            finite = tot == tot and tot != float("inf")
-            norm = (tot ** 0.5) * mult if finite else float("inf")
-            coef = min(1.0, max_norm / (norm + 1e-6)) if max_norm > 0 and finite else 1.0
-            self._dev_scale = torch.tensor([mult * coef, 0.0 if finite else 1.0, norm],
-                                           dtype=torch.float32)
-        self.last_grad_norm = self._dev_scale[2:3]
+        slices = [st.buf.grad[a:b] for st in self._order for a0, a1, _ in st.owned
+                  for a, b in self._norm_ranges(st.buf, [(a0, a1)])]
+        groups = [self.pg] if self.world > 1 else []
+        if self.norm_group is not None:
+            groups.append(self.norm_group)
+        self._finish_norm(self._sumsq(slices), max_norm, loss_scale, groups)
 
     # ------------------------------------------------------------------ step
     @torch.no_grad()

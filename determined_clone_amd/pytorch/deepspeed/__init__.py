@@ -9,3 +9,6 @@ from determined_clone_amd.pytorch.deepspeed._trial import (DeepSpeedTrial, DeepS
                                                            DeepSpeedTrialController, Trainer, init,
                                                            overwrite_deepspeed_config,
                                                            run_deepspeed_trial)
+from determined_clone_amd.parallel.pipeline import (LayerSpec, PipelineGrid, PipelineModule,
+                                                    TiedLayerSpec)
+from determined_clone_amd.pytorch.deepspeed._pipe import PipelineEngine

@@ -240,7 +240,8 @@ class DeepSpeedEngine(torch.nn.Module):
         if model_parameters is not None and not isinstance(model_parameters, list):
             model_parameters = list(model_parameters)
         if self.world_size > 1:
-            ddp.broadcast_module_state(model, group)
+            src = 0 if group is None or group is dist.group.WORLD else dist.get_global_rank(group, 0)
+            ddp.broadcast_module_state(model, group, src=src)
         self.optimizer = self._build_optimizer(optimizer, model_parameters)
         self.basic_optimizer = self.optimizer
         self.lr_scheduler = self._build_scheduler(lr_scheduler)
@@ -527,7 +528,9 @@ def initialize(args: Any = None, model: Optional[torch.nn.Module] = None,
                collate_fn: Any = None, config: Any = None, config_params: Any = None,
                group: Any = None) -> Tuple[DeepSpeedEngine, Any, Any, Any]:
     """``deepspeed.initialize`` equivalent: returns ``(engine, optimizer, None, lr_scheduler)``.
-    The config comes from ``config`` / ``config_params`` or ``args.deepspeed_config``."""
+    The config comes from ``config`` / ``config_params`` or ``args.deepspeed_config``. A
+    :class:`~determined_clone_amd.parallel.pipeline.PipelineModule` gets a pipeline-parallel
+    :class:`~determined_clone_amd.parallel.pipeline.PipelineEngine`."""
     if model is None:
         raise ValueError("initialize() requires a model")
     cfg = config if config is not None else config_params
@@ -535,6 +538,16 @@ def initialize(args: Any = None, model: Optional[torch.nn.Module] = None,
         cfg = getattr(args, "deepspeed_config", None) or getattr(args, "deepscale_config", None)
     if cfg is None:
         raise ValueError("initialize() requires a DeepSpeed config")
-    engine = DeepSpeedEngine(model, cfg, optimizer=optimizer, model_parameters=model_parameters,
-                             lr_scheduler=lr_scheduler, group=group)
+    from determined_clone_amd.parallel import pipeline
+    from determined_clone_amd.pytorch.deepspeed._pipe import PipelineEngine
+
+    if isinstance(model, pipeline.PipelineModule):
+        # DeepSpeed returns its PipelineEngine for a PipelineModule; the data-parallel group comes
+        # from the module's stage x data grid
+        engine: DeepSpeedEngine = PipelineEngine(
+            model, cfg, optimizer=optimizer, model_parameters=model_parameters,
+            lr_scheduler=lr_scheduler)
+    else:
+        engine = DeepSpeedEngine(model, cfg, optimizer=optimizer, model_parameters=model_parameters,
+                                 lr_scheduler=lr_scheduler, group=group)
     return engine, engine.optimizer, None, engine.lr_scheduler

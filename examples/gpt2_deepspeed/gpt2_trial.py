@@ -2,6 +2,9 @@
 gpt2_trial.py, which drives GPT-NeoX through DeepSpeed; here ``det_ds.initialize`` builds the
 MI355X engine: ZeRO-1/2 over RCCL, fused HIP AdamW, MFMA flash attention, fused LN / GELU / CE).
 
+``hyperparameters.pipe_parallel_size: N`` trains the same GPT as an N-stage pipeline
+(``pipe.yaml``; the reference example's ``pipe_parallel_size: 2``).
+
 The DeepSpeed JSON config is ``ds_config.json`` overlaid with ``hyperparameters.overwrite_deepspeed_args``
 (same convention as the reference's ``overwrite_deepspeed_config``). Synthetic token data."""
 import json
@@ -32,14 +35,26 @@ class GPT2Trial(det_ds.DeepSpeedTrial):
         self.context = context
         hp = context.get_hparams()
         self.seq = int(hp.get("seq_len", 1024))
-        model = gpt2.gpt2(hp.get("model", "gpt2-medium"), max_seq_len=self.seq)
+        cfg = gpt2.config_for(hp.get("model", "gpt2-medium"), max_seq_len=self.seq)
         base = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "ds_config.json")))
         ds_config = det_ds.overwrite_deepspeed_config(base, hp.get("overwrite_deepspeed_args", {}))
+        self.pipe = int(hp.get("pipe_parallel_size", 0))
+        if self.pipe >= 1:
+            # GPT-NeoX style pipeline (reference gpt_neox/zero1.yaml: pipe_parallel_size 2):
+            # embedding | blocks | final norm | tied LM head over `pipe` stages, 1F1B schedule
+            model = det_ds.PipelineModule(gpt2.pipeline_specs(cfg), num_stages=self.pipe,
+                                          loss_fn=gpt2.pipeline_loss, seed_layers=True,
+                                          activation_checkpoint_interval=int(
+                                              hp.get("activation_checkpoint_interval", 0)))
+        else:
+            model = gpt2.GPT(cfg)
         engine, _, _, _ = det_ds.initialize(model=model, config=ds_config)
         self.engine = context.wrap_model_engine(engine)
-        self.vocab = model.cfg.vocab_size
+        self.vocab = cfg.vocab_size
 
     def train_batch(self, it, epoch_idx, batch_idx):
+        if self.context.use_pipeline_parallel:
+            return {"loss": self.engine.train_batch(it)}
         x, y = self.context.to_device(next(it))
         _, loss = self.engine(x, y)
         self.engine.backward(loss)
@@ -47,6 +62,8 @@ class GPT2Trial(det_ds.DeepSpeedTrial):
         return {"loss": loss}
 
     def evaluate_batch(self, it, batch_idx):
+        if self.context.use_pipeline_parallel:
+            return {"lm_loss": self.engine.eval_batch(it)}
         x, y = self.context.to_device(next(it))
         with torch.no_grad():
             _, loss = self.engine(x, y)

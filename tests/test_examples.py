@@ -109,3 +109,25 @@ def test_gpt2_deepspeed_trial_local(tmp_path):
         t = m.GPT2Trial(ctx)
         c = det_ds.Trainer(t, ctx).fit(max_length=pytorch.Batch(3), checkpoint_policy="none")
     assert c.state.batches_trained == 3 and t.engine.global_steps == 3
+
+
+def test_gpt2_pipeline_example_on_cluster(cluster):
+    """The GPT-2 DeepSpeed example as a 2-stage pipeline over 2 slots: launch layer ->
+    torch.distributed.run -> DeepSpeedTrial with a PipelineEngine (gloo on CPU slots)."""
+    s = cluster
+    cfg = yaml.safe_load(open(os.path.join(EX, "gpt2_deepspeed", "pipe.yaml")))
+    cfg["hyperparameters"].update({"model": "tiny", "seq_len": 32, "pipe_parallel_size": 2})
+    cfg["hyperparameters"]["overwrite_deepspeed_args"] = {
+        "train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2,
+        "bf16": {"enabled": False}, "zero_optimization": {"stage": 0},
+        "scheduler": {"params": {"warmup_num_steps": 2, "total_num_steps": 10}}}
+    cfg["resources"]["slots_per_trial"] = 2
+    cfg["searcher"]["max_length"] = {"batches": 4}
+    cfg["min_validation_period"] = {"batches": 4}
+    eid, st = _run(s, os.path.join(EX, "gpt2_deepspeed"), cfg)
+    t = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]
+    if st != "COMPLETED":
+        logs = s.get(f"/api/v1/trials/{t['id']}/logs")["logs"]
+        raise AssertionError("\n".join(l["log"] for l in logs[-60:]))
+    val = s.get(f"/api/v1/trials/{t['id']}/metrics", params={"group": "validation"})["metrics"]
+    assert val[-1]["steps_completed"] == 4 and val[-1]["metrics"]["lm_loss"] > 0
