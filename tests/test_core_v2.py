@@ -74,3 +74,21 @@ def test_unmanaged_resume_by_external_ids(master):
                                                                   external_trial_id="ext-trial-2"), steps=(1,))
     assert eid3 == eid1 and tid3 != tid1
     assert master.db.one("SELECT COUNT(*) AS n FROM trials WHERE experiment_id=?", [eid1])["n"] == 2
+
+
+def test_lightning_det_logger(master):
+    """``lightning.experimental.DetLogger`` driven the way a Lightning Trainer drives a logger."""
+    from determined_clone_amd.lightning.experimental import DetLogger
+
+    d = sdk.Determined(master.master_url, "admin", "")
+    logger = DetLogger(defaults=core_v2.DefaultConfig(name="ptl-logger"), client=d)
+    assert logger.name == "DetLogger" and logger.version == "0.1"
+    logger.log_hyperparams({"lr": 0.1})
+    for step in (10, 20):
+        logger.log_metrics({"train_loss": 1.0 / step}, step=step)
+    tid = core_v2.info.trial.trial_id
+    logger.save()
+    logger.finalize("success")
+    rows = master.db.all("SELECT steps_completed FROM metrics WHERE trial_id=? AND grp='training' "
+                         "ORDER BY id", [tid])
+    assert [r["steps_completed"] for r in rows] == [10, 20]
