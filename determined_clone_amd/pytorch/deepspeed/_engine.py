@@ -20,7 +20,9 @@ Supported config keys: train_batch_size, train_micro_batch_size_per_gpu,
 gradient_accumulation_steps, optimizer {type: Adam|AdamW|SGD|Lamb, params}, scheduler
 {type: WarmupLR|WarmupDecayLR|WarmupCosineLR, params}, gradient_clipping, bf16.enabled,
 fp16 {enabled, loss_scale, initial_scale_power, loss_scale_window, min_loss_scale},
-zero_optimization {stage (0-2), reduce_bucket_size, allgather_bucket_size, overlap_comm},
+zero_optimization {stage (0-3), reduce_bucket_size, allgather_bucket_size, overlap_comm}
+(stage 3: :mod:`determined_clone_amd.parallel.zero3`, per-module parameter gather /
+gradient reduce-scatter; the stage3_* tuning keys are accepted),
 steps_per_print. Unknown keys are accepted and ignored (with a debug log), like DeepSpeed's
 permissive parsing of e.g. ``wall_clock_breakdown``.
 """
@@ -89,9 +91,10 @@ class DeepSpeedConfig:
         if isinstance(z, bool):
             z = {"stage": 1 if z else 0}
         self.zero_stage = int(z.get("stage", 0))
-        if self.zero_stage > 2:
-            raise ValueError("ZeRO stage 3 (parameter partitioning) is not implemented; use stage "
-                             "<= 2 (a 288 GB MI355X holds GPT-2 XL-class parameters unpartitioned)")
+        if self.zero_stage > 3:
+            raise ValueError(f"invalid ZeRO stage {self.zero_stage}")
+        self.stage3_gather_16bit_weights_on_model_save = bool(
+            z.get("stage3_gather_16bit_weights_on_model_save", True))
         self.reduce_bucket_size = int(z.get("reduce_bucket_size", 32 * 2 ** 20))  # elements
         self.allgather_bucket_size = int(z.get("allgather_bucket_size", 32 * 2 ** 20))
         self.overlap_comm = bool(z.get("overlap_comm", True))
@@ -232,6 +235,7 @@ class DeepSpeedEngine(torch.nn.Module):
                 else torch.device("cpu")
         self.device = device
         self.module = model
+        self._z3: Any = None  # ZeRO-3 partitioner (stage 3 only)
         if cfg.bf16:
             _cast_module(model, torch.bfloat16)
         elif cfg.fp16:
@@ -307,6 +311,21 @@ class DeepSpeedEngine(torch.nn.Module):
                 raise ValueError(f"unsupported DeepSpeed optimizer type {cfg.optimizer['type']}")
             defaults = _filter_defaults(kind, p)
             groups = self._param_groups(model_parameters)
+        if stage == 3:
+            from determined_clone_amd.parallel import zero3
+
+            self._z3 = zero3.Zero3Partitioner(self.module, [list(g["params"]) for g in groups],
+                                              group=self.group)
+            shards = self._z3.shard_param_groups(len(groups))
+            z3_groups = [dict(g, params=shards[i]) for i, g in enumerate(groups) if shards[i]]
+            cls = {"adam": fopt.FusedAdam, "adamw": fopt.FusedAdamW, "sgd": fopt.FusedSGD,
+                   "lamb": fopt.FusedLAMB}[kind]
+            opt = cls(z3_groups, **defaults)
+            if self.world_size > 1:
+                opt.grad_multiplier = 1.0 / self.world_size  # reduce-scatter sums
+                # shard norms -> global norm (None would mean "no extra reduction")
+                opt.norm_group = self.group if self.group is not None else dist.group.WORLD
+            return opt
         if stage >= 1:
             cls = zero.zero_optimizer_for(kind)
             esz = 2 if (cfg.bf16 or cfg.fp16) else 4
@@ -388,6 +407,8 @@ class DeepSpeedEngine(torch.nn.Module):
         elif self._static_scale is not None:
             scaled = scaled * self._static_scale.to(scaled.dtype)
         scaled.backward(retain_graph=retain_graph)
+        if self._z3 is not None:
+            self._z3.finish_backward()
         return loss
 
     def step(self, lr_kwargs: Optional[Dict[str, Any]] = None) -> None:
@@ -424,6 +445,12 @@ class DeepSpeedEngine(torch.nn.Module):
     def zero_grad(self) -> None:
         self.optimizer.zero_grad()
 
+    def module_state_dict(self) -> Dict[str, torch.Tensor]:
+        """The module's full state dict (under ZeRO-3 every rank must call it: it gathers)."""
+        if self._z3 is not None:
+            return self._z3.full_state_dict()
+        return self.module.state_dict()
+
     # ------------------------------------------------------------------ checkpoint
     def _ckpt_dir(self, save_dir: Union[str, pathlib.Path], tag: Optional[str]) -> pathlib.Path:
         return pathlib.Path(save_dir) / str(tag)
@@ -437,9 +464,10 @@ class DeepSpeedEngine(torch.nn.Module):
         tag = tag or f"global_step{self.global_steps}"
         d = self._ckpt_dir(save_dir, tag)
         d.mkdir(parents=True, exist_ok=True)
+        module_sd = self.module_state_dict()  # collective under ZeRO-3
         if self.global_rank == 0:
             state = {
-                "module": self.module.state_dict(),
+                "module": module_sd,
                 "lr_scheduler": self.lr_scheduler.state_dict() if self.lr_scheduler is not None else None,
                 "global_steps": self.global_steps, "global_samples": self.global_samples,
                 "micro_steps": self.micro_steps, "skipped_steps": self.skipped_steps,
@@ -473,7 +501,10 @@ class DeepSpeedEngine(torch.nn.Module):
         if not path.exists():
             raise FileNotFoundError(f"DeepSpeed-format checkpoint not found at {path}")
         state = torch.load(path, map_location="cpu", weights_only=True)
-        self.module.load_state_dict(state["module"], strict=load_module_strict)
+        if self._z3 is not None:
+            self._z3.load_full_state_dict(state["module"], strict=load_module_strict)
+        else:
+            self.module.load_state_dict(state["module"], strict=load_module_strict)
         self.global_steps = int(state.get("global_steps", 0))
         self.global_samples = int(state.get("global_samples", 0))
         self.micro_steps = int(state.get("micro_steps", 0))
@@ -483,7 +514,18 @@ class DeepSpeedEngine(torch.nn.Module):
         if self.scaler is not None and state.get("scaler"):
             self.scaler.load_state_dict(state["scaler"])
         if load_optimizer_states:
-            if isinstance(self.optimizer, zero.ZeroShardMixin):
+            own = d / f"zero_pp_rank_{self.global_rank}_mp_rank_00_optim_states.pt"
+            if self._z3 is not None:
+                if int(state.get("dp_world_size", -1)) == self.world_size and own.exists():
+                    osd = torch.load(own, map_location="cpu", weights_only=True)["optimizer_state_dict"]
+                    self.optimizer.load_state_dict(osd)
+                    if not any("master_param" in s for s in osd["state"].values()):
+                        self.optimizer.sync_master_from_model()
+                else:
+                    logger.warning("ZeRO-3 checkpoint from another data-parallel size: weights "
+                                   "loaded, optimizer state reset")
+                    self.optimizer.sync_master_from_model()
+            elif isinstance(self.optimizer, zero.ZeroShardMixin):
                 saved_world = int(state.get("dp_world_size", self.world_size))
                 own = d / f"zero_pp_rank_{self.global_rank}_mp_rank_00_optim_states.pt"
                 if saved_world == self.world_size and own.exists():

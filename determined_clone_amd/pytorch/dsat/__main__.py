@@ -21,7 +21,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     p.add_argument("-mct", "--max-concurrent-trials", type=int, default=d["max_concurrent_trials"])
     p.add_argument("-m", "--metric", default=d["metric"],
                    choices=_defaults.SMALLER_IS_BETTER_METRICS + _defaults.LARGER_IS_BETTER_METRICS)
-    p.add_argument("-z", "--zero-stages", type=int, nargs="+", default=d["zero_stages"], choices=[0, 1, 2])
+    p.add_argument("-z", "--zero-stages", type=int, nargs="+", default=d["zero_stages"], choices=[0, 1, 2, 3])
     p.add_argument("--start-profile-step", type=int, default=d["start_profile_step"])
     p.add_argument("--end-profile-step", type=int, default=d["end_profile_step"])
     p.add_argument("--max-mbs", type=int, default=d["max_mbs"])

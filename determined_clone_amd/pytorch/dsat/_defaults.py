@@ -8,7 +8,7 @@ LARGER_IS_BETTER_METRICS = ["throughput", "FLOPS_per_gpu"]
 ARG_DEFAULTS = {
     "max_trials": 32,
     "max_concurrent_trials": 4,
-    "zero_stages": [1, 2],
+    "zero_stages": [1, 2, 3],
     "start_profile_step": 3,
     "end_profile_step": 5,
     "metric": "throughput",

@@ -122,8 +122,9 @@ def test_config_batch_inference_and_errors():
     with pytest.raises(ValueError):
         det_ds.DeepSpeedConfig({"train_batch_size": 30, "train_micro_batch_size_per_gpu": 4,
                                 "gradient_accumulation_steps": 2}, 2)
+    assert det_ds.DeepSpeedConfig({"train_batch_size": 8, "zero_optimization": {"stage": 3}}, 1).zero_stage == 3
     with pytest.raises(ValueError):
-        det_ds.DeepSpeedConfig({"train_batch_size": 8, "zero_optimization": {"stage": 3}}, 1)
+        det_ds.DeepSpeedConfig({"train_batch_size": 8, "zero_optimization": {"stage": 4}}, 1)
 
 
 def test_warmup_schedulers():
