@@ -215,33 +215,37 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         sc = mfma32(load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf), qf[s], sc);
       // sc[i]: key = kb0 + (i&3) + 8(i>>2) + 4hf, query = my_q
       const bool need_mask = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0);
+      // row max on the RAW scores (scale > 0 commutes with max); the scale is folded into the
+      // exponent's FMA below -- one VALU op per score instead of a multiply and a subtract
       float mx = -INFINITY;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float x = sc[i] * scale_log2;
         if (need_mask) {
           const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-          if (key >= Sk || (CAUSAL && key > my_q)) x = -INFINITY;
+          if (key >= Sk || (CAUSAL && key > my_q)) sc[i] = -INFINITY;
         }
-        sc[i] = x;
-        mx = fmaxf(mx, x);
+        mx = fmaxf(mx, sc[i]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
+      const float mnew = fmaxf(m, mx * scale_log2);
       const float mref = mnew == -INFINITY ? 0.f : mnew;
       const float alpha = fast_exp2(m - mref);
       float rs = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = fast_exp2(sc[i] - mref);
+        const float p = fast_exp2(fmaf(sc[i], scale_log2, -mref));
         sc[i] = p;
         rs += p;
       }
       rs += __shfl_xor(rs, 32, 64);
       l = l * alpha + rs;
       m = mnew;
+      // rescale the output accumulators only when some row's max moved (rare after the first
+      // tiles): skips D/2 multiplies per lane per sub-tile
+      if (__any(alpha != 1.f)) {
 #pragma unroll
-      for (int n = 0; n < D / 32; ++n) oacc[n] *= alpha;
+        for (int n = 0; n < D / 32; ++n) oacc[n] *= alpha;
+      }
       const bf16x8 p0 = pack8(sc, 0), p1 = pack8(sc, 8);
 #pragma unroll
       for (int n = 0; n < D / 32; ++n) {
@@ -347,12 +351,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
       const bool need_mask = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float p = fast_exp2(sc[i] * scale_log2 - lq);
+        float p = fast_exp2(fmaf(sc[i], scale_log2, -lq));
         if (need_mask) {
           const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
           if (key >= Sk || (CAUSAL && key > my_q)) p = 0.f;
         }
-        dp[i] = p * (dp[i] - dsum) * scale;
+        dp[i] = p * (dp[i] - dsum);  // the softmax scale is applied once to dQ at the end
       }
       const bf16x8 s0 = pack8(dp, 0), s1 = pack8(dp, 8);
 #pragma unroll
@@ -371,8 +375,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         uint2 pk;
-        pk.x = pack_bf16x2(dqacc[n][4 * g], dqacc[n][4 * g + 1]);
-        pk.y = pack_bf16x2(dqacc[n][4 * g + 2], dqacc[n][4 * g + 3]);
+        pk.x = pack_bf16x2(dqacc[n][4 * g] * scale, dqacc[n][4 * g + 1] * scale);
+        pk.y = pack_bf16x2(dqacc[n][4 * g + 2] * scale, dqacc[n][4 * g + 3] * scale);
         *reinterpret_cast<uint2*>(row + 32 * n + 8 * g + 4 * hf) = pk;
       }
   }
@@ -471,13 +475,13 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int ql = (i & 3) + 8 * (i >> 2) + 4 * hf;
-      float p = fast_exp2(sacc[i] * scale_log2 - lse_s[ql]);
+      float p = fast_exp2(fmaf(sacc[i], scale_log2, -lse_s[ql]));
       if (need_mask) {
         const int qi = qt + ql;
         if (qi >= Sq || my_key >= Sk || (CAUSAL && my_key > qi)) p = 0.f;
       }
       sacc[i] = p;
-      dpacc[i] = p * (dpacc[i] - del_s[ql]) * scale;
+      dpacc[i] = p * (dpacc[i] - del_s[ql]);  // scale applied once to dK at the end
     }
     const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8);
     const bf16x8 s0 = pack8(dpacc, 0), s1 = pack8(dpacc, 8);
@@ -499,8 +503,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         uint2 pk;
-        pk.x = pack_bf16x2(dkacc[n][4 * g], dkacc[n][4 * g + 1]);
-        pk.y = pack_bf16x2(dkacc[n][4 * g + 2], dkacc[n][4 * g + 3]);
+        pk.x = pack_bf16x2(dkacc[n][4 * g] * scale, dkacc[n][4 * g + 1] * scale);
+        pk.y = pack_bf16x2(dkacc[n][4 * g + 2] * scale, dkacc[n][4 * g + 3] * scale);
         *reinterpret_cast<uint2*>(dkrow + 32 * n + 8 * g + 4 * hf) = pk;
         pk.x = pack_bf16x2(dvacc[n][4 * g], dvacc[n][4 * g + 1]);
         pk.y = pack_bf16x2(dvacc[n][4 * g + 2], dvacc[n][4 * g + 3]);

@@ -1,0 +1,50 @@
+"""Flash-attention kernel throughput (ours) at GPT shapes: one JSON line per (shape, pass).
+Usage: python tools/bench_attn.py [--iters N] [--only fwd|bwd]"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from determined_clone_amd.ops import transformer as T  # noqa: E402
+
+
+def timeit(fn, iters, warmup=5):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--iters", type=int, default=30)
+    p.add_argument("--only", default="")
+    a = p.parse_args()
+    for B, S, H, D in ((16, 1024, 16, 64), (8, 2048, 16, 64), (4, 4096, 8, 128)):
+        q, k, v = (torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+                   for _ in range(3))
+        g = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+        flops = 4 * B * H * S * S * D / 2
+        if a.only in ("", "fwd"):
+            ms = timeit(lambda: T.flash_attention(q, k, v, causal=True), a.iters)
+            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "pass": "fwd", "ms": round(ms, 4),
+                              "tflops": round(flops / ms / 1e9, 1)}), flush=True)
+        if a.only in ("", "bwd"):
+            o = T.flash_attention(q, k, v, causal=True)
+            ms = timeit(lambda: torch.autograd.grad(o, (q, k, v), g, retain_graph=True), a.iters)
+            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "pass": "bwd", "ms": round(ms, 4),
+                              "tflops": round(2.5 * flops / ms / 1e9, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

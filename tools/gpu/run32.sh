@@ -1,0 +1,7 @@
+#!/bin/bash
+# attention after hardware bf16 packs / FMA-folded scale / lazy rescale: numerics + throughput
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+  tests/test_transformer_ops_gpu.py tests/test_ops_gpu.py > gpurun_out/r32_pytest.txt 2>&1 &&
+timeout -k 10 120 python tools/bench_attn.py > gpurun_out/r32_attn.txt 2>&1
