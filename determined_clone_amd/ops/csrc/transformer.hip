@@ -22,6 +22,20 @@ namespace {
 constexpr int kWaves = 4;             // rows (LN) handled concurrently per block
 constexpr int kBlock = kWaves * 64;
 
+// 8 consecutive fp32 affine parameters (gamma or beta) from c, or `fill` when absent / out of range.
+__device__ __forceinline__ void load_affine8(const float* __restrict__ p, int c, bool ok, float fill,
+                                             float (&out)[8]) {
+  if (p && ok) {
+    const float4 a = *reinterpret_cast<const float4*>(p + c);
+    const float4 b = *reinterpret_cast<const float4*>(p + c + 4);
+    out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+    out[4] = b.x; out[5] = b.y; out[6] = b.z; out[7] = b.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = fill;
+  }
+}
+
 template <typename T, int NV>
 __global__ __launch_bounds__(kBlock) void ln_fwd_kernel(
     const void* __restrict__ x, const void* __restrict__ res, void* __restrict__ sum_out,
@@ -30,6 +44,14 @@ __global__ __launch_bounds__(kBlock) void ln_fwd_kernel(
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nvec = D / 8;
+  // gamma / beta: two 16-B loads per 8 columns, once per wave (not 16 scalar loads per row)
+  float gv[NV][8], bv[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (lane + i * 64) * 8;
+    load_affine8(gamma, c, c < D, 1.f, gv[i]);
+    load_affine8(beta, c, c < D, 0.f, bv[i]);
+  }
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wid; row < rows;
        row += static_cast<int64_t>(gridDim.x) * kWaves) {
     const int64_t base = row * D;
@@ -71,11 +93,7 @@ __global__ __launch_bounds__(kBlock) void ln_fwd_kernel(
         const int c = vi * 8;
         float o[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float g = gamma ? gamma[c + k] : 1.f;
-          const float b = beta ? beta[c + k] : 0.f;
-          o[k] = fmaf((v[i][k] - mean) * rstd, g, b);
-        }
+        for (int k = 0; k < 8; ++k) o[k] = fmaf((v[i][k] - mean) * rstd, gv[i][k], bv[i][k]);
         Vec8<T>::store(reinterpret_cast<char*>(y) + (base + c) * Vec8<T>::bytes, o);
       }
     }
@@ -97,11 +115,14 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_kernel(
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nvec = D / 8;
-  float dg[NV][8], db[NV][8];
+  float dg[NV][8], db[NV][8], gam[NV][8];
 #pragma unroll
-  for (int i = 0; i < NV; ++i)
+  for (int i = 0; i < NV; ++i) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) { dg[i][k] = 0.f; db[i][k] = 0.f; }
+    const int c = (lane + i * 64) * 8;
+    load_affine8(gamma, c, c < D, 1.f, gam[i]);
+  }
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wid; row < rows;
        row += static_cast<int64_t>(gridDim.x) * kWaves) {
     const int64_t base = row * D;
@@ -121,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_kernel(
           xh[i][k] = (xv[k] - mean) * rstd;
           dg[i][k] = fmaf(g[i][k], xh[i][k], dg[i][k]);
           db[i][k] += g[i][k];
-          const float gg = g[i][k] * (gamma ? gamma[c + k] : 1.f);
+          const float gg = g[i][k] * gam[i][k];
           g[i][k] = gg;
           s1 += gg;
           s2 = fmaf(gg, xh[i][k], s2);
@@ -256,17 +277,23 @@ __device__ __forceinline__ void load_bias8(const void* bias, bool bf16, int c, f
 }
 
 // ------------------------------------------------------------------ bias + GELU(tanh)
+// 0.5 (1 + tanh(u)) = sigmoid(2u): one v_exp_f32 + one v_rcp_f32 instead of libm tanhf.
+// s = 1 / (1 + 2^(-2u log2 e)); u -> -inf gives 2^+inf = inf -> s = 0, u -> +inf gives s = 1.
+__device__ __forceinline__ float sigmoid2u(float u) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
+}
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float u = k0 * fmaf(k1 * x * x, x, x);
-  return 0.5f * x * (1.f + tanhf(u));
+  return x * sigmoid2u(u);
 }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
+  // d/dx [x s(u)] = s + x s (1 - s) * 2 u',  u' = k0 (1 + 3 k1 x^2)
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float x2 = x * x;
   const float u = k0 * fmaf(k1 * x2, x, x);
-  const float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  const float s = sigmoid2u(u);
+  return fmaf(x * s * (1.f - s), 2.f * k0 * fmaf(3.f * k1, x2, 1.f), s);
 }
 
 template <typename T>
@@ -301,7 +328,29 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
   float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float b[8];
   load_bias8(bias, bias_bf16, c, b);
-  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+  const int64_t step = gridDim.y;
+  int64_t r = blockIdx.y;
+  // 4 rows per iteration: 8 independent 16-B loads in flight per lane (this grid is only
+  // ~2 blocks per CU, so memory-level parallelism has to come from inside the thread)
+  for (; r + 3 * step < rows; r += 4 * step) {
+    float g[4][8], a[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t off = ((r + u * step) * N + c) * Vec8<T>::bytes;
+      Vec8<T>::load(reinterpret_cast<const char*>(dy) + off, g[u]);
+      Vec8<T>::load(reinterpret_cast<const char*>(x) + off, a[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g[u][k] *= gelu_tanh_grad(a[u][k] + b[k]);
+        bsum[k] += g[u][k];
+      }
+      Vec8<T>::store(reinterpret_cast<char*>(dx) + ((r + u * step) * N + c) * Vec8<T>::bytes, g[u]);
+    }
+  }
+  for (; r < rows; r += step) {
     const int64_t off = (r * N + c) * Vec8<T>::bytes;
     float g[8], a[8];
     Vec8<T>::load(reinterpret_cast<const char*>(dy) + off, g);

@@ -11,6 +11,7 @@ Layouts are the ones the model produces without copies: activations [..., D] row
 attention operands [B, S, H, Dh] (slices of the fused QKV projection are accepted as-is).
 """
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -153,6 +154,30 @@ class _BiasGelu(torch.autograd.Function):
         return dx, db.to(ctx.bias.dtype)
 
 
+_WGRAD_SPLITK = os.environ.get("DCA_WGRAD_SPLITK", "1") != "0"
+
+
+def _wgrad_splits(tokens: int, m: int, n: int) -> int:
+    """Split-K factor for the weight gradient dW[m, n] = dY^T X over ``tokens``.
+
+    A transformer's dW GEMMs have a small output (1-4M elements: 64-256 macro tiles for 256 CUs)
+    and a long K (all tokens of the micro-batch), and hipBLASLt's heuristic runs them without
+    split-K. Splitting K four ways as one batched GEMM fills the chip: measured on MI355X at 16k
+    tokens (tools/bench_wgrad.py, profiles/r9_wgrad_splitk.txt) 1024x1024 111 -> 64 us,
+    3072x1024 166 -> 115 us, 4096x1024 166 -> 145 us, 1024x4096 161 -> 143 us."""
+    if not _WGRAD_SPLITK or tokens < 8192 or tokens % 4 or m * n > 16 * 2 ** 20:
+        return 1
+    return 4
+
+
+def _wgrad_split_k(acc: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, s: int) -> None:
+    """``acc += dy2^T x2`` as ``s`` K-slices in one batched GEMM, summed in fp32."""
+    t, m = dy2.shape
+    a = dy2.reshape(s, t // s, m).transpose(1, 2)
+    b = x2.reshape(s, t // s, x2.shape[1])
+    acc.add_(torch.bmm(a, b).sum(0, dtype=torch.float32))
+
+
 class _Linear(torch.autograd.Function):
     """``y = x @ w.T + b`` whose backward accumulates straight into the parameters' flat
     ``.grad`` views: dW by a GEMM with beta = 1 (``grad.addmm_``), db by the fused column
@@ -178,7 +203,11 @@ class _Linear(torch.autograd.Function):
             x2 = x.reshape(-1, x.shape[-1])
             acc = _grad.target(w_param)
             if acc is not None:
-                acc.addmm_(dy2.t(), x2)
+                s = _wgrad_splits(dy2.shape[0], dy2.shape[1], x2.shape[1])
+                if s > 1:
+                    _wgrad_split_k(acc, dy2, x2, s)
+                else:
+                    acc.addmm_(dy2.t(), x2)
             else:
                 dw = dy2.t() @ x2
         if b_param is not None and ctx.needs_input_grad[2]:

@@ -206,13 +206,18 @@ def _flat(params):
 
 
 @pytest.mark.parametrize("bias", [True, False])
-def test_linear_direct_grad_accumulation(bias):
-    """T.linear accumulates dW (GEMM beta=1) and db (fused column sum) into flat .grad views;
-    equals autograd's F.linear over two backward passes; post-accumulate hooks fire."""
+@pytest.mark.parametrize("seq", [96, 2048])
+def test_linear_direct_grad_accumulation(bias, seq):
+    """T.linear accumulates dW (GEMM beta=1, or 4-way split-K batched GEMM at >= 8k tokens) and db
+    (fused column sum) into flat .grad views; equals autograd's F.linear over two backward
+    passes; post-accumulate hooks fire."""
     _C()
     torch.manual_seed(0)
-    x = torch.randn(4, 96, 256, device="cuda").bfloat16()
-    g = torch.randn(4, 96, 512, device="cuda").bfloat16()
+    from determined_clone_amd.ops import transformer as tr
+
+    assert tr._wgrad_splits(4 * seq, 512, 256) == (4 if seq == 2048 else 1)
+    x = torch.randn(4, seq, 256, device="cuda").bfloat16()
+    g = torch.randn(4, seq, 512, device="cuda").bfloat16()
     w1 = torch.nn.Parameter(torch.randn(512, 256, device="cuda").bfloat16() * 0.05)
     b1 = torch.nn.Parameter(torch.randn(512, device="cuda").bfloat16()) if bias else None
     w2 = torch.nn.Parameter(w1.detach().clone())

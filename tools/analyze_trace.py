@@ -31,7 +31,8 @@ def category(name: str) -> str:
     return "other"
 
 
-def main(path: str, steps: int = 3, step_marker: str = "sgd_kernel", per_step: int = 2) -> None:
+def main(path: str, steps: int = 3, step_marker: str = "sgd_kernel", per_step: int = 2,
+         neighbors: str = "") -> None:
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if step_marker in r["Kernel_Name"]]
@@ -61,8 +62,21 @@ def main(path: str, steps: int = 3, step_marker: str = "sgd_kernel", per_step: i
     print("\ntop kernels (ms/step, calls/step):")
     for n, (v, c) in sorted(by_name.items(), key=lambda x: -x[1][0])[:25]:
         print(f"  {v / steps:8.3f} {c / steps:5.0f}  {n}")
+    if neighbors:
+        # which kernels surround the launches matching `neighbors` (who issues them)
+        ctx = defaultdict(int)
+        for i, r in enumerate(seg):
+            if neighbors in r["Kernel_Name"]:
+                prev = seg[i - 1]["Kernel_Name"][:60] if i else "-"
+                nxt = seg[i + 1]["Kernel_Name"][:60] if i + 1 < len(seg) else "-"
+                ctx[(prev, nxt)] += 1
+        print(f"\nneighbours of '{neighbors}' (count/step: previous | next):")
+        for (p, n), c in sorted(ctx.items(), key=lambda x: -x[1])[:12]:
+            print(f"  {c / steps:5.1f}  {p} | {n}")
 
 
 if __name__ == "__main__":
     main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 3,
-         per_step=int(sys.argv[3]) if len(sys.argv) > 3 else 2)
+         per_step=int(sys.argv[3]) if len(sys.argv) > 3 else 2,
+         step_marker=sys.argv[4] if len(sys.argv) > 4 else "sgd_kernel",
+         neighbors=sys.argv[5] if len(sys.argv) > 5 else "")
