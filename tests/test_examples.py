@@ -74,7 +74,7 @@ def _import_example(name, mod):
     import sys
 
     path = os.path.join(EX, name, mod + ".py")
-    spec = importlib.util.spec_from_file_location(f"ex_{name}_{mod}", path)
+    spec = importlib.util.spec_from_file_location("ex_" + name.replace(os.sep, "_") + "_" + mod, path)
     m = importlib.util.module_from_spec(spec)
     sys.modules[spec.name] = m
     spec.loader.exec_module(m)
@@ -131,3 +131,163 @@ def test_gpt2_pipeline_example_on_cluster(cluster):
         raise AssertionError("\n".join(l["log"] for l in logs[-60:]))
     val = s.get(f"/api/v1/trials/{t['id']}/metrics", params={"group": "validation"})["metrics"]
     assert val[-1]["steps_completed"] == 4 and val[-1]["metrics"]["lm_loss"] > 0
+
+
+# ---------------------------------------------------------------- tutorials/core_api_pytorch_mnist
+def test_core_api_pytorch_mnist_tutorial_on_cluster(cluster):
+    """Plain PyTorch loop on the Core API: metrics, per-epoch checkpoints, searcher ops."""
+    s = cluster
+    d = os.path.join(EX, "tutorials", "core_api_pytorch_mnist")
+    cfg = yaml.safe_load(open(os.path.join(d, "const.yaml")))
+    cfg["hyperparameters"]["synthetic_size"] = 1200
+    eid, st = _run(s, d, cfg)
+    t = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]
+    if st != "COMPLETED":
+        logs = s.get(f"/api/v1/trials/{t['id']}/logs")["logs"]
+        raise AssertionError("\n".join(l["log"] for l in logs[-40:]))
+    val = s.get(f"/api/v1/trials/{t['id']}/metrics", params={"group": "validation"})["metrics"]
+    assert len(val) == 2 and val[-1]["metrics"]["accuracy"] > 0.5
+    ckpts = s.get(f"/api/v1/trials/{t['id']}/checkpoints")["checkpoints"]
+    assert len(ckpts) == 2
+
+
+def test_core_api_pytorch_mnist_distributed_on_cluster(cluster):
+    """Same script under the torch_distributed launcher on 2 slots (gloo on CPU)."""
+    s = cluster
+    d = os.path.join(EX, "tutorials", "core_api_pytorch_mnist")
+    cfg = yaml.safe_load(open(os.path.join(d, "distributed.yaml")))
+    cfg["hyperparameters"]["synthetic_size"] = 1200
+    cfg["searcher"]["max_length"] = 1
+    eid, st = _run(s, d, cfg)
+    t = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]
+    if st != "COMPLETED":
+        logs = s.get(f"/api/v1/trials/{t['id']}/logs")["logs"]
+        raise AssertionError("\n".join(l["log"] for l in logs[-40:]))
+    val = s.get(f"/api/v1/trials/{t['id']}/metrics", params={"group": "validation"})["metrics"]
+    assert val[-1]["metrics"]["accuracy"] > 0.5
+
+
+# ---------------------------------------------------------------- features/unmanaged
+@pytest.fixture(scope="module")
+def master_client():
+    from determined_clone_amd.experimental import client as sdk
+    from determined_clone_amd.master import Master, MasterServer
+
+    tmp = tempfile.mkdtemp(prefix="det-unmanaged-")
+    m = Master(os.path.join(tmp, "m.db"),
+               checkpoint_storage={"type": "shared_fs", "host_path": os.path.join(tmp, "ckpt")})
+    srv = MasterServer(m, "127.0.0.1", 0).start()
+    yield m, sdk.Determined(m.master_url, "admin", "")
+    srv.stop()
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_unmanaged_singleton_example(master_client):
+    m, d = master_client
+    ex = _import_example(os.path.join("features", "unmanaged"), "1_singleton")
+    tid = ex.main(steps=20, client=d)
+    rows = m.db.all("SELECT grp FROM metrics WHERE trial_id=?", [tid])
+    assert sum(r["grp"] == "training" for r in rows) == 20
+    assert sum(r["grp"] == "validation" for r in rows) == 2
+
+
+def test_unmanaged_checkpoints_example_resumes(master_client):
+    m, d = master_client
+    ex = _import_example(os.path.join("features", "unmanaged"), "2_checkpoints")
+    tid1, start1 = ex.main(steps=20, client=d, external_id="ex-unmanaged-2")
+    tid2, start2 = ex.main(steps=20, client=d, external_id="ex-unmanaged-2")
+    assert tid1 == tid2 and start1 == 0 and start2 == 20  # resumed after checkpoint at step 19
+    n = m.db.one("SELECT COUNT(*) AS n FROM checkpoints WHERE trial_id=?", [tid1])["n"]
+    assert n == 4
+
+
+def _unmanaged_dist_worker(rank, world, port, url, out):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "LOCAL_WORLD_SIZE": str(world), "DET_MASTER": url})
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "ex_unmanaged_3", os.path.join(EX, "features", "unmanaged", "3_torch_distributed.py"))
+    ex = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ex)
+    from determined_clone_amd.experimental import client as sdk
+
+    tid = ex.main(steps=20, client=sdk.Determined(url, "admin", ""))
+    if rank == 0:
+        with open(out, "w") as f:
+            f.write(str(tid))
+
+
+def test_unmanaged_torch_distributed_example(master_client, tmp_path):
+    import socket
+
+    import torch.multiprocessing as mp
+
+    m, _ = master_client
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "tid")
+    mp.spawn(_unmanaged_dist_worker, args=(2, port, m.master_url, out), nprocs=2, join=True)
+    tid = int(open(out).read())
+    rows = m.db.all("SELECT grp FROM metrics WHERE trial_id=?", [tid])
+    assert sum(r["grp"] == "training" for r in rows) == 2
+
+
+# ---------------------------------------------------------------- features/torch_batch_process_*
+def test_embedding_generation_example(tmp_path, monkeypatch):
+    import torch
+
+    monkeypatch.setenv("DET_LOCAL_STORAGE", str(tmp_path))
+    ex = _import_example(os.path.join("features", "torch_batch_process_embeddings"),
+                         "embedding_generation")
+    ex.main(n_docs=40, batch_size=8, checkpoint_interval=2)
+    files = [os.path.join(r, f) for r, _, fs in os.walk(tmp_path) for f in fs
+             if f.startswith("embeddings_")]
+    parts = [torch.load(f, weights_only=True) for f in files]
+    idx = torch.cat([p["index"] for p in parts])
+    assert sorted(idx.tolist()) == list(range(40))
+    assert all(p["embedding"].shape[1] == 128 for p in parts)
+
+
+def test_inference_mnist_example(tmp_path, monkeypatch, caplog):
+    import logging
+
+    from determined_clone_amd import pytorch
+    from determined_clone_amd.common.storage import SharedFSStorageManager
+
+    train = _import_example("mnist_pytorch", "train")
+    hp = {"learning_rate": 1.0, "n_filters1": 8, "n_filters2": 8, "dropout1": 0.25,
+          "dropout2": 0.5}
+    ckdir = tmp_path / "ckpt"
+    monkeypatch.chdir(tmp_path)  # no ./data: synthetic MNIST
+    with pytorch.init(hparams=hp, exp_conf={}) as ctx:
+        ctx._core.checkpoint._storage_manager = SharedFSStorageManager(str(ckdir))
+        t = train.MNistTrial(ctx, hp)
+        pytorch.Trainer(t, ctx).fit(max_length=pytorch.Batch(40))
+    paths = [p for p in ckdir.iterdir() if (p / "state_dict.pth").exists()]
+    assert paths
+    monkeypatch.setenv("MNIST_CHECKPOINT_PATH", str(paths[-1]))
+    monkeypatch.setenv("DET_LOCAL_STORAGE", str(tmp_path / "out"))
+    ex = _import_example(os.path.join("features", "inference_mnist_pytorch"), "inference")
+    with caplog.at_level(logging.INFO):
+        ex.main(n=300, batch_size=50)
+    acc = [r.getMessage() for r in caplog.records if "accuracy" in r.getMessage()]
+    assert acc, "no reduced inference metrics were reported"
+
+
+def test_hf_image_classification_example_on_cluster(cluster):
+    """HF Trainer + DetCallback: eval accuracy and checkpoints reach the master."""
+    s = cluster
+    d = os.path.join(EX, "hf_trainer")
+    cfg = yaml.safe_load(open(os.path.join(d, "image_classification.yaml")))
+    cfg["searcher"]["max_length"] = {"batches": 40}
+    eid, st = _run(s, d, cfg)
+    t = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]
+    if st != "COMPLETED":
+        logs = s.get(f"/api/v1/trials/{t['id']}/logs")["logs"]
+        raise AssertionError("\n".join(l["log"] for l in logs[-40:]))
+    val = s.get(f"/api/v1/trials/{t['id']}/metrics", params={"group": "validation"})["metrics"]
+    assert val[-1]["metrics"]["eval_accuracy"] > 0.3  # 10 separable classes, chance is 0.1
