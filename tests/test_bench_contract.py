@@ -1,0 +1,35 @@
+"""bench.py driver contract on CPU: 2 ranks under torch.distributed.run (gloo), rank 0 prints ONE
+JSON line whose value is the whole-job aggregate of the max-over-ranks step time."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_prints_one_aggregate_json_line():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "2"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in r
+    assert r["n_gpus"] == 2 and r["steps"] == 2 and r["warmup"] == 1
+    assert r["scaling"] == "weak" and r["higher_is_better"] is True
+    assert r["config"]["model"] == "resnet50" and r["config"]["global_batch"] == 4
+    assert r["config"]["parallelism"] == "dp2"
+    # whole-job images/s from the slowest rank's step time
+    assert abs(r["value"] - 4 / (r["ms_per_step"] / 1000.0)) / r["value"] < 0.01
