@@ -101,8 +101,6 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
-    ap.add_argument("--hip-graph", type=int, default=0,
-                    help="optimizations.hip_graph (refused for MIOpen convolutions: runs eager)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
@@ -110,8 +108,9 @@ def main() -> None:
     if torch.cuda.is_available():
         torch.backends.cudnn.benchmark = True
     hparams = {"global_batch_size": args.batch * world, "warmup": args.warmup, "steps": args.steps}
-    exp_conf = {"optimizations": {"aggregation_frequency": 1, "average_training_metrics": True,
-                                  "hip_graph": bool(args.hip_graph)}}
+    # the timed step runs eagerly: optimizations.hip_graph is refused for MIOpen convolutions
+    # (pytorch/_graph.py), and train_batch's timestamps must run on every step
+    exp_conf = {"optimizations": {"aggregation_frequency": 1, "average_training_metrics": True}}
     with pytorch.init(hparams=hparams, exp_conf=exp_conf) as ctx:
         trial = ResNet50BenchTrial(ctx)
         trainer = pytorch.Trainer(trial, ctx)

@@ -480,19 +480,46 @@ class Master:
         except Exception:
             return None
 
-    def delete_checkpoints(self, uuids: List[str], exp: Optional[Experiment] = None) -> None:
+    def delete_checkpoints(self, uuids: List[str], exp: Optional[Experiment] = None,
+                           globs: Optional[List[str]] = None) -> None:
+        """Delete checkpoint files. ``globs`` None / ``["**/*"]`` removes the whole checkpoint
+        (state DELETED); otherwise only the matching files go and the stored resources (and size)
+        are updated to what is left (state PARTIALLY_DELETED) -- as the reference's checkpoint GC
+        task does (`master/internal/api_checkpoint.go` CheckpointsRemoveFiles)."""
+        full = not globs or list(globs) == ["**/*"]
         for u in uuids:
             row = self.db.one("SELECT * FROM checkpoints WHERE uuid=?", [u])
             if row is None:
                 continue
             e = exp or (self.experiments.get(row["experiment_id"]) if row.get("experiment_id") else None)
             sm = self._storage_for(e) if e else None
+            left: Optional[Dict[str, int]] = None
             if sm is not None:
                 try:
-                    sm.delete(u)
+                    left = sm.delete(u, None if full else list(globs))
                 except Exception:
                     logger.exception(f"failed deleting checkpoint {u}")
-            self.db.update("checkpoints", "uuid", u, {"state": "DELETED"})
+            if full:
+                self.db.update("checkpoints", "uuid", u, {"state": "DELETED"})
+                continue
+            if left is None:  # storage could not list what is left: drop matching resource keys
+                import fnmatch
+
+                res = dec(row.get("resources"), {}) or {}
+                left = {k: v for k, v in res.items()
+                        if not any(fnmatch.fnmatch(k, g) for g in globs)}
+            size = sum(int(v) for v in left.values() if isinstance(v, (int, float)))
+            self.db.update("checkpoints", "uuid", u, {
+                "resources": left, "size": size,
+                "state": "PARTIALLY_DELETED" if left else "DELETED"})
+
+    def registered_checkpoints(self, uuids: List[str]) -> List[str]:
+        """Checkpoints referenced by a model version (the model registry keeps them alive)."""
+        out = []
+        for u in uuids:
+            if self.db.one("SELECT id FROM model_versions WHERE checkpoint_uuid=?", [u]):
+                out.append(u)
+        return out
 
     def _gc_candidates(self, exp: Experiment, trial: Optional[Trial]) -> List[str]:
         cs = exp.config.get("checkpoint_storage") or {}

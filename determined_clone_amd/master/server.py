@@ -825,18 +825,45 @@ def get_checkpoint(r: Req) -> Any:
     return {"checkpoint": c}
 
 
+def _checkpoint_edit_check(r: Req, uuids: List[str]) -> None:
+    """The caller must be allowed to edit every owning experiment (the reference's
+    checkpointsRBACEditCheck, `master/internal/api_checkpoint.go`)."""
+    for u in uuids:
+        row = r.m.db.one("SELECT experiment_id FROM checkpoints WHERE uuid=?", [u])
+        if row is None:
+            raise HTTPError(404, f"checkpoint {u} not found")
+        eid = row.get("experiment_id")
+        if eid is None:
+            require(r, "UPDATE_EXPERIMENT")
+            continue
+        erow = r.m.db.one("SELECT project_id FROM experiments WHERE id=?", [eid])
+        require(r, "UPDATE_EXPERIMENT", _project_workspace(r.m, erow["project_id"] if erow else None))
+
+
+def _remove_checkpoint_files(r: Req, uuids: List[str], globs: List[str]) -> None:
+    for g in globs:
+        if not isinstance(g, str) or not g:
+            raise HTTPError(400, "cannot have empty string glob")
+        if ".." in g:
+            raise HTTPError(400, f"glob '{g}' cannot contain '..'")
+    _checkpoint_edit_check(r, uuids)
+    registered = r.m.registered_checkpoints(uuids)
+    if registered:
+        raise HTTPError(400, "this subset of checkpoints provided are in the model registry and "
+                             f"cannot be deleted: {registered}")
+    r.m.delete_checkpoints(uuids, globs=globs)
+
+
 @route("POST", "/api/v1/checkpoints/rm")
 def rm_checkpoint_files(r: Req) -> Any:
-    uuids = r.body.get("checkpoint_uuids", [])
-    globs = r.body.get("globs") or ["**/*"]
-    if globs == ["**/*"]:
-        r.m.delete_checkpoints(uuids)
+    _remove_checkpoint_files(r, list(r.body.get("checkpoint_uuids", [])),
+                             list(r.body.get("checkpoint_globs") or r.body.get("globs") or ["**/*"]))
     return {}
 
 
 @route("DELETE", "/api/v1/checkpoints")
 def delete_checkpoints(r: Req) -> Any:
-    r.m.delete_checkpoints(r.body.get("checkpoint_uuids", []))
+    _remove_checkpoint_files(r, list(r.body.get("checkpoint_uuids", [])), ["**/*"])
     return {}
 
 
@@ -845,6 +872,7 @@ def patch_checkpoint_md(r: Req) -> Any:
     row = r.m.db.one("SELECT metadata FROM checkpoints WHERE uuid=?", [r.p["uuid"]])
     if row is None:
         raise HTTPError(404, "checkpoint not found")
+    _checkpoint_edit_check(r, [r.p["uuid"]])
     md = dec(row["metadata"], {})
     md.update(r.body.get("metadata", {}))
     r.m.db.update("checkpoints", "uuid", r.p["uuid"], {"metadata": md})

@@ -297,6 +297,40 @@ class Zero3Partitioner:
             u.shard.data.copy_(u.full[s0:s0 + u.shard_numel])
             u.release()
 
+    def optimizer_param_units(self, num_groups: int) -> List[_Unit]:
+        """Units in the optimizer's flattened parameter order (group by group, as
+        :meth:`shard_param_groups` lays them out): state index i belongs to unit i of this list."""
+        out: List[_Unit] = []
+        for g in range(num_groups):
+            out.extend(u for u in self.units if u.group_idx == g)
+        return out
+
+    def reshard_optimizer_state(self, saved: List[Dict[str, Any]], num_groups: int) -> Dict[str, Any]:
+        """Build THIS rank's optimizer state dict from the per-rank shard state dicts written at
+        another data-parallel size. A unit's flat layout depends on the world size only through
+        the tail padding, so the old shards are concatenated, cut to the unit's true numel,
+        re-padded for the current world size and sliced at this rank's offset."""
+        units = self.optimizer_param_units(num_groups)
+        old = [{int(k): v for k, v in sd["state"].items()} for sd in saved]
+        state: Dict[int, Dict[str, Any]] = {}
+        for i, u in enumerate(units):
+            parts = [o.get(i) for o in old]
+            if any(p is None for p in parts):
+                continue
+            total = sum(u.numels)
+            s0 = u.rank * u.shard_numel
+            new: Dict[str, Any] = {}
+            for key, v0 in parts[0].items():
+                if torch.is_tensor(v0) and v0.dim() == 1:
+                    flat = torch.cat([p[key].reshape(-1) for p in parts])[:total]
+                    full = torch.zeros(u.padded, dtype=v0.dtype)
+                    full[:total].copy_(flat)
+                    new[key] = full[s0:s0 + u.shard_numel].clone()
+                else:
+                    new[key] = v0
+            state[i] = new
+        return {"state": state, "param_groups": saved[0]["param_groups"]}
+
     def remove_hooks(self) -> None:
         for h in self._handles:
             h.remove()

@@ -113,6 +113,8 @@ class PyTorchTrialContext(_PyTorchReducerContext):
         self.lr_schedulers: List[LRScheduler] = []
         self._scaler: Any = None
         self._syncs: Dict[int, ddp.GradientSync] = {}  # id(optimizer) -> gradient sync
+        # id(user optimizer) -> the fused optimizer wrap_optimizer replaced it with
+        self._optimizer_alias: Dict[int, torch.optim.Optimizer] = {}
         self._spaces: Dict[int, FlatParamSpace] = {}
         self._loose_params: Dict[int, List[torch.Tensor]] = {}
         self._current_batch_idx: Optional[int] = None
@@ -250,6 +252,13 @@ class PyTorchTrialContext(_PyTorchReducerContext):
             f = fused_optim.fuse_optimizer(optimizer)
             if f is not None:
                 out = f
+        if out is not optimizer:
+            # the reference hands back the user's own optimizer object; code that keeps using the
+            # original (step_optimizer(orig), LR schedulers built on it) must drive the fused
+            # replacement: alias it for step_optimizer and share the param-group dicts so
+            # hyper-parameter changes made through either object reach the one that trains
+            self._optimizer_alias[id(optimizer)] = out
+            optimizer.param_groups = out.param_groups
         if isinstance(out, fused_optim.FusedOptimizerBase):
             space = out.space
         else:
@@ -337,6 +346,12 @@ class PyTorchTrialContext(_PyTorchReducerContext):
                 "if optimizations.aggregation_frequency is larger than 1, auto_zero_grads must be true")
         if not self._should_communicate_and_update():
             return
+        optimizer = self._optimizer_alias.get(id(optimizer), optimizer)
+        if self.distributed.size > 1 and all(optimizer is not o for o in self.optimizers):
+            # an unregistered optimizer would step on un-all-reduced gradients: ranks diverge
+            raise errors.InvalidExperimentException(
+                "step_optimizer() got an optimizer that was not passed through wrap_optimizer(); "
+                "its gradients would not be synchronised across slots")
         sync = self._syncs.get(id(optimizer))
         if sync is not None:
             sync.finish()

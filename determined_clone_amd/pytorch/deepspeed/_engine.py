@@ -314,6 +314,11 @@ class DeepSpeedEngine(torch.nn.Module):
         if stage == 3:
             from determined_clone_amd.parallel import zero3
 
+            if kind == "lamb":
+                # a ZeRO-3 shard is a flat 1/W slice spanning several parameters: LAMB's per-tensor
+                # trust ratio ||w|| / ||update|| over such a slice is wrong and world-size dependent
+                raise ValueError("ZeRO stage 3 is implemented for Adam/AdamW/SGD, not LAMB "
+                                 "(LAMB's per-tensor trust ratio needs whole tensors; use stage 0)")
             self._z3 = zero3.Zero3Partitioner(self.module, [list(g["params"]) for g in groups],
                                               group=self.group)
             shards = self._z3.shard_param_groups(len(groups))
@@ -522,9 +527,20 @@ class DeepSpeedEngine(torch.nn.Module):
                     if not any("master_param" in s for s in osd["state"].values()):
                         self.optimizer.sync_master_from_model()
                 else:
-                    logger.warning("ZeRO-3 checkpoint from another data-parallel size: weights "
-                                   "loaded, optimizer state reset")
-                    self.optimizer.sync_master_from_model()
+                    # written at another data-parallel size: re-partition every rank's shards
+                    saved_world = int(state.get("dp_world_size", -1))
+                    files = [d / f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt"
+                             for r in range(max(saved_world, 0))]
+                    if saved_world < 1 or not all(f.exists() for f in files):
+                        raise FileNotFoundError(
+                            f"ZeRO-3 optimizer shards for dp_world_size={saved_world} are missing "
+                            f"under {d}; pass load_optimizer_states=False to load weights only")
+                    saved = [torch.load(f, map_location="cpu", weights_only=True)["optimizer_state_dict"]
+                             for f in files]
+                    osd = self._z3.reshard_optimizer_state(saved, len(self.optimizer.param_groups))
+                    self.optimizer.load_state_dict(osd)
+                    if not any("master_param" in s for s in osd["state"].values()):
+                        self.optimizer.sync_master_from_model()
             elif isinstance(self.optimizer, zero.ZeroShardMixin):
                 saved_world = int(state.get("dp_world_size", self.world_size))
                 own = d / f"zero_pp_rank_{self.global_rank}_mp_rank_00_optim_states.pt"

@@ -33,7 +33,8 @@ def _data(n=8):
     return torch.randn(n, 16, generator=g), torch.randn(n, 4, generator=g)
 
 
-def _worker_sync(rank: int, world: int, port: int, fused: bool, agg: int, out_dir: str) -> None:
+def _worker_sync(rank: int, world: int, port: int, fused: bool, agg: int, out_dir: str,
+                 keep_original: bool = False) -> None:
     _init(rank, world, port)
     from determined_clone_amd import core, pytorch
 
@@ -41,7 +42,15 @@ def _worker_sync(rank: int, world: int, port: int, fused: bool, agg: int, out_di
     with pytorch.init(hparams={}, distributed=dist_ctx, aggregation_frequency=agg,
                       exp_conf={"optimizations": {}}) as ctx:
         model = ctx.wrap_model(_model())
-        opt = ctx.wrap_optimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), fused=fused)
+        orig = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9)
+        sched = None
+        if keep_original:
+            # user code that ignores wrap_optimizer's return value and schedules the original
+            ctx.wrap_optimizer(orig, fused=fused)
+            opt = orig
+            sched = torch.optim.lr_scheduler.StepLR(orig, step_size=1, gamma=0.5)
+        else:
+            opt = ctx.wrap_optimizer(orig, fused=fused)
         x, y = _data(8 * agg)
         for step in range(3):
             for micro in range(agg):
@@ -51,14 +60,17 @@ def _worker_sync(rank: int, world: int, port: int, fused: bool, agg: int, out_di
                 loss = torch.nn.functional.mse_loss(model(xb), yb)
                 ctx.backward(loss)
                 ctx.step_optimizer(opt)
+            if sched is not None:
+                sched.step()
         torch.save({k: v.detach().clone() for k, v in model.state_dict().items()},
                    os.path.join(out_dir, f"r{rank}.pt"))
     torch.distributed.destroy_process_group()
 
 
-def _reference(agg: int):
+def _reference(agg: int, scheduled: bool = False):
     model = _model()
     opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9)
+    sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5) if scheduled else None
     x, y = _data(8 * agg)
     for step in range(3):
         opt.zero_grad()
@@ -66,6 +78,8 @@ def _reference(agg: int):
             xb, yb = x[micro * 8:(micro + 1) * 8], y[micro * 8:(micro + 1) * 8]
             (torch.nn.functional.mse_loss(model(xb), yb) / agg).backward()
         opt.step()
+        if sched is not None:
+            sched.step()
     return model.state_dict()
 
 
@@ -81,6 +95,40 @@ def test_data_parallel_matches_single_process(fused, agg):
         for k in ref:
             torch.testing.assert_close(r0[k], r1[k], atol=0, rtol=0)
             torch.testing.assert_close(r0[k], ref[k], atol=1e-5, rtol=1e-5)
+
+
+def test_data_parallel_original_optimizer_object_drives_fused_replacement():
+    # wrap_optimizer swaps torch SGD for the fused flat-buffer SGD; stepping (and LR-scheduling)
+    # the ORIGINAL object must still all-reduce gradients and train the replacement
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker_sync, args=(world, _free_port(), True, 1, d, True),
+                           nprocs=world, start_method="spawn")
+        ref = _reference(1, scheduled=True)
+        r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)
+        for k in ref:
+            torch.testing.assert_close(r0[k], r1[k], atol=0, rtol=0)
+            torch.testing.assert_close(r0[k], ref[k], atol=1e-5, rtol=1e-5)
+
+
+def test_step_optimizer_refuses_unwrapped_optimizer_when_distributed():
+    from determined_clone_amd import errors
+    from determined_clone_amd.pytorch._context import PyTorchTrialContext
+
+    ctx = PyTorchTrialContext.__new__(PyTorchTrialContext)
+    ctx._aggregation_frequency = 1
+    ctx._managed_training = False
+    ctx._optimizer_alias = {}
+    ctx.optimizers = []
+
+    class _D:
+        size = 2
+
+    ctx.distributed = _D()
+    opt = torch.optim.SGD(_model().parameters(), lr=0.1)
+    with pytest.raises(errors.InvalidExperimentException, match="wrap_optimizer"):
+        ctx.step_optimizer(opt)
 
 
 def _worker_core(rank: int, world: int, port: int, out_dir: str) -> None:

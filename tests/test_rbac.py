@@ -152,3 +152,53 @@ def test_cli_user_groups_and_rbac(cluster, tmp_path, monkeypatch, capsys):
     assert cli.main(base + ["user-group", "list"]) == 0
     assert "ml2" in capsys.readouterr().out
     assert cli.main(base + ["user-group", "delete", "ml2"]) == 0
+
+
+def test_checkpoint_delete_needs_experiment_edit_permission(cluster):
+    # reference: master/internal/api_checkpoint.go CheckpointsRemoveFiles -- edit permission on the
+    # owning experiment, no model-registry checkpoints, no empty / '..' globs, partial globs update
+    # the stored resources
+    m, tmp = cluster
+    admin = _login(m, "admin")
+    admin.post("/api/v1/users", {"user": {"username": "carol"}, "password": "pw"})
+    uid = {u["username"]: u["id"] for u in admin.get("/api/v1/users")["users"]}
+    ws = admin.post("/api/v1/workspaces", {"name": "team-ck"})["workspace"]
+    proj = admin.post(f"/api/v1/workspaces/{ws['id']}/projects", {"name": "pck"})["project"]
+    eid = admin.post("/api/v1/experiments", {"config": _exp_cfg("ck"), "project_id": proj["id"],
+                                             "activate": False})["experiment"]["id"]
+    ckdir = os.path.join(tmp, "ckpt")
+    uuids = []
+    for i in range(2):
+        u = f"00000000-0000-0000-0000-00000000000{i}"
+        os.makedirs(os.path.join(ckdir, u, "sub"), exist_ok=True)
+        for f in ("state_dict.pth", "sub/extra.bin"):
+            with open(os.path.join(ckdir, u, f), "w") as fh:
+                fh.write("x" * 10)
+        m.db.upsert("checkpoints", {"uuid": u, "experiment_id": eid, "state": "COMPLETED",
+                                    "resources": {"state_dict.pth": 10, "sub/extra.bin": 10}, "size": 20})
+        uuids.append(u)
+    carol = _login(m, "carol", "pw")
+    viewer = rbac.role_by_name("Viewer").id
+    admin.post("/api/v1/roles/add-assignments", {"userRoleAssignments": [
+        {"userId": uid["carol"], "roleAssignment": {"role": {"roleId": viewer}, "scopeWorkspaceId": ws["id"]}}]})
+    with pytest.raises(APIException, match="403|permission"):
+        carol.post("/api/v1/checkpoints/rm", {"checkpoint_uuids": uuids[:1], "checkpoint_globs": ["**/*"]})
+    with pytest.raises(APIException, match="403|permission"):
+        carol.patch(f"/api/v1/checkpoints/{uuids[0]}/metadata", {"metadata": {"k": 1}})
+    assert os.path.exists(os.path.join(ckdir, uuids[0], "state_dict.pth"))
+    for bad in ([""], ["../x"]):
+        with pytest.raises(APIException, match="400|glob"):
+            admin.post("/api/v1/checkpoints/rm", {"checkpoint_uuids": uuids[:1], "checkpoint_globs": bad})
+    # partial delete: only sub/ goes, resources and state follow
+    admin.post("/api/v1/checkpoints/rm", {"checkpoint_uuids": uuids[:1], "checkpoint_globs": ["sub"]})
+    ck = admin.get(f"/api/v1/checkpoints/{uuids[0]}")["checkpoint"]
+    assert ck["state"] == "PARTIALLY_DELETED" and set(ck["resources"]) == {"state_dict.pth"}
+    assert not os.path.exists(os.path.join(ckdir, uuids[0], "sub"))
+    # a checkpoint registered as a model version cannot be deleted
+    admin.post("/api/v1/models", {"name": "ck-model", "workspace_id": ws["id"]})
+    admin.post("/api/v1/models/ck-model/versions", {"checkpoint_uuid": uuids[1]})
+    with pytest.raises(APIException, match="400|registry"):
+        admin.delete("/api/v1/checkpoints", body={"checkpoint_uuids": uuids[1:]})
+    admin.delete("/api/v1/checkpoints", body={"checkpoint_uuids": uuids[:1]})
+    assert admin.get(f"/api/v1/checkpoints/{uuids[0]}")["checkpoint"]["state"] == "DELETED"
+    assert not os.path.exists(os.path.join(ckdir, uuids[0]))

@@ -107,8 +107,10 @@ def _worker(rank: int, world: int, port: int, out: str) -> None:
     more = _train(eng, steps=1, rank=rank, world=world)
     more2 = _train(eng2, steps=1, rank=rank, world=world)
     assert more2 == more
+    sd_more = eng2.module_state_dict()
     if rank == 0:
-        torch.save({"sd": sd, "losses": losses}, os.path.join(out, "final.pt"))
+        torch.save({"sd": sd, "losses": losses, "sd_more": sd_more, "more": more},
+                   os.path.join(out, "final.pt"))
     torch.distributed.destroy_process_group()
 
 
@@ -119,6 +121,13 @@ def test_stage3_two_ranks_matches_single_process(tmp_path):
     _train(ref)
     for k, v in ref.module_state_dict().items():
         torch.testing.assert_close(res["sd"][k], v, rtol=1e-4, atol=2e-5, msg=k)
+    # resume the 2-rank checkpoint on ONE rank: the optimizer shards are re-partitioned (not
+    # reset), so the next step equals the 2-rank resumed run's next step
+    eng1 = _engine(3, micro=4)
+    eng1.load_checkpoint(tmp_path, tag="t")
+    _train(eng1, steps=1)  # full batch on one rank == the two half batches
+    for k, v in res["sd_more"].items():
+        torch.testing.assert_close(eng1.module_state_dict()[k], v, rtol=1e-4, atol=2e-5, msg=k)
     # consolidated checkpoint weights load into an unpartitioned engine
     eng0 = _engine(0)
     eng0.load_checkpoint(tmp_path, tag="t", load_optimizer_states=False)
@@ -181,3 +190,14 @@ def test_stage3_deepspeed_trial_checkpoint_resume(tmp_path):
     want = straight.module_state_dict()
     for k, v in resumed.module_state_dict().items():
         torch.testing.assert_close(v, want[k], msg=k)
+
+
+def test_stage3_refuses_lamb():
+    # a ZeRO-3 shard spans several parameters: LAMB's per-tensor trust ratio would be computed over
+    # unrelated slices and change with world size, so stage 3 refuses it (as stages 1/2 do)
+    torch.manual_seed(0)
+    model = gpt2.gpt2("tiny", n_layer=1)
+    cfg = dict(CFG, optimizer={"type": "Lamb", "params": {"lr": 1e-3}},
+               zero_optimization={"stage": 3})
+    with pytest.raises(ValueError, match="LAMB"):
+        det_ds.initialize(model=model, model_parameters=model.parameters(), config=cfg)
