@@ -66,16 +66,131 @@ def supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     return w.stride(0) == conv.in_channels and w.stride(1) == 1
 
 
+# ----------------------------------------------------------------------------- library chooser
+# Measured per direction on MI355X (tools/bench_conv_ops.py, profiles/s2_conv_ops_miopen_vs_gemm.txt):
+# for a 1x1 convolution in NHWC the backward-data product dX[rows, Cin] = dY[rows, Cout] @ W is a
+# plain GEMM, and hipBLASLt runs it 1.3-1.8x faster than MIOpen's implicit-GEMM solvers on most
+# ResNet-50 shapes (MIOpen also zero-fills its output first); MIOpen stays ahead on the
+# 64-channel layer1 shapes, on most forwards and on every weight gradient (a GEMM reducing over
+# 10^5-10^6 rows, where hipBLASLt has no split-K tile). Which one runs is decided per shape and
+# direction by timing both once, on the first training call (like cudnn.benchmark), and cached.
+_CHOICE = {}
+AUTOTUNE = os.environ.get("DCA_CONV_AUTOTUNE", "1") != "0"
+
+
+def _time_us(fn, reps: int = 5) -> float:
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e3 / reps
+
+
+def _choose(key, candidates) -> int:
+    """Index of the fastest candidate for ``key`` (timed once per process, then cached)."""
+    got = _CHOICE.get(key)
+    if got is not None:
+        return got
+    if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
+        return 0
+    times = [_time_us(fn) for fn in candidates]
+    best = min(range(len(times)), key=times.__getitem__)
+    _CHOICE[key] = best
+    return best
+
+
+def _rows(x: torch.Tensor, stride: int) -> torch.Tensor:
+    """[N*Ho*Wo, C] matrix of an NHWC tensor (strided spatial subsample copied for stride > 1)."""
+    v = x.permute(0, 2, 3, 1)
+    if stride > 1:
+        v = v[:, ::stride, ::stride, :]
+    return v.reshape(-1, x.shape[1])
+
+
+def _from_rows(m: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    return m.view(n, h, w, m.shape[1]).permute(0, 3, 1, 2)  # channels_last NCHW view
+
+
+class _PointwiseLib(torch.autograd.Function):
+    """1x1 / no-padding convolution with per-direction library choice (MIOpen or hipBLASLt)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride):
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
+        W = weight.view(cout, cin)
+        key = ("fwd", tuple(x.shape), cout, stride, x.dtype)
+
+        def lib():
+            return F.conv2d(x, weight, stride=stride)
+
+        def gemm():
+            return _from_rows(torch.mm(_rows(x, stride), W.t()), n, ho, wo)
+
+        y = (lib, gemm)[_choose(key, (lib, gemm))]()
+        ctx.save_for_backward(x, weight)
+        ctx.stride = stride
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        st = ctx.stride
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        args = (dy, x, weight, None, [st, st], [0, 0], [1, 1], False, [0, 0], 1)
+        bwd = torch.ops.aten.convolution_backward
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            def lib():
+                return bwd(*args, [True, False, False])[0]
+
+            if st == 1:
+                W = weight.view(cout, cin)
+
+                def gemm():
+                    return _from_rows(torch.mm(_rows(dy, 1), W), n, h, w)
+
+                cands = (lib, gemm)
+                dx = cands[_choose(("dgrad", tuple(x.shape), cout, st, x.dtype), cands)]()
+            else:
+                dx = lib()
+        if ctx.needs_input_grad[1]:
+            dw = bwd(*args, [False, True, False])[1]
+        return dx, dw, None
+
+
+def _lib_supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    if not (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16)):
+        return False
+    if conv.kernel_size != (1, 1) or conv.padding != (0, 0) or conv.stride[0] != conv.stride[1]:
+        return False
+    if conv.groups != 1 or conv.dilation != (1, 1) or conv.bias is not None:
+        return False
+    w = conv.weight
+    return w.dtype == x.dtype and w.is_contiguous(memory_format=torch.channels_last)
+
+
 def pointwise_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> torch.Tensor:
-    """``conv(x)`` for a 1x1/stride-1 convolution in NHWC bf16; with ``bn_stats`` the output
-    carries the partial BatchNorm statistics of the forward epilogue (training only)."""
-    if not supported(conv, x):
-        return conv(x)
-    x = x.contiguous(memory_format=torch.channels_last)
-    y, partial = _Conv1x1.apply(x, conv.weight, bool(bn_stats))
-    if partial is not None:
-        y._dca_bn_partials = partial
-    return y
+    """``conv(x)`` for a 1x1 convolution in NHWC. With ``DCA_CONV1X1=1`` (stride 1, bf16) the
+    hand-written MFMA kernels run and, with ``bn_stats``, the output carries the partial BatchNorm
+    statistics of the forward epilogue; otherwise each direction runs on the faster of MIOpen and
+    hipBLASLt for its shape."""
+    if supported(conv, x):
+        x = x.contiguous(memory_format=torch.channels_last)
+        y, partial = _Conv1x1.apply(x, conv.weight, bool(bn_stats))
+        if partial is not None:
+            y._dca_bn_partials = partial
+        return y
+    if _lib_supported(conv, x):
+        x = x.contiguous(memory_format=torch.channels_last)
+        return _PointwiseLib.apply(x, conv.weight, conv.stride[0])
+    return conv(x)
 
 
 def take_bn_partials(x: torch.Tensor) -> Optional[torch.Tensor]:

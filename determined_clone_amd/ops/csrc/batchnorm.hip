@@ -16,8 +16,10 @@
 //   bn_finalize_bwd  : dgamma, dbeta and the affine form dx = k1*dy' + k2*x + k3
 //   bn_apply_bwd     : dx (and d_residual = dy' when the residual add was fused)
 // Every lane moves 8 channels (16 B of bf16) per access; reductions are deterministic.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include "common.h"
 
 namespace dca {
@@ -28,23 +30,102 @@ namespace {
 
 constexpr int kBlock = 256;
 
-// Geometry shared by the reduce kernels. TPR = threads per row (8 channels each), RPI = rows per
-// block iteration, channel groups on grid.y when C/8 > 256.
-struct ReduceGeom {
+// Row-tile geometry shared by every pass over a [M rows][C channels] channels_last tensor:
+// TPR threads cover one row (8 channels = 16 B of bf16 each), RPI = rows per block iteration,
+// channel groups on grid.y when C/8 > 256. Each workgroup owns ONE contiguous run of rows (a
+// multiple of RPI), so its loads stream through a contiguous region, every thread keeps the same
+// 8 channels for the whole kernel (per-channel parameters are loaded once, no per-vector modulo),
+// and U rows per thread are loaded before any of them is used (U x 16 B in flight per lane).
+struct RowGeom {
   int tpr, rpi, cgroups;
 };
-inline ReduceGeom reduce_geom(int C) {
+// At most 32 threads (256 channels, 512 B of bf16) per row: wide tensors are split over grid.y
+// channel groups, which multiplies the workgroups of the reduce passes without growing their
+// [blocks][2][C] partials.
+inline int max_tpr() {
+  // DCA_BN_MAXTPR (8..256, a power of two) overrides the cap (tuning sweeps only).
+  static const int v = [] {
+    const char* e = std::getenv("DCA_BN_MAXTPR");
+    int t = e ? std::atoi(e) : 32;
+    return (t >= 8 && t <= kBlock && (t & (t - 1)) == 0) ? t : 32;
+  }();
+  return v;
+}
+inline RowGeom row_geom(int C) {
   int c8 = C / 8;
-  ReduceGeom g;
-  g.tpr = c8 < kBlock ? c8 : kBlock;
-  // tpr must divide 256 for the row mapping; fall back to the largest power of two <= c8.
+  RowGeom g;
+  const int cap = max_tpr();
+  g.tpr = c8 < cap ? c8 : cap;
+  // tpr must divide 256 for the row mapping; fall back to the largest divisor <= c8.
   while (kBlock % g.tpr != 0) --g.tpr;
   g.rpi = kBlock / g.tpr;
   g.cgroups = (c8 + g.tpr - 1) / g.tpr;
   return g;
 }
+using ReduceGeom = RowGeom;
+inline ReduceGeom reduce_geom(int C) { return row_geom(C); }
 
-template <typename T, bool BWD>
+struct RowRange {
+  int64_t begin, end;
+};
+// Rows of chunk `bx` out of `nb` equal contiguous chunks (each a multiple of rpi).
+__device__ __forceinline__ RowRange chunk_rows(int64_t M, int rpi, int bx, int nb) {
+  int64_t per = (M + nb - 1) / nb;
+  per = (per + rpi - 1) / rpi * rpi;
+  int64_t b = static_cast<int64_t>(bx) * per;
+  int64_t e = b + per;
+  if (b > M) b = M;
+  if (e > M) e = M;
+  return {b, e};
+}
+
+// Raw 8-element vectors: loads are issued into these (no conversion in between), so the U loads
+// of an unrolled iteration are all in flight before the first use; unpacked afterwards.
+template <typename T> struct Raw8;
+template <> struct Raw8<BF16> { uint4 q; };
+template <> struct Raw8<F16> { uint4 q; };
+template <> struct Raw8<F32> { float4 a, b; };
+
+template <typename T>
+__device__ __forceinline__ Raw8<T> ld8(const void* base, int64_t elem_off) {
+  Raw8<T> r;
+  if constexpr (std::is_same<T, F32>::value) {
+    const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(base) + elem_off);
+    r.a = p[0];
+    r.b = p[1];
+  } else {
+    r.q = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(base) + elem_off);
+  }
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ void unpack8(const Raw8<T>& r, float (&v)[8]) {
+  if constexpr (std::is_same<T, F32>::value) {
+    v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w;
+    v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
+  } else if constexpr (std::is_same<T, BF16>::value) {
+    v[0] = bf16_lo(r.q.x); v[1] = bf16_hi(r.q.x); v[2] = bf16_lo(r.q.y); v[3] = bf16_hi(r.q.y);
+    v[4] = bf16_lo(r.q.z); v[5] = bf16_hi(r.q.z); v[6] = bf16_lo(r.q.w); v[7] = bf16_hi(r.q.w);
+  } else {
+    const uint32_t w[4] = {r.q.x, r.q.y, r.q.z, r.q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = h2f(w[i] & 0xffffu);
+      v[2 * i + 1] = h2f(w[i] >> 16);
+    }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8(void* base, int64_t elem_off, const float (&v)[8]) {
+  Vec8<T>::store(reinterpret_cast<char*>(base) + elem_off * Vec8<T>::bytes, v);
+}
+
+// Statistics pass. FWD: per-chunk (sum x, sum x^2); BWD: (sum dy', sum dy'*(x-mean)) with
+// dy' = (dy [+ dy2]) masked by the forward's ReLU bit. Chunks are visited in DESCENDING order:
+// the tensors' producer (a convolution, or the previous pass) wrote/read them ascending, so the
+// rows it touched last are still in the 256 MB Infinity Cache when the first chunks run here;
+// the apply pass then walks ascending and starts on the rows this pass read last.
+template <typename T, bool BWD, int U>
 __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
     const void* __restrict__ x, const void* __restrict__ dy, const void* __restrict__ dy2,
     const uint8_t* __restrict__ mask, const float* __restrict__ mean, int64_t M, int C, int tpr,
@@ -54,6 +135,8 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
   const int lc = tid % tpr, r0 = tid / tpr;
   const int c = (blockIdx.y * tpr + lc) * 8;
   const bool active = c < C;
+  const int bx = static_cast<int>(gridDim.x) - 1 - static_cast<int>(blockIdx.x);
+  const RowRange rr = chunk_rows(M, rpi, bx, gridDim.x);
   float s[8], q[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
@@ -63,58 +146,58 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
     for (int k = 0; k < 8; ++k) mu[k] = mean[c + k];
   }
   if (active) {
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * rpi;
-    int64_t r = static_cast<int64_t>(blockIdx.x) * rpi + r0;
-    // 4 rows in flight per thread (independent 16-B loads) before any accumulation, so each wave
-    // keeps several HBM requests outstanding instead of one load -> use -> load chain.
-    constexpr int U = BWD ? 2 : 4;
-    for (; r + (U - 1) * stride < M; r += U * stride) {
-      float xv[U][8];
-      float g[U][8];
+    int64_t r = rr.begin + r0;
+    for (; r + (U - 1) * rpi < rr.end; r += U * rpi) {
+      Raw8<T> rx[U], rg[U], rg2[U];
       uint32_t mk[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t off = (r + u * stride) * C + c;
-        Vec8<T>::load(reinterpret_cast<const char*>(x) + off * Vec8<T>::bytes, xv[u]);
+        const int64_t off = (r + u * rpi) * C + c;
+        rx[u] = ld8<T>(x, off);
         if (BWD) {
-          Vec8<T>::load(reinterpret_cast<const char*>(dy) + off * Vec8<T>::bytes, g[u]);
-          if (dy2) {
-            float g2[8];
-            Vec8<T>::load(reinterpret_cast<const char*>(dy2) + off * Vec8<T>::bytes, g2);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) g[u][k] += g2[k];
-          }
+          rg[u] = ld8<T>(dy, off);
+          if (dy2) rg2[u] = ld8<T>(dy2, off);
           mk[u] = relu ? mask[off >> 3] : 0xffu;
         }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        float xv[8];
+        unpack8<T>(rx[u], xv);
         if (!BWD) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) { s[k] += xv[u][k]; q[k] = fmaf(xv[u][k], xv[u][k], q[k]); }
+          for (int k = 0; k < 8; ++k) { s[k] += xv[k]; q[k] = fmaf(xv[k], xv[k], q[k]); }
         } else {
+          float g[8];
+          unpack8<T>(rg[u], g);
+          if (dy2) {
+            float g2[8];
+            unpack8<T>(rg2[u], g2);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) g[k] += g2[k];
+          }
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            const float gk = ((mk[u] >> k) & 1u) ? g[u][k] : 0.f;
+            const float gk = ((mk[u] >> k) & 1u) ? g[k] : 0.f;
             s[k] += gk;
-            q[k] = fmaf(gk, xv[u][k] - mu[k], q[k]);
+            q[k] = fmaf(gk, xv[k] - mu[k], q[k]);
           }
         }
       }
     }
-    for (; r < M; r += stride) {
+    for (; r < rr.end; r += rpi) {
       const int64_t off = r * C + c;
       float xv[8];
-      Vec8<T>::load(reinterpret_cast<const char*>(x) + off * Vec8<T>::bytes, xv);
+      unpack8<T>(ld8<T>(x, off), xv);
       if (!BWD) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) { s[k] += xv[k]; q[k] = fmaf(xv[k], xv[k], q[k]); }
       } else {
         float g[8];
-        Vec8<T>::load(reinterpret_cast<const char*>(dy) + off * Vec8<T>::bytes, g);
+        unpack8<T>(ld8<T>(dy, off), g);
         if (dy2) {
           float g2[8];
-          Vec8<T>::load(reinterpret_cast<const char*>(dy2) + off * Vec8<T>::bytes, g2);
+          unpack8<T>(ld8<T>(dy2, off), g2);
 #pragma unroll
           for (int k = 0; k < 8; ++k) g[k] += g2[k];
         }
@@ -139,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
     for (int r = 0; r < rpi; ++r) acc += lds[r * width + o];
     const int lco = o / 16, k = o % 16;
     const int ch = (blockIdx.y * tpr + lco) * 8 + (k & 7);
-    if (ch < C) partial[(static_cast<int64_t>(blockIdx.x) * 2 + (k >> 3)) * C + ch] = acc;
+    if (ch < C) partial[(static_cast<int64_t>(bx) * 2 + (k >> 3)) * C + ch] = acc;
   }
 }
 
@@ -238,32 +321,28 @@ __global__ __launch_bounds__(kBlock) void bn_finalize_bwd_kernel(
   }
 }
 
-template <typename T>
+// y = act(x*scale + shift [+ res]) (+ ReLU bitmask), row-tile mapping, U rows in flight per lane.
+// Bit k of mask byte (row*C + c)/8 is the ReLU decision of channel c+k.
+template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
     const void* __restrict__ x, const void* __restrict__ res, void* __restrict__ y,
-    const float* __restrict__ scale, const float* __restrict__ shift, int64_t nvec, int c8,
-    bool relu, uint8_t* __restrict__ mask) {
-  // nvec < 2^31 is checked on the host: 32-bit index math (a 64-bit modulo is a long
-  // software sequence on CDNA), 64-bit byte offsets.
-  const uint32_t stride = gridDim.x * blockDim.x, n = static_cast<uint32_t>(nvec);
-  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += stride) {
-    const int c = static_cast<int>(v % static_cast<uint32_t>(c8)) * 8;
-    float xv[8];
-    Vec8<T>::load(reinterpret_cast<const char*>(x) + static_cast<int64_t>(v) * 8 * Vec8<T>::bytes, xv);
-    const float4* sc = reinterpret_cast<const float4*>(scale + c);
-    const float4* sh = reinterpret_cast<const float4*>(shift + c);
-    const float4 a0 = sc[0], a1 = sc[1], b0 = sh[0], b1 = sh[1];
-    const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-    float o[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = fmaf(xv[k], a[k], b[k]);
-    if (res) {
-      float rv[8];
-      Vec8<T>::load(reinterpret_cast<const char*>(res) + static_cast<int64_t>(v) * 8 * Vec8<T>::bytes, rv);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] += rv[k];
-    }
+    const float* __restrict__ scale, const float* __restrict__ shift, int64_t M, int C, int tpr,
+    int rpi, bool relu, uint8_t* __restrict__ mask) {
+  const int tid = threadIdx.x;
+  const int lc = tid % tpr, r0 = tid / tpr;
+  const int c = (blockIdx.y * tpr + lc) * 8;
+  if (c >= C) return;
+  const RowRange rr = chunk_rows(M, rpi, blockIdx.x, gridDim.x);
+  float a[8], b[8];
+  {
+    const float4 a0 = *reinterpret_cast<const float4*>(scale + c);
+    const float4 a1 = *reinterpret_cast<const float4*>(scale + c + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(shift + c);
+    const float4 b1 = *reinterpret_cast<const float4*>(shift + c + 4);
+    a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
+    b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+  }
+  auto finish = [&](int64_t off, float (&o)[8]) {
     if (relu) {
       uint32_t bits = 0;
 #pragma unroll
@@ -271,45 +350,122 @@ __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
         bits |= (o[k] > 0.f ? 1u : 0u) << k;
         o[k] = fmaxf(o[k], 0.f);
       }
-      if (mask) mask[v] = static_cast<uint8_t>(bits);
+      if (mask) mask[off >> 3] = static_cast<uint8_t>(bits);
     }
-    Vec8<T>::store(reinterpret_cast<char*>(y) + static_cast<int64_t>(v) * 8 * Vec8<T>::bytes, o);
+    st8<T>(y, off, o);
+  };
+  int64_t r = rr.begin + r0;
+  for (; r + (U - 1) * rpi < rr.end; r += U * rpi) {
+    Raw8<T> rx[U], rres[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = (r + u * rpi) * C + c;
+      rx[u] = ld8<T>(x, off);
+      if (res) rres[u] = ld8<T>(res, off);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = (r + u * rpi) * C + c;
+      float xv[8], o[8];
+      unpack8<T>(rx[u], xv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = fmaf(xv[k], a[k], b[k]);
+      if (res) {
+        float rv[8];
+        unpack8<T>(rres[u], rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] += rv[k];
+      }
+      finish(off, o);
+    }
+  }
+  for (; r < rr.end; r += rpi) {
+    const int64_t off = r * C + c;
+    float xv[8], o[8];
+    unpack8<T>(ld8<T>(x, off), xv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = fmaf(xv[k], a[k], b[k]);
+    if (res) {
+      float rv[8];
+      unpack8<T>(ld8<T>(res, off), rv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] += rv[k];
+    }
+    finish(off, o);
   }
 }
 
-template <typename T>
+// dx = k1*dy' + k2*x + k3 with dy' = (dy [+ dy2]) masked by the ReLU bit; dres = dy' when the
+// forward fused a residual add. Row-tile mapping, coefficients held in registers.
+template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
     const void* __restrict__ dy, const void* __restrict__ dy2, const uint8_t* __restrict__ mask,
     const void* __restrict__ x, const float* __restrict__ coef, void* __restrict__ dx,
-    void* __restrict__ dres, int64_t nvec, int c8, int C, bool relu) {
-  // nvec < 2^31 is checked on the host: 32-bit index math (a 64-bit modulo is a long
-  // software sequence on CDNA), 64-bit byte offsets.
-  const uint32_t stride = gridDim.x * blockDim.x, n = static_cast<uint32_t>(nvec);
-  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += stride) {
-    const int c = static_cast<int>(v % static_cast<uint32_t>(c8)) * 8;
-    const int64_t off = static_cast<int64_t>(v) * 8 * Vec8<T>::bytes;
-    float g[8], xv[8];
-    Vec8<T>::load(reinterpret_cast<const char*>(dy) + off, g);
-    if (dy2) {
-      float g2[8];
-      Vec8<T>::load(reinterpret_cast<const char*>(dy2) + off, g2);
+    void* __restrict__ dres, int64_t M, int C, int tpr, int rpi, bool relu) {
+  const int tid = threadIdx.x;
+  const int lc = tid % tpr, r0 = tid / tpr;
+  const int c = (blockIdx.y * tpr + lc) * 8;
+  if (c >= C) return;
+  const RowRange rr = chunk_rows(M, rpi, blockIdx.x, gridDim.x);
+  float k1[8], k2[8], k3[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] += g2[k];
-    }
+  for (int k = 0; k < 8; ++k) { k1[k] = coef[c + k]; k2[k] = coef[C + c + k]; k3[k] = coef[2 * C + c + k]; }
+  auto body = [&](int64_t off, float (&g)[8], const float (&xv)[8], uint32_t m) {
     if (relu) {
-      const uint32_t m = mask[v];
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] = ((m >> k) & 1u) ? g[k] : 0.f;
     }
-    Vec8<T>::load(reinterpret_cast<const char*>(x) + off, xv);
     float o[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      o[k] = fmaf(coef[c + k], g[k], fmaf(coef[C + c + k], xv[k], coef[2 * C + c + k]));
-    Vec8<T>::store(reinterpret_cast<char*>(dx) + off, o);
-    if (dres) Vec8<T>::store(reinterpret_cast<char*>(dres) + off, g);
+    for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], g[k], fmaf(k2[k], xv[k], k3[k]));
+    st8<T>(dx, off, o);
+    if (dres) st8<T>(dres, off, g);
+  };
+  int64_t r = rr.begin + r0;
+  for (; r + (U - 1) * rpi < rr.end; r += U * rpi) {
+    Raw8<T> rg[U], rg2[U], rx[U];
+    uint32_t mk[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = (r + u * rpi) * C + c;
+      rg[u] = ld8<T>(dy, off);
+      if (dy2) rg2[u] = ld8<T>(dy2, off);
+      rx[u] = ld8<T>(x, off);
+      mk[u] = relu ? mask[off >> 3] : 0xffu;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t off = (r + u * rpi) * C + c;
+      float g[8], xv[8];
+      unpack8<T>(rg[u], g);
+      if (dy2) {
+        float g2[8];
+        unpack8<T>(rg2[u], g2);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] += g2[k];
+      }
+      unpack8<T>(rx[u], xv);
+      body(off, g, xv, mk[u]);
+    }
+  }
+  for (; r < rr.end; r += rpi) {
+    const int64_t off = r * C + c;
+    float g[8], xv[8];
+    unpack8<T>(ld8<T>(dy, off), g);
+    if (dy2) {
+      float g2[8];
+      unpack8<T>(ld8<T>(dy2, off), g2);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] += g2[k];
+    }
+    unpack8<T>(ld8<T>(x, off), xv);
+    body(off, g, xv, relu ? mask[off >> 3] : 0xffu);
   }
 }
+
+constexpr int kUReduceFwd = 8;  // rows in flight per lane: 8 x 16 B (x)
+constexpr int kUReduceBwd = 4;  // 4 x (16 B dy + 16 B x [+ 16 B dy2] + 1 B mask)
+constexpr int kUApply = 4;
 
 struct ReduceTuning {
   int64_t elems_per_block, min_blocks, max_blocks;
@@ -317,7 +473,7 @@ struct ReduceTuning {
 inline const ReduceTuning& reduce_tuning() {
   // DCA_BN_REDUCE="elems,min,max" overrides the workgroup-count heuristic (tuning sweeps only).
   static const ReduceTuning t = [] {
-    ReduceTuning r{65536, 256, 1024};
+    ReduceTuning r{32768, 256, 2048};
     if (const char* e = std::getenv("DCA_BN_REDUCE")) {
       long long a = 0, b = 0, c = 0;
       if (std::sscanf(e, "%lld,%lld,%lld", &a, &b, &c) == 3 && a > 0 && b > 0 && c >= b) r = {a, b, c};
@@ -329,14 +485,25 @@ inline const ReduceTuning& reduce_tuning() {
 
 inline int reduce_blocks(int64_t M, int C, const ReduceGeom& g) {
   // ~elems_per_block elements per workgroup, clamped to [min_blocks, max_blocks] in x (x cgroups
-  // in y).
+  // in y); the per-block partials (B x 2 x C floats, re-read by the finalize pass) are capped at
+  // 2^18 floats per statistic, and every block gets at least one row-iteration.
   const ReduceTuning& t = reduce_tuning();
   int64_t total = M * static_cast<int64_t>(C);
   int64_t b = (total + t.elems_per_block - 1) / t.elems_per_block;
   if (b < t.min_blocks) b = t.min_blocks;
   if (b > t.max_blocks) b = t.max_blocks;
+  const int64_t cap = std::max<int64_t>(64, (int64_t(1) << 18) / C);
+  if (b > cap) b = cap;
   int64_t rows_iter = (M + g.rpi - 1) / g.rpi;
   if (b > rows_iter) b = rows_iter;
+  if (b < 1) b = 1;
+  return static_cast<int>(b);
+}
+
+// Workgroups (in x) for the apply passes: up to 8 per CU, each with >= 2 unrolled iterations.
+inline int apply_blocks(int64_t M, const RowGeom& g) {
+  int64_t b = (M + static_cast<int64_t>(g.rpi) * kUApply * 2 - 1) / (static_cast<int64_t>(g.rpi) * kUApply * 2);
+  if (b > 2048) b = 2048;
   if (b < 1) b = 1;
   return static_cast<int>(b);
 }
@@ -349,13 +516,32 @@ void launch_reduce(bool bwd, const void* x, const void* dy, const void* dy2, con
   dim3 grid(B, g.cgroups);
   size_t lds = static_cast<size_t>(g.rpi) * g.tpr * 16 * sizeof(float);
   if (bwd)
-    hipLaunchKernelGGL((bn_reduce_kernel<T, true>), grid, dim3(kBlock), lds, st, x, dy, dy2, y,
-                       mean, M, C, g.tpr, g.rpi, relu, partial);
+    hipLaunchKernelGGL((bn_reduce_kernel<T, true, kUReduceBwd>), grid, dim3(kBlock), lds, st, x,
+                       dy, dy2, y, mean, M, C, g.tpr, g.rpi, relu, partial);
   else
-    hipLaunchKernelGGL((bn_reduce_kernel<T, false>), grid, dim3(kBlock), lds, st, x, dy, dy2, y,
-                       mean, M, C, g.tpr, g.rpi, relu, partial);
+    hipLaunchKernelGGL((bn_reduce_kernel<T, false, kUReduceFwd>), grid, dim3(kBlock), lds, st, x,
+                       dy, dy2, y, mean, M, C, g.tpr, g.rpi, relu, partial);
 }
 
+template <typename T>
+void launch_apply_fwd(const void* x, const void* res, void* y, const float* scale,
+                      const float* shift, int64_t M, int C, bool relu, uint8_t* mask,
+                      hipStream_t st) {
+  const RowGeom g = row_geom(C);
+  dim3 grid(apply_blocks(M, g), g.cgroups);
+  hipLaunchKernelGGL((bn_apply_fwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, x, res, y,
+                     scale, shift, M, C, g.tpr, g.rpi, relu, mask);
+}
+
+template <typename T>
+void launch_apply_bwd(const void* dy, const void* dy2, const uint8_t* mask, const void* x,
+                      const float* coef, void* dx, void* dres, int64_t M, int C, bool relu,
+                      hipStream_t st) {
+  const RowGeom g = row_geom(C);
+  dim3 grid(apply_blocks(M, g), g.cgroups);
+  hipLaunchKernelGGL((bn_apply_bwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, dy, dy2, mask,
+                     x, coef, dx, dres, M, C, g.tpr, g.rpi, relu);
+}
 
 // ------------------------------------------------------------------ stem: BN + ReLU + MaxPool(3,2,1)
 // ResNet stem fusion: the pre-pool activation (N x 112 x 112 x 64 for ImageNet -- the largest
@@ -445,7 +631,17 @@ __device__ __forceinline__ void gather_pool_grad(const void* __restrict__ dyp, c
   }
 }
 
-template <typename T>
+// Row (n, h, w) of the pre-pool tensor; M < 2^31 is checked on the host (32-bit division).
+__device__ __forceinline__ void pool_row(int64_t r, const PoolGeom& g, int64_t& n, int& h, int& w) {
+  const uint32_t ru = static_cast<uint32_t>(r);
+  const uint32_t nh = ru / static_cast<uint32_t>(g.W);
+  w = static_cast<int>(ru - nh * static_cast<uint32_t>(g.W));
+  const uint32_t nn = nh / static_cast<uint32_t>(g.H);
+  h = static_cast<int>(nh - nn * static_cast<uint32_t>(g.H));
+  n = nn;
+}
+
+template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void bn_pool_reduce_bwd_kernel(
     const void* __restrict__ x, const void* __restrict__ dyp, const uint8_t* __restrict__ idx,
     const float* __restrict__ mean, int64_t M, int C, int tpr, int rpi, PoolGeom g,
@@ -455,20 +651,36 @@ __global__ __launch_bounds__(kBlock) void bn_pool_reduce_bwd_kernel(
   const int lc = tid % tpr, r0 = tid / tpr;
   const int c = (blockIdx.y * tpr + lc) * 8;
   const bool active = c < C;
+  const int bx = static_cast<int>(gridDim.x) - 1 - static_cast<int>(blockIdx.x);
+  const RowRange rr = chunk_rows(M, rpi, bx, gridDim.x);
   float s[8], q[8], mu[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; mu[k] = active ? mean[c + k] : 0.f; }
   if (active) {
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * rpi;
-    for (int64_t r = static_cast<int64_t>(blockIdx.x) * rpi + r0; r < M; r += stride) {
-      const int w = static_cast<int>(r % g.W);
-      const int h = static_cast<int>((r / g.W) % g.H);
-      const int64_t n = r / (static_cast<int64_t>(g.W) * g.H);
-      float gr[8], xv[8];
-      gather_pool_grad<T>(dyp, idx, n, h, w, c, C, g, gr);
-      Vec8<T>::load(reinterpret_cast<const char*>(x) + (r * C + c) * Vec8<T>::bytes, xv);
+    int64_t r = rr.begin + r0;
+    for (; r < rr.end; r += U * rpi) {
+      Raw8<T> rx[U];
+      float gr[U][8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { s[k] += gr[k]; q[k] = fmaf(gr[k], xv[k] - mu[k], q[k]); }
+      for (int u = 0; u < U; ++u) {
+        const int64_t ru = r + u * rpi;
+        if (ru < rr.end) {
+          rx[u] = ld8<T>(x, ru * C + c);
+          int64_t n;
+          int h, w;
+          pool_row(ru, g, n, h, w);
+          gather_pool_grad<T>(dyp, idx, n, h, w, c, C, g, gr[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (r + u * rpi < rr.end) {
+          float xv[8];
+          unpack8<T>(rx[u], xv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { s[k] += gr[u][k]; q[k] = fmaf(gr[u][k], xv[k] - mu[k], q[k]); }
+        }
+      }
     }
   }
   const int width = tpr * 16;
@@ -481,28 +693,48 @@ __global__ __launch_bounds__(kBlock) void bn_pool_reduce_bwd_kernel(
     for (int r = 0; r < rpi; ++r) acc += lds[r * width + o];
     const int lco = o / 16, k = o % 16;
     const int ch = (blockIdx.y * tpr + lco) * 8 + (k & 7);
-    if (ch < C) partial[(static_cast<int64_t>(blockIdx.x) * 2 + (k >> 3)) * C + ch] = acc;
+    if (ch < C) partial[(static_cast<int64_t>(bx) * 2 + (k >> 3)) * C + ch] = acc;
   }
 }
 
-template <typename T>
+template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void bn_pool_apply_bwd_kernel(
     const void* __restrict__ x, const void* __restrict__ dyp, const uint8_t* __restrict__ idx,
-    const float* __restrict__ coef, void* __restrict__ dx, int64_t nvec, int C, PoolGeom g) {
-  const int c8 = C / 8;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; v < nvec;
-       v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int c = static_cast<int>(v % c8) * 8;
-    const int64_t r = v / c8;
-    const int w = static_cast<int>(r % g.W);
-    const int h = static_cast<int>((r / g.W) % g.H);
-    const int64_t n = r / (static_cast<int64_t>(g.W) * g.H);
-    float gr[8], xv[8], o[8];
-    gather_pool_grad<T>(dyp, idx, n, h, w, c, C, g, gr);
-    Vec8<T>::load(reinterpret_cast<const char*>(x) + v * 8 * Vec8<T>::bytes, xv);
+    const float* __restrict__ coef, void* __restrict__ dx, int64_t M, int C, int tpr, int rpi,
+    PoolGeom g) {
+  const int tid = threadIdx.x;
+  const int lc = tid % tpr, r0 = tid / tpr;
+  const int c = (blockIdx.y * tpr + lc) * 8;
+  if (c >= C) return;
+  const RowRange rr = chunk_rows(M, rpi, blockIdx.x, gridDim.x);
+  float k1[8], k2[8], k3[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = fmaf(coef[c + k], gr[k], fmaf(coef[C + c + k], xv[k], coef[2 * C + c + k]));
-    Vec8<T>::store(reinterpret_cast<char*>(dx) + v * 8 * Vec8<T>::bytes, o);
+  for (int k = 0; k < 8; ++k) { k1[k] = coef[c + k]; k2[k] = coef[C + c + k]; k3[k] = coef[2 * C + c + k]; }
+  for (int64_t r = rr.begin + r0; r < rr.end; r += U * rpi) {
+    Raw8<T> rx[U];
+    float gr[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t ru = r + u * rpi;
+      if (ru < rr.end) {
+        rx[u] = ld8<T>(x, ru * C + c);
+        int64_t n;
+        int h, w;
+        pool_row(ru, g, n, h, w);
+        gather_pool_grad<T>(dyp, idx, n, h, w, c, C, g, gr[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t ru = r + u * rpi;
+      if (ru < rr.end) {
+        float xv[8], o[8];
+        unpack8<T>(rx[u], xv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], gr[u][k], fmaf(k2[k], xv[k], k3[k]));
+        st8<T>(dx, ru * C + c, o);
+      }
+    }
   }
 }
 
@@ -541,12 +773,10 @@ void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64
   hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
                      C, M, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
                      save_invstd, scale, shift, num_batches);
-  const int64_t nvec = M * C / 8;
-  const int grid = stream_grid(nvec, kBlock);
   switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
-    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
-    default: hipLaunchKernelGGL(bn_apply_fwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
+    case BnDtype::kBF16: launch_apply_fwd<BF16>(x, res, y, scale, shift, M, C, relu, mask, st); break;
+    case BnDtype::kF16: launch_apply_fwd<F16>(x, res, y, scale, shift, M, C, relu, mask, st); break;
+    default: launch_apply_fwd<F32>(x, res, y, scale, shift, M, C, relu, mask, st); break;
   }
 }
 
@@ -554,12 +784,10 @@ void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64
 void bn_forward_affine(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
                        const float* scale, const float* shift, bool relu, hipStream_t st) {
   uint8_t* mask = nullptr;
-  const int64_t nvec = M * C / 8;
-  const int grid = stream_grid(nvec, kBlock);
   switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
-    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_fwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
-    default: hipLaunchKernelGGL(bn_apply_fwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, x, res, y, scale, shift, nvec, C / 8, relu, mask); break;
+    case BnDtype::kBF16: launch_apply_fwd<BF16>(x, res, y, scale, shift, M, C, relu, mask, st); break;
+    case BnDtype::kF16: launch_apply_fwd<F16>(x, res, y, scale, shift, M, C, relu, mask, st); break;
+    default: launch_apply_fwd<F32>(x, res, y, scale, shift, M, C, relu, mask, st); break;
   }
 }
 
@@ -579,12 +807,10 @@ void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_
   }
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
                      C, M, gamma, save_mean, save_invstd, dgamma, dbeta, accumulate_dw, coef);
-  const int64_t nvec = M * C / 8;
-  const int grid = stream_grid(nvec, kBlock);
   switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL(bn_apply_bwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, dy, dy2, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
-    case BnDtype::kF16: hipLaunchKernelGGL(bn_apply_bwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, dy, dy2, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
-    default: hipLaunchKernelGGL(bn_apply_bwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, dy, dy2, y, x, coef, dx, dres, nvec, C / 8, C, relu); break;
+    case BnDtype::kBF16: launch_apply_bwd<BF16>(dy, dy2, y, x, coef, dx, dres, M, C, relu, st); break;
+    case BnDtype::kF16: launch_apply_bwd<F16>(dy, dy2, y, x, coef, dx, dres, M, C, relu, st); break;
+    default: launch_apply_bwd<F32>(dy, dy2, y, x, coef, dx, dres, M, C, relu, st); break;
   }
 }
 
@@ -636,18 +862,17 @@ void bn_relu_pool_backward(BnDtype dt, const void* dyp, const uint8_t* idx, cons
   dim3 grid(B, rg.cgroups);
   size_t lds = static_cast<size_t>(rg.rpi) * rg.tpr * 16 * sizeof(float);
   switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL(bn_pool_reduce_bwd_kernel<BF16>, grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
-    case BnDtype::kF16: hipLaunchKernelGGL(bn_pool_reduce_bwd_kernel<F16>, grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
-    default: hipLaunchKernelGGL(bn_pool_reduce_bwd_kernel<F32>, grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
+    case BnDtype::kBF16: hipLaunchKernelGGL((bn_pool_reduce_bwd_kernel<BF16, 2>), grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
+    case BnDtype::kF16: hipLaunchKernelGGL((bn_pool_reduce_bwd_kernel<F16, 2>), grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
+    default: hipLaunchKernelGGL((bn_pool_reduce_bwd_kernel<F32, 2>), grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
   }
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
                      C, M, gamma, save_mean, save_invstd, dgamma, dbeta, false, coef);
-  const int64_t nvec = M * C / 8;
-  const int ag = stream_grid(nvec, kBlock);
+  dim3 ag(apply_blocks(M, rg), rg.cgroups);
   switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL(bn_pool_apply_bwd_kernel<BF16>, dim3(ag), dim3(kBlock), 0, st, x, dyp, idx, coef, dx, nvec, C, g); break;
-    case BnDtype::kF16: hipLaunchKernelGGL(bn_pool_apply_bwd_kernel<F16>, dim3(ag), dim3(kBlock), 0, st, x, dyp, idx, coef, dx, nvec, C, g); break;
-    default: hipLaunchKernelGGL(bn_pool_apply_bwd_kernel<F32>, dim3(ag), dim3(kBlock), 0, st, x, dyp, idx, coef, dx, nvec, C, g); break;
+    case BnDtype::kBF16: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<BF16, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;
+    case BnDtype::kF16: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<F16, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;
+    default: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<F32, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;
   }
 }
 

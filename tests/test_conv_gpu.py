@@ -130,3 +130,33 @@ def test_resnet_bottleneck_uses_pointwise_kernels(pointwise_on):
     out = m(torch.randn(2, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last))
     out.float().sum().backward()
     assert torch.isfinite(blk.conv1.weight.grad.float()).all()
+
+
+@pytest.mark.parametrize("choice", [0, 1])
+@pytest.mark.parametrize("shape,stride", [((4, 256, 28, 28, 128), 1), ((2, 64, 15, 17, 256), 1),
+                                          ((4, 256, 28, 28, 512), 2), ((3, 1024, 14, 14, 256), 1)])
+def test_pointwise_library_choice_matches_fp32(shape, stride, choice):
+    """Both library paths of ops.conv._PointwiseLib (MIOpen / hipBLASLt GEMM on the NHWC row
+    view), forced per direction, against an fp32 F.conv2d reference."""
+    N, ci, H, W, co = shape
+    torch.manual_seed(0)
+    c = nn.Conv2d(ci, co, 1, stride=stride, bias=False).cuda().bfloat16().to(memory_format=torch.channels_last)
+    x = torch.randn(N, ci, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    conv._CHOICE.clear()
+    for d in ("fwd", "dgrad"):
+        conv._CHOICE[(d, tuple(x.shape), co, stride, x.dtype)] = choice
+    try:
+        x1 = x.clone().requires_grad_(True)
+        y = conv.pointwise_conv(c, x1)
+        assert y.is_contiguous(memory_format=torch.channels_last)
+        g = torch.randn_like(y)
+        y.backward(g)
+        x2 = x.float().clone().requires_grad_(True)
+        w2 = c.weight.detach().float().clone().requires_grad_(True)
+        y2 = F.conv2d(x2, w2, stride=stride)
+        y2.backward(g.float())
+        _close(y, y2, 2e-2, "fwd")
+        _close(x1.grad, x2.grad, 2e-2, "dgrad")
+        _close(c.weight.grad, w2.grad, 2e-2, "wgrad")
+    finally:
+        conv._CHOICE.clear()

@@ -15,7 +15,8 @@ def _ext_loaded():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 7), (2, 2048, 3, 3), (16, 24, 5, 5)])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 7), (2, 2048, 3, 3), (16, 24, 5, 5),
+                                   (32, 128, 28, 28), (3, 64, 17, 19)])
 @pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
 def test_bn_act_forward_backward(dtype, shape, relu, res):
     _ext_loaded()

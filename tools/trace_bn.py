@@ -9,7 +9,7 @@ import sys
 def short(n: str) -> str:
     m = re.search(r"dca::\(anonymous namespace\)::(\w+)", n)
     if m:
-        return m.group(1) + ("<bwd>" if "true>" in n[:160] else "")
+        return m.group(1) + ("<bwd>" if ("true>" in n[:160] or "true," in n[:160]) else "")
     return n[:60]
 
 
