@@ -22,7 +22,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from determined_clone_amd.ops import batchnorm as bn_ops
-from determined_clone_amd.ops.conv import pointwise_conv
+from determined_clone_amd.ops import conv as conv_ops
+from determined_clone_amd.ops.conv import pointwise_conv, pointwise_dual
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -82,10 +83,18 @@ class Bottleneck(nn.Module):
         # epilogue also reduces the following BatchNorm's statistics)
         if self.downsample is None:
             identity = x
+            out = self.bn1(pointwise_conv(self.conv1, x, self.bn1.training))
         else:
+            # conv1 and the projection shortcut read the same x: one op, one input gradient
+            # (the shortcut's strided backward-data is accumulated in place, ops/conv.py)
             ds_conv, ds_bn = self.downsample
-            identity = ds_bn(pointwise_conv(ds_conv, x, ds_bn.training))
-        out = self.bn1(pointwise_conv(self.conv1, x, self.bn1.training))
+            if conv_ops.ENABLED or not conv_ops.DUAL:
+                y1 = pointwise_conv(self.conv1, x, self.bn1.training)
+                yd = pointwise_conv(ds_conv, x, ds_bn.training)
+            else:
+                y1, yd = pointwise_dual(self.conv1, ds_conv, x)
+            identity = ds_bn(yd)
+            out = self.bn1(y1)
         out = self.bn2(self.conv2(out))
         # identity shortcut: x also feeds conv1, so its gradient can be summed inside the
         # producer's BN backward (no separate autograd add)
@@ -132,7 +141,7 @@ class ResNet(nn.Module):
                                            momentum=bn.momentum, eps=bn.eps,
                                            num_batches_tracked=bn.num_batches_tracked)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        x = bn_ops.global_avg_pool(x)
         return self.fc(x)
 
 

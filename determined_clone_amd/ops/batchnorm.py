@@ -213,3 +213,23 @@ def batch_norm_relu_maxpool(x: torch.Tensor, weight: Optional[torch.Tensor],
         y = F.relu(x * scale.view(shape).to(x.dtype) + shift.view(shape).to(x.dtype))
         return F.max_pool2d(y, 3, 2, 1)
     return _ext.load().bn_pool_fwd_affine(x, scale, shift)
+
+
+# ----------------------------------------------------------------------------- global avg pool
+class _SpatialMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[2], x.shape[3])
+        return x.mean(dim=(2, 3))
+
+    @staticmethod
+    def backward(ctx, g):
+        return _ext.load().spatial_mean_bwd(g, *ctx.hw)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """``flatten(adaptive_avg_pool2d(x, 1), 1)`` for an NHWC activation; on the GPU the backward
+    broadcast g / (H*W) is one streaming kernel (``csrc/batchnorm.hip``)."""
+    if _hip_ok(x) and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
+        return _SpatialMean.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -76,6 +76,7 @@ def supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
 # direction by timing both once, on the first training call (like cudnn.benchmark), and cached.
 _CHOICE = {}
 AUTOTUNE = os.environ.get("DCA_CONV_AUTOTUNE", "1") != "0"
+DUAL = os.environ.get("DCA_PW_DUAL", "1") != "0"  # pointwise_dual for downsampling blocks
 
 
 def _time_us(fn, reps: int = 5) -> float:
@@ -114,24 +115,27 @@ def _from_rows(m: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
     return m.view(n, h, w, m.shape[1]).permute(0, 3, 1, 2)  # channels_last NCHW view
 
 
+def _pw_forward(x: torch.Tensor, weight: torch.Tensor, stride: int) -> torch.Tensor:
+    n, cin, h, w = x.shape
+    cout = weight.shape[0]
+    ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
+    W = weight.view(cout, cin)
+
+    def lib():
+        return F.conv2d(x, weight, stride=stride)
+
+    def gemm():
+        return _from_rows(torch.mm(_rows(x, stride), W.t()), n, ho, wo)
+
+    return (lib, gemm)[_choose(("fwd", tuple(x.shape), cout, stride, x.dtype), (lib, gemm))]()
+
+
 class _PointwiseLib(torch.autograd.Function):
     """1x1 / no-padding convolution with per-direction library choice (MIOpen or hipBLASLt)."""
 
     @staticmethod
     def forward(ctx, x, weight, stride):
-        n, cin, h, w = x.shape
-        cout = weight.shape[0]
-        ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
-        W = weight.view(cout, cin)
-        key = ("fwd", tuple(x.shape), cout, stride, x.dtype)
-
-        def lib():
-            return F.conv2d(x, weight, stride=stride)
-
-        def gemm():
-            return _from_rows(torch.mm(_rows(x, stride), W.t()), n, ho, wo)
-
-        y = (lib, gemm)[_choose(key, (lib, gemm))]()
+        y = _pw_forward(x, weight, stride)
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
         return y
@@ -163,6 +167,60 @@ class _PointwiseLib(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = bwd(*args, [False, True, False])[1]
         return dx, dw, None
+
+
+class _PointwiseDual(torch.autograd.Function):
+    """Two 1x1 convolutions of the SAME input -- a ResNet downsampling block's conv1 (stride 1)
+    and its projection shortcut (stride s) -- with one input gradient: for s > 1 the shortcut's
+    backward-data GEMM runs on the 1/s^2 subsampled rows only and is added in place into conv1's
+    input gradient at the strided positions, instead of MIOpen writing a full-size, mostly-zero
+    gradient (after zero-filling it) that autograd then sums with a full-size add."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w2, stride):
+        y1 = _pw_forward(x, w1, 1)
+        y2 = _pw_forward(x, w2, stride)
+        ctx.save_for_backward(x, w1, w2)
+        ctx.stride = stride
+        return y1, y2
+
+    @staticmethod
+    def backward(ctx, dy1, dy2):
+        x, w1, w2 = ctx.saved_tensors
+        st = ctx.stride
+        n, cin, h, w = x.shape
+        bwd = torch.ops.aten.convolution_backward
+        dy1 = dy1.contiguous(memory_format=torch.channels_last)
+        dy2 = dy2.contiguous(memory_format=torch.channels_last)
+        a1 = (dy1, x, w1, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+        a2 = (dy2, x, w2, None, [st, st], [0, 0], [1, 1], False, [0, 0], 1)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            W1 = w1.view(w1.shape[0], cin)
+            c1 = (lambda: bwd(*a1, [True, False, False])[0],
+                  lambda: _from_rows(torch.mm(_rows(dy1, 1), W1), n, h, w))
+            dx = c1[_choose(("dgrad", tuple(x.shape), w1.shape[0], 1, x.dtype), c1)]()
+            W2 = w2.view(w2.shape[0], cin)
+            if st == 1:
+                c2 = (lambda: bwd(*a2, [True, False, False])[0],
+                      lambda: _from_rows(torch.mm(_rows(dy2, 1), W2), n, h, w))
+                dx.add_(c2[_choose(("dgrad", tuple(x.shape), w2.shape[0], 1, x.dtype), c2)]())
+            else:
+                ho, wo = dy2.shape[2], dy2.shape[3]
+                small = torch.mm(_rows(dy2, 1), W2).view(n, ho, wo, cin)
+                dx.permute(0, 2, 3, 1)[:, ::st, ::st, :].add_(small)
+        dw1 = bwd(*a1, [False, True, False])[1] if ctx.needs_input_grad[1] else None
+        dw2 = bwd(*a2, [False, True, False])[1] if ctx.needs_input_grad[2] else None
+        return dx, dw1, dw2, None
+
+
+def pointwise_dual(conv1: nn.Conv2d, proj: nn.Conv2d, x: torch.Tensor):
+    """``(conv1(x), proj(x))`` for a downsampling bottleneck (see :class:`_PointwiseDual`)."""
+    if (not supported(conv1, x) and _lib_supported(conv1, x) and _lib_supported(proj, x)
+            and conv1.stride == (1, 1)):
+        x = x.contiguous(memory_format=torch.channels_last)
+        return _PointwiseDual.apply(x, conv1.weight, proj.weight, proj.stride[0])
+    return pointwise_conv(conv1, x), pointwise_conv(proj, x)
 
 
 def _lib_supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:

@@ -738,6 +738,25 @@ __global__ __launch_bounds__(kBlock) void bn_pool_apply_bwd_kernel(
   }
 }
 
+// Backward of a global average pool over an NHWC tensor: dx[n, hw, c] = g[n, c] * inv_hw,
+// written at streaming bandwidth (16 B per lane) instead of an expand + divide.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void spatial_mean_bwd_kernel(const void* __restrict__ g,
+                                                                 void* __restrict__ dx, int64_t nvec,
+                                                                 int c8, int hw, float inv_hw) {
+  const uint32_t stride = gridDim.x * blockDim.x, n = static_cast<uint32_t>(nvec);
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += stride) {
+    const uint32_t row = v / static_cast<uint32_t>(c8);
+    const uint32_t cv = v - row * static_cast<uint32_t>(c8);
+    const uint32_t img = row / static_cast<uint32_t>(hw);
+    float gv[8];
+    unpack8<T>(ld8<T>(g, (static_cast<int64_t>(img) * c8 + cv) * 8), gv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gv[k] *= inv_hw;
+    st8<T>(dx, static_cast<int64_t>(v) * 8, gv);
+  }
+}
+
 }  // namespace
 
 // Workspace floats needed by bn_forward_train / bn_backward_train for (M, C).
@@ -873,6 +892,18 @@ void bn_relu_pool_backward(BnDtype dt, const void* dyp, const uint8_t* idx, cons
     case BnDtype::kBF16: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<BF16, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;
     case BnDtype::kF16: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<F16, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;
     default: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<F32, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;
+  }
+}
+
+void spatial_mean_backward(BnDtype dt, const void* g, void* dx, int N, int HW, int C,
+                           hipStream_t st) {
+  const int64_t nvec = static_cast<int64_t>(N) * HW * C / 8;
+  const int grid = stream_grid(nvec, kBlock);
+  const float inv = 1.f / static_cast<float>(HW);
+  switch (dt) {
+    case BnDtype::kBF16: hipLaunchKernelGGL(spatial_mean_bwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, g, dx, nvec, C / 8, HW, inv); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(spatial_mean_bwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, g, dx, nvec, C / 8, HW, inv); break;
+    default: hipLaunchKernelGGL(spatial_mean_bwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, g, dx, nvec, C / 8, HW, inv); break;
   }
 }
 

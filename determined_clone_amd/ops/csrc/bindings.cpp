@@ -34,6 +34,9 @@ void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_
                        bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
                        bool accumulate_dw, float* workspace, hipStream_t st);
 
+void spatial_mean_backward(BnDtype dt, const void* g, void* dx, int N, int HW, int C,
+                           hipStream_t st);
+
 int sumsq_partial_blocks(int64_t n);
 void sumsq_partial(OptDtype g, const void* grad, int64_t n, float* partial, int blocks,
                    hipStream_t st);
@@ -266,6 +269,21 @@ std::vector<Tensor> bn_pool_bwd(const Tensor& dyp_in, const Tensor& x, const Ten
   return {dx, dgamma, dbeta};
 }
 
+// Backward of the global average pool of an NHWC tensor: g [N, C] -> dx [N, C, H, W]
+// (channels_last), every spatial position g / (H*W).
+Tensor spatial_mean_bwd(const Tensor& g_in, int64_t H, int64_t W) {
+  CHECK_DEV(g_in);
+  const c10::DeviceGuard guard(g_in.device());
+  Tensor g = g_in.contiguous();
+  TORCH_CHECK(g.dim() == 2 && g.size(1) % 8 == 0, "spatial_mean_bwd: grad must be [N, C], C % 8 == 0");
+  const int64_t N = g.size(0), C = g.size(1);
+  TORCH_CHECK(N * H * W * C / 8 < (int64_t(1) << 31), "spatial_mean_bwd: tensor too large");
+  Tensor dx = torch::empty({N, C, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dca::spatial_mean_backward(bn_dtype(g), g.data_ptr(), dx.data_ptr(), static_cast<int>(N),
+                             static_cast<int>(H * W), static_cast<int>(C), cur_stream());
+  return dx;
+}
+
 // Global gradient norm over one flat buffer: returns a 3-float device tensor
 // [grad multiplier, found_inf, norm] (see optim.hip norm_finalize_kernel).
 Tensor grad_norm_scale(const std::vector<Tensor>& grads, const OptT& loss_scale, double extra_scale,
@@ -448,6 +466,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_pool_fwd_train", &bn_pool_fwd_train);
   m.def("bn_pool_fwd_affine", &bn_pool_fwd_affine);
   m.def("bn_pool_bwd", &bn_pool_bwd);
+  m.def("spatial_mean_bwd", &spatial_mean_bwd);
   m.def("grad_norm_scale", &grad_norm_scale);
   m.def("sumsq_partials", &sumsq_partials);
   m.def("norm_finalize", &norm_finalize_t);

@@ -160,3 +160,28 @@ def test_pointwise_library_choice_matches_fp32(shape, stride, choice):
         _close(c.weight.grad, w2.grad, 2e-2, "wgrad")
     finally:
         conv._CHOICE.clear()
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_pointwise_dual_matches_two_convs(stride):
+    """conv1(x) and the projection shortcut proj(x) through ops.conv.pointwise_dual (one input
+    gradient, the strided shortcut's dgrad accumulated in place) against fp32 autograd."""
+    torch.manual_seed(0)
+    N, ci, H = 4, 256, 28
+    c1 = nn.Conv2d(ci, 128, 1, bias=False).cuda().bfloat16().to(memory_format=torch.channels_last)
+    cp = nn.Conv2d(ci, 512, 1, stride=stride, bias=False).cuda().bfloat16().to(memory_format=torch.channels_last)
+    x = torch.randn(N, ci, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    x1 = x.clone().requires_grad_(True)
+    y1, yp = conv.pointwise_dual(c1, cp, x1)
+    g1, gp = torch.randn_like(y1), torch.randn_like(yp)
+    torch.autograd.backward([y1, yp], [g1, gp])
+    x2 = x.float().clone().requires_grad_(True)
+    w1 = c1.weight.detach().float().clone().requires_grad_(True)
+    wp = cp.weight.detach().float().clone().requires_grad_(True)
+    r1, rp = F.conv2d(x2, w1), F.conv2d(x2, wp, stride=stride)
+    torch.autograd.backward([r1, rp], [g1.float(), gp.float()])
+    _close(y1, r1, 2e-2, "y1")
+    _close(yp, rp, 2e-2, "yp")
+    _close(x1.grad, x2.grad, 2e-2, "dx")
+    _close(c1.weight.grad, w1.grad, 2e-2, "dw1")
+    _close(cp.weight.grad, wp.grad, 2e-2, "dwp")

@@ -247,3 +247,19 @@ def test_bn_direct_grad_accumulation_into_flat_buffer():
     torch.testing.assert_close(w1.grad, w2.grad, atol=1e-3, rtol=1e-4)
     torch.testing.assert_close(b1.grad, b2.grad, atol=1e-3, rtol=1e-4)
     assert space.grads_are_views()
+
+
+def test_global_avg_pool_matches_torch():
+    _ext_loaded()
+    torch.manual_seed(0)
+    x = torch.randn(6, 64, 7, 7, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    x1 = x.clone().requires_grad_(True)
+    y = batchnorm.global_avg_pool(x1)
+    x2 = x.float().clone().requires_grad_(True)
+    y2 = torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x2, 1), 1)
+    torch.testing.assert_close(y.float(), y2, atol=2e-2, rtol=2e-2)
+    g = torch.randn_like(y2)
+    y.backward(g.bfloat16())
+    y2.backward(g)
+    assert x1.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(x1.grad.float(), x2.grad, atol=1e-3, rtol=1e-2)
