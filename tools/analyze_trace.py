@@ -32,7 +32,7 @@ def category(name: str) -> str:
 
 
 def main(path: str, steps: int = 3, step_marker: str = "sgd_kernel", per_step: int = 2,
-         neighbors: str = "") -> None:
+         neighbors: str = "", by_grid: str = "") -> None:
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if step_marker in r["Kernel_Name"]]
@@ -62,6 +62,19 @@ def main(path: str, steps: int = 3, step_marker: str = "sgd_kernel", per_step: i
     print("\ntop kernels (ms/step, calls/step):")
     for n, (v, c) in sorted(by_name.items(), key=lambda x: -x[1][0])[:25]:
         print(f"  {v / steps:8.3f} {c / steps:5.0f}  {n}")
+    if by_grid:
+        # per-launch-shape times of the kernels matching `by_grid` (grid size identifies the layer)
+        shapes = defaultdict(lambda: [0.0, 0])
+        for r in seg:
+            if by_grid in r["Kernel_Name"]:
+                short = re.sub(r"\(.*", "", r["Kernel_Name"]).split("::")[-1][:40]
+                key = (short, r.get("Grid_Size_X", "?"), r.get("Grid_Size_Y", "?"))
+                d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+                shapes[key][0] += d
+                shapes[key][1] += 1
+        print(f"\nlaunch shapes of '{by_grid}' (us/launch, launches/step, us/step):")
+        for (nm, gx, gy), (v, c) in sorted(shapes.items(), key=lambda x: -x[1][0]):
+            print(f"  {v / c:8.1f} {c / steps:5.1f} {v / steps:8.1f}  {nm} grid=({gx},{gy})")
     if neighbors:
         # which kernels surround the launches matching `neighbors` (who issues them)
         ctx = defaultdict(int)
@@ -79,4 +92,5 @@ if __name__ == "__main__":
     main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 3,
          per_step=int(sys.argv[3]) if len(sys.argv) > 3 else 2,
          step_marker=sys.argv[4] if len(sys.argv) > 4 else "sgd_kernel",
-         neighbors=sys.argv[5] if len(sys.argv) > 5 else "")
+         neighbors=sys.argv[5] if len(sys.argv) > 5 else "",
+         by_grid=sys.argv[6] if len(sys.argv) > 6 else "")
