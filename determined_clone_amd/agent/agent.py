@@ -18,7 +18,6 @@ waves), which is how 16 concurrent ASHA trials fit on 8 GPUs. Slot ``i`` maps to
 ``i // K``; ``HIP_VISIBLE_DEVICES`` lists the distinct physical devices of the task's slots.
 """
 import argparse
-import base64
 import json
 import logging
 import os
@@ -26,18 +25,15 @@ import shutil
 import signal
 import socket
 import subprocess
-import sys
 import tempfile
 import threading
 import time
-import uuid
 from typing import Any, Dict, List, Optional
 
+from determined_clone_amd.agent import runtime
 from determined_clone_amd.common.api import Session
 
 logger = logging.getLogger("determined_clone_amd.agent")
-
-FRAMEWORK_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def share_devices(devs: List[Dict[str, Any]], slots_per_gpu: int) -> List[Dict[str, Any]]:
@@ -123,63 +119,10 @@ class Agent:
     # ------------------------------------------------------------------ task lifecycle
     def _start(self, spec: Dict[str, Any]) -> None:
         alloc = spec["allocation_id"]
-        task_id = spec["task_id"]
         wd = os.path.join(self.workdir, alloc.replace("/", "_"))
         ctx_dir = os.path.join(wd, "context")
-        os.makedirs(ctx_dir, exist_ok=True)
-        try:
-            blob = self.session.get(f"/api/v1/tasks/{task_id}/context").get("b64_tgz")
-            if blob:
-                from determined_clone_amd.util import untar_to
-
-                untar_to(base64.b64decode(blob), ctx_dir)
-        except Exception as e:
-            logger.warning(f"could not fetch context for {task_id}: {e}")
-        info = dict(spec["cluster_info"])
-        info["agent_id"] = self.id
-        info["slot_ids"] = list(spec.get("slots") or [])
-        mine = [d for d in self.devices if d["id"] in set(spec.get("slots") or [])]
-        info["gpu_uuids"] = [d["uuid"] for d in mine if d["type"] == "rocm"]
-        if spec.get("num_containers", 1) > 1:
-            info["rendezvous"] = {"container_addrs": ["127.0.0.1"] * spec["num_containers"],
-                                  "container_rank": spec.get("container_rank", 0)}
-        env = dict(os.environ)
-        user_env = (spec.get("environment") or {}).get("environment_variables") or {}
-        if isinstance(user_env, list):
-            user_env = dict(x.split("=", 1) for x in user_env if "=" in x)
-        elif isinstance(user_env, dict) and ("rocm" in user_env or "cpu" in user_env or "cuda" in user_env):
-            user_env = dict(x.split("=", 1) for x in (user_env.get("rocm") or user_env.get("cpu") or []) if "=" in x)
-        env.update({str(k): str(v) for k, v in user_env.items()})
-        env["DET_CLUSTER_INFO"] = json.dumps(info)
-        env["DET_CONTEXT_DIR"] = ctx_dir
-        env["DET_MASTER"] = self.master_url
-        env["DET_AGENT_ID"] = self.id
-        env["DET_ALLOCATION_ID"] = alloc
-        env["DET_TASK_ID"] = task_id
-        env["PYTHONUNBUFFERED"] = "1"
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        env["PYTHONPATH"] = os.pathsep.join([ctx_dir, FRAMEWORK_ROOT] + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))
-        slots = spec.get("slots") or []
-        if any(d["type"] == "rocm" for d in self.devices):
-            phys = sorted({int(d.get("device_index", d["id"])) for d in mine})
-            if spec["kind"] == "TRIAL" and len(mine) > 1 and len(phys) < len(mine):
-                # RCCL needs one rank per device: a multi-slot trial must not land on two shares
-                # of the same GPU.
-                raise RuntimeError(f"task {task_id}: {len(mine)} slots map to only {len(phys)} "
-                                   "GPU(s); --slots-per-gpu > 1 supports single-slot trials only")
-            env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in phys)
-        else:
-            env["DET_SLOTS"] = str(max(len(slots), 1))
-            # CPU slots: give each task its share of the host's cores so concurrent trials do not
-            # oversubscribe the CPU with one full-size OpenMP pool each.
-            share = max(1, (os.cpu_count() or 1) * max(len(slots), 1) // max(len(self.devices), 1))
-            env.setdefault("OMP_NUM_THREADS", str(share))
-        if spec["kind"] == "TRIAL":
-            cmd = [sys.executable, "-m", "determined_clone_amd.exec.launch"]
-        else:
-            cmd = list(spec.get("entrypoint") or ["true"])
-            if cmd and cmd[0] in ("python", "python3"):
-                cmd[0] = sys.executable
+        runtime.fetch_context(self.session, spec["task_id"], ctx_dir)
+        cmd, env = runtime.build_task(spec, self.master_url, self.id, self.devices, ctx_dir)
         proc = subprocess.Popen(cmd, cwd=ctx_dir, env=env, stdout=subprocess.PIPE,
                                 stderr=subprocess.STDOUT, start_new_session=True)
         t = _Task(spec, proc, wd)
@@ -190,35 +133,7 @@ class Agent:
 
     def _pump(self, t: _Task) -> None:
         alloc = t.spec["allocation_id"]
-        task_id = t.spec["task_id"]
-        buf: List[Dict[str, Any]] = []
-        last = time.time()
-
-        def flush() -> None:
-            nonlocal buf, last
-            if buf:
-                try:
-                    self.session.post("/api/v1/task/logs", {"logs": buf})
-                except Exception as e:
-                    logger.warning(f"log shipping failed: {e}")
-                buf = []
-            last = time.time()
-
-        for raw in iter(t.proc.stdout.readline, b""):
-            line = raw.decode(errors="replace").rstrip("\n")
-            rank = None
-            if line.startswith("[rank"):
-                try:
-                    rank = int(line[line.index("=") + 1: line.index("]")])
-                except ValueError:
-                    rank = None
-            buf.append({"task_id": task_id, "allocation_id": alloc, "agent_id": self.id,
-                        "log": line, "timestamp": time.time(), "rank_id": rank,
-                        "container_id": str(t.spec.get("container_rank", 0))})
-            if len(buf) >= 200 or time.time() - last > 1.0:
-                flush()
-        code = t.proc.wait()
-        flush()
+        code = runtime.pump_logs(t.proc, self.session, t.spec, self.id)
         with self._lock:
             self.tasks.pop(alloc, None)
         self._event(alloc, "TERMINATED", code if not t.killed else (code or 137))

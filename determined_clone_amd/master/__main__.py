@@ -35,7 +35,8 @@ def main() -> None:
                fit=args.fit or sched.get("fitting_policy", "best"),
                preemption=bool(sched.get("preemption", True)), checkpoint_storage=cs,
                cluster_name=cfg.get("cluster_name", "default"),
-               authz=args.authz or ((cfg.get("security") or {}).get("authz") or {}).get("type", "basic"))
+               authz=args.authz or ((cfg.get("security") or {}).get("authz") or {}).get("type", "basic"),
+               resource_manager=cfg.get("resource_manager"), resource_pools=cfg.get("resource_pools"))
     srv = MasterServer(m, args.host, int(cfg.get("port", args.port))).start()
     logging.info(f"master listening on {m.master_url}")
     stop = threading.Event()

@@ -19,7 +19,8 @@ from determined_clone_amd.master.rbac import Authz
 from determined_clone_amd.master.db import DB, dec, now
 from determined_clone_amd.master.experiment import (ACTIVE, PAUSED, TERMINAL, Experiment, Trial,
                                                     experiment_row_to_api, trial_row_to_api)
-from determined_clone_amd.master.rm import AgentState, AllocationRequest, ResourceManager
+from determined_clone_amd.master.rm import AgentState, AllocationRequest
+from determined_clone_amd.master.rm_setup import make_resource_manager
 
 logger = logging.getLogger("determined_clone_amd.master")
 
@@ -119,7 +120,8 @@ class Master:
     def __init__(self, db_path: str = ":memory:", scheduler: str = "priority", fit: str = "best",
                  preemption: bool = True, checkpoint_storage: Optional[Dict[str, Any]] = None,
                  cluster_name: str = "default", master_url: str = "http://127.0.0.1:8080",
-                 authz: str = "basic") -> None:
+                 authz: str = "basic", resource_manager: Optional[Dict[str, Any]] = None,
+                 resource_pools: Optional[List[Dict[str, Any]]] = None) -> None:
         self.db = DB(db_path)
         self.authz = Authz(self.db, authz)
         self.log_buffer = MasterLogBuffer()
@@ -133,8 +135,9 @@ class Master:
         self.master_url = master_url
         self.checkpoint_storage = checkpoint_storage or {
             "type": "shared_fs", "host_path": os.path.join(os.path.expanduser("~"), ".det-clone-ckpts")}
-        self.rm = ResourceManager(scheduler, fit, preemption, on_start=self._on_alloc_start,
-                                  on_preempt=self._on_alloc_preempt)
+        self.rm = make_resource_manager(resource_manager, scheduler, fit, preemption,
+                                        self._on_alloc_start, self._on_alloc_preempt,
+                                        self.container_event, resource_pools)
         self.experiments: Dict[int, Experiment] = {}
         self.allocations: Dict[str, Allocation] = {}
         self.tasks: Dict[str, Dict[str, Any]] = {}
@@ -298,15 +301,16 @@ class Master:
         spec["task_id"] = a.task_id
         n_containers = len(req.placements)
         a.containers_running = n_containers
+        specs = []
         for rank, p in enumerate(req.placements):
-            agent = self.rm.agents.get(p["agent_id"])
-            if agent is None:
-                continue
             s = dict(spec)
             s["slots"] = p["slots"]
             s["container_rank"] = rank
             s["num_containers"] = n_containers
-            agent.push({"type": "start", "spec": s})
+            s["agent_id"] = p["agent_id"]
+            specs.append(s)
+        # agents: long-poll action queues; Kubernetes: pods; Slurm/PBS: one batch job
+        self.rm.start_containers(req, specs)
 
     def _on_alloc_preempt(self, req: AllocationRequest) -> None:
         self.preempt_allocation(req.alloc_id)
@@ -330,10 +334,7 @@ class Master:
             self.rm.release(alloc_id)
             self._allocation_done(a, 137, "killed")
             return
-        for p in a.placements:
-            agent = self.rm.agents.get(p["agent_id"])
-            if agent:
-                agent.push({"type": "kill", "allocation_id": alloc_id})
+        self.rm.kill_containers(alloc_id, a.placements)
 
     def container_event(self, agent_id: str, alloc_id: str, state: str,
                         exit_code: Optional[int] = None) -> None:

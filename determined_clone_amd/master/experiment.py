@@ -201,6 +201,8 @@ class Experiment:
         req = AllocationRequest(alloc_id, t.task_id, self.job_id, self.slots_per_trial,
                                 self.priority, self.weight, self.pool, True,
                                 name=f"Trial {t.id} (Experiment {self.id})")
+        # HPC launcher options (expconf `slurm` / `pbs`: slots_per_node, gpu_type, sbatch_args)
+        req.hpc = {"slurm": self.config.get("slurm") or {}, "pbs": self.config.get("pbs") or {}}
         self.master.db.upsert("allocations", {"allocation_id": alloc_id, "task_id": t.task_id,
                                               "slots": self.slots_per_trial, "resource_pool": self.pool,
                                               "state": "PENDING", "start_time": now()})

@@ -76,6 +76,7 @@ class AllocationRequest:
         self.placements: List[Dict[str, Any]] = []
         self.start_time: Optional[float] = None
         self.preempt_requested = False
+        self.hpc: Dict[str, Any] = {}  # expconf `slurm` / `pbs` sections (dispatcher RM)
 
 
 class ResourceManager:
@@ -93,6 +94,9 @@ class ResourceManager:
         self.on_start = on_start
         self.on_preempt = on_preempt
         self._lock = threading.RLock()
+        self.provisioners: Dict[str, Any] = {}
+        self.provisioner_configs: List[Any] = []  # [(pool, provider config)]
+        self.on_container_event: Optional[Callable[..., None]] = None
 
     # ------------------------------------------------------------------ agents
     def register_agent(self, agent: AgentState) -> None:
@@ -236,6 +240,49 @@ class ResourceManager:
         for r in preempts:
             if self.on_preempt:
                 self.on_preempt(r)
+
+    # ------------------------------------------------------------------ containers
+    def start_containers(self, req: AllocationRequest, specs: List[Dict[str, Any]]) -> None:
+        """Run one container per placement: each spec goes to its agent's action queue."""
+        for s in specs:
+            agent = self.agents.get(s["agent_id"])
+            if agent is not None:
+                agent.push({"type": "start", "spec": s})
+
+    def kill_containers(self, alloc_id: str, placements: List[Dict[str, Any]]) -> None:
+        for p in placements:
+            agent = self.agents.get(p["agent_id"])
+            if agent is not None:
+                agent.push({"type": "kill", "allocation_id": alloc_id})
+
+    def close(self) -> None:
+        """Stop background work (watchers, provisioners)."""
+        for p in self.provisioners.values():
+            p.stop()
+
+    # ------------------------------------------------------------------ dynamic agents
+    def start_provisioners(self, master_url: str) -> None:
+        """Build and start the configured pools' cloud provisioners."""
+        from determined_clone_amd.master.provisioner import Provisioner, make_provider
+
+        for name, cfg in self.provisioner_configs:
+            if name not in self.provisioners:
+                p = Provisioner(name, cfg, make_provider(name, cfg, master_url))
+                self.attach_provisioner(name, p)
+                p.start()
+
+    def attach_provisioner(self, pool: str, provisioner: Any) -> None:
+        """Give ``pool`` a cloud provisioner (``master/provisioner.py``) fed from this RM."""
+        provisioner.scaling_info = lambda: self.scaling_info(pool)
+        self.provisioners[pool] = provisioner
+
+    def scaling_info(self, pool: str):
+        """(unscheduled requests of ``pool``, its connected agents with their idle flag)."""
+        with self._lock:
+            pending = [r for r in self.pending.values() if r.pool == pool]
+            agents = [{"name": a.id, "idle": not any(a.slot_owner) and a.zero_slot_used == 0}
+                      for a in self.agents.values() if a.pool == pool]
+            return pending, agents
 
     # ------------------------------------------------------------------ views
     def pools(self) -> List[Dict[str, Any]]:

@@ -1319,11 +1319,13 @@ class MasterServer:
     def start(self) -> "MasterServer":
         self._thread = threading.Thread(target=self.httpd.serve_forever, daemon=True, name="master-http")
         self._thread.start()
+        self.master.rm.start_provisioners(self.master.master_url)
         return self
 
     def stop(self) -> None:
         self.httpd.shutdown()
         self.httpd.server_close()
+        self.master.rm.close()
 
 
 # routes that live in their own modules register on import

@@ -1,0 +1,415 @@
+"""Kubernetes RM, Slurm/PBS dispatcher RM and cloud provisioner (reference:
+`master/internal/rm/kubernetesrm/*_test.go`, `agentrm/provisioner/*_test.go`,
+`scaledecider/scale_decider_test.go`, `agentrm/scaling.go`) against in-process fakes of the API
+server / workload-manager CLI / EC2 / GCE (``tests/fake_cluster.py``)."""
+import base64
+import os
+import shutil
+import tempfile
+import time
+
+import pytest
+
+from determined_clone_amd.agent.runtime import decode_spec
+from determined_clone_amd.common.api import Session
+from determined_clone_amd.master import Master, MasterServer
+from determined_clone_amd.master import provisioner as prov
+from determined_clone_amd.master.rm import AgentState, AllocationRequest, ResourceManager
+from determined_clone_amd.master.rm_dispatcher import DispatcherResourceManager
+from determined_clone_amd.master.rm_kubernetes import KubeClient, KubernetesResourceManager, parse_quantity
+from determined_clone_amd.util import tar_directory
+from tests.fake_cluster import FakeEC2, FakeGCE, FakeKubeAPI, install_fake_hpc
+from tests.test_cluster_e2e import MODEL_DEF
+
+ONEVAR_CFG = {
+    "name": "rm-onevar", "entrypoint": "model_def:OneVar",
+    "hyperparameters": {"global_batch_size": 4, "lr": 0.1},
+    "searcher": {"name": "single", "metric": "val_loss", "max_length": {"batches": 4}},
+    "min_validation_period": {"batches": 4},
+    "resources": {"slots_per_trial": 1}, "max_restarts": 0,
+}
+
+
+def _login(url):
+    s = Session(url)
+    s.token = s.post("/api/v1/auth/login", {"username": "admin", "password": ""})["token"]
+    return s
+
+
+def _ctx(tmp):
+    ctx = os.path.join(tmp, "ctx")
+    os.makedirs(ctx, exist_ok=True)
+    with open(os.path.join(ctx, "model_def.py"), "w") as f:
+        f.write(MODEL_DEF)
+    return base64.b64encode(tar_directory(ctx)).decode()
+
+
+def _wait_exp(s, eid, timeout=240):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        st = s.get(f"/api/v1/experiments/{eid}")["experiment"]["state"]
+        if st in ("COMPLETED", "CANCELED", "ERROR"):
+            return st
+        time.sleep(0.5)
+    raise TimeoutError(f"experiment {eid} still {st}")
+
+
+def _wait(pred, timeout=60.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if pred():
+            return True
+        time.sleep(0.2)
+    return False
+
+
+# ================================================================================== Kubernetes
+def test_parse_quantity():
+    assert parse_quantity("8") == 8 and parse_quantity("7800m") == pytest.approx(7.8)
+    assert parse_quantity("2Gi") == 2 * 1024 ** 3 and parse_quantity("1k") == 1000
+
+
+def test_k8s_nodes_become_slot_groups():
+    api = FakeKubeAPI([FakeKubeAPI.node("mi355x-a", gpus=8),
+                       FakeKubeAPI.node("mi355x-b", gpus=8, labels={"determined.ai/resource_pool": "big"}),
+                       FakeKubeAPI.node("down", gpus=8, ready=False),
+                       FakeKubeAPI.node("cordoned", gpus=8, unschedulable=True)])
+    try:
+        rm = KubernetesResourceManager({"max_slots_per_pod": 4}, client=KubeClient(api.url, api.token),
+                                       start_watcher=False)
+        rm.sync_nodes()
+        assert sorted(rm.agents) == ["mi355x-a#0", "mi355x-a#1", "mi355x-b#0", "mi355x-b#1"]
+        assert all(len(a.slots) == 4 for a in rm.agents.values())
+        assert rm.agents["mi355x-b#1"].pool == "big"
+        # unauthenticated clients are refused by the API server
+        with pytest.raises(Exception):
+            KubeClient(api.url, "wrong").list_nodes()
+    finally:
+        api.stop()
+
+
+def test_k8s_pod_manifest_and_gang_placement():
+    api = FakeKubeAPI([FakeKubeAPI.node("n1", gpus=8), FakeKubeAPI.node("n2", gpus=8)])
+    started = []
+    try:
+        rm = KubernetesResourceManager({"namespace": "det", "default_image": "img:rocm"},
+                                       client=KubeClient(api.url, api.token), start_watcher=False,
+                                       on_start=started.append)
+        rm.sync_nodes()
+        rm.allocate(AllocationRequest("exp-1.trial-1.0", "t1", "job1", 16))
+        assert len(started) == 1 and len(started[0].placements) == 2  # 2 pods x 8 GPUs
+        spec = {"kind": "TRIAL", "allocation_id": "exp-1.trial-1.0", "task_id": "t1",
+                "cluster_info": {"master_url": "http://m:8080", "session_token": "tok"},
+                "environment": {"image": {"rocm": "img:custom"}, "pod_spec": {
+                    "metadata": {"labels": {"team": "llm"}},
+                    "spec": {"tolerations": [{"key": "amd.com/gpu", "operator": "Exists"}],
+                             "containers": [{"name": "determined-container",
+                                             "env": [{"name": "FOO", "value": "1"}]}]}}},
+                "slots": list(range(8)), "container_rank": 1, "num_containers": 2,
+                "agent_id": started[0].placements[1]["agent_id"]}
+        pod = rm.pod_manifest(spec)
+        c = pod["spec"]["containers"][0]
+        assert pod["metadata"]["namespace"] == "det"
+        assert pod["metadata"]["labels"]["team"] == "llm"
+        assert pod["metadata"]["labels"]["determined.ai/container-rank"] == "1"
+        assert pod["spec"]["nodeName"] == spec["agent_id"].split("#")[0]
+        assert pod["spec"]["tolerations"][0]["key"] == "amd.com/gpu"
+        assert pod["spec"]["restartPolicy"] == "Never"
+        assert c["image"] == "img:custom"
+        assert c["resources"]["limits"] == {"amd.com/gpu": "8"}
+        env = {e["name"]: e for e in c["env"]}
+        assert decode_spec(env["DET_TASK_SPEC"]["value"])["container_rank"] == 1
+        assert env["DET_CONTAINER_ADDR"]["valueFrom"]["fieldRef"]["fieldPath"] == "status.podIP"
+        assert env["FOO"]["value"] == "1"
+        assert {"name": "dshm", "mountPath": "/dev/shm"} in c["volumeMounts"]
+        assert c["command"][-1] == "determined_clone_amd.exec.task_runner"
+        # a request larger than the cluster stays queued
+        rm.allocate(AllocationRequest("big.0", "t2", "job2", 24))
+        assert "big.0" in rm.pending
+    finally:
+        api.stop()
+
+
+@pytest.fixture
+def k8s_cluster():
+    tmp = tempfile.mkdtemp(prefix="det-k8s-")
+    api = FakeKubeAPI([FakeKubeAPI.node("cpu-node", gpus=0, cpu="4")],
+                      env={"PYTHONPATH": os.path.dirname(os.path.dirname(os.path.abspath(__file__)))})
+    m = Master(os.path.join(tmp, "m.db"), checkpoint_storage={"type": "shared_fs", "host_path": os.path.join(tmp, "ckpt")},
+               resource_manager={"type": "kubernetes", "api_server": api.url, "token": api.token,
+                                 "slot_type": "cpu", "cpu_per_slot": 1, "poll_interval": 0.2,
+                                 "namespace": "default"})
+    srv = MasterServer(m, "127.0.0.1", 0).start()
+    yield m, api, tmp
+    srv.stop()
+    api.stop()
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_k8s_experiment_runs_in_pods(k8s_cluster):
+    m, api, tmp = k8s_cluster
+    s = _login(m.master_url)
+    assert _wait(lambda: "cpu-node" in m.rm.agents)
+    assert len(m.rm.agents["cpu-node"].slots) == 4
+    eid = s.post("/api/v1/experiments", {"config": ONEVAR_CFG, "model_definition": _ctx(tmp)})["experiment"]["id"]
+    assert _wait_exp(s, eid) == "COMPLETED"
+    assert len(api.created) >= 1
+    pod = api.created[0]
+    assert pod["spec"]["nodeName"] == "cpu-node"
+    assert pod["spec"]["containers"][0]["resources"]["requests"] == {"cpu": "1.0"}
+    assert _wait(lambda: not api.pods)  # finished pods are cleaned up
+    t = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]
+    assert t["steps_completed"] == 4
+    logs = s.get(f"/api/v1/trials/{t['id']}/logs")
+    assert logs  # the task runner shipped the trial's output
+
+
+def test_k8s_kill_deletes_pod(k8s_cluster):
+    m, api, tmp = k8s_cluster
+    s = _login(m.master_url)
+    assert _wait(lambda: "cpu-node" in m.rm.agents)
+    tid = s.post("/api/v1/commands", {"entrypoint": ["sleep", "60"],
+                                      "config": {"resources": {"slots": 1}}})["command"]["id"]
+    assert _wait(lambda: any(p["status"]["phase"] == "Running" for p in list(api.pods.values())))
+    s.post(f"/api/v1/commands/{tid}/kill")
+    assert _wait(lambda: not api.pods)
+    assert api.deleted
+    assert _wait(lambda: m.tasks[tid].get("state") == "TERMINATED")
+
+
+# ================================================================================== Slurm / PBS
+@pytest.fixture
+def hpc_env(monkeypatch):
+    tmp = tempfile.mkdtemp(prefix="det-hpc-")
+    env = install_fake_hpc(os.path.join(tmp, "bin"), os.path.join(tmp, "state"))
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    yield tmp
+    shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_slurm_and_pbs_batch_scripts(hpc_env):
+    for kind in ("slurm", "pbs"):
+        rm = DispatcherResourceManager({"type": kind, "slots_per_node": 8, "job_storage_root": hpc_env,
+                                        "sbatch_args": ["--time=01:00:00"]}, start_watcher=False)
+        started = []
+        rm.on_start = started.append
+        req = AllocationRequest("e1.t1.0", "t1", "j1", 16, pool="mi355x")
+        req.hpc = {"slurm": {"gpu_type": "mi355x", "sbatch_args": ["--exclusive"]},
+                   "pbs": {"pbsbatch_args": ["-l walltime=1:00:00"]}}
+        rm.allocate(req)
+        assert len(started) == 1 and len(req.placements) == 2
+        spec = {"kind": "TRIAL", "allocation_id": "e1.t1.0", "task_id": "t1", "slots": list(range(8)),
+                "cluster_info": {"master_url": "http://m:1", "session_token": "x"}}
+        text = rm.batch_script(req, spec, 2)
+        if kind == "slurm":
+            for line in ("#SBATCH --nodes=2", "#SBATCH --ntasks-per-node=1",
+                         "#SBATCH --gpus-per-node=mi355x:8", "#SBATCH --partition=mi355x",
+                         "#SBATCH --time=01:00:00", "#SBATCH --exclusive"):
+                assert line in text, line
+            assert "srun --kill-on-bad-exit=1" in text
+        else:
+            for line in ("#PBS -l select=2:ngpus=8", "#PBS -q mi355x", "#PBS -l walltime=1:00:00"):
+                assert line in text, line
+            assert "pbsdsh -u" in text
+        assert "determined_clone_amd.exec.task_runner" in text
+        pools = rm.pools()
+        assert pools and pools[0]["name"] in ("mi355x", "workq")
+        if kind == "slurm":
+            assert pools[0]["slots_available"] == 16
+
+
+@pytest.mark.parametrize("kind", ["slurm", "pbs"])
+def test_hpc_experiment_runs_as_batch_job(hpc_env, kind):
+    m = Master(os.path.join(hpc_env, "m.db"),
+               checkpoint_storage={"type": "shared_fs", "host_path": os.path.join(hpc_env, "ckpt")},
+               resource_manager={"type": kind, "slot_type": "cpu", "slots_per_node": 4,
+                                 "poll_interval": 0.3, "job_storage_root": os.path.join(hpc_env, "jobs")})
+    srv = MasterServer(m, "127.0.0.1", 0).start()
+    try:
+        s = _login(m.master_url)
+        eid = s.post("/api/v1/experiments", {"config": ONEVAR_CFG, "model_definition": _ctx(hpc_env)})["experiment"]["id"]
+        assert _wait_exp(s, eid) == "COMPLETED"
+        with open(os.path.join(hpc_env, "state", "submitted.log")) as f:
+            assert len(f.read().splitlines()) >= 1
+        t = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]
+        assert t["steps_completed"] == 4
+        # kill: scancel / qdel ends a running command
+        tid = s.post("/api/v1/commands", {"entrypoint": ["sleep", "60"],
+                                          "config": {"resources": {"slots": 1}}})["command"]["id"]
+        assert _wait(lambda: any(j.running for j in list(m.rm.jobs.values())), 30)
+        s.post(f"/api/v1/commands/{tid}/kill")
+        assert _wait(lambda: m.tasks[tid].get("state") == "TERMINATED", 30)
+    finally:
+        srv.stop()
+
+
+# ================================================================================== provisioner
+class _Req:
+    def __init__(self, slots, job="j"):
+        self.slots, self.job_id = slots, job
+
+
+def test_desired_new_instances():
+    assert prov.desired_new_instances([_Req(8), _Req(8), _Req(4)], 8) == 3
+    assert prov.desired_new_instances([_Req(16)], 8) == 2
+    assert prov.desired_new_instances([_Req(12)], 8) == 0  # cannot fit any instance shape
+    assert prov.desired_new_instances([_Req(0)] * 150, 8, max_zero_slot_tasks_per_agent=100) == 2
+    assert prov.desired_new_instances([_Req(8, "a"), _Req(8, "a"), _Req(8, "a")], 8, max_slots={"a": 16}) == 2
+
+
+def _inst(i, state=prov.RUNNING, age=3600.0, now=10000.0):
+    return prov.Instance(i, i, state, now - age)
+
+
+def test_scale_decider_instance_states():
+    now = 10000.0
+    d = prov.ScaleDecider(600, 600, 600, 0, 10, clock=lambda: now)
+    insts = [_inst("stopped", prov.STOPPED), _inst("unconnected starting", age=60),
+             _inst("unconnected running", age=60), _inst("past disconnected"),
+             _inst("new disconnected"), _inst("long disconnected"), _inst("past idle"),
+             _inst("new idle"), _inst("long idle"), _inst("occupied")]
+    d.update_instance_snapshot(insts)
+    d.update_scaling_info(1, [{"name": "past disconnected"}, {"name": "past idle"},
+                              {"name": "new idle", "idle": True}, {"name": "long idle", "idle": True},
+                              {"name": "occupied"}])
+    d.disconnected = {"past disconnected": now - 3600, "long disconnected": now - 3600}
+    d.idle = {"past idle": now - 3600, "long idle": now - 3600}
+    d.calculate_instance_states()
+    assert d.disconnected == {"new disconnected": now, "long disconnected": now - 3600}
+    assert d.idle == {"new idle": now, "long idle": now - 3600}
+    assert d.long_disconnected == {"long disconnected": True}
+    assert d.long_idle == {"long idle": True}
+    assert d.stopped == {"stopped": True}
+    assert d.recently_launched == {"unconnected starting": True, "unconnected running": True}
+
+
+def test_scale_decider_terminate_and_launch():
+    now = 10000.0
+    d = prov.ScaleDecider(600, 600, 600, 1, 3, clock=lambda: now)
+    d.instances = {k: _inst(k) for k in ("a", "b", "c", "d", "e")}
+    d.stopped = {"a": True}
+    d.long_idle = {"b": True}
+    d.idle = {"b": now - 3600, "c": now}
+    term = d.find_instances_to_terminate()
+    assert term["a"] == prov.TERMINATE_STOPPED and term["b"] == prov.TERMINATE_LONG_IDLE
+    assert len(d.instances) - len(term) == 3  # trimmed to max_instances
+    # long-idle instances are kept down to min_instances
+    d2 = prov.ScaleDecider(600, 600, 600, 2, 5, clock=lambda: now)
+    d2.instances = {k: _inst(k) for k in ("x", "y")}
+    d2.long_idle = {"x": True, "y": True}
+    assert d2.find_instances_to_terminate() == {}
+    # launches: clamp(min - n, desired - recently_launched, max - n)
+    d3 = prov.ScaleDecider(600, 600, 600, 0, 4, clock=lambda: now)
+    d3.instances = {"r": _inst("r")}
+    d3.recently_launched = {"r": True}
+    d3.desired = 3
+    assert d3.num_instances_to_launch() == 2
+    d3.desired = 10
+    assert d3.num_instances_to_launch() == 3
+    d4 = prov.ScaleDecider(600, 600, 600, 2, 4, clock=lambda: now)
+    assert d4.num_instances_to_launch() == 2  # min_instances
+
+
+def test_aws_provider_against_fake_ec2():
+    ec2 = FakeEC2()
+    try:
+        p = prov.AWSProvider("gpu-pool", {"endpoint_url": ec2.url, "access_key": "AKIDEXAMPLE",
+                                          "secret_key": "s3cr3t", "region": "us-east-2",
+                                          "image_id": "ami-rocm", "instance_type": "mi355x.48xlarge",
+                                          "slots_per_instance": 8,
+                                          "custom_tags": [{"key": "team", "value": "llm"}]},
+                             "http://10.0.0.1:8080")
+        assert p.list() == []
+        p.launch(2)
+        insts = p.list()
+        assert len(insts) == 2 and all(i.state == prov.STARTING for i in insts)
+        rec = next(iter(ec2.instances.values()))
+        assert rec["tags"]["team"] == "llm" and rec["tags"]["determined-resource-pool"] == "gpu-pool"
+        ud = base64.b64decode(rec["user_data"]).decode()
+        assert "determined_clone_amd.agent --master http://10.0.0.1:8080 --resource-pool gpu-pool" in ud
+        run = [c for c in ec2.calls if c["Action"] == "RunInstances"][0]
+        assert run["ImageId"] == "ami-rocm" and run["InstanceType"] == "mi355x.48xlarge"
+        assert run["MaxCount"] == "2" and run["MetadataOptions.HttpTokens"] == "required"
+        p.terminate([insts[0].id])
+        assert len(p.list()) == 1
+        bad = prov.AWSProvider("gpu-pool", {"endpoint_url": ec2.url, "access_key": "WRONG",
+                                            "secret_key": "x"}, "http://m")
+        with pytest.raises(RuntimeError):
+            bad.list()
+    finally:
+        ec2.stop()
+
+
+def test_gcp_provider_against_fake_gce():
+    gce = FakeGCE()
+    try:
+        p = prov.GCPProvider("pool-a", {"endpoint_url": gce.url, "token": gce.token, "project": "proj",
+                                        "zone": "us-central1-a",
+                                        "instance_type": {"machine_type": "a3-mi355x", "gpu_num": 8}},
+                             "http://master.example.com:8080")
+        p.launch(3)
+        insts = p.list()
+        assert len(insts) == 3 and all(i.state == prov.STARTING for i in insts)
+        props = gce.bodies[0]["instanceProperties"]
+        assert props["labels"]["determined-master-host"] == "master-example-com"
+        assert "startup-script" in props["metadata"]["items"][0]["key"]
+        p.terminate([insts[0].id])
+        assert len(p.list()) == 2
+    finally:
+        gce.stop()
+
+
+def test_provisioner_scales_agent_pool_with_fake_ec2():
+    """Pending 16-slot request on an empty pool -> 2 instances launched; instances whose agents
+    connected and stayed idle past max_idle_agent_period are terminated."""
+    ec2 = FakeEC2()
+    tmp = tempfile.mkdtemp(prefix="det-prov-")
+    clock = [1_000_000.0]
+    try:
+        rm = ResourceManager()
+        p = prov.Provisioner("gpu", {"max_instances": 4, "max_idle_agent_period": "5m"},
+                             prov.AWSProvider("gpu", {"endpoint_url": ec2.url, "access_key": "AKIDEXAMPLE",
+                                                      "secret_key": "x", "slots_per_instance": 8},
+                                              "http://127.0.0.1:1"), clock=lambda: clock[0])
+        rm.attach_provisioner("gpu", p)
+        rm.allocate(AllocationRequest("a.0", "t", "job", 16, pool="gpu"))
+        p.provision()
+        assert len(ec2.instances) == 2
+        p.provision()  # recently launched instances are not launched again
+        assert len(ec2.instances) == 2
+        for iid in list(ec2.instances):  # instances boot, their agents register (idle)
+            ec2.instances[iid]["state"] = "running"
+            rm.register_agent(AgentState(iid, [{"id": i, "uuid": f"{iid}-{i}", "type": "rocm"}
+                                               for i in range(8)], "gpu"))
+        assert "a.0" in rm.running  # the 16-slot gang fits on the two new agents
+        rm.release("a.0")
+        p.provision()
+        clock[0] += 400  # idle past 5m
+        p.provision()
+        assert all(d["state"] == "terminated" for d in ec2.instances.values())
+        rm.close()
+    finally:
+        ec2.stop()
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_seconds_parser():
+    assert prov._seconds("20m") == 1200 and prov._seconds("1h30m") == 5400
+    assert prov._seconds("300ms") == pytest.approx(0.3) and prov._seconds(7) == 7.0
+
+
+def test_master_config_builds_pool_provisioner():
+    ec2 = FakeEC2()
+    tmp = tempfile.mkdtemp(prefix="det-prov-")
+    try:
+        m = Master(os.path.join(tmp, "m.db"), resource_pools=[{"pool_name": "gpu", "provider": {
+            "type": "aws", "endpoint_url": ec2.url, "access_key": "AKIDEXAMPLE", "secret_key": "x",
+            "slots_per_instance": 8, "action_cooldown": "1h"}}])
+        srv = MasterServer(m, "127.0.0.1", 0).start()
+        p = m.rm.provisioners["gpu"]
+        assert m.master_url in p.provider.user_data
+        srv.stop()
+    finally:
+        ec2.stop()
+        shutil.rmtree(tmp, ignore_errors=True)
