@@ -95,7 +95,7 @@ class Bottleneck(nn.Module):
                 y1, yd = pointwise_dual(self.conv1, ds_conv, x)
             identity = ds_bn(yd)
             out = self.bn1(y1)
-        out = self.bn2(self.conv2(out))
+        out = self.bn2(conv_ops.spatial_conv(self.conv2, out))
         # identity shortcut: x also feeds conv1, so its gradient can be summed inside the
         # producer's BN backward (no separate autograd add)
         return self.bn3(pointwise_conv(self.conv3, out, self.bn3.training), residual=identity,
@@ -136,7 +136,7 @@ class ResNet(nn.Module):
         # stem: conv -> fused BN + ReLU + 3x3/2 max-pool (the 112x112 pre-pool activation is never
         # written; its gradient is gathered inside the BN backward)
         bn = self.bn1
-        x = bn_ops.batch_norm_relu_maxpool(self.conv1(x), bn.weight, bn.bias, bn.running_mean,
+        x = bn_ops.batch_norm_relu_maxpool(conv_ops.spatial_conv(self.conv1, x), bn.weight, bn.bias, bn.running_mean,
                                            bn.running_var, training=bn.training,
                                            momentum=bn.momentum, eps=bn.eps,
                                            num_batches_tracked=bn.num_batches_tracked)

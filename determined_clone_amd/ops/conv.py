@@ -150,6 +150,8 @@ class _PointwiseLib(torch.autograd.Function):
         args = (dy, x, weight, None, [st, st], [0, 0], [1, 1], False, [0, 0], 1)
         bwd = torch.ops.aten.convolution_backward
         dx = dw = None
+        if ctx.needs_input_grad[1]:  # issued first: on the side stream it overlaps the dgrad
+            dw = _wgrad(args, weight)
         if ctx.needs_input_grad[0]:
             def lib():
                 return bwd(*args, [True, False, False])[0]
@@ -164,8 +166,6 @@ class _PointwiseLib(torch.autograd.Function):
                 dx = cands[_choose(("dgrad", tuple(x.shape), cout, st, x.dtype), cands)]()
             else:
                 dx = lib()
-        if ctx.needs_input_grad[1]:
-            dw = bwd(*args, [False, True, False])[1]
         return dx, dw, None
 
 
@@ -195,6 +195,8 @@ class _PointwiseDual(torch.autograd.Function):
         a1 = (dy1, x, w1, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
         a2 = (dy2, x, w2, None, [st, st], [0, 0], [1, 1], False, [0, 0], 1)
         dx = None
+        dw1 = _wgrad(a1, w1) if ctx.needs_input_grad[1] else None
+        dw2 = _wgrad(a2, w2) if ctx.needs_input_grad[2] else None
         if ctx.needs_input_grad[0]:
             W1 = w1.view(w1.shape[0], cin)
             c1 = (lambda: bwd(*a1, [True, False, False])[0],
@@ -209,8 +211,6 @@ class _PointwiseDual(torch.autograd.Function):
                 ho, wo = dy2.shape[2], dy2.shape[3]
                 small = torch.mm(_rows(dy2, 1), W2).view(n, ho, wo, cin)
                 dx.permute(0, 2, 3, 1)[:, ::st, ::st, :].add_(small)
-        dw1 = bwd(*a1, [False, True, False])[1] if ctx.needs_input_grad[1] else None
-        dw2 = bwd(*a2, [False, True, False])[1] if ctx.needs_input_grad[2] else None
         return dx, dw1, dw2, None
 
 
@@ -221,6 +221,53 @@ def pointwise_dual(conv1: nn.Conv2d, proj: nn.Conv2d, x: torch.Tensor):
         x = x.contiguous(memory_format=torch.channels_last)
         return _PointwiseDual.apply(x, conv1.weight, proj.weight, proj.stride[0])
     return pointwise_conv(conv1, x), pointwise_conv(proj, x)
+
+
+def _wgrad(args, weight: torch.Tensor) -> Optional[torch.Tensor]:
+    """Weight gradient of ``convolution_backward(*args)``: on the side stream (accumulated into
+    ``weight.grad``, returns None) when the parameter has a persistent ``.grad`` view
+    (``ops/_grad.py``; ``DCA_WGRAD_STREAM=0`` disables), else computed inline and returned."""
+    bwd = torch.ops.aten.convolution_backward
+    s = _grad.side_stream_for(weight)
+    if s is None:
+        return bwd(*args, [False, True, False])[1]
+    _grad.fork(s, (args[0], args[1]))
+    with torch.cuda.stream(s):
+        dw = bwd(*args, [False, True, False])[1]
+        _grad.target(weight).add_(dw)
+    return None
+
+
+class _SpatialConv(torch.autograd.Function):
+    """k x k convolution (no bias, groups 1) whose backward issues the weight gradient on the side
+    stream before the data gradient (``ops/_grad.py``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding):
+        ctx.save_for_backward(x, weight)
+        ctx.stride, ctx.padding = stride, padding
+        return F.conv2d(x, weight, None, stride, padding)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        args = (dy, x, w, None, list(ctx.stride), list(ctx.padding), [1, 1], False, [0, 0], 1)
+        dw = _wgrad(args, w) if ctx.needs_input_grad[1] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
+        return dx, dw, None, None
+
+
+def spatial_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """``conv(x)``; on a GPU its weight gradient runs on the side stream (``ops/_grad.py``)."""
+    if (_grad.SIDE_STREAM and x.is_cuda and conv.bias is None and conv.groups == 1
+            and conv.dilation == (1, 1) and isinstance(conv.padding, tuple) and conv.training
+            and conv.weight.requires_grad):
+        return _SpatialConv.apply(x.contiguous(memory_format=torch.channels_last), conv.weight,
+                                  conv.stride, conv.padding)
+    return conv(x)
 
 
 def _lib_supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:

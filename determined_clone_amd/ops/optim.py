@@ -20,7 +20,7 @@ from typing import Any, Callable, Dict, List, Optional
 
 import torch
 
-from determined_clone_amd.ops import _ext
+from determined_clone_amd.ops import _ext, _grad
 from determined_clone_amd.parallel.flat import FlatBuffer, FlatParamSpace
 
 
@@ -73,6 +73,7 @@ class FusedOptimizerBase(torch.optim.Optimizer):
     def prepare_grads(self, max_norm: float = 0.0, loss_scale: Optional[torch.Tensor] = None) -> None:
         """Compute (on device) the global grad norm, found_inf and the combined multiplier
         ``grad_multiplier / loss_scale * clip_coef`` consumed by the next :meth:`step`."""
+        _grad.join()
         self.space.ensure_views()
         if self.norm_group is not None or self.norm_exclude:
             slices = [st.buf.grad[a:b] for st in self.flat.values()
@@ -191,6 +192,7 @@ class FusedOptimizerBase(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure: Optional[Callable] = None) -> Any:  # type: ignore[override]
         loss = closure() if closure is not None else None
+        _grad.join()
         self.space.ensure_views()
         self._step += 1
         if self._dyn is not None and not torch.cuda.is_current_stream_capturing():

@@ -23,6 +23,7 @@ from typing import Any, Iterator, List, Optional
 import torch
 import torch.distributed as dist
 
+from determined_clone_amd.ops import _grad
 from determined_clone_amd.parallel.flat import FlatBuffer, FlatParamSpace
 
 logger = logging.getLogger("determined_clone_amd.parallel")
@@ -120,11 +121,15 @@ class GradientSync:
         return dist.ReduceOp.SUM
 
     def _launch(self, b: _Bucket) -> None:
-        t = b.buf.grad[b.start:b.end]
-        if self.comm_dtype is not None and t.dtype != self.comm_dtype:
-            b.comm = t.to(self.comm_dtype)
-            t = b.comm
-        b.work = dist.all_reduce(t, op=self._op(), group=self.group, async_op=True)
+        # weight gradients still running on the side stream (ops/_grad.py): issue the collective
+        # there, after the main stream's work so far, instead of stalling the main stream
+        side = _grad.comm_stream() if b.buf.grad.is_cuda else None
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            t = b.buf.grad[b.start:b.end]
+            if self.comm_dtype is not None and t.dtype != self.comm_dtype:
+                b.comm = t.to(self.comm_dtype)
+                t = b.comm
+            b.work = dist.all_reduce(t, op=self._op(), group=self.group, async_op=True)
         b.launched = True
 
     def finish(self) -> None:
@@ -136,6 +141,8 @@ class GradientSync:
             if not b.launched:
                 self._launch(b)
         self._next = len(self.buckets)
+        if self.space.buffers and next(iter(self.space.buffers.values())).grad.is_cuda:
+            _grad.join()
         manual_div = self.average and not self.fold_average and self._op() == dist.ReduceOp.SUM
         for b in self.buckets:
             if b.work is not None:

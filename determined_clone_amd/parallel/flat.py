@@ -149,6 +149,9 @@ class FlatParamSpace:
             p._dca_direct_grad = False
 
     def zero_grad(self) -> None:
+        from determined_clone_amd.ops import _grad
+
+        _grad.join()  # side-stream weight gradients may still be accumulating
         for buf in self.buffers.values():
             buf.grad.zero_()
         self.ensure_views()

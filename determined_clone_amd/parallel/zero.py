@@ -35,7 +35,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import torch
 import torch.distributed as dist
 
-from determined_clone_amd.ops import _ext
+from determined_clone_amd.ops import _ext, _grad
 from determined_clone_amd.ops import optim as fopt
 from determined_clone_amd.parallel.flat import ALIGN, FlatBuffer
 
@@ -164,6 +164,8 @@ class ZeroShardMixin:
     def _on_grad(self, p: torch.Tensor) -> None:
         if not self.sync_enabled:
             return
+        if p.is_cuda:
+            _grad.join()  # a reduce-scatter must see side-stream weight gradients (ops/_grad.py)
         st = self._param_state.get(id(p))
         if st is None:
             return

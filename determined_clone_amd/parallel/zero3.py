@@ -37,6 +37,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from determined_clone_amd.ops import _grad
 from determined_clone_amd.parallel.flat import ALIGN
 
 logger = logging.getLogger("determined_clone_amd.parallel.zero3")
@@ -224,6 +225,8 @@ class Zero3Partitioner:
 
     def _on_grad(self, u: _Unit):
         def hook(p: torch.Tensor) -> None:
+            if p.is_cuda:
+                _grad.join()  # side-stream weight gradients (ops/_grad.py) land before reducing
             if not u.in_backward:
                 # gradient produced without the output hook (e.g. a parameter used outside its
                 # unit's forward): adopt it into the unit's gradient buffer

@@ -185,3 +185,40 @@ def test_pointwise_dual_matches_two_convs(stride):
     _close(x1.grad, x2.grad, 2e-2, "dx")
     _close(c1.weight.grad, w1.grad, 2e-2, "dw1")
     _close(cp.weight.grad, wp.grad, 2e-2, "dwp")
+
+
+@pytest.mark.parametrize("model_fn", ["tiny"])
+def test_side_stream_weight_gradients_match_inline(monkeypatch, model_fn):
+    """DCA_WGRAD_STREAM: conv weight gradients on the side stream, accumulated into the flat
+    .grad views, match the inline path (same MIOpen solvers, same bf16 accumulation)."""
+    from determined_clone_amd.models import resnet
+    from determined_clone_amd.ops import _grad
+    from determined_clone_amd.ops import optim as fopt
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    model = resnet.to_mi355x_layout(resnet.resnet18_bottleneck_tiny(num_classes=10)).to(dev)
+    opt = fopt.FusedSGD(model.parameters(), lr=0.1, momentum=0.9)
+    x = torch.randn(16, 3, 64, 64, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device=dev)
+    grads = []
+    for side in (False, True):
+        monkeypatch.setattr(_grad, "SIDE_STREAM", side)
+        opt.zero_grad()
+        loss = F.cross_entropy(model(x).float(), y)
+        loss.backward()
+        if side:
+            assert _grad.pending()
+        _grad.join()
+        torch.cuda.synchronize()
+        grads.append([p.grad.clone() for p in model.parameters()])
+    for a, b in zip(*grads):
+        # MIOpen's split-K weight-gradient solvers reduce with atomics: compare in norm
+        a, b = a.float(), b.float()
+        assert (a - b).norm() <= 2e-2 * a.norm() + 1e-6
+    # the optimizer step joins by itself when the caller did not
+    monkeypatch.setattr(_grad, "SIDE_STREAM", True)
+    opt.zero_grad()
+    F.cross_entropy(model(x).float(), y).backward()
+    opt.step()
+    assert not _grad.pending()
