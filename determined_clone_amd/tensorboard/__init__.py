@@ -67,6 +67,19 @@ def encode_scalar_event(tag: str, value: float, step: int, wall_time: Optional[f
     return ev
 
 
+def encode_image_event(tag: str, png: bytes, height: int, width: int, step: int,
+                       channels: int = 3, wall_time: Optional[float] = None) -> bytes:
+    """Event with one Summary.Value.image (PNG-encoded) -- what TensorBoard's image dashboard
+    reads (field numbers of tensorflow/core/framework/summary.proto)."""
+    img = (_field(1, 0) + _varint(int(height)) + _field(2, 0) + _varint(int(width))
+           + _field(3, 0) + _varint(int(channels)) + _bytes_field(4, png))
+    val = _bytes_field(1, tag.encode()) + _bytes_field(4, img)
+    ev = _field(1, 1) + struct.pack("<d", wall_time or time.time())
+    ev += _field(2, 0) + _varint(int(step))
+    ev += _bytes_field(5, _bytes_field(1, val))
+    return ev
+
+
 def encode_file_version_event() -> bytes:
     return _field(1, 1) + struct.pack("<d", time.time()) + _bytes_field(3, b"brain.Event:2")
 
@@ -104,6 +117,18 @@ class EventFileWriter:
 
     def add_scalar(self, tag: str, value: float, step: int) -> None:
         self._write(encode_scalar_event(tag, value, step))
+
+    def add_image(self, tag: str, image: Any, step: int) -> None:
+        """``image``: HxWx3 uint8 array-like (or a PIL image); stored PNG-encoded."""
+        import io
+
+        from PIL import Image
+
+        im = image if hasattr(image, "save") else Image.fromarray(image)
+        buf = io.BytesIO()
+        im.save(buf, format="PNG")
+        self._write(encode_image_event(tag, buf.getvalue(), im.height, im.width, step,
+                                       len(im.getbands())))
 
     def flush(self) -> None:
         with self._lock:
