@@ -673,6 +673,70 @@ def cmd_kill(path: str):
     return f
 
 
+def _wait_service(s: Session, path: str, task_id: str, timeout: float = 120.0) -> str:
+    """Proxy URL of a running NTSC task once its service registered (``/proxy/<task_id>/``)."""
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        t = s.get(f"/api/v1/{path}/{task_id}")[path[:-1]]
+        if t.get("state") == "TERMINATED":
+            raise SystemExit(f"task {task_id} terminated")
+        if t.get("service_ready"):
+            return f"{s.master}/proxy/{task_id}/"
+        time.sleep(0.5)
+    raise SystemExit(f"task {task_id}: service not ready after {timeout:.0f}s")
+
+
+def ntsc_open(path: str):
+    """det notebook|tensorboard open ID: print (and try to open) the proxied URL."""
+    def f(args):
+        s = session(args)
+        url = _wait_service(s, path, args.task_id) + f"?token={s.token}"
+        print(url)
+        if not args.no_browser:
+            import webbrowser
+
+            webbrowser.open(url)
+    return f
+
+
+def shell_open(args):
+    """det shell open ID: interactive session over the master proxy (stdin lines -> terminal)."""
+    import threading
+
+    s = session(args)
+    base = _wait_service(s, "shells", args.task_id).rstrip("/")
+    state = {"next": 0, "closed": False}
+
+    def pump() -> None:
+        while not state["closed"]:
+            out = s.get(base[len(s.master):] + "/output", params={"since": state["next"], "wait": 10})
+            sys.stdout.write(out["data"])
+            sys.stdout.flush()
+            state["next"], state["closed"] = out["next"], out["closed"]
+
+    th = threading.Thread(target=pump, daemon=True)
+    th.start()
+    try:
+        for line in sys.stdin:
+            s.post(base[len(s.master):] + "/input", {"data": line})
+            if line.strip() == "exit":
+                break
+    except KeyboardInterrupt:
+        pass
+    time.sleep(0.5)
+    state["closed"] = True
+
+
+def shell_run(args):
+    """det shell run ID -- CMD...: one command in the shell task's container."""
+    s = session(args)
+    base = _wait_service(s, "shells", args.task_id).rstrip("/")
+    cmdline = " ".join(args.command[1:] if args.command[:1] == ["--"] else args.command)
+    out = s.post(base[len(s.master):] + "/run", {"cmd": cmdline})
+    sys.stdout.write(out["output"])
+    sys.exit(out["exit_code"])
+
+
 def workspace_list(args):
     render_table(session(args).get("/api/v1/workspaces")["workspaces"], ["id", "name", "num_projects", "archived"], args.json)
 
@@ -847,6 +911,13 @@ def build_parser() -> argparse.ArgumentParser:
             sp.add_argument("experiment_ids", nargs="*", type=int)
         cmd(g, "list ls", cmd_list(path))
         sp = cmd(g, "kill", cmd_kill(path)); sp.add_argument("task_id")
+        if kind in ("NOTEBOOK", "TENSORBOARD"):
+            sp = cmd(g, "open", ntsc_open(path)); sp.add_argument("task_id")
+            sp.add_argument("--no-browser", action="store_true")
+        if kind == "SHELL":
+            sp = cmd(g, "open", shell_open); sp.add_argument("task_id")
+            sp = cmd(g, "run", shell_run); sp.add_argument("task_id")
+            sp.add_argument("command", nargs=argparse.REMAINDER)
 
     w = group("workspace")
     cmd(w, "list ls", workspace_list)

@@ -29,6 +29,7 @@ from typing import List
 from determined_clone_amd.agent import agent as agent_mod
 from determined_clone_amd.agent import runtime
 from determined_clone_amd.common.api import Session
+from determined_clone_amd.util import routable_address
 
 logger = logging.getLogger("determined_clone_amd.exec.task_runner")
 
@@ -39,18 +40,6 @@ def _rank_from_env(default: int) -> int:
         if v is not None and v.strip().isdigit():
             return int(v)
     return default
-
-
-def _my_addr() -> str:
-    a = os.environ.get("DET_CONTAINER_ADDR")
-    if a:
-        return a
-    try:
-        with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
-            s.connect(("10.255.255.255", 1))
-            return s.getsockname()[0]
-    except OSError:
-        return "127.0.0.1"
 
 
 def rendezvous(session: Session, alloc_id: str, rank: int, n: int, addr: str) -> List[str]:
@@ -76,7 +65,7 @@ def main() -> int:
     n = int(spec.get("num_containers", 1))
     addrs = None
     if n > 1:
-        addrs = rendezvous(session, spec["allocation_id"], spec["container_rank"], n, _my_addr())
+        addrs = rendezvous(session, spec["allocation_id"], spec["container_rank"], n, routable_address())
     agent_id = os.environ.get("DET_AGENT_ID") or socket.gethostname()
     devices = agent_mod.detect_devices()
     wd = tempfile.mkdtemp(prefix="det-task-")

@@ -13,7 +13,6 @@ import argparse
 import html
 import json
 import os
-import socket
 import sys
 import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
@@ -22,6 +21,7 @@ from urllib.parse import parse_qs, urlparse
 
 from determined_clone_amd import _info
 from determined_clone_amd.tensorboard import read_scalars
+from determined_clone_amd.util import routable_address
 
 
 def collect(logdirs: Dict[str, str]) -> Dict[str, Dict[str, list]]:
@@ -99,8 +99,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     if a.experiment_ids:
         logdirs.update(_experiment_logdirs(a.experiment_ids))
     srv = make_server(logdirs, port=a.port)
-    host = socket.gethostname()
-    addr = f"http://{host}:{srv.server_address[1]}"
+    addr = f"http://{routable_address()}:{srv.server_address[1]}"
     print(f"serving tensorboard scalars at {addr}", flush=True)
     info = _info.get_cluster_info()
     if info is not None:

@@ -428,6 +428,11 @@ class Master:
                                            preemptible=False, name=name or kind.lower()))
         return {"id": task_id, "allocation_id": alloc_id, "state": "QUEUED", "type": kind}
 
+    def task_owner(self, task_id: str) -> Optional[int]:
+        """Owner user id of an NTSC task (None for trials / unknown tasks)."""
+        row = self.db.one("SELECT owner_id FROM tasks WHERE task_id=?", [task_id])
+        return row["owner_id"] if row else None
+
     # ------------------------------------------------------------------ agents
     def register_agent(self, body: Dict[str, Any]) -> None:
         a = AgentState(body["agent_id"], body.get("slots", []), body.get("resource_pool") or "default",

@@ -8,8 +8,11 @@ import logging
 import re
 import threading
 import time
+import http.cookies
 import traceback
+import urllib.error
 import urllib.parse
+import urllib.request
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
@@ -775,12 +778,19 @@ for _kind, _path in (("COMMAND", "commands"), ("SHELL", "shells"), ("NOTEBOOK", 
                 ep = ["bash", "-c", ep]
             if kind == "TENSORBOARD" and not ep:
                 ep = ["python3", "-m", "determined_clone_amd.exec.tensorboard"] + [str(x) for x in r.body.get("experiment_ids", [])]
-            if kind in ("NOTEBOOK", "SHELL") and not ep:
-                ep = ["python3", "-m", "determined_clone_amd.exec.idle"]
+            if kind == "NOTEBOOK" and not ep:
+                ep = ["python3", "-m", "determined_clone_amd.exec.notebook"]
+            if kind == "SHELL" and not ep:
+                ep = ["python3", "-m", "determined_clone_amd.exec.shell"]
             ctx = base64.b64decode(r.body["files"]) if r.body.get("files") else None
+            env = dict((cfg.get("environment") or {}).get("environment_variables") or {})
+            idle = cfg.get("idle_timeout")
+            if idle and kind in ("NOTEBOOK", "SHELL"):  # expconf duration ("30m") or seconds
+                from determined_clone_amd.master.provisioner import _seconds
+
+                env[f"DET_{kind}_IDLE_TIMEOUT"] = str(_seconds(idle))
             t = r.m.launch_command(kind, ep, int(res.get("slots", 0)), int(res.get("priority") or 42),
-                                   res.get("resource_pool") or "default",
-                                   (cfg.get("environment") or {}).get("environment_variables") or {},
+                                   res.get("resource_pool") or "default", env,
                                    r.user["id"], ctx, cfg.get("description"))
             return {path[:-1]: t}
 
@@ -793,7 +803,10 @@ for _kind, _path in (("COMMAND", "commands"), ("SHELL", "shells"), ("NOTEBOOK", 
             t = r.m.tasks.get(r.p["task_id"])
             if t is None or t.get("type") != kind:
                 raise HTTPError(404, f"{kind.lower()} not found")
-            return {path[:-1]: dict(t, id=t["task_id"])}
+            ready = any(a.task_id == t["task_id"] and a.proxy_address and not a.exited
+                        for a in list(r.m.allocations.values()))
+            return {path[:-1]: dict(t, id=t["task_id"], service_ready=ready,
+                                    proxy_path=f"/proxy/{t['task_id']}/")}
 
         @route("POST", f"/api/v1/{path}/{{task_id}}/kill")
         def kill_(r: Req, kind: str = kind) -> Any:
@@ -1262,6 +1275,8 @@ class _Handler(BaseHTTPRequestHandler):
         query = urllib.parse.parse_qs(parsed.query)
         length = int(self.headers.get("Content-Length") or 0)
         raw = self.rfile.read(length) if length else b""
+        if parsed.path.startswith("/proxy/"):
+            return self._proxy(method, parsed, query, raw)
         try:
             body = json.loads(raw) if raw else None
         except ValueError:
@@ -1289,6 +1304,59 @@ class _Handler(BaseHTTPRequestHandler):
                 logger.error(traceback.format_exc())
                 return self._send(500, {"error": f"{type(e).__name__}: {e}"})
         self._send(404, {"error": f"no route for {method} {parsed.path}"})
+
+    # ------------------------------------------------------------------ task proxy
+    def _proxy_user(self, query: Dict[str, List[str]]) -> Optional[Dict[str, Any]]:
+        hdr = self.headers.get("Authorization", "")
+        token = hdr[7:] if hdr.startswith("Bearer ") else None
+        if token is None:
+            cookies = http.cookies.SimpleCookie(self.headers.get("Cookie", ""))
+            token = cookies["auth"].value if "auth" in cookies else None
+        if token is None and query.get("token"):
+            token = query["token"][0]
+        return self.master.user_for_token(token) if token else None
+
+    def _proxy(self, method: str, parsed: Any, query: Dict[str, List[str]], raw: bytes) -> None:
+        """Reverse proxy ``/proxy/{task_id}/<path>`` to the service a task registered with
+        ``POST /api/v1/allocations/{id}/proxy_address`` (notebooks, shells, TensorBoards;
+        reference: `master/internal/proxy`). Authenticated by bearer token, the ``auth`` cookie
+        or ``?token=`` (browsers); a token in the query is moved into the cookie."""
+        parts = parsed.path.split("/", 3)
+        task_id = parts[2] if len(parts) > 2 else ""
+        rest = "/" + (parts[3] if len(parts) > 3 else "")
+        user = self._proxy_user(query)
+        if user is None:
+            return self._send(401, {"error": "unauthenticated"})
+        alloc = next((a for a in list(self.master.allocations.values())
+                      if a.task_id == task_id and not a.exited and a.proxy_address), None)
+        if alloc is None:
+            return self._send(404, {"error": f"no running service for task {task_id}"})
+        if not (user["admin"] or self.master.task_owner(task_id) in (None, user["id"])):
+            return self._send(403, {"error": "not the task owner"})
+        q = [(k, v) for k, vs in query.items() if k != "token" for v in vs]
+        url = alloc.proxy_address.rstrip("/") + rest + ("?" + urllib.parse.urlencode(q) if q else "")
+        fwd = {k: v for k, v in self.headers.items()
+               if k.lower() not in ("host", "authorization", "cookie", "content-length", "connection")}
+        fwd["X-Forwarded-Prefix"] = f"/proxy/{task_id}"
+        try:
+            req = urllib.request.Request(url, data=raw or None, method=method, headers=fwd)
+            try:
+                resp = urllib.request.urlopen(req, timeout=300)
+            except urllib.error.HTTPError as e:
+                resp = e
+            body = resp.read()
+            status = resp.status if hasattr(resp, "status") else resp.code
+            self.send_response(status)
+            for k, v in resp.headers.items():
+                if k.lower() not in ("transfer-encoding", "connection", "content-length", "server", "date"):
+                    self.send_header(k, v)
+            if query.get("token"):
+                self.send_header("Set-Cookie", f"auth={query['token'][0]}; Path=/proxy/{task_id}; HttpOnly")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+        except (urllib.error.URLError, OSError) as e:
+            self._send(502, {"error": f"task service unreachable: {e}"})
 
     def do_GET(self) -> None:
         self._dispatch("GET")

@@ -142,3 +142,19 @@ def write_user_code(path: pathlib.Path, on_cluster: bool) -> None:
 def chunks(lst: List[Any], n: int) -> Iterable[List[Any]]:
     for i in range(0, len(lst), n):
         yield lst[i:i + n]
+
+
+def routable_address() -> str:
+    """This container's address as other hosts reach it: ``DET_CONTAINER_ADDR`` (e.g. a pod IP),
+    else the source address of the default route, else 127.0.0.1 (no network)."""
+    import socket
+
+    a = os.environ.get("DET_CONTAINER_ADDR")
+    if a:
+        return a
+    try:
+        with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+            s.connect(("10.255.255.255", 1))
+            return s.getsockname()[0]
+    except OSError:
+        return "127.0.0.1"
