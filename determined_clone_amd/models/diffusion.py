@@ -12,8 +12,9 @@ guidance) and runs with random-init weights:
   ``ops/csrc/attention.hip`` (bf16, never materialising the score matrix; ``Sq != Sk`` for the
   77-token cross attention) -- the SD-2 convention (``attention_head_dim=64``) rather than SD-1's
   8 fixed heads, which would give 40/80/160-wide heads;
-* activations are NHWC bf16 on the GPU (MIOpen NHWC implicit-GEMM convolutions), GroupNorm /
-  LayerNorm statistics in fp32;
+* activations are NHWC bf16 on the GPU (MIOpen NHWC implicit-GEMM convolutions); every
+  GroupNorm (+ SiLU) is one fused NHWC HIP kernel family (``ops/csrc/groupnorm.hip``), statistics in
+  fp32/fp64;
 * ``UNetConfig.sd()`` is the SD-2-base UNet shape (320/640/1280/1280 channels, 2 layers per block,
   1024-wide context), ``.tiny()`` a small one for tests.
 
@@ -33,6 +34,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from determined_clone_amd.ops.groupnorm import GroupNormAct
 from determined_clone_amd.ops.transformer import flash_attention, reference_attention
 
 
@@ -135,18 +137,18 @@ def timestep_embedding(t: torch.Tensor, dim: int, max_period: float = 10000.0) -
 class ResnetBlock(nn.Module):
     def __init__(self, cin: int, cout: int, temb: Optional[int], groups: int) -> None:
         super().__init__()
-        self.norm1 = nn.GroupNorm(_groups(cin, groups), cin, eps=1e-5 if temb else 1e-6)
+        self.norm1 = GroupNormAct(_groups(cin, groups), cin, eps=1e-5 if temb else 1e-6, act=True)
         self.conv1 = nn.Conv2d(cin, cout, 3, padding=1)
         self.time_emb_proj = nn.Linear(temb, cout) if temb else None
-        self.norm2 = nn.GroupNorm(_groups(cout, groups), cout, eps=1e-5 if temb else 1e-6)
+        self.norm2 = GroupNormAct(_groups(cout, groups), cout, eps=1e-5 if temb else 1e-6, act=True)
         self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
         self.shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
 
     def forward(self, x: torch.Tensor, temb: Optional[torch.Tensor] = None) -> torch.Tensor:
-        h = self.conv1(F.silu(self.norm1(x)))
+        h = self.conv1(self.norm1(x))  # GroupNorm + SiLU: one fused NHWC kernel on the GPU
         if self.time_emb_proj is not None and temb is not None:
             h = h + self.time_emb_proj(F.silu(temb)).to(h.dtype)[:, :, None, None]
-        h = self.conv2(F.silu(self.norm2(h)))
+        h = self.conv2(self.norm2(h))
         return (x if self.shortcut is None else self.shortcut(x)) + h
 
 
@@ -202,7 +204,7 @@ class SpatialTransformer(nn.Module):
 
     def __init__(self, ch: int, head_dim: int, ctx_dim: int, groups: int) -> None:
         super().__init__()
-        self.norm = nn.GroupNorm(_groups(ch, groups), ch, eps=1e-6)
+        self.norm = GroupNormAct(_groups(ch, groups), ch, eps=1e-6)
         self.proj_in = nn.Linear(ch, ch)
         self.block = TransformerBlock(ch, head_dim, ctx_dim)
         self.proj_out = nn.Linear(ch, ch)
@@ -278,7 +280,7 @@ class UNet2DCondition(nn.Module):
                 cin = c
             blk.upsample = Upsample(c) if i < len(rev) - 1 else None
             self.up.append(blk)
-        self.norm_out = nn.GroupNorm(_groups(ch[0], g), ch[0], eps=1e-5)
+        self.norm_out = GroupNormAct(_groups(ch[0], g), ch[0], eps=1e-5, act=True)
         self.conv_out = nn.Conv2d(ch[0], cfg.out_channels, 3, padding=1)
 
     def forward(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
@@ -303,14 +305,14 @@ class UNet2DCondition(nn.Module):
                 h = h if isinstance(attn, nn.Identity) else attn(h, ctx)
             if blk.upsample is not None:
                 h = blk.upsample(h)
-        return self.conv_out(F.silu(self.norm_out(h)))
+        return self.conv_out(self.norm_out(h))
 
 
 # ============================================================================ VAE
 class _VAEAttention(nn.Module):
     def __init__(self, ch: int, groups: int) -> None:
         super().__init__()
-        self.norm = nn.GroupNorm(_groups(ch, groups), ch, eps=1e-6)
+        self.norm = GroupNormAct(_groups(ch, groups), ch, eps=1e-6)
         self.attn = MultiHeadAttention(ch, 64, bias=True)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -337,7 +339,7 @@ class AutoencoderKL(nn.Module):
             cin = c
         self.enc_mid = nn.ModuleList([ResnetBlock(ch[-1], ch[-1], None, g), _VAEAttention(ch[-1], g),
                                       ResnetBlock(ch[-1], ch[-1], None, g)])
-        self.enc_norm = nn.GroupNorm(_groups(ch[-1], g), ch[-1], eps=1e-6)
+        self.enc_norm = GroupNormAct(_groups(ch[-1], g), ch[-1], eps=1e-6, act=True)
         self.enc_out = nn.Conv2d(ch[-1], 2 * cfg.latent_channels, 3, padding=1)
         self.quant_conv = nn.Conv2d(2 * cfg.latent_channels, 2 * cfg.latent_channels, 1)
         self.post_quant_conv = nn.Conv2d(cfg.latent_channels, cfg.latent_channels, 1)
@@ -353,7 +355,7 @@ class AutoencoderKL(nn.Module):
                 mods.append(Upsample(c))
             self.dec_blocks.append(nn.ModuleList(mods))
             cin = c
-        self.dec_norm = nn.GroupNorm(_groups(ch[0], g), ch[0], eps=1e-6)
+        self.dec_norm = GroupNormAct(_groups(ch[0], g), ch[0], eps=1e-6, act=True)
         self.dec_out = nn.Conv2d(ch[0], cfg.in_channels, 3, padding=1)
 
     def encode(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -364,7 +366,7 @@ class AutoencoderKL(nn.Module):
                 h = m(h)
         for m in self.enc_mid:
             h = m(h)
-        moments = self.quant_conv(self.enc_out(F.silu(self.enc_norm(h))))
+        moments = self.quant_conv(self.enc_out(self.enc_norm(h)))
         mean, logvar = moments.chunk(2, dim=1)
         return mean, logvar.clamp(-30.0, 20.0)
 
@@ -380,7 +382,7 @@ class AutoencoderKL(nn.Module):
         for blk in self.dec_blocks:
             for m in blk:
                 h = m(h)
-        return self.dec_out(F.silu(self.dec_norm(h)))
+        return self.dec_out(self.dec_norm(h))
 
 
 # ============================================================================ text encoder
@@ -578,6 +580,18 @@ SCHEDULERS = {"ddim": DDIMScheduler, "pndm": PNDMScheduler}
 
 
 # ============================================================================ model + pipeline
+def to_mi355x_layout(module: nn.Module, device: torch.device, dtype: torch.dtype = torch.bfloat16):
+    """bf16 weights + NHWC on the GPU, GroupNorm affine parameters kept fp32 (read as fp32 by the
+    fused NHWC GroupNorm kernels)."""
+    module.to(device=device, dtype=dtype)
+    if device.type == "cuda":
+        module.to(memory_format=torch.channels_last)
+        for m in module.modules():
+            if isinstance(m, GroupNormAct):
+                m.float()
+    return module
+
+
 class LatentDiffusion(nn.Module):
     def __init__(self, cfg: LDMConfig) -> None:
         super().__init__()
@@ -588,11 +602,9 @@ class LatentDiffusion(nn.Module):
         self.tokenizer = HashTokenizer(cfg.text.vocab_size, cfg.text.max_length)
 
     def to_mi355x_layout(self, device: torch.device, dtype: torch.dtype = torch.bfloat16) -> "LatentDiffusion":
-        """GPU layout: bf16 weights, NHWC convolutions (norm statistics stay fp32 inside)."""
-        self.to(device=device, dtype=dtype)
-        if device.type == "cuda":
-            self.to(memory_format=torch.channels_last)
-        return self
+        """GPU layout: bf16 weights, NHWC convolutions; GroupNorm affine parameters stay fp32 (the
+        fused NHWC GroupNorm kernels read them as fp32)."""
+        return to_mi355x_layout(self, device, dtype)
 
     def encode_text(self, texts: Sequence[str]) -> torch.Tensor:
         ids = self.tokenizer(texts).to(self.text_encoder.final_ln.weight.device)

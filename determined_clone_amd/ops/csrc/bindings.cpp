@@ -450,6 +450,7 @@ void scale_(const Tensor& x, double s, const OptT& dev_scale) {
 // Extra kernel families register themselves from their own translation units.
 void register_transformer_ops(pybind11::module& m);
 void register_conv_ops(pybind11::module& m);
+void register_groupnorm_ops(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "determined_clone_amd MI355X (gfx950) HIP kernels";
@@ -485,4 +486,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("scale_", &scale_);
   register_transformer_ops(m);
   register_conv_ops(m);
+  register_groupnorm_ops(m);
 }

@@ -12,7 +12,8 @@ def category(name: str) -> str:
     n = name
     if "bn_" in n and "dca" in n:
         return "dca BatchNorm(+add+ReLU)"
-    if "sgd_kernel" in n or "adam_kernel" in n or "lamb" in n or "sumsq" in n or "norm_finalize" in n:
+    if "dca" in n and ("sgd_kernel" in n or "adam_kernel" in n or "lamb_" in n or "sumsq" in n
+                       or "norm_finalize" in n):
         return "dca optimizer"
     if "igemm_fwd" in n or "conv_fwd" in n or "ConvFwd" in n or ("fwd" in n and "conv" in n.lower()):
         return "conv fwd (MIOpen)"
@@ -20,6 +21,8 @@ def category(name: str) -> str:
         return "conv bwd-data (MIOpen)"
     if "wrw" in n or "bwd_weight" in n:
         return "conv bwd-weight (MIOpen)"
+    if "dca" in n and "attn" in n:
+        return "dca flash attention"
     if "gemm" in n.lower() or "Cijk" in n:
         return "gemm (fc)"
     if "fillBuffer" in n or "copyBuffer" in n:

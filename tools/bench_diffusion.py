@@ -1,6 +1,6 @@
 """Microbenchmark: SD2-base-shaped latent-diffusion UNet (865M params) training step on MI355X --
-bf16 NHWC, MFMA flash attention, fused HIP AdamW over the UNet -- and the textual-inversion step
-(frozen UNet, gradient only into the text-embedding rows). Prints one JSON line per mode.
+bf16 NHWC, MFMA flash attention, fused NHWC GroupNorm+SiLU, fused HIP AdamW over the UNet.
+Prints one JSON line (``DCA_GN_TORCH=1`` runs GroupNorm through PyTorch for an A/B).
 
 Usage: ``python tools/bench_diffusion.py [--batch 8 --res 512 --steps 10 --warmup 3]``.
 """
@@ -31,7 +31,7 @@ def main() -> None:
     torch.backends.cudnn.benchmark = True
     cfg = ldm.LDMConfig.preset(args.preset)
     torch.manual_seed(0)
-    unet = ldm.UNet2DCondition(cfg.unet).to(dev, torch.bfloat16).to(memory_format=torch.channels_last)
+    unet = ldm.to_mi355x_layout(ldm.UNet2DCondition(cfg.unet), dev)
     text = ldm.TextEncoder(cfg.text).to(dev, torch.bfloat16)
     opt = fopt.FusedAdamW(unet.parameters(), lr=1e-5)
     lat = args.res // 8
