@@ -1,0 +1,987 @@
+"""The rest of the master's v1 REST surface (reference: `proto/src/determined/api/v1/api.proto`,
+handlers in `master/internal/api_*.go`): bulk experiment actions and search, model-definition file
+tree, metric streams and comparisons, trial patch / workloads / metric reports, allocation
+bookkeeping (waiting, rendezvous, accelerator data, daemon resources), user settings and activity,
+telemetry, slots, job-queue v2 + stats, template patch, NTSC priorities and idle reports,
+model/checkpoint extras, resource-allocation accounting, workspace/project archive / move /
+columns / metric ranges, resource-pool <-> workspace bindings and webhook tests.
+
+Routes with a literal segment where an older route has a parameter (``/api/v1/tasks/count`` vs
+``/api/v1/tasks/{task_id}``) are registered ``first``.
+"""
+import base64
+import io
+import json
+import tarfile
+import time
+from typing import Any, Dict, List, Optional
+
+from determined_clone_amd.master.db import dec, now
+from determined_clone_amd.master.experiment import TERMINAL, experiment_row_to_api, trial_row_to_api
+from determined_clone_amd.master.server import (HTTPError, Req, _alloc, _exp, _int, _logs,
+                                                _project_workspace, _trial, require, route)
+from determined_clone_amd.master import server as S
+
+
+def _sub(r: Req, params: Dict[str, str], body: Any = None) -> Req:
+    """A request for another handler (same user, master and query)."""
+    return Req(r.m, params, r.q, body if body is not None else {}, r.user)
+
+
+def _kv(r: Req, key: str, default: Any) -> Any:
+    v = r.m.db.kv_get(key)
+    return json.loads(v) if v else default
+
+
+def _kv_set(r: Req, key: str, value: Any) -> None:
+    r.m.db.kv_set(key, json.dumps(value))
+
+
+# =========================================================================== users
+@route("GET", "/api/v1/auth/user")
+def current_user(r: Req) -> Any:
+    return {"user": S.Master.user_api(r.user)}
+
+
+@route("GET", "/api/v1/users/setting", first=True)
+def get_user_setting(r: Req) -> Any:
+    row = r.m.db.one("SELECT settings FROM users WHERE id=?", [r.user["id"]])
+    st = dec(row["settings"] if row else None, {}) or {}
+    return {"settings": [{"key": k, "value": v.get("value"), "store_path": v.get("store_path", "")}
+                         for k, v in sorted(st.items())]}
+
+
+@route("POST", "/api/v1/users/setting", first=True)
+def post_user_setting(r: Req) -> Any:
+    row = r.m.db.one("SELECT settings FROM users WHERE id=?", [r.user["id"]])
+    st = dec(row["settings"] if row else None, {}) or {}
+    for s in r.body.get("settings", []):
+        key = f"{s.get('store_path', '')}/{s['key']}" if s.get("store_path") else s["key"]
+        st[key] = {"value": s.get("value"), "store_path": s.get("store_path", "")}
+    r.m.db.update("users", "id", r.user["id"], {"settings": st})
+    return {}
+
+
+@route("POST", "/api/v1/users/setting/reset", first=True)
+def reset_user_setting(r: Req) -> Any:
+    r.m.db.update("users", "id", r.user["id"], {"settings": {}})
+    return {}
+
+
+@route("GET", "/api/v1/users/{username}/by-username", first=True)
+def user_by_username(r: Req) -> Any:
+    u = r.m.db.one("SELECT * FROM users WHERE username=?", [r.p["username"]])
+    if u is None:
+        raise HTTPError(404, "user not found")
+    return {"user": S.Master.user_api(u)}
+
+
+@route("PATCH", "/api/v1/users")
+def patch_users(r: Req) -> Any:
+    """Bulk activate / deactivate (``{"user_ids": [...], "activate": bool}``)."""
+    require(r, "ADMINISTRATE_USER")
+    results = []
+    for uid in r.body.get("user_ids", []):
+        if r.m.db.one("SELECT id FROM users WHERE id=?", [uid]) is None:
+            results.append({"id": uid, "error": "user not found"})
+            continue
+        r.m.db.update("users", "id", uid, {"active": int(bool(r.body.get("activate", True)))})
+        results.append({"id": uid, "error": ""})
+    return {"results": results}
+
+
+@route("PATCH", "/api/v1/users/assignments")
+def assign_multiple_groups(r: Req) -> Any:
+    require(r, "UPDATE_GROUP")
+    for uid in r.body.get("user_ids", []):
+        for gid in r.body.get("add_groups", []):
+            r.m.db.execute("INSERT OR IGNORE INTO group_members (group_id, user_id) VALUES (?, ?)", [gid, uid])
+        for gid in r.body.get("remove_groups", []):
+            r.m.db.execute("DELETE FROM group_members WHERE group_id=? AND user_id=?", [gid, uid])
+    return {}
+
+
+@route("POST", "/api/v1/users/activity")
+def post_user_activity(r: Req) -> Any:
+    act = _kv(r, f"activity:{r.user['id']}", {})
+    key = f"{r.body.get('entity_type', 'ENTITY_TYPE_PROJECT')}:{r.body.get('entity_id')}"
+    act[key] = {"activity_type": r.body.get("activity_type", "ACTIVITY_TYPE_GET"), "time": now()}
+    _kv_set(r, f"activity:{r.user['id']}", act)
+    return {}
+
+
+@route("GET", "/api/v1/user/projects/activity")
+def projects_by_activity(r: Req) -> Any:
+    act = _kv(r, f"activity:{r.user['id']}", {})
+    ids = [(v["time"], int(k.split(":")[1])) for k, v in act.items()
+           if k.startswith("ENTITY_TYPE_PROJECT:") and k.split(":")[1].isdigit()]
+    out = []
+    for _, pid in sorted(ids, reverse=True)[: _int(r.qget("limit", 100))]:
+        row = r.m.db.one("SELECT * FROM projects WHERE id=?", [pid])
+        if row:
+            out.append({"id": row["id"], "name": row["name"], "workspace_id": row["workspace_id"]})
+    return {"projects": out}
+
+
+# =========================================================================== master / agents
+@route("GET", "/api/v1/master/telemetry")
+def telemetry(r: Req) -> Any:
+    # this build never phones home (reference: segment.io when enabled in master.yaml)
+    return {"enabled": False, "segment_key": ""}
+
+
+@route("PATCH", "/api/v1/master/config")
+def patch_master_config(r: Req) -> Any:
+    """Runtime-adjustable master settings: the log level (reference: PatchMasterConfig)."""
+    require(r, "UPDATE_MASTER_CONFIG")
+    import logging
+
+    lvl = ((r.body.get("config") or {}).get("log") or {}).get("level")
+    if lvl:
+        logging.getLogger("determined_clone_amd").setLevel(str(lvl).upper())
+    return {"config": S.master_config(r)["config"]}
+
+
+def _slot_api(a: Any, i: int) -> Dict[str, Any]:
+    return {"id": str(i), "device": a.slots[i], "enabled": a.slot_enabled[i],
+            "container": {"id": a.slot_owner[i]} if a.slot_owner[i] else None, "draining": a.draining}
+
+
+@route("GET", "/api/v1/agents/{aid}/slots")
+def get_slots(r: Req) -> Any:
+    a = r.m.rm.agents.get(r.p["aid"])
+    if a is None:
+        raise HTTPError(404, "agent not found")
+    return {"slots": [_slot_api(a, i) for i in range(len(a.slots))]}
+
+
+@route("GET", "/api/v1/agents/{aid}/slots/{sid}")
+def get_slot(r: Req) -> Any:
+    a = r.m.rm.agents.get(r.p["aid"])
+    i = _int(r.p["sid"])
+    if a is None or not 0 <= i < len(a.slots):
+        raise HTTPError(404, "slot not found")
+    return {"slot": _slot_api(a, i)}
+
+
+# =========================================================================== experiments (bulk, search, files)
+def _bulk_ids(r: Req) -> List[int]:
+    ids = [int(i) for i in r.body.get("experiment_ids") or []]
+    f = r.body.get("filters")
+    if f is not None:
+        for row in r.m.db.all("SELECT * FROM experiments ORDER BY id"):
+            d = experiment_row_to_api(row, r.m.experiments.get(row["id"]))
+            if f.get("project_id") and d["project_id"] != f["project_id"]:
+                continue
+            if f.get("states") and d["state"] not in f["states"]:
+                continue
+            if "archived" in f and f["archived"] is not None and d["archived"] != bool(f["archived"]):
+                continue
+            if f.get("name") and f["name"] not in (d["name"] or ""):
+                continue
+            if f.get("labels") and not set(f["labels"]) <= set(d["labels"] or []):
+                continue
+            ids.append(d["id"])
+    return sorted(set(ids))
+
+
+def _bulk(action: Any, body_fn: Any = None):
+    def handler(r: Req) -> Any:
+        results = []
+        for eid in _bulk_ids(r):
+            try:
+                action(_sub(r, {"eid": str(eid)}, body_fn(r) if body_fn else {}))
+                results.append({"id": eid, "error": ""})
+            except HTTPError as e:
+                results.append({"id": eid, "error": str(e)})
+            except Exception as e:  # surfaced per experiment, like the reference's bulk results
+                results.append({"id": eid, "error": f"{type(e).__name__}: {e}"})
+        return {"results": results}
+    return handler
+
+
+for _verb, _fn in (("activate", S.exp_activate), ("pause", S.exp_pause), ("cancel", S.exp_cancel),
+                   ("kill", S.exp_kill), ("archive", S.exp_archive), ("unarchive", S.exp_unarchive)):
+    route("POST", f"/api/v1/experiments/{_verb}", first=True)(_bulk(_fn))
+route("DELETE", "/api/v1/experiments/delete", first=True)(_bulk(S.exp_delete))
+route("POST", "/api/v1/experiments/move", first=True)(
+    _bulk(S.move_experiment, lambda r: {"destination_project_id": r.body["destination_project_id"]}))
+
+
+@route("GET", "/api/v1/experiment/labels")
+def experiment_labels_v2(r: Req) -> Any:
+    return S.experiment_labels(r)
+
+
+@route("PUT", "/api/v1/experiments/{eid}/labels/{label}")
+def put_experiment_label(r: Req) -> Any:
+    e = _exp(r, "UPDATE_EXPERIMENT_METADATA")
+    labels = list(e.config.get("labels") or [])
+    if r.p["label"] not in labels:
+        labels.append(r.p["label"])
+    S.exp_patch(_sub(r, r.p, {"labels": labels}))
+    return {"labels": labels}
+
+
+@route("DELETE", "/api/v1/experiments/{eid}/labels/{label}")
+def delete_experiment_label(r: Req) -> Any:
+    e = _exp(r, "UPDATE_EXPERIMENT_METADATA")
+    labels = [x for x in e.config.get("labels") or [] if x != r.p["label"]]
+    S.exp_patch(_sub(r, r.p, {"labels": labels}))
+    return {"labels": labels}
+
+
+def _model_def_tar(r: Req) -> tarfile.TarFile:
+    row = r.m.db.one("SELECT model_definition FROM experiments WHERE id=?", [_int(r.p["eid"])])
+    if row is None:
+        raise HTTPError(404, "experiment not found")
+    return tarfile.open(fileobj=io.BytesIO(row["model_definition"] or b""), mode="r:*") \
+        if row["model_definition"] else tarfile.open(fileobj=io.BytesIO(_empty_tar()), mode="r:")
+
+
+def _empty_tar() -> bytes:
+    b = io.BytesIO()
+    tarfile.open(fileobj=b, mode="w").close()
+    return b.getvalue()
+
+
+@route("GET", "/api/v1/experiments/{eid}/file_tree")
+def model_def_tree(r: Req) -> Any:
+    """Nested file tree of the experiment's context directory (reference: GetModelDefTree)."""
+    root: Dict[str, Any] = {}
+    with _model_def_tar(r) as tf:
+        for m in tf.getmembers():
+            name = m.name.lstrip("./")
+            if not name:
+                continue
+            node = root
+            parts = name.split("/")
+            for p in parts[:-1]:
+                node = node.setdefault(p, {"__dir__": True})
+            if m.isdir():
+                node.setdefault(parts[-1], {"__dir__": True})
+            else:
+                node[parts[-1]] = {"__size__": m.size}
+
+    def conv(d: Dict[str, Any], prefix: str) -> List[Dict[str, Any]]:
+        out = []
+        for k, v in sorted(d.items()):
+            if k.startswith("__"):
+                continue
+            path = f"{prefix}{k}"
+            if "__size__" in v:
+                out.append({"path": path, "name": k, "is_dir": False, "content_length": v["__size__"]})
+            else:
+                out.append({"path": path, "name": k, "is_dir": True, "files": conv(v, path + "/")})
+        return out
+
+    return {"files": conv(root, "")}
+
+
+@route("POST", "/api/v1/experiments/{eid}/file")
+def model_def_file(r: Req) -> Any:
+    want = str(r.body.get("path", "")).lstrip("./")
+    with _model_def_tar(r) as tf:
+        for m in tf.getmembers():
+            if m.isfile() and m.name.lstrip("./") == want:
+                return {"file": base64.b64encode(tf.extractfile(m).read()).decode()}
+    raise HTTPError(404, f"file {want!r} not in the model definition")
+
+
+@route("GET", "/api/v1/experiments-search")
+def search_experiments(r: Req) -> Any:
+    """Experiments with their best trial (reference: SearchExperiments), filtered by project,
+    name substring and state, sorted by ``sort`` (``field[=asc|desc]``)."""
+    rows = r.m.db.all("SELECT * FROM experiments ORDER BY id")
+    out = []
+    for row in rows:
+        d = experiment_row_to_api(row, r.m.experiments.get(row["id"]))
+        if r.qget("project_id") and str(d["project_id"]) != r.qget("project_id"):
+            continue
+        flt = r.qget("filter")
+        if flt and flt not in (d["name"] or "") and flt != d["state"]:
+            continue
+        e = r.m.experiments.get(row["id"])
+        smaller = e.smaller_is_better if e else True
+        best = r.m.db.one("SELECT * FROM trials WHERE experiment_id=? AND best_validation IS NOT NULL "
+                          f"ORDER BY best_validation {'ASC' if smaller else 'DESC'} LIMIT 1", [row["id"]])
+        out.append({"experiment": d, "best_trial": trial_row_to_api(best) if best else None})
+    sort = r.qget("sort")
+    if sort:
+        key, _, order = sort.partition("=")
+        out.sort(key=lambda x: (x["experiment"].get(key) is None, x["experiment"].get(key)),
+                 reverse=order == "desc")
+    p = S._paginate(out, r)
+    return {"experiments": p["items"], "pagination": p["pagination"]}
+
+
+@route("DELETE", "/api/v1/experiments/{eid}/tensorboard-files")
+def delete_tensorboard_files(r: Req) -> Any:
+    import os
+    import shutil
+
+    e = _exp(r, "DELETE_EXPERIMENT")
+    cs = e.config.get("checkpoint_storage") or {}
+    root = cs.get("host_path") or cs.get("container_path")
+    if root:
+        if cs.get("storage_path"):
+            root = os.path.join(root, cs["storage_path"])
+        shutil.rmtree(os.path.join(root, "tensorboard", r.m.cluster_id, "experiment", str(e.id)),
+                      ignore_errors=True)
+    return {}
+
+
+# ---------------------------------------------------------------- metric streams
+def _trial_ids(r: Req, eid: int) -> List[int]:
+    return [t["id"] for t in r.m.db.all("SELECT id FROM trials WHERE experiment_id=? ORDER BY id", [eid])]
+
+
+@route("GET", "/api/v1/experiments/metrics-stream/metric-names")
+def exp_metric_names(r: Req) -> Any:
+    names: Dict[str, set] = {}
+    for eid in [_int(x) for x in r.qlist("ids")]:
+        for tid in _trial_ids(r, eid):
+            for row in r.m.db.all("SELECT grp, metrics FROM metrics WHERE trial_id=?", [tid]):
+                names.setdefault(row["grp"], set()).update((dec(row["metrics"], {}) or {}).keys())
+    return {"training_metrics": sorted(names.get("training", [])),
+            "validation_metrics": sorted(names.get("validation", [])),
+            "metric_names": [{"group": g, "name": n} for g, v in sorted(names.items()) for n in sorted(v)]}
+
+
+@route("GET", "/api/v1/experiments/{eid}/metrics-stream/batches")
+def exp_metric_batches(r: Req) -> Any:
+    grp = "validation" if r.qget("metric_type", "").upper().endswith("VALIDATION") else "training"
+    steps = set()
+    for tid in _trial_ids(r, _int(r.p["eid"])):
+        for row in r.m.db.all("SELECT steps_completed FROM metrics WHERE trial_id=? AND grp=?", [tid, grp]):
+            steps.add(row["steps_completed"])
+    return {"batches": sorted(steps)}
+
+
+@route("GET", "/api/v1/experiments/{eid}/metrics-stream/trials-snapshot")
+def exp_trials_snapshot(r: Req) -> Any:
+    name = r.qget("metric_name")
+    grp = "validation" if r.qget("metric_type", "").upper().endswith("VALIDATION") else "training"
+    batches = _int(r.qget("batches_processed", 0))
+    margin = _int(r.qget("batches_margin", 10))
+    out = []
+    for tid in _trial_ids(r, _int(r.p["eid"])):
+        row = r.m.db.one("SELECT * FROM metrics WHERE trial_id=? AND grp=? AND steps_completed BETWEEN ? AND ? "
+                         "ORDER BY ABS(steps_completed - ?) LIMIT 1",
+                         [tid, grp, batches - margin, batches + margin, batches])
+        if row is None:
+            continue
+        v = (dec(row["metrics"], {}) or {}).get(name)
+        if v is not None:
+            t = r.m.db.one("SELECT hparams FROM trials WHERE id=?", [tid])
+            out.append({"trial_id": tid, "hparams": dec(t["hparams"], {}), "metric": v,
+                        "batches_processed": row["steps_completed"]})
+    return {"trials": out}
+
+
+@route("GET", "/api/v1/experiments/{eid}/metrics-stream/trials-sample")
+def exp_trials_sample(r: Req) -> Any:
+    name = r.qget("metric_name")
+    grp = "validation" if r.qget("metric_type", "").upper().endswith("VALIDATION") else "training"
+    max_trials = _int(r.qget("max_trials", 25))
+    out = []
+    for tid in _trial_ids(r, _int(r.p["eid"]))[:max_trials]:
+        data = [{"batches": row["steps_completed"], "value": (dec(row["metrics"], {}) or {}).get(name),
+                 "time": row["end_time"]}
+                for row in r.m.db.all("SELECT * FROM metrics WHERE trial_id=? AND grp=? ORDER BY steps_completed",
+                                      [tid, grp])]
+        out.append({"trial": r.m.trial_api(tid), "data": [d for d in data if d["value"] is not None]})
+    return {"trials": out}
+
+
+# =========================================================================== trials
+@route("PATCH", "/api/v1/trials/{tid}")
+def patch_trial(r: Req) -> Any:
+    """Trial state change (only to a terminal state, i.e. kill) and user tags."""
+    t = _trial(r)
+    fields: Dict[str, Any] = {}
+    if "tags" in r.body:
+        fields["tags"] = r.body["tags"]
+    state = r.body.get("state")
+    if state:
+        if state.replace("STATE_", "") not in ("CANCELED", "COMPLETED", "ERROR"):
+            raise HTTPError(400, "a trial can only be moved to a terminal state")
+        t.exp.kill_trial(t)
+    if fields:
+        r.m.db.update("trials", "id", t.id, fields)
+    return {"trial": r.m.trial_api(t.id)}
+
+
+@route("GET", "/api/v1/trials/{tid}/workloads")
+def trial_workloads(r: Req) -> Any:
+    """Training / validation / checkpoint workloads of a trial in step order (reference:
+    GetTrialWorkloads; filter ``FILTER_OPTION_VALIDATION`` / ``CHECKPOINT``)."""
+    tid = _int(r.p["tid"])
+    flt = (r.qget("filter") or "").upper()
+    out = []
+    if "CHECKPOINT" not in flt:
+        for row in r.m.db.all("SELECT * FROM metrics WHERE trial_id=? ORDER BY steps_completed, id", [tid]):
+            if "VALIDATION" in flt and row["grp"] != "validation":
+                continue
+            kind = "validation" if row["grp"] == "validation" else "training"
+            out.append({kind: {"total_batches": row["steps_completed"], "metrics": {"avg_metrics": dec(row["metrics"], {})},
+                               "end_time": row["end_time"]}, "_k": (row["steps_completed"], 0)})
+    if "VALIDATION" not in flt:
+        for row in r.m.db.all("SELECT * FROM checkpoints WHERE trial_id=?", [tid]):
+            out.append({"checkpoint": {"uuid": row["uuid"], "total_batches": row["steps_completed"],
+                                       "state": row["state"], "end_time": row["report_time"]},
+                        "_k": (row["steps_completed"] or 0, 1)})
+    out.sort(key=lambda w: w.pop("_k") if "_k" in w else (0, 0))
+    p = S._paginate(out, r)
+    return {"workloads": p["items"], "pagination": p["pagination"]}
+
+
+@route("GET", "/api/v1/trials/{tid}/logs/fields")
+def trial_logs_fields(r: Req) -> Any:
+    row = r.m.db.one("SELECT task_id FROM trials WHERE id=?", [_int(r.p["tid"])])
+    if row is None:
+        raise HTTPError(404, "trial not found")
+    return task_logs_fields(_sub(r, {"task_id": row["task_id"]}))
+
+
+@route("GET", "/api/v1/tasks/{task_id}/logs/fields")
+def task_logs_fields(r: Req) -> Any:
+    rows = r.m.db.all("SELECT DISTINCT agent_id, container_id, rank_id, stdtype, source, level, allocation_id "
+                      "FROM task_logs WHERE task_id=?", [r.p["task_id"]])
+
+    def uniq(k: str) -> List[Any]:
+        return sorted({x[k] for x in rows if x[k] is not None}, key=str)
+
+    return {"agent_ids": uniq("agent_id"), "container_ids": uniq("container_id"), "rank_ids": uniq("rank_id"),
+            "stdtypes": uniq("stdtype"), "sources": uniq("source"), "levels": uniq("level"),
+            "allocation_ids": uniq("allocation_id")}
+
+
+@route("GET", "/api/v1/trials/time-series", first=True)
+def compare_trials(r: Req) -> Any:
+    names = set(r.qlist("metric_names"))
+    grp = r.qget("group")
+    out = []
+    for tid in [_int(x) for x in r.qlist("trial_ids")]:
+        series: Dict[str, List[Any]] = {}
+        for row in r.m.db.all("SELECT * FROM metrics WHERE trial_id=? ORDER BY steps_completed", [tid]):
+            if grp and row["grp"] != grp:
+                continue
+            for k, v in (dec(row["metrics"], {}) or {}).items():
+                if names and k not in names:
+                    continue
+                series.setdefault(f"{row['grp']}.{k}", []).append(
+                    {"steps_completed": row["steps_completed"], "value": v, "time": row["end_time"]})
+        out.append({"trial": r.m.trial_api(tid), "metrics": series})
+    return {"trials": out}
+
+
+def _metric_rows(r: Req, grp: Optional[str]) -> Any:
+    out = []
+    for tid in [_int(x) for x in r.qlist("trial_ids")]:
+        sql, args = "SELECT * FROM metrics WHERE trial_id=?", [tid]
+        g = grp or r.qget("group")
+        if g:
+            sql += " AND grp=?"
+            args.append(g)
+        for row in r.m.db.all(sql + " ORDER BY steps_completed, id", args):
+            out.append({"trial_id": tid, "trial_run_id": row["trial_run_id"], "group": row["grp"],
+                        "steps_completed": row["steps_completed"], "end_time": row["end_time"],
+                        "metrics": {"avg_metrics": dec(row["metrics"], {}),
+                                    "batch_metrics": dec(row["batch_metrics"], None)}})
+    return {"metrics": out}
+
+
+@route("GET", "/api/v1/trials/metrics/trial_metrics")
+def trial_metrics(r: Req) -> Any:
+    return _metric_rows(r, None)
+
+
+@route("GET", "/api/v1/trials/metrics/training_metrics")
+def training_metrics(r: Req) -> Any:
+    return _metric_rows(r, "training")
+
+
+@route("GET", "/api/v1/trials/metrics/validation_metrics")
+def validation_metrics(r: Req) -> Any:
+    return _metric_rows(r, "validation")
+
+
+def _report(group: str):
+    def handler(r: Req) -> Any:
+        m = r.body.get(f"{group}_metrics") or r.body.get("metrics") or {}
+        r.m.report_metrics(_int(r.p["tid"]), {"group": group, "metrics": m})
+        return {}
+    return handler
+
+
+route("POST", "/api/v1/trials/{tid}/training_metrics")(_report("training"))
+route("POST", "/api/v1/trials/{tid}/validation_metrics")(_report("validation"))
+
+
+@route("POST", "/api/v1/trial-source-info")
+def report_trial_source_info(r: Req) -> Any:
+    """Record that a trial was produced from / evaluated on a checkpoint (inference and
+    fine-tuning lineage; reference: ReportTrialSourceInfo)."""
+    info = r.body.get("trial_source_info") or r.body
+    src = _kv(r, "trial_source_info", [])
+    src.append({"trial_id": info.get("trial_id"), "checkpoint_uuid": info.get("checkpoint_uuid"),
+                "model_id": info.get("model_id"), "model_version": info.get("model_version"),
+                "source_type": info.get("trial_source_info_type", "TRIAL_SOURCE_INFO_TYPE_INFERENCE")})
+    _kv_set(r, "trial_source_info", src)
+    return {"trial_id": info.get("trial_id"), "checkpoint_uuid": info.get("checkpoint_uuid")}
+
+
+def _source_metrics(r: Req, pred: Any) -> Any:
+    out = []
+    for s in _kv(r, "trial_source_info", []):
+        if not pred(s) or s.get("trial_id") is None:
+            continue
+        tid = int(s["trial_id"])
+        for row in r.m.db.all("SELECT * FROM metrics WHERE trial_id=? ORDER BY steps_completed", [tid]):
+            if r.qget("trial_source_info_type") and r.qget("trial_source_info_type") != s["source_type"]:
+                continue
+            out.append({"trial_id": tid, "group": row["grp"], "steps_completed": row["steps_completed"],
+                        "metrics": {"avg_metrics": dec(row["metrics"], {})}})
+    return {"metrics": out}
+
+
+@route("GET", "/api/v1/checkpoints/{uuid}/metrics")
+def metrics_by_checkpoint(r: Req) -> Any:
+    return _source_metrics(r, lambda s: s.get("checkpoint_uuid") == r.p["uuid"])
+
+
+@route("GET", "/api/v1/trials/{tid}/profiler/available_series")
+def profiler_series(r: Req) -> Any:
+    rows = r.m.db.all("SELECT DISTINCT name FROM profiler_metrics WHERE trial_id=?", [_int(r.p["tid"])])
+    return {"labels": [{"trial_id": _int(r.p["tid"]), "name": x["name"]} for x in rows]}
+
+
+@route("POST", "/api/v1/trials/profiler/metrics")
+def profiler_metrics_batch(r: Req) -> Any:
+    for batch in r.body.get("batches", []):
+        tid = (batch.get("labels") or {}).get("trial_id")
+        for ts, vals in zip(batch.get("timestamps", []), batch.get("values", [])):
+            r.m.db.insert("profiler_metrics", {"trial_id": tid, "name": (batch.get("labels") or {}).get("name", "system"),
+                                               "ts": ts, "value": {"time": ts, "value": vals}})
+    return {}
+
+
+# =========================================================================== allocations / tasks
+@route("GET", "/api/v1/allocations/{aid}")
+def get_allocation(r: Req) -> Any:
+    row = r.m.db.one("SELECT * FROM allocations WHERE allocation_id=?", [r.p["aid"]])
+    a = r.m.allocations.get(r.p["aid"])
+    if row is None and a is None:
+        raise HTTPError(404, "allocation not found")
+    d = dict(row or {})
+    if a is not None:
+        d.update({"allocation_id": a.id, "task_id": a.task_id, "state": a.state, "ready": a.ready,
+                  "is_ready": a.ready, "proxy_address": a.proxy_address, "exit_code": a.exit_code})
+    d["agent_ids"] = dec(d.get("agent_ids"), []) if isinstance(d.get("agent_ids"), str) else d.get("agent_ids")
+    return {"allocation": d}
+
+
+@route("POST", "/api/v1/allocations/{aid}/waiting")
+def allocation_waiting(r: Req) -> Any:
+    a = _alloc(r)
+    a.state = "WAITING"
+    return {}
+
+
+@route("POST", "/api/v1/allocations/{aid}/signals/pending_preemption")
+def pending_preemption(r: Req) -> Any:
+    a = _alloc(r)
+    to = min(float(r.body.get("timeout_seconds", 60)), 3600)
+    return {"preempt": bool(a.preempt.wait(to))}
+
+
+@route("POST", "/api/v1/allocations/{aid}/resources/{rid}/daemon")
+def mark_daemon(r: Req) -> Any:
+    """A container that may be killed once its non-daemon peers exit (reference: sidecars)."""
+    a = _alloc(r)
+    a.spec.setdefault("daemon_resources", []).append(r.p["rid"])
+    return {}
+
+
+@route("GET", "/api/v1/allocations/{aid}/resources/{rid}/rendezvous")
+def rendezvous_info(r: Req) -> Any:
+    a = _alloc(r)
+    data = a.allgather.get("det-rendezvous") or []
+    addrs = [d["addr"] for d in sorted(data, key=lambda d: d["rank"])] if data else \
+        [(r.m.rm.agents[p["agent_id"]].addresses or ["127.0.0.1"])[0] if p["agent_id"] in r.m.rm.agents else "127.0.0.1"
+         for p in a.placements]
+    rank = next((i for i, p in enumerate(a.placements) if p["agent_id"] == r.p["rid"]), 0)
+    return {"rendezvous_info": {"addresses": addrs, "rank": rank,
+                                "slots": [len(p["slots"]) for p in a.placements]}}
+
+
+@route("POST", "/api/v1/allocations/{aid}/acceleratorData")
+def post_accelerator_data(r: Req) -> Any:
+    a = _alloc(r)
+    d = r.body.get("accelerator_data") or r.body
+    data = _kv(r, f"accel:{a.task_id}", [])
+    data.append(dict(d, allocation_id=a.id, task_id=a.task_id))
+    _kv_set(r, f"accel:{a.task_id}", data)
+    return {}
+
+
+@route("GET", "/api/v1/tasks/{task_id}/acceleratorData")
+def get_accelerator_data(r: Req) -> Any:
+    return {"accelerator_data": _kv(r, f"accel:{r.p['task_id']}", [])}
+
+
+@route("POST", "/api/v1/allocations/{aid}/notify_container_running")
+def notify_container_running(r: Req) -> Any:
+    """Containers of one allocation report RUNNING; returns once ``num_peers`` have (reference:
+    NotifyContainerRunning, used before the rendezvous)."""
+    a = _alloc(r)
+    n = int(r.body.get("num_peers", len(a.placements) or 1))
+    key = "det-container-running"
+    with a.allgather_cv:
+        lst = a.allgather.setdefault(key, [])
+        lst.append(r.body.get("node_name") or r.body.get("rank"))
+        a.allgather_cv.notify_all()
+        a.allgather_cv.wait_for(lambda: len(a.allgather[key]) >= n, timeout=600)
+        return {"data": list(a.allgather[key])}
+
+
+@route("GET", "/api/v1/tasks/{task_id}/context_directory")
+def task_context_directory(r: Req) -> Any:
+    return {"b64_tgz": S.task_context(r).get("b64_tgz", "")}
+
+
+@route("GET", "/api/v1/tasks/count", first=True)
+def active_tasks_count(r: Req) -> Any:
+    counts = {"commands": 0, "notebooks": 0, "shells": 0, "tensorboards": 0}
+    for t in r.m.tasks.values():
+        k = {"COMMAND": "commands", "NOTEBOOK": "notebooks", "SHELL": "shells",
+             "TENSORBOARD": "tensorboards"}.get(t.get("type"))
+        if k and t.get("state") != "TERMINATED":
+            counts[k] += 1
+    return counts
+
+
+for _kind, _path in (("COMMAND", "commands"), ("SHELL", "shells"), ("NOTEBOOK", "notebooks"),
+                     ("TENSORBOARD", "tensorboards")):
+    def _mk_prio(path: str) -> None:
+        @route("POST", f"/api/v1/{path}/{{task_id}}/set_priority")
+        def set_priority(r: Req) -> Any:
+            t = r.m.tasks.get(r.p["task_id"])
+            if t is None:
+                raise HTTPError(404, "task not found")
+            r.m.rm.set_job_priority(r.p["task_id"], int(r.body["priority"]))
+            t["priority"] = int(r.body["priority"])
+            return {path[:-1]: dict(t, id=r.p["task_id"])}
+
+    _mk_prio(_path)
+
+
+@route("PUT", "/api/v1/notebooks/{task_id}/report_idle")
+def notebook_report_idle(r: Req) -> Any:
+    t = r.m.tasks.get(r.p["task_id"])
+    if t is None:
+        raise HTTPError(404, "notebook not found")
+    t["idle"] = bool(r.body.get("idle", True))
+    return {}
+
+
+# =========================================================================== jobs / templates
+@route("GET", "/api/v1/job-queues-v2")
+def jobs_v2(r: Req) -> Any:
+    jobs = r.m.rm.queue()
+    pool = r.qget("resource_pool")
+    out = [{"summary": {"state": j["state"], "jobs_ahead": i}, "job": j} for i, j in enumerate(jobs)
+           if not pool or j.get("resource_pool") == pool]
+    return {"jobs": out}
+
+
+@route("GET", "/api/v1/job-queues/stats", first=True)
+def job_queue_stats(r: Req) -> Any:
+    stats: Dict[str, Dict[str, int]] = {}
+    for j in r.m.rm.queue():
+        s = stats.setdefault(j.get("resource_pool") or "default", {"queued_count": 0, "scheduled_count": 0})
+        s["queued_count" if j["state"] == "QUEUED" else "scheduled_count"] += 1
+    return {"results": [{"resource_pool": k, "stats": v} for k, v in sorted(stats.items())]}
+
+
+@route("POST", "/api/v1/templates/{name}", first=True)
+def post_template_named(r: Req) -> Any:
+    body = dict(r.body.get("template") or r.body)
+    return S.put_template(_sub(r, {"name": r.p["name"]}, body))
+
+
+@route("PATCH", "/api/v1/templates/{name}")
+def patch_template_config(r: Req) -> Any:
+    from determined_clone_amd.util import merge_dicts
+
+    row = r.m.db.one("SELECT * FROM templates WHERE name=?", [r.p["name"]])
+    if row is None:
+        raise HTTPError(404, "template not found")
+    cfg = merge_dicts(dec(row["config"], {}), r.body.get("config") or r.body)
+    return S.put_template(_sub(r, {"name": r.p["name"]}, {"config": cfg, "workspace_id": row["workspace_id"]}))
+
+
+# =========================================================================== models / checkpoints
+@route("POST", "/api/v1/models/{name}/move")
+def move_model(r: Req) -> Any:
+    row = r.m.db.one("SELECT * FROM models WHERE name=?", [r.p["name"]])
+    if row is None:
+        raise HTTPError(404, "model not found")
+    dest = _int(r.body.get("destination_workspace_id"))
+    require(r, "CREATE_MODEL_REGISTRY", dest)
+    r.m.db.update("models", "id", row["id"], {"workspace_id": dest})
+    return {}
+
+
+@route("GET", "/api/v1/model/labels")
+def model_labels(r: Req) -> Any:
+    labels: Dict[str, int] = {}
+    for row in r.m.db.all("SELECT labels FROM models"):
+        for l in dec(row["labels"], []) or []:
+            labels[l] = labels.get(l, 0) + 1
+    return {"labels": sorted(labels, key=lambda k: -labels[k])}
+
+
+@route("GET", "/api/v1/models/{name}/versions/{ver}/metrics")
+def metrics_by_model_version(r: Req) -> Any:
+    m = r.m.db.one("SELECT id FROM models WHERE name=?", [r.p["name"]])
+    if m is None:
+        raise HTTPError(404, "model not found")
+    return _source_metrics(r, lambda s: s.get("model_id") == m["id"] and
+                           str(s.get("model_version")) == r.p["ver"])
+
+
+@route("POST", "/api/v1/checkpoints/{uuid}/metadata")
+def post_checkpoint_metadata(r: Req) -> Any:
+    body = r.body.get("checkpoint") or r.body
+    return S.patch_checkpoint_md(_sub(r, {"uuid": r.p["uuid"]}, {"metadata": body.get("metadata", {})}))
+
+
+@route("PATCH", "/api/v1/checkpoints")
+def patch_checkpoints(r: Req) -> Any:
+    """Bulk checkpoint updates: resources (partial deletes) and state (reference: PatchCheckpoints)."""
+    uuids = [c["uuid"] for c in r.body.get("checkpoints", [])]
+    S._checkpoint_edit_check(r, uuids)
+    for c in r.body.get("checkpoints", []):
+        fields: Dict[str, Any] = {}
+        if "resources" in c and c["resources"] is not None:
+            res = (c["resources"] or {}).get("resources", c["resources"])
+            fields["resources"] = res
+            fields["size"] = sum(int(v) for v in res.values()) if isinstance(res, dict) else 0
+            if not res:
+                fields["state"] = "DELETED"
+        if c.get("state"):
+            fields["state"] = c["state"].replace("STATE_", "")
+        if fields:
+            r.m.db.update("checkpoints", "uuid", c["uuid"], fields)
+    return {}
+
+
+# =========================================================================== resource accounting
+def _alloc_rows(r: Req) -> List[Dict[str, Any]]:
+    start = float(r.qget("timestamp_after", 0) or 0)
+    end = float(r.qget("timestamp_before", 0) or 0) or now()
+    out = []
+    for row in r.m.db.all("SELECT * FROM allocations"):
+        s, e = row["start_time"] or 0.0, row["end_time"] or now()
+        if e < start or s > end:
+            continue
+        slots = row["slots"] or 0
+        a = r.m.allocations.get(row["allocation_id"])
+        if a is not None and a.placements:
+            slots = sum(len(p["slots"]) for p in a.placements)
+        secs = max(0.0, min(e, end) - max(s, start))
+        t = r.m.tasks.get(row["task_id"]) or {}
+        kind = t.get("type") or ("TRIAL" if row["task_id"] and "." in row["task_id"] else "UNKNOWN")
+        out.append({"allocation_id": row["allocation_id"], "task_id": row["task_id"], "kind": kind,
+                    "resource_pool": row["resource_pool"] or "default", "start_time": s,
+                    "end_time": row["end_time"], "slots": slots, "seconds": secs,
+                    "slot_seconds": slots * secs, "state": row["state"]})
+    return out
+
+
+@route("GET", "/api/v1/resources/allocation/raw")
+def allocation_raw(r: Req) -> Any:
+    return {"resource_entries": _alloc_rows(r)}
+
+
+@route("GET", "/api/v1/resources/allocation/aggregated")
+def allocation_aggregated(r: Req) -> Any:
+    """Slot-seconds per day, split by resource pool and task kind (reference:
+    ResourceAllocationAggregated, period ``RESOURCE_ALLOCATION_AGGREGATION_PERIOD_DAILY``)."""
+    by_day: Dict[str, Dict[str, Any]] = {}
+    for x in _alloc_rows(r):
+        day = time.strftime("%Y-%m-%d", time.gmtime(x["start_time"] or 0))
+        d = by_day.setdefault(day, {"period_start": day, "seconds": 0.0, "by_resource_pool": {},
+                                    "by_task_kind": {}})
+        d["seconds"] += x["slot_seconds"]
+        d["by_resource_pool"][x["resource_pool"]] = d["by_resource_pool"].get(x["resource_pool"], 0.0) + x["slot_seconds"]
+        d["by_task_kind"][x["kind"]] = d["by_task_kind"].get(x["kind"], 0.0) + x["slot_seconds"]
+    return {"resource_entries": [by_day[k] for k in sorted(by_day)]}
+
+
+# =========================================================================== workspaces / projects
+def _set_ws_archived(r: Req, value: int) -> Any:
+    wid = _int(r.p["wid"])
+    require(r, "ARCHIVE_WORKSPACE" if value else "UNARCHIVE_WORKSPACE", wid)
+    if r.m.db.one("SELECT id FROM workspaces WHERE id=?", [wid]) is None:
+        raise HTTPError(404, "workspace not found")
+    r.m.db.update("workspaces", "id", wid, {"archived": value})
+    return {}
+
+
+route("POST", "/api/v1/workspaces/{wid}/archive")(lambda r: _set_ws_archived(r, 1))
+route("POST", "/api/v1/workspaces/{wid}/unarchive")(lambda r: _set_ws_archived(r, 0))
+
+
+def _project(r: Req) -> Dict[str, Any]:
+    row = r.m.db.one("SELECT * FROM projects WHERE id=?", [_int(r.p["pid"])])
+    if row is None:
+        raise HTTPError(404, "project not found")
+    return row
+
+
+def _set_proj_archived(r: Req, value: int) -> Any:
+    p = _project(r)
+    require(r, "ARCHIVE_PROJECT" if value else "UNARCHIVE_PROJECT", p["workspace_id"])
+    r.m.db.update("projects", "id", p["id"], {"archived": value})
+    return {}
+
+
+route("POST", "/api/v1/projects/{pid}/archive")(lambda r: _set_proj_archived(r, 1))
+route("POST", "/api/v1/projects/{pid}/unarchive")(lambda r: _set_proj_archived(r, 0))
+
+
+@route("PUT", "/api/v1/projects/{pid}/notes")
+def put_project_notes(r: Req) -> Any:
+    p = _project(r)
+    notes = r.body.get("notes", [])
+    r.m.db.update("projects", "id", p["id"], {"notes": notes})
+    return {"notes": notes}
+
+
+@route("POST", "/api/v1/projects/{pid}/move")
+def move_project(r: Req) -> Any:
+    p = _project(r)
+    dest = _int(r.body.get("destination_workspace_id"))
+    require(r, "CREATE_PROJECT", dest)
+    if r.m.db.one("SELECT id FROM workspaces WHERE id=?", [dest]) is None:
+        raise HTTPError(404, "destination workspace not found")
+    r.m.db.update("projects", "id", p["id"], {"workspace_id": dest})
+    return {}
+
+
+def _project_experiments(r: Req, pid: int) -> List[Dict[str, Any]]:
+    return [row for row in r.m.db.all("SELECT * FROM experiments WHERE project_id=?", [pid])]
+
+
+@route("GET", "/api/v1/projects/{pid}/columns")
+def project_columns(r: Req) -> Any:
+    cols = [{"column": c, "location": "LOCATION_TYPE_EXPERIMENT", "type": t} for c, t in (
+        ("id", "COLUMN_TYPE_NUMBER"), ("name", "COLUMN_TYPE_TEXT"), ("state", "COLUMN_TYPE_TEXT"),
+        ("startTime", "COLUMN_TYPE_DATE"), ("searcherType", "COLUMN_TYPE_TEXT"),
+        ("numTrials", "COLUMN_TYPE_NUMBER"), ("user", "COLUMN_TYPE_TEXT"))]
+    hps, metrics = set(), set()
+    for row in _project_experiments(r, _int(r.p["pid"])):
+        hps.update((dec(row["config"], {}).get("hyperparameters") or {}).keys())
+        for t in r.m.db.all("SELECT summary_metrics FROM trials WHERE experiment_id=?", [row["id"]]):
+            for grp, vals in (dec(t["summary_metrics"], {}) or {}).items():
+                metrics.update(f"{grp}.{k}" for k in vals)
+    cols += [{"column": f"hp.{h}", "location": "LOCATION_TYPE_HYPERPARAMETERS", "type": "COLUMN_TYPE_UNSPECIFIED"}
+             for h in sorted(hps)]
+    cols += [{"column": m, "location": "LOCATION_TYPE_CUSTOM_METRIC" if not m.startswith(("training", "validation"))
+              else ("LOCATION_TYPE_VALIDATIONS" if m.startswith("validation") else "LOCATION_TYPE_TRAINING"),
+              "type": "COLUMN_TYPE_NUMBER"} for m in sorted(metrics)]
+    return {"columns": cols}
+
+
+@route("GET", "/api/v1/projects/{pid}/experiments/metric-ranges")
+def project_metric_ranges(r: Req) -> Any:
+    ranges: Dict[str, List[float]] = {}
+    for row in _project_experiments(r, _int(r.p["pid"])):
+        for t in r.m.db.all("SELECT summary_metrics FROM trials WHERE experiment_id=?", [row["id"]]):
+            for grp, vals in (dec(t["summary_metrics"], {}) or {}).items():
+                for k, s in vals.items():
+                    if isinstance(s, dict) and "min" in s:
+                        lo, hi = ranges.get(f"{grp}.{k}", [s["min"], s["max"]])
+                        ranges[f"{grp}.{k}"] = [min(lo, s["min"]), max(hi, s["max"])]
+    return {"ranges": [{"metrics_name": k, "min": v[0], "max": v[1]} for k, v in sorted(ranges.items())]}
+
+
+# ---------------------------------------------------------------- resource-pool bindings
+def _bindings(r: Req) -> Dict[str, List[int]]:
+    return _kv(r, "rp_bindings", {})
+
+
+@route("POST", "/api/v1/resource-pools/{pool}/workspace-bindings")
+def bind_rp(r: Req) -> Any:
+    r.require_admin()
+    b = _bindings(r)
+    cur = set(b.get(r.p["pool"], []))
+    cur.update(int(w) for w in r.body.get("workspace_ids", []))
+    b[r.p["pool"]] = sorted(cur)
+    _kv_set(r, "rp_bindings", b)
+    return {}
+
+
+@route("DELETE", "/api/v1/resource-pools/{pool}/workspace-bindings")
+def unbind_rp(r: Req) -> Any:
+    r.require_admin()
+    b = _bindings(r)
+    drop = {int(w) for w in r.body.get("workspace_ids", [])}
+    b[r.p["pool"]] = [w for w in b.get(r.p["pool"], []) if w not in drop]
+    _kv_set(r, "rp_bindings", b)
+    return {}
+
+
+@route("PUT", "/api/v1/resource-pools/{pool}/workspace-bindings")
+def overwrite_rp(r: Req) -> Any:
+    r.require_admin()
+    b = _bindings(r)
+    b[r.p["pool"]] = sorted({int(w) for w in r.body.get("workspace_ids", [])})
+    _kv_set(r, "rp_bindings", b)
+    return {}
+
+
+@route("GET", "/api/v1/resource-pools/{pool}/workspace-bindings")
+def list_rp_workspaces(r: Req) -> Any:
+    return {"workspace_ids": _bindings(r).get(r.p["pool"], [])}
+
+
+@route("GET", "/api/v1/workspaces/{wid}/available-resource-pools")
+def workspace_pools(r: Req) -> Any:
+    """Pools a workspace may use: unbound pools plus pools bound to it."""
+    wid = _int(r.p["wid"])
+    b = _bindings(r)
+    pools = [p["name"] for p in r.m.rm.pools()]
+    return {"resource_pool_names": [p for p in pools if not b.get(p) or wid in b[p]]}
+
+
+# =========================================================================== webhooks
+@route("POST", "/api/v1/webhooks/{wid}/test")
+def test_webhook(r: Req) -> Any:
+    require(r, "EDIT_WEBHOOKS")
+    row = r.m.db.one("SELECT * FROM webhooks WHERE id=?", [_int(r.p["wid"])])
+    if row is None:
+        raise HTTPError(404, "webhook not found")
+    import urllib.request
+
+    body = json.dumps({"event_type": "TEST", "event_data": {"message": "test webhook"},
+                       "timestamp": int(now())}).encode()
+    try:
+        urllib.request.urlopen(urllib.request.Request(row["url"], data=body, method="POST",
+                                                      headers={"Content-Type": "application/json"}), timeout=10)
+        return {"completed": True}
+    except Exception as e:
+        return {"completed": False, "error": str(e)}
+
+
+_ = TERMINAL, _project_workspace, _logs  # re-exported helpers used by extensions
+
+
+@route("PUT", "/api/v1/experiments/by-external-id/{external_experiment_id}", first=True)
+def put_experiment_by_external_id(r: Req) -> Any:
+    from determined_clone_amd.master import unmanaged_api
+
+    return unmanaged_api.put_experiment(_sub(r, {"external_id": r.p["external_experiment_id"]}, r.body))

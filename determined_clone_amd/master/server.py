@@ -34,11 +34,16 @@ class HTTPError(Exception):
         super().__init__(msg)
 
 
-def route(method: str, pattern: str, auth: bool = True) -> Callable[[Handler], Handler]:
+def route(method: str, pattern: str, auth: bool = True, first: bool = False) -> Callable[[Handler], Handler]:
+    """Register a handler; ``first`` puts it ahead of earlier routes (a literal path such as
+    ``/api/v1/tasks/count`` must win over ``/api/v1/tasks/{task_id}``)."""
     rx = re.compile("^" + re.sub(r"\{(\w+)\}", r"(?P<\1>[^/]+)", pattern) + "$")
 
     def deco(fn: Handler) -> Handler:
-        ROUTES.append((method, rx, fn, auth))
+        if first:
+            ROUTES.insert(0, (method, rx, fn, auth))
+        else:
+            ROUTES.append((method, rx, fn, auth))
         return fn
 
     return deco
@@ -1397,4 +1402,4 @@ class MasterServer:
 
 
 # routes that live in their own modules register on import
-from determined_clone_amd.master import rbac_api, unmanaged_api  # noqa: E402,F401
+from determined_clone_amd.master import api_extra, rbac_api, unmanaged_api  # noqa: E402,F401
