@@ -10,6 +10,7 @@ NeoX model with `fused_softmax`, `scaled_upper_triang_masked_softmax` and apex F
 Layouts are the ones the model produces without copies: activations [..., D] row-major,
 attention operands [B, S, H, Dh] (slices of the fused QKV projection are accepted as-is).
 """
+import contextlib
 import math
 import os
 from typing import Optional, Tuple
@@ -155,6 +156,8 @@ class _BiasGelu(torch.autograd.Function):
 
 
 _WGRAD_SPLITK = os.environ.get("DCA_WGRAD_SPLITK", "1") != "0"
+# linear-layer weight gradients on the side stream (ops/_grad.py); A/B switch
+LINEAR_SIDE_STREAM = os.environ.get("DCA_LINEAR_WGRAD_STREAM", "1") != "0"
 
 
 def _wgrad_splits(tokens: int, m: int, n: int) -> int:
@@ -197,19 +200,23 @@ class _Linear(torch.autograd.Function):
         w_param, b_param = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1]:  # first: on the side stream it overlaps the data gradient
             x2 = x.reshape(-1, x.shape[-1])
             acc = _grad.target(w_param)
             if acc is not None:
                 s = _wgrad_splits(dy2.shape[0], dy2.shape[1], x2.shape[1])
-                if s > 1:
-                    _wgrad_split_k(acc, dy2, x2, s)
-                else:
-                    acc.addmm_(dy2.t(), x2)
+                side = _grad.side_stream_for(w_param) if LINEAR_SIDE_STREAM else None
+                if side is not None:
+                    _grad.fork(side, (dy2, x2))
+                with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                    if s > 1:
+                        _wgrad_split_k(acc, dy2, x2, s)
+                    else:
+                        acc.addmm_(dy2.t(), x2)
             else:
                 dw = dy2.t() @ x2
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
         if b_param is not None and ctx.needs_input_grad[2]:
             acc = _grad.target(b_param)
             if dy2.shape[-1] % 8 == 0 and dy2.is_cuda:

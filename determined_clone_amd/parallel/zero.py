@@ -29,6 +29,7 @@ MI355X design, on top of the flat parameter space (`parallel/flat.py`):
 (DeepSpeed frees non-owned gradient memory; here the memory that matters -- fp32 master + moments --
 is what is partitioned).
 """
+import contextlib
 import logging
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -164,8 +165,6 @@ class ZeroShardMixin:
     def _on_grad(self, p: torch.Tensor) -> None:
         if not self.sync_enabled:
             return
-        if p.is_cuda:
-            _grad.join()  # a reduce-scatter must see side-stream weight gradients (ops/_grad.py)
         st = self._param_state.get(id(p))
         if st is None:
             return
@@ -188,17 +187,22 @@ class ZeroShardMixin:
     def _launch(self, st: _ShardState, b: _Bucket) -> None:
         g = st.buf.grad
         full = g[b.start:b.end]
-        if self.zero_stage >= 2 and self._nccl:
-            out = g[b.start + self.rank * b.chunk: b.start + (self.rank + 1) * b.chunk]
-            b.work = dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.pg,
-                                                async_op=True)
-        else:
-            b.work = dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        # weight gradients still running on the side stream (ops/_grad.py): issue the collective
+        # from there (after the main stream's work so far) instead of stalling the main stream
+        side = _grad.comm_stream() if g.is_cuda else None
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            if self.zero_stage >= 2 and self._nccl:
+                out = g[b.start + self.rank * b.chunk: b.start + (self.rank + 1) * b.chunk]
+                b.work = dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.pg,
+                                                    async_op=True)
+            else:
+                b.work = dist.all_reduce(full, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         b.launched = True
 
     def finish_grad_sync(self) -> None:
         """Launch any bucket not yet launched (unused params / overlap off) and wait for all."""
         if self.world == 1:
+            _grad.join()
             return
         self.space.ensure_views()
         for st in self._order:
@@ -212,6 +216,7 @@ class ZeroShardMixin:
                 b.launched = False
                 b.pending = b.nparams
             self._next[id(st)] = 0
+        _grad.join()
 
     def reset_grad_sync(self) -> None:
         for st in self._order:
@@ -221,6 +226,7 @@ class ZeroShardMixin:
 
     # ------------------------------------------------------------------ clip / overflow
     def prepare_grads(self, max_norm: float = 0.0, loss_scale: Optional[torch.Tensor] = None) -> None:
+        _grad.join()
         self.space.ensure_views()
         slices = [st.buf.grad[a:b] for st in self._order for a0, a1, _ in st.owned
                   for a, b in self._norm_ranges(st.buf, [(a0, a1)])]
@@ -233,6 +239,7 @@ class ZeroShardMixin:
     @torch.no_grad()
     def step(self, closure: Any = None) -> Any:  # type: ignore[override]
         loss = closure() if closure is not None else None
+        _grad.join()
         self.space.ensure_views()
         self._step += 1
         dev_scale = self._dev_scale
