@@ -25,6 +25,7 @@ import shutil
 import signal
 import socket
 import subprocess
+import sys
 import tempfile
 import threading
 import time
@@ -110,6 +111,17 @@ class Agent:
         self.workdir = workdir or tempfile.mkdtemp(prefix="det-clone-agent-")
         self._stop = threading.Event()
         self._lock = threading.Lock()
+        # pre-warmed fork server for task processes (exec/zygote.py), started in the background
+        self.zygote = None
+        threading.Thread(target=self._start_zygote, daemon=True).start()
+
+    def _start_zygote(self) -> None:
+        from determined_clone_amd.exec.zygote import ZygoteClient
+
+        try:
+            self.zygote = ZygoteClient.start(self.workdir)
+        except Exception as e:  # plain subprocesses still work
+            logger.warning(f"zygote unavailable: {e}")
 
     def register(self) -> None:
         self.session.post("/api/v1/agents/register", {
@@ -123,8 +135,15 @@ class Agent:
         ctx_dir = os.path.join(wd, "context")
         runtime.fetch_context(self.session, spec["task_id"], ctx_dir)
         cmd, env = runtime.build_task(spec, self.master_url, self.id, self.devices, ctx_dir)
-        proc = subprocess.Popen(cmd, cwd=ctx_dir, env=env, stdout=subprocess.PIPE,
-                                stderr=subprocess.STDOUT, start_new_session=True)
+        proc = None
+        if self.zygote is not None and len(cmd) >= 3 and cmd[0] == sys.executable and cmd[1] == "-m":
+            try:
+                proc = self.zygote.spawn(cmd[2], cmd[3:], env, ctx_dir)
+            except Exception as e:
+                logger.warning(f"zygote spawn failed ({e}); starting {cmd[2]} as a subprocess")
+        if proc is None:
+            proc = subprocess.Popen(cmd, cwd=ctx_dir, env=env, stdout=subprocess.PIPE,
+                                    stderr=subprocess.STDOUT, start_new_session=True)
         t = _Task(spec, proc, wd)
         with self._lock:
             self.tasks[alloc] = t
@@ -201,6 +220,8 @@ class Agent:
         self._stop.set()
         for alloc in list(self.tasks):
             self._kill(alloc, grace=2.0)
+        if self.zygote is not None:
+            self.zygote.close()
 
 
 def main() -> None:

@@ -5,8 +5,8 @@ Reads the experiment's ``entrypoint``:
   torch-distributed launcher when the trial has more than one slot);
 * anything else is a command line run as-is (it may itself call a launch layer, e.g.
   ``python3 -m determined_clone_amd.launch.torch_distributed python3 train.py``).
-The child is started as a subprocess (never exec'd, see the GPU-box rules) and its exit code is
-propagated.
+A single-slot class-based trial runs the harness in this process; anything else is started as a
+subprocess (never exec'd, see the GPU-box rules) and its exit code is propagated.
 """
 import os
 import shlex
@@ -46,6 +46,12 @@ def main() -> int:
     if not cmd:
         print("no entrypoint configured", file=sys.stderr)
         return 1
+    if cmd[:3] == [sys.executable, "-m", "determined_clone_amd.exec.harness"]:
+        # single-slot class-based trial: run the harness in this process (one interpreter start
+        # per trial instead of two; with the agent's zygote this process is already warm)
+        from determined_clone_amd.exec import harness
+
+        return harness.main(cmd[3])
     proc = subprocess.Popen(cmd)
     try:
         return proc.wait()
