@@ -786,10 +786,13 @@ def build_parser() -> argparse.ArgumentParser:
         sp.set_defaults(func=fn)
         return sp
 
+    groups: Dict[str, Any] = {}
+
     def group(names, help_=""):
         name, *aliases = names.split()
         g = sub.add_parser(name, aliases=aliases, help=help_)
-        return g.add_subparsers(dest="subcmd")
+        groups[name] = g.add_subparsers(dest="subcmd")
+        return groups[name]
 
     cmd(sub, "version", version)
     u = group("user u")
@@ -936,6 +939,10 @@ def build_parser() -> argparse.ArgumentParser:
     from determined_clone_amd.cli import rbac as rbac_cli
 
     rbac_cli.register(cmd, group)
+
+    from determined_clone_amd.cli import extra as extra_cli
+
+    extra_cli.register(cmd, group, groups.__getitem__)
 
     d = group("deploy")
     lo = d.add_parser("local").add_subparsers(dest="deploy_cmd")

@@ -151,3 +151,53 @@ def test_bulk_projects_workspaces_bindings(env):
     assert res[0]["error"] == ""
     with pytest.raises(APIException):
         s.get(f"/api/v1/experiments/{e2}")
+
+
+def _det(m, *argv):
+    import io
+    from contextlib import redirect_stdout
+
+    from determined_clone_amd.cli import cli
+
+    buf = io.StringIO()
+    with redirect_stdout(buf):
+        rc = cli.main(["-m", m.master_url, "-u", "admin", *argv])
+    assert rc in (0, None), buf.getvalue()
+    return buf.getvalue()
+
+
+def test_extra_cli_commands(env, tmp_path, monkeypatch):
+    m, s, eid, _ = env
+    monkeypatch.setenv("HOME", str(tmp_path))  # token cache
+    out = _det(m, "resources", "raw")
+    assert out.splitlines()[0].startswith("allocation_id,task_id,kind")
+    assert "period_start" in _det(m, "res", "agg")
+    assert len(_det(m, "dev", "auth-token").strip()) > 10
+    assert '"cluster_id"' in _det(m, "dev", "curl", "/api/v1/master")
+    assert "/api/v1/tasks/count" in _det(m, "dev", "bindings", "list")
+    _det(m, "workspace", "create", "cliws")
+    _det(m, "rp", "bindings", "add", "default", "cliws")
+    assert "cliws" in _det(m, "rp", "bindings", "list-workspaces", "default")
+    _det(m, "rp", "bindings", "replace", "default")
+    assert "default" in _det(m, "workspace", "list-pools", "Uncategorized")
+    _det(m, "project", "create", "cliws", "cp")
+    assert "cp" in _det(m, "workspace", "list-projects", "cliws")
+    _det(m, "project", "edit", "cliws", "cp", "--description", "d")
+    assert "(none)" in _det(m, "project", "list-experiments", "cliws", "cp")
+    cfgf = tmp_path / "tpl.yaml"
+    cfgf.write_text("resources:\n  slots_per_trial: 1\n")
+    _det(m, "template", "create", "t1", str(cfgf))
+    _det(m, "template", "set-value", "t1", "resources.priority=7")
+    assert "priority: 7" in _det(m, "template", "config", "t1")
+    _det(m, "user", "create", "bob")
+    _det(m, "user", "rename", "bob", "robert")
+    _det(m, "user", "edit", "robert", "--display-name", "Rob")
+    assert s.get("/api/v1/users/robert/by-username")["user"]["display_name"] == "Rob"
+    tid = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]["id"]
+    bundle = _det(m, "trial", "support-bundle", str(tid), "-o", str(tmp_path)).strip()
+    import tarfile
+
+    with tarfile.open(bundle) as tf:
+        assert {"trial.json", "metrics.json", "logs.txt"} <= set(tf.getnames())
+    _det(m, "master", "config", "set", "--log-level", "info")
+    assert "scheduler" in _det(m, "master", "config", "show")
