@@ -676,6 +676,39 @@ class Project:
         rows = self._session.get("/api/v1/experiments", params={"project_id": self.id})["experiments"]
         return [Experiment(self._session, e["id"], e) for e in rows]
 
+    def reload(self) -> None:
+        d = self._session.get(f"/api/v1/projects/{self.id}")["project"]
+        self.__init__(self._session, d)  # type: ignore[misc]
+
+    def archive(self) -> None:
+        self._session.post(f"/api/v1/projects/{self.id}/archive")
+        self.archived = True
+
+    def unarchive(self) -> None:
+        self._session.post(f"/api/v1/projects/{self.id}/unarchive")
+        self.archived = False
+
+    def set_description(self, description: str) -> None:
+        self._session.patch(f"/api/v1/projects/{self.id}", {"description": description})
+        self.description = description
+
+    def set_name(self, name: str) -> None:
+        self._session.patch(f"/api/v1/projects/{self.id}", {"name": name})
+        self.name = name
+
+    def add_note(self, name: str, contents: str) -> None:
+        self._session.post(f"/api/v1/projects/{self.id}/notes", {"name": name, "contents": contents})
+
+    def list_notes(self) -> List[Dict[str, Any]]:
+        return list(self._session.get(f"/api/v1/projects/{self.id}")["project"].get("notes") or [])
+
+    def move_to_workspace(self, workspace_name: str) -> None:
+        ws = [w for w in self._session.get("/api/v1/workspaces")["workspaces"] if w["name"] == workspace_name]
+        if not ws:
+            raise errors.NotFoundException(f"workspace {workspace_name} not found")
+        self._session.post(f"/api/v1/projects/{self.id}/move", {"destination_workspace_id": ws[0]["id"]})
+        self.workspace_id = ws[0]["id"]
+
     def __repr__(self) -> str:
         return f"Project(id={self.id}, name={self.name!r})"
 
@@ -704,8 +737,58 @@ class Workspace:
         return [m for m in (Model(self._session, x) for x in self._session.get("/api/v1/models")["models"])
                 if m.workspace_id == self.id]
 
+    def archive(self) -> None:
+        self._session.post(f"/api/v1/workspaces/{self.id}/archive")
+        self.archived = True
+
+    def unarchive(self) -> None:
+        self._session.post(f"/api/v1/workspaces/{self.id}/unarchive")
+        self.archived = False
+
+    def list_pools(self) -> List["ResourcePool"]:
+        names = self._session.get(f"/api/v1/workspaces/{self.id}/available-resource-pools")["resource_pool_names"]
+        return [ResourcePool(self._session, n) for n in names]
+
+    def delete_project(self, name: str) -> None:
+        self._session.delete(f"/api/v1/projects/{self.get_project(name).id}")
+
     def __repr__(self) -> str:
         return f"Workspace(id={self.id}, name={self.name!r})"
+
+
+class ResourcePool:
+    """A resource pool and its workspace bindings (reference: common/experimental/resource_pool.py)."""
+
+    def __init__(self, session: Session, name: str) -> None:
+        self._session = session
+        self.name = name
+
+    def _ids(self, workspace_names: List[str]) -> List[int]:
+        ws = {w["name"]: w["id"] for w in self._session.get("/api/v1/workspaces")["workspaces"]}
+        missing = [n for n in workspace_names if n not in ws]
+        if missing:
+            raise errors.NotFoundException(f"workspaces not found: {missing}")
+        return [ws[n] for n in workspace_names]
+
+    def add_bindings(self, workspace_names: List[str]) -> None:
+        self._session.post(f"/api/v1/resource-pools/{self.name}/workspace-bindings",
+                           {"workspace_ids": self._ids(workspace_names)})
+
+    def remove_bindings(self, workspace_names: List[str]) -> None:
+        self._session.request("DELETE", f"/api/v1/resource-pools/{self.name}/workspace-bindings",
+                              {"workspace_ids": self._ids(workspace_names)})
+
+    def replace_bindings(self, workspace_names: List[str]) -> None:
+        self._session.put(f"/api/v1/resource-pools/{self.name}/workspace-bindings",
+                          {"workspace_ids": self._ids(workspace_names)})
+
+    def list_workspaces(self) -> List[str]:
+        ids = self._session.get(f"/api/v1/resource-pools/{self.name}/workspace-bindings")["workspace_ids"]
+        names = {w["id"]: w["name"] for w in self._session.get("/api/v1/workspaces")["workspaces"]}
+        return [names[i] for i in ids if i in names]
+
+    def __repr__(self) -> str:
+        return f"ResourcePool(name={self.name!r})"
 
 
 # ---------------------------------------------------------------------------------- Determined
@@ -846,6 +929,13 @@ class Determined:
     def delete_workspace(self, name: str) -> None:
         self._session.delete(f"/api/v1/workspaces/{self.get_workspace(name).id}")
 
+    # resource pools
+    def list_resource_pools(self) -> List[ResourcePool]:
+        return [ResourcePool(self._session, p["name"]) for p in self._session.get("/api/v1/resource-pools")["resource_pools"]]
+
+    def get_resource_pool(self, name: str) -> ResourcePool:
+        return ResourcePool(self._session, name)
+
     # models
     def create_model(self, name: str, description: Optional[str] = "",
                      metadata: Optional[Dict[str, Any]] = None, labels: Optional[List[str]] = None,
@@ -958,6 +1048,8 @@ get_workspace = _export("get_workspace")
 list_workspaces = _export("list_workspaces")
 create_workspace = _export("create_workspace")
 delete_workspace = _export("delete_workspace")
+list_resource_pools = _export("list_resource_pools")
+get_resource_pool = _export("get_resource_pool")
 create_model = _export("create_model")
 get_model = _export("get_model")
 get_model_by_id = _export("get_model_by_id")
