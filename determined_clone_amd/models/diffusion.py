@@ -34,6 +34,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from determined_clone_amd.ops import conv as conv_ops
+from determined_clone_amd.ops import transformer as tops
 from determined_clone_amd.ops.groupnorm import GroupNormAct
 from determined_clone_amd.ops.transformer import flash_attention, reference_attention
 
@@ -44,6 +46,30 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = 
     if q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128):
         return flash_attention(q.contiguous(), k.contiguous(), v.contiguous(), causal=causal)
     return reference_attention(q.float(), k.float(), v.float(), causal).to(q.dtype)
+
+
+class Conv2d(nn.Conv2d):
+    """Convolution whose weight/bias gradients run on the side HIP stream (``ops/conv.py``)."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return conv_ops.spatial_conv(self, x)
+
+
+class Linear(nn.Linear):
+    """Linear layer with gradient accumulation into flat ``.grad`` views and side-stream weight
+    gradients on the GPU (``ops/transformer.py``)."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return tops.linear(x, self.weight, self.bias)
+
+
+class LayerNorm(nn.LayerNorm):
+    """LayerNorm on the fused HIP kernel (fp32 statistics) on the GPU."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.is_cuda:
+            return tops.layer_norm(x, self.weight, self.bias, self.eps)
+        return super().forward(x)
 
 
 def _groups(ch: int, want: int) -> int:
@@ -138,11 +164,11 @@ class ResnetBlock(nn.Module):
     def __init__(self, cin: int, cout: int, temb: Optional[int], groups: int) -> None:
         super().__init__()
         self.norm1 = GroupNormAct(_groups(cin, groups), cin, eps=1e-5 if temb else 1e-6, act=True)
-        self.conv1 = nn.Conv2d(cin, cout, 3, padding=1)
-        self.time_emb_proj = nn.Linear(temb, cout) if temb else None
+        self.conv1 = Conv2d(cin, cout, 3, padding=1)
+        self.time_emb_proj = Linear(temb, cout) if temb else None
         self.norm2 = GroupNormAct(_groups(cout, groups), cout, eps=1e-5 if temb else 1e-6, act=True)
-        self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
-        self.shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
+        self.conv2 = Conv2d(cout, cout, 3, padding=1)
+        self.shortcut = Conv2d(cin, cout, 1) if cin != cout else None
 
     def forward(self, x: torch.Tensor, temb: Optional[torch.Tensor] = None) -> torch.Tensor:
         h = self.conv1(self.norm1(x))  # GroupNorm + SiLU: one fused NHWC kernel on the GPU
@@ -160,10 +186,10 @@ class MultiHeadAttention(nn.Module):
         super().__init__()
         self.heads, self.head_dim, self.causal = max(1, dim // head_dim), head_dim, causal
         inner = self.heads * head_dim
-        self.to_q = nn.Linear(dim, inner, bias=bias)
-        self.to_k = nn.Linear(ctx_dim or dim, inner, bias=bias)
-        self.to_v = nn.Linear(ctx_dim or dim, inner, bias=bias)
-        self.to_out = nn.Linear(inner, dim)
+        self.to_q = Linear(dim, inner, bias=bias)
+        self.to_k = Linear(ctx_dim or dim, inner, bias=bias)
+        self.to_v = Linear(ctx_dim or dim, inner, bias=bias)
+        self.to_out = Linear(inner, dim)
 
     def forward(self, x: torch.Tensor, ctx: Optional[torch.Tensor] = None) -> torch.Tensor:
         c = x if ctx is None else ctx
@@ -178,8 +204,8 @@ class MultiHeadAttention(nn.Module):
 class GEGLU(nn.Module):
     def __init__(self, dim: int, mult: int = 4) -> None:
         super().__init__()
-        self.proj = nn.Linear(dim, dim * mult * 2)
-        self.out = nn.Linear(dim * mult, dim)
+        self.proj = Linear(dim, dim * mult * 2)
+        self.out = Linear(dim * mult, dim)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         h, gate = self.proj(x).chunk(2, dim=-1)
@@ -189,9 +215,9 @@ class GEGLU(nn.Module):
 class TransformerBlock(nn.Module):
     def __init__(self, dim: int, head_dim: int, ctx_dim: int) -> None:
         super().__init__()
-        self.norm1, self.attn1 = nn.LayerNorm(dim), MultiHeadAttention(dim, head_dim)
-        self.norm2, self.attn2 = nn.LayerNorm(dim), MultiHeadAttention(dim, head_dim, ctx_dim)
-        self.norm3, self.ff = nn.LayerNorm(dim), GEGLU(dim)
+        self.norm1, self.attn1 = LayerNorm(dim), MultiHeadAttention(dim, head_dim)
+        self.norm2, self.attn2 = LayerNorm(dim), MultiHeadAttention(dim, head_dim, ctx_dim)
+        self.norm3, self.ff = LayerNorm(dim), GEGLU(dim)
 
     def forward(self, x: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
         x = x + self.attn1(self.norm1(x))
@@ -205,9 +231,9 @@ class SpatialTransformer(nn.Module):
     def __init__(self, ch: int, head_dim: int, ctx_dim: int, groups: int) -> None:
         super().__init__()
         self.norm = GroupNormAct(_groups(ch, groups), ch, eps=1e-6)
-        self.proj_in = nn.Linear(ch, ch)
+        self.proj_in = Linear(ch, ch)
         self.block = TransformerBlock(ch, head_dim, ctx_dim)
-        self.proj_out = nn.Linear(ch, ch)
+        self.proj_out = Linear(ch, ch)
 
     def forward(self, x: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
         B, C, H, W = x.shape
@@ -220,7 +246,7 @@ class Downsample(nn.Module):
     def __init__(self, ch: int, asym_pad: bool = False) -> None:
         super().__init__()
         self.asym = asym_pad
-        self.conv = nn.Conv2d(ch, ch, 3, stride=2, padding=0 if asym_pad else 1)
+        self.conv = Conv2d(ch, ch, 3, stride=2, padding=0 if asym_pad else 1)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.asym:
@@ -231,7 +257,7 @@ class Downsample(nn.Module):
 class Upsample(nn.Module):
     def __init__(self, ch: int) -> None:
         super().__init__()
-        self.conv = nn.Conv2d(ch, ch, 3, padding=1)
+        self.conv = Conv2d(ch, ch, 3, padding=1)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
@@ -245,8 +271,8 @@ class UNet2DCondition(nn.Module):
         ch = cfg.block_out_channels
         temb = ch[0] * 4
         g, hd, cd = cfg.norm_groups, cfg.head_dim, cfg.cross_attention_dim
-        self.conv_in = nn.Conv2d(cfg.in_channels, ch[0], 3, padding=1)
-        self.time_mlp = nn.Sequential(nn.Linear(ch[0], temb), nn.SiLU(), nn.Linear(temb, temb))
+        self.conv_in = Conv2d(cfg.in_channels, ch[0], 3, padding=1)
+        self.time_mlp = nn.Sequential(Linear(ch[0], temb), nn.SiLU(), Linear(temb, temb))
         self.down = nn.ModuleList()
         skips = [ch[0]]
         cin = ch[0]
@@ -281,7 +307,7 @@ class UNet2DCondition(nn.Module):
             blk.upsample = Upsample(c) if i < len(rev) - 1 else None
             self.up.append(blk)
         self.norm_out = GroupNormAct(_groups(ch[0], g), ch[0], eps=1e-5, act=True)
-        self.conv_out = nn.Conv2d(ch[0], cfg.out_channels, 3, padding=1)
+        self.conv_out = Conv2d(ch[0], cfg.out_channels, 3, padding=1)
 
     def forward(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
         if t.dim() == 0:
@@ -328,7 +354,7 @@ class AutoencoderKL(nn.Module):
         super().__init__()
         self.cfg = cfg
         ch, g, n = cfg.block_out_channels, cfg.norm_groups, cfg.layers_per_block
-        self.enc_in = nn.Conv2d(cfg.in_channels, ch[0], 3, padding=1)
+        self.enc_in = Conv2d(cfg.in_channels, ch[0], 3, padding=1)
         self.enc_blocks = nn.ModuleList()
         cin = ch[0]
         for i, c in enumerate(ch):
@@ -340,10 +366,10 @@ class AutoencoderKL(nn.Module):
         self.enc_mid = nn.ModuleList([ResnetBlock(ch[-1], ch[-1], None, g), _VAEAttention(ch[-1], g),
                                       ResnetBlock(ch[-1], ch[-1], None, g)])
         self.enc_norm = GroupNormAct(_groups(ch[-1], g), ch[-1], eps=1e-6, act=True)
-        self.enc_out = nn.Conv2d(ch[-1], 2 * cfg.latent_channels, 3, padding=1)
-        self.quant_conv = nn.Conv2d(2 * cfg.latent_channels, 2 * cfg.latent_channels, 1)
-        self.post_quant_conv = nn.Conv2d(cfg.latent_channels, cfg.latent_channels, 1)
-        self.dec_in = nn.Conv2d(cfg.latent_channels, ch[-1], 3, padding=1)
+        self.enc_out = Conv2d(ch[-1], 2 * cfg.latent_channels, 3, padding=1)
+        self.quant_conv = Conv2d(2 * cfg.latent_channels, 2 * cfg.latent_channels, 1)
+        self.post_quant_conv = Conv2d(cfg.latent_channels, cfg.latent_channels, 1)
+        self.dec_in = Conv2d(cfg.latent_channels, ch[-1], 3, padding=1)
         self.dec_mid = nn.ModuleList([ResnetBlock(ch[-1], ch[-1], None, g), _VAEAttention(ch[-1], g),
                                       ResnetBlock(ch[-1], ch[-1], None, g)])
         self.dec_blocks = nn.ModuleList()
@@ -356,7 +382,7 @@ class AutoencoderKL(nn.Module):
             self.dec_blocks.append(nn.ModuleList(mods))
             cin = c
         self.dec_norm = GroupNormAct(_groups(ch[0], g), ch[0], eps=1e-6, act=True)
-        self.dec_out = nn.Conv2d(ch[0], cfg.in_channels, 3, padding=1)
+        self.dec_out = Conv2d(ch[0], cfg.in_channels, 3, padding=1)
 
     def encode(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """Images in [-1, 1] -> (mean, logvar) of the latent posterior."""
@@ -423,13 +449,13 @@ class TextEncoder(nn.Module):
         self.layers = nn.ModuleList()
         for _ in range(cfg.layers):
             layer = nn.Module()
-            layer.ln1 = nn.LayerNorm(d)
+            layer.ln1 = LayerNorm(d)
             layer.attn = MultiHeadAttention(d, cfg.head_dim, bias=True, causal=True)
-            layer.ln2 = nn.LayerNorm(d)
-            layer.fc1 = nn.Linear(d, 4 * d)
-            layer.fc2 = nn.Linear(4 * d, d)
+            layer.ln2 = LayerNorm(d)
+            layer.fc1 = Linear(d, 4 * d)
+            layer.fc2 = Linear(4 * d, d)
             self.layers.append(layer)
-        self.final_ln = nn.LayerNorm(d)
+        self.final_ln = LayerNorm(d)
 
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         pos = torch.arange(ids.shape[1], device=ids.device)

@@ -239,14 +239,15 @@ def _wgrad(args, weight: torch.Tensor) -> Optional[torch.Tensor]:
 
 
 class _SpatialConv(torch.autograd.Function):
-    """k x k convolution (no bias, groups 1) whose backward issues the weight gradient on the side
-    stream before the data gradient (``ops/_grad.py``)."""
+    """k x k convolution (groups 1, optional bias) whose backward issues the weight (and bias)
+    gradient on the side stream before the data gradient (``ops/_grad.py``)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, padding):
+    def forward(ctx, x, weight, bias, stride, padding):
         ctx.save_for_backward(x, weight)
         ctx.stride, ctx.padding = stride, padding
-        return F.conv2d(x, weight, None, stride, padding)
+        ctx.bias = bias
+        return F.conv2d(x, weight, bias, stride, padding)
 
     @staticmethod
     def backward(ctx, dy):
@@ -254,20 +255,34 @@ class _SpatialConv(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         args = (dy, x, w, None, list(ctx.stride), list(ctx.padding), [1, 1], False, [0, 0], 1)
         dw = _wgrad(args, w) if ctx.needs_input_grad[1] else None
+        db = _bgrad(dy, ctx.bias) if ctx.bias is not None and ctx.needs_input_grad[2] else None
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
-        return dx, dw, None, None
+        return dx, dw, db, None, None
+
+
+def _bgrad(dy: torch.Tensor, bias: torch.Tensor) -> Optional[torch.Tensor]:
+    """Bias gradient (sum of dy over N, H, W): on the side stream into ``bias.grad`` when it is a
+    persistent view, else returned to autograd."""
+    s = _grad.side_stream_for(bias)
+    if s is None:
+        return dy.sum((0, 2, 3), dtype=torch.float32).to(bias.dtype)
+    _grad.fork(s, (dy,))
+    with torch.cuda.stream(s):
+        _grad.target(bias).add_(dy.sum((0, 2, 3), dtype=torch.float32).to(bias.dtype))
+    return None
 
 
 def spatial_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
-    """``conv(x)``; on a GPU its weight gradient runs on the side stream (``ops/_grad.py``)."""
-    if (_grad.SIDE_STREAM and x.is_cuda and conv.bias is None and conv.groups == 1
-            and conv.dilation == (1, 1) and isinstance(conv.padding, tuple) and conv.training
-            and conv.weight.requires_grad):
+    """``conv(x)``; on a GPU its weight (and bias) gradient runs on the side stream
+    (``ops/_grad.py``)."""
+    if (_grad.SIDE_STREAM and x.is_cuda and conv.groups == 1 and conv.dilation == (1, 1)
+            and isinstance(conv.padding, tuple) and conv.training and conv.weight.requires_grad
+            and conv.padding_mode == "zeros"):
         return _SpatialConv.apply(x.contiguous(memory_format=torch.channels_last), conv.weight,
-                                  conv.stride, conv.padding)
-    return conv(x)
+                                  conv.bias, conv.stride, conv.padding)
+    return nn.Conv2d.forward(conv, x)  # (not conv(x): subclasses route their forward here)
 
 
 def _lib_supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:

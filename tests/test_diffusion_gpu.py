@@ -62,3 +62,27 @@ def test_textual_inversion_steps_on_gpu():
     assert torch.equal(base, tr.model.text_encoder.token_embedding.original.weight)
     imgs = tr.generate(["a det-logo"], seed=1)
     assert imgs.shape == (1, 64, 64, 3)
+
+
+def test_unet_flat_grads_side_stream_match_autograd():
+    """Fused linear / LayerNorm / GroupNorm / conv paths accumulating into flat .grad views
+    (side-stream weight gradients included) give the same gradients as plain autograd."""
+    import copy
+
+    from determined_clone_amd.ops import _grad
+    from determined_clone_amd.parallel.flat import FlatParamSpace
+
+    torch.manual_seed(0)
+    ref = ldm.to_mi355x_layout(ldm.UNet2DCondition(ldm.UNetConfig.tiny()), torch.device("cuda"))
+    m = copy.deepcopy(ref)
+    FlatParamSpace([[p for p in m.parameters() if p.dtype == torch.bfloat16],
+                    [p for p in m.parameters() if p.dtype == torch.float32]])
+    z = torch.randn(2, 4, 16, 16, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    ctx = torch.randn(2, 16, 64, device="cuda").bfloat16()
+    t = torch.tensor([3, 600], device="cuda")
+    m(z, t, ctx).float().square().mean().backward()
+    _grad.join()
+    ref(z, t, ctx).float().square().mean().backward()
+    for (n, a), b in zip(m.named_parameters(), ref.parameters()):
+        ga, gb = a.grad.float(), b.grad.float()
+        assert (ga - gb).norm() <= 3e-2 * gb.norm() + 1e-4, n
