@@ -149,6 +149,10 @@ class GradientSync:
                 b.work.wait()
             if b.comm is not None:
                 b.buf.grad[b.start:b.end].copy_(b.comm)
+                if b.comm.is_cuda:
+                    # allocated on the comm stream, last read here: keep it alive until this
+                    # stream's copy has run before the allocator can hand it out again
+                    b.comm.record_stream(torch.cuda.current_stream())
                 b.comm = None
             if manual_div:
                 b.buf.grad[b.start:b.end].div_(self.world)
