@@ -28,6 +28,7 @@ import signal
 import socket
 import sys
 import threading
+import time
 import traceback
 from typing import Any, Dict, List, Optional
 
@@ -118,6 +119,15 @@ def serve(path: str) -> None:
     srv.bind(path)
     srv.listen(64)
     print("ready", flush=True)
+    parent = os.getppid()
+
+    def watchdog() -> None:  # the agent died without stopping us: do not linger as an orphan
+        while True:
+            time.sleep(2.0)
+            if os.getppid() != parent:
+                os._exit(0)
+
+    threading.Thread(target=watchdog, daemon=True).start()
     quiet = os.open(os.devnull, os.O_WRONLY)  # nobody reads our pipe after "ready"
     os.dup2(quiet, 1)
     os.dup2(quiet, 2)
