@@ -1282,6 +1282,8 @@ class _Handler(BaseHTTPRequestHandler):
         raw = self.rfile.read(length) if length else b""
         if parsed.path.startswith("/proxy/"):
             return self._proxy(method, parsed, query, raw)
+        if method == "GET" and not parsed.path.startswith("/api/"):
+            return self._static(parsed.path)
         try:
             body = json.loads(raw) if raw else None
         except ValueError:
@@ -1309,6 +1311,27 @@ class _Handler(BaseHTTPRequestHandler):
                 logger.error(traceback.format_exc())
                 return self._send(500, {"error": f"{type(e).__name__}: {e}"})
         self._send(404, {"error": f"no route for {method} {parsed.path}"})
+
+    def _static(self, path: str) -> None:
+        """The web UI (``determined_clone_amd/webui``): ``/`` redirects to ``/det/``."""
+        from determined_clone_amd import webui
+
+        if path == "/":
+            self.send_response(302)
+            self.send_header("Location", "/det/")
+            self.send_header("Content-Length", "0")
+            self.end_headers()
+            return
+        found = webui.resolve(path)
+        if found is None:
+            return self._send(404, {"error": f"no route for GET {path}"})
+        ctype, body = found
+        self.send_response(200)
+        self.send_header("Content-Type", ctype)
+        self.send_header("Content-Length", str(len(body)))
+        self.send_header("Cache-Control", "no-cache")
+        self.end_headers()
+        self.wfile.write(body)
 
     # ------------------------------------------------------------------ task proxy
     def _proxy_user(self, query: Dict[str, List[str]]) -> Optional[Dict[str, Any]]:

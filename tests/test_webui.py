@@ -1,0 +1,119 @@
+"""Web UI served by the master (determined_clone_amd/webui; reference: webui/react/src/pages).
+
+Checks that the SPA shell and assets are served, path traversal is refused, the script parses
+(when node is on PATH), and -- the contract that keeps the UI from rotting -- every REST call the
+UI makes resolves to a registered master route for that method."""
+import os
+import re
+import shutil
+import subprocess
+import urllib.error
+import urllib.request
+
+import pytest
+
+from determined_clone_amd import webui
+from determined_clone_amd.master.core import Master
+from determined_clone_amd.master.server import ROUTES, MasterServer
+
+APP_JS = os.path.join(webui.STATIC_DIR, "app.js")
+
+
+@pytest.fixture()
+def server(tmp_path):
+    srv = MasterServer(Master(str(tmp_path / "m.db")), port=0).start()
+    yield f"http://127.0.0.1:{srv.port}"
+    srv.stop()
+
+
+class _NoRedirect(urllib.request.HTTPRedirectHandler):
+    def redirect_request(self, *a, **k):
+        return None
+
+
+def test_serves_shell_and_assets(server):
+    opener = urllib.request.build_opener(_NoRedirect)
+    with pytest.raises(urllib.error.HTTPError) as e:
+        opener.open(server + "/")
+    assert e.value.code == 302 and e.value.headers["Location"] == "/det/"
+    for path, ctype, needle in (("/det/", "text/html", b"app.js"),
+                                ("/det/experiments/3", "text/html", b"<main"),
+                                ("/det/static/app.js", "javascript", b"ROUTES"),
+                                ("/det/static/app.css", "text/css", b"--acc")):
+        with urllib.request.urlopen(server + path) as r:
+            assert ctype in r.headers["Content-Type"]
+            assert needle in r.read()
+
+
+def test_refuses_traversal_and_unknown(server):
+    for path in ("/det/static/../__init__.py", "/det/static/%2e%2e/__init__.py", "/det/static/nope.js", "/etc/passwd"):
+        with pytest.raises(urllib.error.HTTPError) as e:
+            urllib.request.urlopen(server + path)
+        assert e.value.code == 404
+    assert webui.resolve("/det/static/../../master/server.py") is None
+
+
+def test_api_still_json(server):
+    import json
+
+    with urllib.request.urlopen(server + "/api/v1/master") as r:
+        assert json.loads(r.read())["product"] == "determined_clone_amd"
+
+
+@pytest.mark.skipif(shutil.which("node") is None, reason="node not installed")
+def test_script_parses():
+    subprocess.run(["node", "--check", APP_JS], check=True)
+
+
+def _ui_calls():
+    src = open(APP_JS).read()
+    calls = []
+    # api.get(`...`) / api.post("...") / api.patch / api.del ; template parts become a sample id
+    for m in re.finditer(r'api\.(get|post|patch|del)\(\s*([`"])(/api/v1/[^`"]*)\2', src):
+        method = {"get": "GET", "post": "POST", "patch": "PATCH", "del": "DELETE"}[m.group(1)]
+        path = re.sub(r"\$\{[^}]*\}", "7", m.group(3)).split("?")[0]
+        if path.endswith("/") or "/7/7" in path or path.startswith("/api/v1/7"):
+            continue  # computed resource kinds / verbs: expanded below
+        calls.append((method, path))
+    calls += [("POST", f"/api/v1/experiments/7/{verb}")
+              for verb in ("pause", "activate", "cancel", "kill", "archive", "unarchive")]
+    calls += [("POST", f"/api/v1/models/m/{verb}") for verb in ("archive", "unarchive")]
+    calls += [("POST", f"/api/v1/workspaces/7/{verb}") for verb in ("pin", "unpin")]
+    # "/api/v1/" + p with the NTSC kinds
+    for kind in re.findall(r'\["(commands|notebooks|shells|tensorboards)", "[A-Z]+"\]', src):
+        calls += [("GET", f"/api/v1/{kind}"), ("POST", f"/api/v1/{kind}"), ("POST", f"/api/v1/{kind}/7/kill")]
+    return calls
+
+
+def test_every_ui_call_has_a_route():
+    calls = _ui_calls()
+    assert len(calls) > 40
+    missing = [(m, p) for m, p in calls
+               if not any(rm == m and rx.match(p) for rm, rx, _, _ in ROUTES)]
+    assert not missing, missing
+
+
+def test_ui_pages_against_live_master(server, tmp_path):
+    """Drive the read endpoints the pages load, with a real experiment in the db."""
+    import json
+
+    def call(method, path, body=None, token=None):
+        req = urllib.request.Request(server + path, method=method,
+                                     data=json.dumps(body).encode() if body is not None else None,
+                                     headers={"Content-Type": "application/json",
+                                              **({"Authorization": "Bearer " + token} if token else {})})
+        with urllib.request.urlopen(req) as r:
+            return json.loads(r.read())
+
+    tok = call("POST", "/api/v1/auth/login", {"username": "admin", "password": ""})["token"]
+    cfg = {"name": "ui", "entrypoint": "model_def:T", "searcher": {"name": "single", "metric": "loss",
+                                                                      "max_length": {"batches": 4}},
+           "hyperparameters": {"lr": 0.1}}
+    eid = call("POST", "/api/v1/experiments", {"config": cfg, "activate": False}, tok)["experiment"]["id"]
+    for path in ("/api/v1/experiments?archived=false", f"/api/v1/experiments/{eid}",
+                 f"/api/v1/experiments/{eid}/trials", f"/api/v1/experiments/{eid}/validation-history",
+                 f"/api/v1/experiments/{eid}/checkpoints?sort_by=searcher_metric", "/api/v1/agents",
+                 "/api/v1/resource-pools", "/api/v1/job-queues", "/api/v1/notebooks", "/api/v1/models",
+                 "/api/v1/workspaces", "/api/v1/workspaces/1/projects", "/api/v1/projects/1",
+                 "/api/v1/webhooks", "/api/v1/master/logs?after_id=0&tail=500", "/api/v1/users"):
+        assert isinstance(call("GET", path, token=tok), dict), path
