@@ -945,6 +945,9 @@ def build_parser() -> argparse.ArgumentParser:
     extra_cli.register(cmd, group, groups.__getitem__)
 
     d = group("deploy")
+    from determined_clone_amd.deploy import cli as deploy_cli
+
+    deploy_cli.register(d)
     lo = d.add_parser("local").add_subparsers(dest="deploy_cmd")
     for name in ("cluster-up", "cluster-down", "master-up", "agent-up"):
         sp = lo.add_parser(name)

@@ -16,6 +16,7 @@ import hashlib
 import hmac
 import os
 import pathlib
+import time
 import urllib.parse
 import xml.etree.ElementTree as ET
 from typing import Any, Dict, List, Optional, Tuple
@@ -151,6 +152,27 @@ def sigv4_headers(method: str, url: str, headers: Dict[str, str], payload_sha256
     return out
 
 
+def imds_credentials(http: requests.Session, imds: str = "http://169.254.169.254") -> Dict[str, Any]:
+    """Instance-profile credentials from the EC2 metadata service (IMDSv2): the role the
+    machine was launched with (``det deploy aws`` gives the master and agents one each).
+    Returns ``{"access_key", "secret_key", "token", "expiry"}``."""
+    imds = imds.rstrip("/")
+    tok = http.put(f"{imds}/latest/api/token", timeout=5,
+                   headers={"X-aws-ec2-metadata-token-ttl-seconds": "21600"}).text
+    hdr = {"X-aws-ec2-metadata-token": tok}
+    base = f"{imds}/latest/meta-data/iam/security-credentials/"
+    role = http.get(base, headers=hdr, timeout=5).text.strip().splitlines()[0]
+    c = http.get(base + role, headers=hdr, timeout=5).json()
+    exp = time.time() + 3600.0
+    if c.get("Expiration"):
+        try:
+            exp = datetime.datetime.fromisoformat(c["Expiration"].replace("Z", "+00:00")).timestamp()
+        except ValueError:
+            pass
+    return {"access_key": c["AccessKeyId"], "secret_key": c["SecretAccessKey"], "token": c.get("Token"),
+            "expiry": exp}
+
+
 class S3Store(ObjectStore):
     def __init__(self, bucket: str, access_key: Optional[str] = None, secret_key: Optional[str] = None,
                  endpoint_url: Optional[str] = None, region: Optional[str] = None,
@@ -163,12 +185,18 @@ class S3Store(ObjectStore):
         # path-style addressing works for AWS and every S3-compatible server
         self.endpoint = (endpoint_url or f"https://s3.{self.region}.amazonaws.com").rstrip("/")
         self.http = session or requests.Session()
+        self.imds = os.environ.get("DET_AWS_IMDS_ENDPOINT", "http://169.254.169.254")
+        self._expiry = 0.0  # > 0: credentials came from the instance profile and expire
 
     def _url(self, key: str = "", query: str = "") -> str:
         k = urllib.parse.quote(key, safe="/~")
         return f"{self.endpoint}/{self.bucket}" + (f"/{k}" if key else "") + (f"?{query}" if query else "")
 
     def _req(self, method: str, url: str, payload_sha: str = EMPTY_SHA256, **kw: Any) -> requests.Response:
+        if (not self.access_key and not self._expiry) or (self._expiry and time.time() > self._expiry - 300):
+            c = imds_credentials(self.http, self.imds)
+            self.access_key, self.secret_key, self.token, self._expiry = (
+                c["access_key"], c["secret_key"], c["token"], c["expiry"])
         h = sigv4_headers(method, url, {"x-amz-content-sha256": payload_sha}, payload_sha,
                           self.access_key, self.secret_key, self.region, "s3", session_token=self.token)
         return self.http.request(method, url, headers=h, **kw)

@@ -37,7 +37,10 @@ def main() -> None:
                cluster_name=cfg.get("cluster_name", "default"),
                authz=args.authz or ((cfg.get("security") or {}).get("authz") or {}).get("type", "basic"),
                resource_manager=cfg.get("resource_manager"), resource_pools=cfg.get("resource_pools"))
-    srv = MasterServer(m, args.host, int(cfg.get("port", args.port))).start()
+    srv = MasterServer(m, cfg.get("host", args.host), int(cfg.get("port", args.port)))
+    if cfg.get("external_url"):  # the address tasks, agents and provisioned instances dial
+        m.master_url = str(cfg["external_url"]).rstrip("/")
+    srv.start()
     logging.info(f"master listening on {m.master_url}")
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *a: stop.set())

@@ -36,7 +36,7 @@ from typing import Any, Callable, Dict, List, Optional
 
 import requests
 
-from determined_clone_amd.common.storage._cloud import sigv4_headers
+from determined_clone_amd.common.storage._cloud import imds_credentials, sigv4_headers
 
 logger = logging.getLogger("determined_clone_amd.master.provisioner")
 
@@ -216,7 +216,7 @@ def agent_setup_script(master_url: str, resource_pool: str, agent_id_cmd: str,
         "export HSA_ENABLE_IPC_MODE_LEGACY=0",
         startup_script or ":",
         f'AGENT_ID="{agent_id_cmd}"',
-        f"exec {python} -m determined_clone_amd.agent --master {master_url} "
+        f"exec {python} -m determined_clone_amd.agent --master-url {master_url} "
         f"--resource-pool {resource_pool} --agent-id \"$AGENT_ID\" {agent_args}".rstrip(),
         "",
     ])
@@ -284,6 +284,8 @@ class AWSProvider(Provider):
         self.access_key = config.get("access_key") or os.environ.get("AWS_ACCESS_KEY_ID", "")
         self.secret_key = config.get("secret_key") or os.environ.get("AWS_SECRET_ACCESS_KEY", "")
         self.token = os.environ.get("AWS_SESSION_TOKEN")
+        self.imds = (config.get("imds_endpoint") or "http://169.254.169.254").rstrip("/")
+        self._imds_expiry = 0.0
         self.tag_key = config.get("tag_key", "determined-clone-amd")
         self.tag_value = config.get("tag_value", "determined-clone-amd-agent")
         self.instance_type = (config.get("instance_type") or {}).get("name", "") \
@@ -295,7 +297,18 @@ class AWSProvider(Provider):
             master_url, pool, "$(curl -s http://169.254.169.254/latest/meta-data/instance-id)",
             config.get("startup_script", ""), config.get("agent_args", ""))
 
+    def _refresh_credentials(self) -> None:
+        """No static keys: use the instance profile of the machine the master runs on (IMDSv2),
+        which is how ``det deploy aws`` grants the master its EC2 permissions."""
+        if (self.access_key and not self._imds_expiry) or \
+                (self._imds_expiry and time.time() < self._imds_expiry - 300):
+            return
+        c = imds_credentials(self.http, self.imds)
+        self.access_key, self.secret_key, self.token = c["access_key"], c["secret_key"], c["token"]
+        self._imds_expiry = c["expiry"]
+
     def _call(self, action: str, params: Dict[str, str]) -> ET.Element:
+        self._refresh_credentials()
         body = urllib.parse.urlencode({"Action": action, "Version": "2016-11-15", **params})
         sha = hashlib.sha256(body.encode()).hexdigest()
         h = sigv4_headers("POST", self.endpoint,
@@ -345,6 +358,8 @@ class AWSProvider(Provider):
             params[f"TagSpecification.1.Tag.{i}.Value"] = v
         if c.get("ssh_key_name"):
             params["KeyName"] = c["ssh_key_name"]
+        if c.get("iam_instance_profile_arn"):
+            params["IamInstanceProfile.Arn"] = c["iam_instance_profile_arn"]
         if (c.get("network_interface") or {}).get("subnet_id"):
             params["SubnetId"] = c["network_interface"]["subnet_id"]
         if (c.get("network_interface") or {}).get("security_group_id"):
@@ -374,6 +389,8 @@ class GCPProvider(Provider):
         self.project, self.zone = config["project"], config["zone"]
         self.endpoint = (config.get("endpoint_url") or "https://compute.googleapis.com/compute/v1").rstrip("/")
         self.token = config.get("token") or os.environ.get("GCE_ACCESS_TOKEN", "")
+        self.metadata = (config.get("metadata_endpoint") or "http://metadata.google.internal").rstrip("/")
+        self._token_expiry = 0.0
         self.instance_type = (config.get("instance_type") or {}).get("machine_type", "")
         self.slots_per_instance = int(config.get("slots_per_instance",
                                                  (config.get("instance_type") or {}).get("gpu_num", 8)))
@@ -388,7 +405,20 @@ class GCPProvider(Provider):
             '$(curl -s "http://metadata.google.internal/computeMetadata/v1/instance/name" '
             '-H "Metadata-Flavor: Google")', config.get("startup_script", ""), config.get("agent_args", ""))
 
+    def _refresh_token(self) -> None:
+        """No configured token: the service account of the VM the master runs on (metadata
+        server), which is how ``det deploy gcp`` grants the master its Compute permissions."""
+        if self.token and not self._token_expiry:
+            return
+        if self._token_expiry and time.time() < self._token_expiry - 300:
+            return
+        d = self.http.get(f"{self.metadata}/computeMetadata/v1/instance/service-accounts/default/token",
+                          headers={"Metadata-Flavor": "Google"}, timeout=5).json()
+        self.token = d["access_token"]
+        self._token_expiry = time.time() + float(d.get("expires_in", 3600))
+
     def _req(self, method: str, path: str, **kw: Any) -> Any:
+        self._refresh_token()
         r = self.http.request(method, f"{self.endpoint}/projects/{self.project}/zones/{self.zone}{path}",
                               headers={"Authorization": f"Bearer {self.token}"}, timeout=60, **kw)
         if r.status_code >= 300:
@@ -424,6 +454,12 @@ class GCPProvider(Provider):
                                    "subnetwork": c.get("network_interface", {}).get("subnetwork", "")}],
             "scheduling": {"onHostMaintenance": "TERMINATE", "preemptible": bool(c.get("preemptible", False))},
         }
+        if c.get("service_account"):  # the agents' identity (checkpoint bucket access)
+            sa = c["service_account"]
+            props["serviceAccounts"] = [{"email": sa.get("email", "default"),
+                                         "scopes": sa.get("scopes") or ["https://www.googleapis.com/auth/cloud-platform"]}]
+        if c.get("network_interface", {}).get("external_ip", True):
+            props["networkInterfaces"][0]["accessConfigs"] = [{"type": "ONE_TO_ONE_NAT", "name": "External NAT"}]
         if c.get("instance_type", {}).get("gpu_type"):
             props["guestAccelerators"] = [{"acceleratorType": c["instance_type"]["gpu_type"],
                                            "acceleratorCount": self.slots_per_instance}]

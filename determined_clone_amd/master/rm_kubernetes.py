@@ -177,6 +177,8 @@ class KubernetesResourceManager(ResourceManager):
         self.poll_interval = float(config.get("poll_interval", 1.0))
         self.missing_grace = float(config.get("missing_pod_grace", 30.0))
         self.default_pool = config.get("default_resource_pool", "default")
+        # PVCs every task pod mounts (shared_fs checkpoint storage): [{name, claim_name, mount_path}]
+        self.volumes: List[Dict[str, str]] = list(config.get("task_volumes") or [])
         self.on_container_event: Optional[Callable[..., None]] = None
         self.pods: Dict[str, _PodRecord] = {}
         self._stop = threading.Event()
@@ -262,7 +264,8 @@ class KubernetesResourceManager(ResourceManager):
             "name": CONTAINER_NAME, "image": image,
             "command": ["python3", "-m", "determined_clone_amd.exec.task_runner"],
             "env": env, "resources": {"requests": res, "limits": limits},
-            "volumeMounts": [{"name": "dshm", "mountPath": "/dev/shm"}],
+            "volumeMounts": [{"name": "dshm", "mountPath": "/dev/shm"}] + [
+                {"name": v["name"], "mountPath": v["mount_path"]} for v in self.volumes],
         }
         pod = {
             "apiVersion": "v1", "kind": "Pod",
@@ -273,7 +276,9 @@ class KubernetesResourceManager(ResourceManager):
                          "annotations": {"determined.ai/allocation-id": alloc}},
             "spec": {"restartPolicy": "Never", "nodeName": node_of(spec["agent_id"]),
                      "containers": [container],
-                     "volumes": [{"name": "dshm", "emptyDir": {"medium": "Memory"}}]},
+                     "volumes": [{"name": "dshm", "emptyDir": {"medium": "Memory"}}] + [
+                         {"name": v["name"], "persistentVolumeClaim": {"claimName": v["claim_name"]}}
+                         for v in self.volumes]},
         }
         user = env_cfg.get("pod_spec")
         if user:

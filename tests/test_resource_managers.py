@@ -327,7 +327,7 @@ def test_aws_provider_against_fake_ec2():
         rec = next(iter(ec2.instances.values()))
         assert rec["tags"]["team"] == "llm" and rec["tags"]["determined-resource-pool"] == "gpu-pool"
         ud = base64.b64decode(rec["user_data"]).decode()
-        assert "determined_clone_amd.agent --master http://10.0.0.1:8080 --resource-pool gpu-pool" in ud
+        assert "determined_clone_amd.agent --master-url http://10.0.0.1:8080 --resource-pool gpu-pool" in ud
         run = [c for c in ec2.calls if c["Action"] == "RunInstances"][0]
         assert run["ImageId"] == "ami-rocm" and run["InstanceType"] == "mi355x.48xlarge"
         assert run["MaxCount"] == "2" and run["MetadataOptions.HttpTokens"] == "required"
