@@ -14,6 +14,8 @@
 // Backward (FlashAttention-2 ordering), one workgroup = 64 keys; dK/dV accumulate in VGPRs while
 //   the workgroup sweeps the query tiles; recomputed P^T = exp2(S^T - LSE), dP^T = V dO^T,
 //   dS^T = P^T (dP^T - rowsum(dO*O)); dQ partials are added into an fp32 buffer with float atomics.
+#include <type_traits>
+
 #include "common.h"
 
 namespace dca {
@@ -24,7 +26,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 64;   // query rows per forward block / keys per backward block
-constexpr int kPad = 8;     // LDS row padding (elements) to break power-of-two bank strides
+constexpr int kPad = 8;
+constexpr bool FWD_ONE_COPY = true;     // LDS row padding (elements) to break power-of-two bank strides
 
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -174,7 +177,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Ks = smem;           // [KT][RS]
   uint16_t* Vs = Ks + KT * RS;   // [KT][RS]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  // wave index in an SGPR: the causal extent checks below are uniform branches
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hf = lane >> 5;
   const int b = blockIdx.z, h = blockIdx.y;
   // heaviest (largest causal extent) query blocks first
@@ -297,7 +302,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Ks = smem;
   uint16_t* Vs = Ks + KT * RS;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  // wave index in an SGPR: every per-wave condition below (causal extents, masking) is a
+  // uniform branch instead of per-lane exec masking
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hf = lane >> 5;
   const int b = blockIdx.z, h = blockIdx.y;
   const int q_blk = (CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * QB;
@@ -337,24 +345,33 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     pf.store(Ks, Vs);
     __syncthreads();
     if (kt + KT < k_end) pf.fetch(kb, ks, vb, vs, kt + KT, Sk);
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      const int kb0 = kt + 32 * sub;
-      if (kb0 >= k_end) break;
-      if (CAUSAL && kb0 > q0 + 31) break;
+    auto sub_tile = [&](auto masked, const int sub, const int kb0) {
       f32x16 sc = zero16(), dp = zero16();
+      if constexpr (D == 64) {  // fragments preloaded (see the forward)
+        bf16x8 kfr[D / 16], vfr[D / 16];
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        sc = mfma32(load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf), qf[s], sc);
-        dp = mfma32(load8(Vs + (32 * sub + r) * RS + 16 * s + 8 * hf), dof[s], dp);
+        for (int s = 0; s < D / 16; ++s) {
+          kfr[s] = load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf);
+          vfr[s] = load8(Vs + (32 * sub + r) * RS + 16 * s + 8 * hf);
+        }
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          sc = mfma32(kfr[s], qf[s], sc);
+          dp = mfma32(vfr[s], dof[s], dp);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          sc = mfma32(load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf), qf[s], sc);
+          dp = mfma32(load8(Vs + (32 * sub + r) * RS + 16 * s + 8 * hf), dof[s], dp);
+        }
       }
-      const bool need_mask = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float p = fast_exp2(fmaf(sc[i], scale_log2, -lq));
-        if (need_mask) {
+        if constexpr (decltype(masked)::value) {
           const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-          if (key >= Sk || (CAUSAL && key > my_q)) p = 0.f;
+          p = (key >= Sk || (CAUSAL && key > my_q)) ? 0.f : p;
         }
         dp[i] = p * (dp[i] - dsum);  // the softmax scale is applied once to dQ at the end
       }
@@ -366,6 +383,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
           const uint16_t* base = Ks + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
           dqacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RS)), s2 ? s1 : s0, dqacc[n]);
         }
+    };
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int kb0 = kt + 32 * sub;
+      if (kb0 >= k_end) break;
+      if (CAUSAL && kb0 > q0 + 31) break;
+      // wave-uniform; D = 128 keeps one (masked) copy: two copies exceed the VGPR budget
+      if (D == 128 || (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0))
+        sub_tile(std::true_type{}, sub, kb0);
+      else
+        sub_tile(std::false_type{}, sub, kb0);
     }
   }
   if (q_ok) {
@@ -398,7 +426,10 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   uint16_t* dOs = Qs + QT * RS;   // [QT][RS]
   float* lse_s = reinterpret_cast<float*>(dOs + QT * RS);
   float* del_s = lse_s + QT;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  // wave index in an SGPR: every per-wave condition below (causal extents, masking) is a
+  // uniform branch instead of per-lane exec masking
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hf = lane >> 5;
   const int b = blockIdx.z, h = blockIdx.y;
   const int k_blk = blockIdx.x * KB;
@@ -465,35 +496,64 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     if (qt + QT < Sq) fetch(qt + QT);
     const bool active = !(CAUSAL && kw0 > qt + QT - 1) && kw0 < Sk;  // wave-uniform
     if (!active) continue;
-    f32x16 sacc = zero16(), dpacc = zero16();
+    auto tile = [&](auto masked) {
+      // this lane's 16 queries are 4 runs of 4 consecutive rows: their LSE / delta come in as
+      // four 16-B LDS reads each instead of sixteen 4-B reads
+      float4 l4[4], d4[4];
 #pragma unroll
-    for (int s = 0; s < D / 16; ++s) {
-      sacc = mfma32(load8(Qs + r * RS + 16 * s + 8 * hf), kf[s], sacc);
-      dpacc = mfma32(load8(dOs + r * RS + 16 * s + 8 * hf), vf[s], dpacc);
-    }
-    const bool need_mask = (qt + QT > Sq) || (my_key >= Sk) || (CAUSAL && kw0 + 31 > qt);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int ql = (i & 3) + 8 * (i >> 2) + 4 * hf;
-      float p = fast_exp2(fmaf(sacc[i], scale_log2, -lse_s[ql]));
-      if (need_mask) {
-        const int qi = qt + ql;
-        if (qi >= Sq || my_key >= Sk || (CAUSAL && my_key > qi)) p = 0.f;
+      for (int g = 0; g < 4; ++g) {
+        l4[g] = *reinterpret_cast<const float4*>(lse_s + 8 * g + 4 * hf);
+        d4[g] = *reinterpret_cast<const float4*>(del_s + 8 * g + 4 * hf);
       }
-      sacc[i] = p;
-      dpacc[i] = p * (dpacc[i] - del_s[ql]);  // scale applied once to dK at the end
-    }
-    const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8);
-    const bf16x8 s0 = pack8(dpacc, 0), s1 = pack8(dpacc, 8);
+      f32x16 sacc = zero16(), dpacc = zero16();
+      if constexpr (D == 64) {  // fragments preloaded (see the forward)
+        bf16x8 qfr[D / 16], dofr[D / 16];
 #pragma unroll
-    for (int n = 0; n < D / 32; ++n) {
+        for (int s = 0; s < D / 16; ++s) {
+          qfr[s] = load8(Qs + r * RS + 16 * s + 8 * hf);
+          dofr[s] = load8(dOs + r * RS + 16 * s + 8 * hf);
+        }
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int off = (16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
-        dvacc[n] = mfma32(cat8(tr_read(dOs + off), tr_read(dOs + off + 8 * RS)), s2 ? p1 : p0, dvacc[n]);
-        dkacc[n] = mfma32(cat8(tr_read(Qs + off), tr_read(Qs + off + 8 * RS)), s2 ? s1 : s0, dkacc[n]);
+        for (int s = 0; s < D / 16; ++s) {
+          sacc = mfma32(qfr[s], kf[s], sacc);
+          dpacc = mfma32(dofr[s], vf[s], dpacc);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          sacc = mfma32(load8(Qs + r * RS + 16 * s + 8 * hf), kf[s], sacc);
+          dpacc = mfma32(load8(dOs + r * RS + 16 * s + 8 * hf), vf[s], dpacc);
+        }
       }
-    }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float lq = reinterpret_cast<const float*>(&l4[i >> 2])[i & 3];
+        const float dl = reinterpret_cast<const float*>(&d4[i >> 2])[i & 3];
+        float p = fast_exp2(fmaf(sacc[i], scale_log2, -lq));
+        if constexpr (decltype(masked)::value) {
+          const int qi = qt + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          p = (qi >= Sq || my_key >= Sk || (CAUSAL && my_key > qi)) ? 0.f : p;
+        }
+        sacc[i] = p;
+        dpacc[i] = p * (dpacc[i] - dl);  // scale applied once to dK at the end
+      }
+      const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8);
+      const bf16x8 s0 = pack8(dpacc, 0), s1 = pack8(dpacc, 8);
+#pragma unroll
+      for (int n = 0; n < D / 32; ++n) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int off = (16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
+          dvacc[n] = mfma32(cat8(tr_read(dOs + off), tr_read(dOs + off + 8 * RS)), s2 ? p1 : p0, dvacc[n]);
+          dkacc[n] = mfma32(cat8(tr_read(Qs + off), tr_read(Qs + off + 8 * RS)), s2 ? s1 : s0, dkacc[n]);
+        }
+      }
+    };
+    // wave-uniform (a key block straddling Sk only exists in the last workgroup)
+    if (D == 128 || (qt + QT > Sq) || (kw0 + 32 > Sk) || (CAUSAL && kw0 + 31 > qt))
+      tile(std::true_type{});
+    else
+      tile(std::false_type{});
   }
   if (my_key < Sk) {
     uint16_t* dkrow = dk + b * dks.b + h * dks.h + static_cast<int64_t>(my_key) * dks.s;

@@ -29,8 +29,10 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--iters", type=int, default=30)
     p.add_argument("--only", default="")
+    p.add_argument("--gpt2", action="store_true", help="only the GPT-2-medium shape (16x1024x16x64)")
     a = p.parse_args()
-    for B, S, H, D in ((16, 1024, 16, 64), (8, 2048, 16, 64), (4, 4096, 8, 128)):
+    shapes = ((16, 1024, 16, 64), (8, 2048, 16, 64), (4, 4096, 8, 128))
+    for B, S, H, D in shapes[:1] if a.gpt2 else shapes:
         q, k, v = (torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
                    for _ in range(3))
         g = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
