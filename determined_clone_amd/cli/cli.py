@@ -765,6 +765,39 @@ def project_create(args):
     print(f"Created project {p['name']} (id {p['id']})")
 
 
+def _serve_tunnels(args, s, task_id: str) -> None:
+    import threading
+
+    from determined_clone_amd.cli import tunnel
+
+    port_map = tunnel.parse_port_map(args.publish)
+    if not port_map:
+        raise SystemExit("pass at least one -p LOCAL[:REMOTE]")
+    with tunnel.listeners(s.master, s.token, task_id, port_map) as ports:
+        for (local, remote), bound in zip(port_map.items(), ports):
+            print(f"127.0.0.1:{bound} -> {task_id}:{remote}", flush=True)
+        try:
+            threading.Event().wait()
+        except KeyboardInterrupt:
+            pass
+
+
+def task_tunnel(args):
+    """det task tunnel TASK -p LOCAL[:REMOTE]: forward local ports to a running task's ports
+    through the master (reference: `cli/proxy.py` _tunnel_task / --publish)."""
+    _serve_tunnels(args, session(args), args.task_id)
+
+
+def experiment_tunnel(args):
+    """det experiment tunnel EXP -p ...: the experiment's first running trial."""
+    s = session(args)
+    trials = s.get(f"/api/v1/experiments/{args.experiment_id}/trials")["trials"]
+    live = [t for t in trials if t.get("task_id") and t.get("state") in ("RUNNING", "ACTIVE")]
+    if not live:
+        raise SystemExit(f"experiment {args.experiment_id} has no running trial")
+    _serve_tunnels(args, s, live[0]["task_id"])
+
+
 def deploy_local(args):
     from determined_clone_amd.deploy import local
 
@@ -900,6 +933,10 @@ def build_parser() -> argparse.ArgumentParser:
     tk = group("task")
     cmd(tk, "list ls", task_list)
     sp = cmd(tk, "logs", task_logs); sp.add_argument("task_id"); sp.add_argument("-f", "--follow", action="store_true")
+    sp = cmd(tk, "tunnel", task_tunnel); sp.add_argument("task_id")
+    sp.add_argument("-p", "--publish", action="append", default=[], help="LOCAL[:REMOTE] port (repeatable)")
+    sp = cmd(groups["experiment"], "tunnel", experiment_tunnel); sp.add_argument("experiment_id", type=int)
+    sp.add_argument("-p", "--publish", action="append", default=[], help="LOCAL[:REMOTE] port (repeatable)")
 
     for kind, names, path in (("COMMAND", "command cmd", "commands"), ("SHELL", "shell", "shells"),
                               ("NOTEBOOK", "notebook", "notebooks"), ("TENSORBOARD", "tensorboard", "tensorboards")):

@@ -1282,6 +1282,8 @@ class _Handler(BaseHTTPRequestHandler):
         raw = self.rfile.read(length) if length else b""
         if parsed.path.startswith("/proxy/"):
             return self._proxy(method, parsed, query, raw)
+        if parsed.path.startswith("/tunnel/") and method == "GET":
+            return self._tunnel(parsed, query)
         if method == "GET" and not parsed.path.startswith("/api/"):
             return self._static(parsed.path)
         try:
@@ -1332,6 +1334,81 @@ class _Handler(BaseHTTPRequestHandler):
         self.send_header("Cache-Control", "no-cache")
         self.end_headers()
         self.wfile.write(body)
+
+    # ------------------------------------------------------------------ TCP tunnel
+    def _task_host(self, task_id: str) -> Optional[Tuple[str, Optional[int]]]:
+        """(host, service port) of a live task: its registered proxy address, else the first
+        address of the agent running its first container."""
+        allocs = [a for a in list(self.master.allocations.values()) if a.task_id == task_id and not a.exited]
+        if not allocs:
+            return None
+        a = allocs[0]
+        if a.proxy_address:
+            u = urllib.parse.urlsplit(a.proxy_address)
+            return u.hostname or "127.0.0.1", u.port
+        for p in a.placements:
+            agent = self.master.rm.agents.get(p.get("agent_id"))
+            if agent is not None and agent.addresses:
+                return agent.addresses[0], None
+        return "127.0.0.1", None
+
+    def _tunnel(self, parsed: Any, query: Dict[str, List[str]]) -> None:
+        """``GET /tunnel/{task_id}?port=N`` with ``Upgrade: det-tcp``: after ``101 Switching
+        Protocols`` the connection is a raw byte pipe to port N (default: the task's service port)
+        on the task's host -- ssh into a shell, or ``det task tunnel -p`` to any port a trial
+        opens (reference: the master's TCP-over-WebSocket proxy, `harness/determined/cli/
+        tunnel.py` / `proxy.py`). Authenticated like ``/proxy/``; task owner or admin only."""
+        import socket
+
+        task_id = parsed.path.split("/", 3)[2] if parsed.path.count("/") >= 2 else ""
+        if self.headers.get("Upgrade", "").lower() != "det-tcp":
+            return self._send(400, {"error": "tunnel requests must send 'Upgrade: det-tcp'"})
+        user = self._proxy_user(query)
+        if user is None:
+            return self._send(401, {"error": "unauthenticated"})
+        if not (user["admin"] or self.master.task_owner(task_id) in (None, user["id"])):
+            return self._send(403, {"error": "not the task owner"})
+        target = self._task_host(task_id)
+        if target is None:
+            return self._send(404, {"error": f"no running task {task_id}"})
+        host, svc_port = target
+        port = int(query["port"][0]) if query.get("port") else svc_port
+        if not port:
+            return self._send(400, {"error": "task has no service port; pass ?port="})
+        try:
+            upstream = socket.create_connection((host, port), timeout=10)
+        except OSError as e:
+            return self._send(502, {"error": f"cannot reach {host}:{port}: {e}"})
+        upstream.settimeout(None)
+        self.send_response(101, "Switching Protocols")
+        self.send_header("Upgrade", "det-tcp")
+        self.send_header("Connection", "Upgrade")
+        self.end_headers()
+        self.wfile.flush()
+        self.close_connection = True
+        client = self.connection
+        client.settimeout(None)
+
+        def pump(src: Any, dst: Any) -> None:
+            try:
+                while True:
+                    data = src.recv(65536)
+                    if not data:
+                        break
+                    dst.sendall(data)
+            except OSError:
+                pass
+            finally:
+                try:
+                    dst.shutdown(socket.SHUT_WR)
+                except OSError:
+                    pass
+
+        t = threading.Thread(target=pump, args=(upstream, client), daemon=True)
+        t.start()
+        pump(client, upstream)
+        t.join()
+        upstream.close()
 
     # ------------------------------------------------------------------ task proxy
     def _proxy_user(self, query: Dict[str, List[str]]) -> Optional[Dict[str, Any]]:
