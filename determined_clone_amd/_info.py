@@ -39,10 +39,12 @@ class TrialInfo:
 
 class RendezvousInfo:
     def __init__(self, container_addrs: List[str], container_rank: int,
-                 container_slot_counts: Optional[List[int]] = None) -> None:
+                 container_slot_counts: Optional[List[int]] = None,
+                 port: Optional[int] = None) -> None:
         self.container_addrs = list(container_addrs)
         self.container_rank = int(container_rank)
         self.container_slot_counts = list(container_slot_counts or [])
+        self.port = int(port) if port else None  # c10d port the master reserved on the chief
 
 
 class ClusterInfo:
@@ -98,6 +100,10 @@ class ClusterInfo:
         return [len(self.slot_ids)]
 
     @property
+    def rendezvous_port(self) -> Optional[int]:
+        return self._rendezvous_info.port if self._rendezvous_info else None
+
+    @property
     def gpu_uuids(self) -> List[str]:
         return self._gpu_uuids
 
@@ -113,7 +119,8 @@ class ClusterInfo:
         if self._rendezvous_info:
             d["rendezvous"] = {"container_addrs": self._rendezvous_info.container_addrs,
                                "container_rank": self._rendezvous_info.container_rank,
-                               "container_slot_counts": self._rendezvous_info.container_slot_counts}
+                               "container_slot_counts": self._rendezvous_info.container_slot_counts,
+                               "port": self._rendezvous_info.port}
         return d
 
     @classmethod

@@ -64,6 +64,8 @@ def build_task(spec: Dict[str, Any], master_url: str, agent_id: str,
     if n > 1:
         info["rendezvous"] = {"container_addrs": list(container_addrs or ["127.0.0.1"] * n),
                               "container_rank": int(spec.get("container_rank", 0))}
+        if spec.get("rendezvous_port"):
+            info["rendezvous"]["port"] = int(spec["rendezvous_port"])
     env = dict(os.environ if base_env is None else base_env)
     env.update(_user_env(spec))
     env["DET_CLUSTER_INFO"] = json.dumps(info)

@@ -54,7 +54,9 @@ def main(argv: List[str]) -> int:
         procs = max(len(info.slot_ids), 1)
         rank = info.container_rank
         addr = info.container_addrs[0] if nodes > 1 else "127.0.0.1"
-    port = C10D_PORT if nodes > 1 else _free_port()
+    # multi-node: the port the master reserved for this allocation on the chief's host
+    # (master/ports.py), so concurrent jobs sharing a chief node never collide
+    port = ((info.rendezvous_port if info is not None else None) or C10D_PORT) if nodes > 1 else _free_port()
     cmd = create_launch_cmd(nodes, procs, rank, addr, port, override, script)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")

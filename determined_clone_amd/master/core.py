@@ -19,6 +19,7 @@ from determined_clone_amd.master.rbac import Authz
 from determined_clone_amd.master.db import DB, dec, now
 from determined_clone_amd.master.experiment import (ACTIVE, PAUSED, TERMINAL, Experiment, Trial,
                                                     experiment_row_to_api, trial_row_to_api)
+from determined_clone_amd.master.ports import PortRegistry
 from determined_clone_amd.master.rm import AgentState, AllocationRequest
 from determined_clone_amd.master.rm_setup import make_resource_manager
 
@@ -140,6 +141,7 @@ class Master:
                                         self.container_event, resource_pools)
         self.experiments: Dict[int, Experiment] = {}
         self.allocations: Dict[str, Allocation] = {}
+        self.ports = PortRegistry()
         self.tasks: Dict[str, Dict[str, Any]] = {}
         self.webhooks = Webhooks(self)
         self.lock = threading.RLock()
@@ -301,6 +303,8 @@ class Master:
         spec["task_id"] = a.task_id
         n_containers = len(req.placements)
         a.containers_running = n_containers
+        if n_containers > 1:  # unique c10d port on the chief's host (master/ports.py)
+            spec["rendezvous_port"] = self.ports.acquire(req.placements[0]["agent_id"], a.id)
         specs = []
         for rank, p in enumerate(req.placements):
             s = dict(spec)
@@ -366,6 +370,7 @@ class Master:
             return
         a.exited = True
         a.exit_code = exit_code
+        self.ports.release(a.id)
         self.db.update("allocations", "allocation_id", a.id,
                        {"state": "TERMINATED", "end_time": now(), "exit_reason": reason or str(exit_code)})
         with self.log_cv:

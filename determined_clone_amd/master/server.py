@@ -23,6 +23,7 @@ from determined_clone_amd.master.db import dec, now
 from determined_clone_amd.master.experiment import TERMINAL, experiment_row_to_api, trial_row_to_api
 
 logger = logging.getLogger("determined_clone_amd.master.api")
+audit_logger = logging.getLogger("determined_clone_amd.master.audit")
 
 Handler = Callable[..., Any]
 ROUTES: List[Tuple[str, "re.Pattern[str]", Handler, bool]] = []
@@ -1284,6 +1285,12 @@ class _Handler(BaseHTTPRequestHandler):
             return self._proxy(method, parsed, query, raw)
         if parsed.path.startswith("/tunnel/") and method == "GET":
             return self._tunnel(parsed, query)
+        if method == "GET" and parsed.path in ("/prom/det-state-metrics", "/debug/prom/metrics"):
+            from determined_clone_amd.master import prom
+
+            ctype, data = (prom.state_metrics(self.master) if parsed.path.startswith("/prom/")
+                           else prom.process_metrics())
+            return self._send_raw(200, ctype, data)
         if method == "GET" and not parsed.path.startswith("/api/"):
             return self._static(parsed.path)
         try:
@@ -1302,17 +1309,48 @@ class _Handler(BaseHTTPRequestHandler):
                 user = self.master.user_for_token(hdr[7:])
             if auth and user is None:
                 return self._send(401, {"error": "unauthenticated"})
+            started = time.time()
+            code, payload = 200, None
             try:
                 out = fn(Req(self.master, match.groupdict(), query, body, user))
-                return self._send(200, out if out is not None else {})
+                payload = out if out is not None else {}
             except HTTPError as e:
-                return self._send(e.status, {"error": str(e)})
+                code, payload = e.status, {"error": str(e)}
             except KeyError as e:
-                return self._send(404, {"error": f"not found: {e}"})
+                code, payload = 404, {"error": f"not found: {e}"}
             except Exception as e:  # pragma: no cover - surfaced to the client
                 logger.error(traceback.format_exc())
-                return self._send(500, {"error": f"{type(e).__name__}: {e}"})
+                code, payload = 500, {"error": f"{type(e).__name__}: {e}"}
+            self._send(code, payload)
+            self._account(fn.__name__, method, parsed.path, code, started, user)
+            return
         self._send(404, {"error": f"no route for {method} {parsed.path}"})
+
+    def _send_raw(self, status: int, ctype: str, data: bytes) -> None:
+        self.send_response(status)
+        self.send_header("Content-Type", ctype)
+        self.send_header("Content-Length", str(len(data)))
+        self.end_headers()
+        self.wfile.write(data)
+
+    # task-plumbing endpoints polled/posted by every running task or agent: not audited
+    _UNAUDITED = ("agent_events", "post_task_logs", "post_metrics", "trial_progress", "trial_heartbeat",
+                  "post_profiler", "runner_metadata", "agent_register", "alloc_allgather", "ack_preemption",
+                  "alloc_ready", "alloc_proxy", "report_checkpoint", "trial_completed_op")
+
+    def _account(self, handler: str, method: str, path: str, code: int, started: float,
+                 user: Optional[Dict[str, Any]]) -> None:
+        """Request metrics (/debug/prom/metrics) and the audit log: one structured line per
+        user-initiated mutating call (reference: `master/internal/audit.go`)."""
+        from determined_clone_amd.master import prom
+
+        prom.observe(handler, method, code, started)
+        if method != "GET" and handler not in self._UNAUDITED:
+            audit_logger.info(json.dumps({
+                "user": (user or {}).get("username"), "user_id": (user or {}).get("id"),
+                "method": method, "path": path, "handler": handler, "status": code,
+                "remote": self.client_address[0] if self.client_address else None,
+                "ms": round((time.time() - started) * 1e3, 1)}))
 
     def _static(self, path: str) -> None:
         """The web UI (``determined_clone_amd/webui``): ``/`` redirects to ``/det/``."""
