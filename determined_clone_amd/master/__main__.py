@@ -36,7 +36,8 @@ def main() -> None:
                preemption=bool(sched.get("preemption", True)), checkpoint_storage=cs,
                cluster_name=cfg.get("cluster_name", "default"),
                authz=args.authz or ((cfg.get("security") or {}).get("authz") or {}).get("type", "basic"),
-               resource_manager=cfg.get("resource_manager"), resource_pools=cfg.get("resource_pools"))
+               resource_manager=cfg.get("resource_manager"), resource_pools=cfg.get("resource_pools"),
+               logging_config=cfg.get("logging"))
     srv = MasterServer(m, cfg.get("host", args.host), int(cfg.get("port", args.port)))
     if cfg.get("external_url"):  # the address tasks, agents and provisioned instances dial
         m.master_url = str(cfg["external_url"]).rstrip("/")

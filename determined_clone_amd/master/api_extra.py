@@ -446,15 +446,10 @@ def trial_logs_fields(r: Req) -> Any:
 
 @route("GET", "/api/v1/tasks/{task_id}/logs/fields")
 def task_logs_fields(r: Req) -> Any:
-    rows = r.m.db.all("SELECT DISTINCT agent_id, container_id, rank_id, stdtype, source, level, allocation_id "
-                      "FROM task_logs WHERE task_id=?", [r.p["task_id"]])
-
-    def uniq(k: str) -> List[Any]:
-        return sorted({x[k] for x in rows if x[k] is not None}, key=str)
-
-    return {"agent_ids": uniq("agent_id"), "container_ids": uniq("container_id"), "rank_ids": uniq("rank_id"),
-            "stdtypes": uniq("stdtype"), "sources": uniq("source"), "levels": uniq("level"),
-            "allocation_ids": uniq("allocation_id")}
+    f = r.m.logs.fields(r.p["task_id"])
+    return {"agent_ids": f["agent_id"], "container_ids": f["container_id"], "rank_ids": f["rank_id"],
+            "stdtypes": f["stdtype"], "sources": f["source"], "levels": f["level"],
+            "allocation_ids": f["allocation_id"]}
 
 
 @route("GET", "/api/v1/trials/time-series", first=True)

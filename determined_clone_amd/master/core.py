@@ -19,6 +19,8 @@ from determined_clone_amd.master.rbac import Authz
 from determined_clone_amd.master.db import DB, dec, now
 from determined_clone_amd.master.experiment import (ACTIVE, PAUSED, TERMINAL, Experiment, Trial,
                                                     experiment_row_to_api, trial_row_to_api)
+from determined_clone_amd.master.logstore import make_log_store
+from determined_clone_amd.master.logstore import normalize as normalize_log
 from determined_clone_amd.master.ports import PortRegistry
 from determined_clone_amd.master.rm import AgentState, AllocationRequest
 from determined_clone_amd.master.rm_setup import make_resource_manager
@@ -122,8 +124,10 @@ class Master:
                  preemption: bool = True, checkpoint_storage: Optional[Dict[str, Any]] = None,
                  cluster_name: str = "default", master_url: str = "http://127.0.0.1:8080",
                  authz: str = "basic", resource_manager: Optional[Dict[str, Any]] = None,
-                 resource_pools: Optional[List[Dict[str, Any]]] = None) -> None:
+                 resource_pools: Optional[List[Dict[str, Any]]] = None,
+                 logging_config: Optional[Dict[str, Any]] = None) -> None:
         self.db = DB(db_path)
+        self.logs = make_log_store(logging_config, self.db)  # master.yaml `logging` (sqlite | elastic)
         self.authz = Authz(self.db, authz)
         self.log_buffer = MasterLogBuffer()
         pkg_logger = logging.getLogger("determined_clone_amd")
@@ -613,12 +617,8 @@ class Master:
 
     # ------------------------------------------------------------------ logs
     def post_logs(self, logs: List[Dict[str, Any]]) -> None:
-        for lg in logs:
-            self.db.insert("task_logs", {"task_id": lg.get("task_id"), "allocation_id": lg.get("allocation_id"),
-                                         "agent_id": lg.get("agent_id"), "container_id": lg.get("container_id"),
-                                         "rank_id": lg.get("rank_id"), "timestamp": lg.get("timestamp") or now(),
-                                         "level": lg.get("level", "INFO"), "log": lg.get("log", ""),
-                                         "source": lg.get("source", "task"), "stdtype": lg.get("stdtype", "stdout")})
+        ts = now()
+        self.logs.append([normalize_log(lg, ts) for lg in logs])
         self._apply_log_policies(logs)
         with self.log_cv:
             self.log_cv.notify_all()
@@ -646,5 +646,4 @@ class Master:
                         req.blocked_agents.append(lg["agent_id"])
 
     def task_logs(self, task_id: str, after_id: int = 0, limit: int = 10000) -> List[Dict[str, Any]]:
-        return self.db.all("SELECT * FROM task_logs WHERE task_id=? AND id>? ORDER BY id LIMIT ?",
-                           [task_id, after_id, limit])
+        return self.logs.after(task_id, after_id, limit)
