@@ -179,8 +179,41 @@ def experiment_create(args):
     s = session(args)
     exp = s.post("/api/v1/experiments", body)["experiment"]
     print(f"Created experiment {exp['id']}")
+    if getattr(args, "publish", None):
+        import threading
+
+        threading.Thread(target=_publish_first_trial, args=(args, s, exp["id"]), daemon=True).start()
     if args.follow_first_trial:
         _follow_first_trial(s, exp["id"])
+    elif getattr(args, "publish", None):
+        _wait_terminal(s, exp["id"])
+
+
+def _wait_terminal(s: Session, eid: int) -> str:
+    while True:
+        st = s.get(f"/api/v1/experiments/{eid}")["experiment"]["state"]
+        if st in ("COMPLETED", "CANCELED", "ERROR", "DELETED"):
+            return st
+        time.sleep(2)
+
+
+def _publish_first_trial(args, s: Session, eid: int) -> None:
+    """``det e create -p LOCAL[:REMOTE]``: once the first trial has a task, serve the port map
+    through the master's tunnel until the experiment ends (reference: `cli/proxy.py`
+    tunnel_experiment)."""
+    from determined_clone_amd.cli import tunnel
+
+    task_id = None
+    while task_id is None:
+        ts = s.get(f"/api/v1/experiments/{eid}/trials")["trials"]
+        task_id = next((t["task_id"] for t in ts if t.get("task_id")), None)
+        if task_id is None:
+            time.sleep(1)
+    port_map = tunnel.parse_port_map(args.publish)
+    with tunnel.listeners(s.master, s.token, task_id, port_map) as ports:
+        for (local, remote), bound in zip(port_map.items(), ports):
+            print(f"published 127.0.0.1:{bound} -> {task_id}:{remote}", flush=True)
+        _wait_terminal(s, eid)
 
 
 def _local_test(cfg: Dict[str, Any], context: Optional[str]) -> None:
@@ -850,6 +883,8 @@ def build_parser() -> argparse.ArgumentParser:
     sp.add_argument("--template"); sp.add_argument("--project-id", type=int)
     sp.add_argument("--config", action="append", help="override: key.path=value")
     sp.add_argument("-f", "--follow-first-trial", action="store_true")
+    sp.add_argument("-p", "--publish", action="append", default=[],
+                    help="LOCAL[:REMOTE]: forward a local port to the first trial's port (repeatable)")
     sp = cmd(e, "list ls", experiment_list); sp.add_argument("--all", "-a", action="store_true")
     for name, fn in (("describe", experiment_describe), ("config", experiment_config),
                      ("list-trials lt", experiment_list_trials), ("delete", experiment_delete),

@@ -101,3 +101,54 @@ def test_stdio_mode_as_proxy_command(cluster):
     p = subprocess.run([sys.executable, "-m", "determined_clone_amd.cli.tunnel", url, "t1", "--token", tok],
                        input=b"ssh-2.0 banner\n", capture_output=True, timeout=60, cwd=REPO)
     assert p.stdout == b"SSH-2.0 BANNER\n", p.stderr
+
+
+def test_ports_example_published_through_master(tmp_path):
+    """examples/features/ports on an in-process cluster: the trial's dashboard port is reached
+    from this machine through `/tunnel/{task}` (what `det e create ports.yaml . -p 8265` does)."""
+    import base64
+    import json
+    import time
+    import urllib.request
+
+    import yaml
+
+    from determined_clone_amd.agent import Agent
+    from determined_clone_amd.common.api import Session
+    from determined_clone_amd.util import tar_directory
+
+    ex = os.path.join(REPO, "examples", "features", "ports")
+    m = Master(str(tmp_path / "m.db"), checkpoint_storage={"type": "shared_fs", "host_path": str(tmp_path / "ck")})
+    srv = MasterServer(m, port=0).start()
+    agent = Agent(m.master_url, "agent-0", artificial_slots=1).start_background()
+    try:
+        s = Session(m.master_url)
+        s.token = s.post("/api/v1/auth/login", {"username": "admin", "password": ""})["token"]
+        with socket.socket() as probe:
+            probe.bind(("127.0.0.1", 0))
+            port = probe.getsockname()[1]
+        cfg = yaml.safe_load(open(os.path.join(ex, "ports.yaml")))
+        cfg["hyperparameters"] = {"steps": 30, "linger_s": 60}
+        cfg["environment"]["environment_variables"] = [f"DASHBOARD_PORT={port}"]
+        cfg["environment"]["proxy_ports"] = [{"proxy_port": port, "proxy_tcp": True}]
+        body = {"config": cfg, "model_definition": base64.b64encode(tar_directory(ex)).decode()}
+        eid = s.post("/api/v1/experiments", body)["experiment"]["id"]
+        task_id, state, deadline = None, None, time.time() + 120
+        while time.time() < deadline:
+            ts = s.get(f"/api/v1/experiments/{eid}/trials")["trials"]
+            task_id = next((t["task_id"] for t in ts if t.get("task_id")), None)
+            if task_id:
+                try:
+                    with tunnel.listeners(m.master_url, s.token, task_id, {0: port}) as (local,):
+                        with urllib.request.urlopen(f"http://127.0.0.1:{local}/", timeout=10) as r:
+                            state = json.loads(r.read())
+                    if state.get("step", 0) >= 30:
+                        break
+                except (OSError, ValueError):
+                    pass
+            time.sleep(0.5)
+        assert state is not None and state["step"] == 30 and state["task"] == task_id, state
+        s.post(f"/api/v1/experiments/{eid}/kill")
+    finally:
+        agent.stop()
+        srv.stop()
