@@ -64,10 +64,13 @@ class TorchBatchProcessorContext(_PyTorchReducerContext):
 
     @contextlib.contextmanager
     def upload_path(self) -> Iterator[pathlib.Path]:
-        """Files written under the yielded path are uploaded into this worker's output folder of
-        the job's output checkpoint."""
-        with self._core.checkpoint.store_path({"steps_completed": 0}, shard=self.distributed.size > 1) as (p, sid):
-            out = pathlib.Path(p) / self._storage_path
+        """Files written under the yielded path land in this worker's folder
+        ``<default_output_uuid>/rank_<r>/`` of checkpoint storage. They are job OUTPUT, not
+        checkpoints: nothing is registered with the master, so checkpoint GC never removes them
+        (the resume-state checkpoints record ``default_output_uuid``)."""
+        out_id, sub = self._storage_path.split("/", 1)
+        with self._core.checkpoint._storage_manager.store_path(out_id) as p:
+            out = pathlib.Path(p) / sub
             out.mkdir(parents=True, exist_ok=True)
             yield out
 
@@ -170,7 +173,10 @@ def torch_batch_process(batch_processor_cls: Type[TorchBatchProcessor], dataset:
         loader = _data.DataLoader(dataset, batch_size=batch_size, shuffle=False, **dataloader_kwargs)
         it = iter(loader.get_data_loader(repeat=False, skip=skip, num_replicas=workers, rank=rank))
         n_iter = _iterations(len(dataset), batch_size, workers, max_batches)
-        op = core.DummySearcherOperation(1, True) if rank == 0 else None
+        # the chief holds the trial's searcher operation (a dummy off-cluster): progress is reported
+        # as a fraction of its length and it is completed at the end, so the experiment finishes
+        ops = core_context.searcher.operations(core.SearcherMode.ChiefOnly) if rank == 0 else None
+        op = next(ops, None) if ops is not None else None
         last_ckpt = -1
         batch_idx = skip - 1
         for batch_idx in range(skip, n_iter):
@@ -182,7 +188,8 @@ def torch_batch_process(batch_processor_cls: Type[TorchBatchProcessor], dataset:
                 _checkpoint(core_context, batch_idx + 1, out_uuid)
                 last_ckpt = batch_idx
                 if op is not None:
-                    op.report_progress(min(1.0, (batch_idx + 1) * batch_size * workers / max(len(dataset), 1)))
+                    op.report_progress(op.length * min(1.0, (batch_idx + 1) * batch_size * workers
+                                                       / max(len(dataset), 1)))
                 if core_context.preempt.should_preempt():
                     _reduce(ctx, core_context, rank, batch_idx + 1)
                     return
@@ -193,6 +200,7 @@ def torch_batch_process(batch_processor_cls: Type[TorchBatchProcessor], dataset:
         _reduce(ctx, core_context, rank, batch_idx + 1)
         if op is not None:
             op.report_completed(0.0)
+            next(ops, None)  # out of operations: the trial is done
 
 
 def _checkpoint(core_context: Any, steps_completed: int, out_uuid: str) -> None:

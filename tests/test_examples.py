@@ -291,3 +291,33 @@ def test_hf_image_classification_example_on_cluster(cluster):
         raise AssertionError("\n".join(l["log"] for l in logs[-40:]))
     val = s.get(f"/api/v1/trials/{t['id']}/metrics", params={"group": "validation"})["metrics"]
     assert val[-1]["metrics"]["eval_accuracy"] > 0.3  # 10 separable classes, chance is 0.1
+
+
+@pytest.mark.parametrize("config", ["core_api_config.yaml", "torch_batch_process_config.yaml"])
+def test_batch_inference_comparison_examples(cluster, config, tmp_path):
+    """features/torch_batch_process_core_api_comparison: both implementations run distributed
+    (2 ranks) to completion on the cluster and predict every sample exactly once."""
+    import torch
+
+    s = cluster
+    ex = os.path.join(EX, "features", "torch_batch_process_core_api_comparison")
+    cfg = yaml.safe_load(open(os.path.join(ex, config)))
+    cfg["environment"] = {"environment_variables": [f"PREDICTIONS_DIR={tmp_path}"]}
+    eid, st = _run(s, ex, cfg, timeout=400)
+    assert st == "COMPLETED"
+    if config.startswith("core_api"):
+        files = sorted(tmp_path.glob("rank*_upto*.pt"))
+        preds = torch.cat([torch.load(f, weights_only=True) for f in files])
+        t = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]
+        val = s.get(f"/api/v1/trials/{t['id']}/metrics", params={"group": "validation"})["metrics"]
+        assert val[-1]["metrics"]["predicted"] == 512
+    else:
+        ckpts = s.get(f"/api/v1/experiments/{eid}/checkpoints")["checkpoints"]
+        assert ckpts, "torch_batch_process checkpoints its progress"
+        import glob
+
+        root = s.get("/api/v1/master/config")["config"]["checkpoint_storage"]["host_path"]
+        files = glob.glob(os.path.join(root, "**", "predictions_*.pt"), recursive=True)
+        assert files, sorted(glob.glob(os.path.join(root, "**"), recursive=True))[:20]
+        preds = torch.cat([torch.load(f, weights_only=True) for f in files])
+    assert sorted(preds[:, 0].tolist()) == list(range(512))
