@@ -500,10 +500,28 @@ inline int reduce_blocks(int64_t M, int C, const ReduceGeom& g) {
   return static_cast<int>(b);
 }
 
+// Apply-pass tuning (A/B sweeps only): DCA_BN_APPLY="U,max_blocks" -- rows in flight per lane
+// (2 | 4 | 8) and the workgroup cap.
+struct ApplyTuning {
+  int u, max_blocks;
+};
+inline const ApplyTuning& apply_tuning() {
+  static const ApplyTuning t = [] {
+    ApplyTuning r{kUApply, 2048};
+    if (const char* e = std::getenv("DCA_BN_APPLY")) {
+      int u = 0, mb = 0;
+      if (std::sscanf(e, "%d,%d", &u, &mb) == 2 && (u == 2 || u == 4 || u == 8) && mb > 0) r = {u, mb};
+    }
+    return r;
+  }();
+  return t;
+}
+
 // Workgroups (in x) for the apply passes: up to 8 per CU, each with >= 2 unrolled iterations.
 inline int apply_blocks(int64_t M, const RowGeom& g) {
-  int64_t b = (M + static_cast<int64_t>(g.rpi) * kUApply * 2 - 1) / (static_cast<int64_t>(g.rpi) * kUApply * 2);
-  if (b > 2048) b = 2048;
+  const ApplyTuning& t = apply_tuning();
+  int64_t b = (M + static_cast<int64_t>(g.rpi) * t.u * 2 - 1) / (static_cast<int64_t>(g.rpi) * t.u * 2);
+  if (b > t.max_blocks) b = t.max_blocks;
   if (b < 1) b = 1;
   return static_cast<int>(b);
 }
@@ -529,8 +547,11 @@ void launch_apply_fwd(const void* x, const void* res, void* y, const float* scal
                       hipStream_t st) {
   const RowGeom g = row_geom(C);
   dim3 grid(apply_blocks(M, g), g.cgroups);
-  hipLaunchKernelGGL((bn_apply_fwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, x, res, y,
-                     scale, shift, M, C, g.tpr, g.rpi, relu, mask);
+  switch (apply_tuning().u) {
+    case 2: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, 2>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
+    case 8: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, 8>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
+    default: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
+  }
 }
 
 template <typename T>
@@ -539,8 +560,11 @@ void launch_apply_bwd(const void* dy, const void* dy2, const uint8_t* mask, cons
                       hipStream_t st) {
   const RowGeom g = row_geom(C);
   dim3 grid(apply_blocks(M, g), g.cgroups);
-  hipLaunchKernelGGL((bn_apply_bwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, dy, dy2, mask,
-                     x, coef, dx, dres, M, C, g.tpr, g.rpi, relu);
+  switch (apply_tuning().u) {
+    case 2: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 2>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
+    case 8: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 8>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
+    default: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
+  }
 }
 
 // ------------------------------------------------------------------ stem: BN + ReLU + MaxPool(3,2,1)
