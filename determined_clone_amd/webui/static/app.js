@@ -102,7 +102,8 @@ function niceTicks(lo, hi, n) {
   return out;
 }
 // series: [{name, points: [[x, y], ...]}]
-function lineChart(title, series, xlabel) {
+function lineChart(title, series, xlabel, opts) {
+  opts = opts || {};
   const NS = "http://www.w3.org/2000/svg";
   const W = 460, H = 240, L = 58, R = 12, T = 10, B = 34;
   const pts = series.flatMap((s) => s.points).filter((p) => isFinite(p[0]) && isFinite(p[1]));
@@ -139,8 +140,8 @@ function lineChart(title, series, xlabel) {
       const p = s.points.filter((q) => isFinite(q[0]) && isFinite(q[1])).sort((a, b) => a[0] - b[0]);
       if (!p.length) return;
       const color = PALETTE[i % PALETTE.length];
-      mk("polyline", { points: p.map((q) => sx(q[0]) + "," + sy(q[1])).join(" "), fill: "none", stroke: color, "stroke-width": 1.6 });
-      if (p.length < 40) p.forEach((q) => mk("circle", { cx: sx(q[0]), cy: sy(q[1]), r: 2.2, fill: color }));
+      if (!opts.scatter) mk("polyline", { points: p.map((q) => sx(q[0]) + "," + sy(q[1])).join(" "), fill: "none", stroke: color, "stroke-width": 1.6 });
+      if (opts.scatter || p.length < 40) p.forEach((q) => mk("circle", { cx: sx(q[0]), cy: sy(q[1]), r: opts.scatter ? 3.2 : 2.2, fill: color, "fill-opacity": opts.scatter ? 0.75 : 1 }));
     });
   }
   const legend = h("div", { class: "legend" }, series.length > 1 ? series.map((s, i) =>
@@ -238,7 +239,7 @@ async function pageExperiment(params, id) {
   const head = h("div", {}, h("h1", {}, `Experiment ${e.id}: ${e.name || ""} `, badge(e.state)),
     h("div", { class: "toolbar" }, experimentActions(e), progressBar(e.progress),
       h("span", { class: "muted" }, `${e.searcher_type} searcher · pool ${e.resource_pool} · started ${fmtTime(e.start_time)}`)),
-    tabs(`#/experiments/${id}`, tab, ["overview", "trials", "checkpoints", "hyperparameters", "configuration", "notes"]));
+    tabs(`#/experiments/${id}`, tab, ["overview", "trials", "visualization", "checkpoints", "hyperparameters", "configuration", "notes"]));
   let body;
   if (tab === "overview" || tab === "trials") {
     const { trials } = await api.get(`/api/v1/experiments/${id}/trials`);
@@ -262,6 +263,23 @@ async function pageExperiment(params, id) {
     }
     parts.push(h("h2", {}, "Trials"), table(cols, trials, { sortKey: "id", desc: false }));
     body = parts;
+  } else if (tab === "visualization") {
+    // hyperparameter search view: learning curves of up to 20 trials + metric vs each numeric hparam
+    const { trials } = await api.get(`/api/v1/experiments/${id}/trials`);
+    const metric = (e.config.searcher || {}).metric;
+    const shown = trials.slice(0, 20);
+    const curves = await Promise.all(shown.map((t) => api.get(`/api/v1/trials/${t.id}/metrics?group=validation`)
+      .then((r) => ({ name: "trial " + t.id, points: r.metrics.filter((m) => typeof (m.metrics || {})[metric] === "number")
+        .map((m) => [m.steps_completed, m.metrics[metric]]) })).catch(() => ({ name: "trial " + t.id, points: [] }))));
+    const numeric = [...new Set(trials.flatMap((t) => Object.keys(t.hparams || {})))]
+      .filter((k) => trials.some((t) => typeof (t.hparams || {})[k] === "number"));
+    const scored = trials.filter((t) => typeof t.best_validation === "number");
+    body = [h("div", { class: "charts" }, lineChart(`Validation ${metric} by trial`, curves, "batches")),
+      h("h2", {}, `Best ${metric} vs hyperparameters`),
+      numeric.length ? h("div", { class: "charts" }, numeric.map((k) => lineChart(k,
+        [{ name: k, points: scored.filter((t) => typeof t.hparams[k] === "number").map((t) => [t.hparams[k], t.best_validation]) }],
+        k, { scatter: true })))
+        : h("div", { class: "muted" }, "no numeric hyperparameters")];
   } else if (tab === "checkpoints") {
     const { checkpoints } = await api.get(`/api/v1/experiments/${id}/checkpoints?sort_by=searcher_metric`);
     body = checkpointTable(checkpoints);
