@@ -321,3 +321,16 @@ def test_batch_inference_comparison_examples(cluster, config, tmp_path):
         assert files, sorted(glob.glob(os.path.join(root, "**"), recursive=True))[:20]
         preds = torch.cat([torch.load(f, weights_only=True) for f in files])
     assert sorted(preds[:, 0].tolist()) == list(range(512))
+
+
+def test_experimental_test_one_batch(tmp_path, monkeypatch):
+    """det.experimental.test_one_batch on the MNIST tutorial trial (reference: experimental/_native.py)."""
+    from determined_clone_amd import experimental
+
+    monkeypatch.chdir(tmp_path)
+    mod = _import_example("cifar10_asha", "model_def")
+    cfg = {"hyperparameters": {"global_batch_size": 16, "learning_rate": {"type": "const", "val": 0.01},
+                               "width": 16, "hidden": 64}}
+    experimental.test_one_batch(mod.CIFARTrial, cfg)
+    with pytest.raises(TypeError):
+        experimental.test_one_batch(object, cfg)
