@@ -104,5 +104,10 @@ def test_dsat_cli_on_cluster(cluster, capsys):
     import json
 
     out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
-    assert out["best"]["train_micro_batch_size_per_gpu"] == 8
+    # the best micro batch is chosen by measured samples/s, which a loaded CPU can reorder among the
+    # fitting sizes; what is pinned is that it fits (the fake OOM is above 8) and that 8 was tried
+    assert out["best"]["train_micro_batch_size_per_gpu"] in (1, 2, 4, 8)
+    assert any(t["mbs"] == 8 and not t["oom"] for t in out["trials"])
+    best = max((t for t in out["trials"] if not t["oom"]), key=lambda t: t["metric"])
+    assert out["best"]["train_micro_batch_size_per_gpu"] == best["mbs"]
     assert any(t["oom"] for t in out["trials"])
