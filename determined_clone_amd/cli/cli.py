@@ -17,7 +17,7 @@ import yaml
 
 from determined_clone_amd import __version__
 from determined_clone_amd.common.api import Session
-from determined_clone_amd.errors import APIException
+from determined_clone_amd.errors import APIException, EnterpriseOnlyError
 
 AUTH_FILE = pathlib.Path(os.environ.get("DET_CLONE_AUTH", pathlib.Path.home() / ".det-clone" / "auth.json"))
 
@@ -1012,6 +1012,10 @@ def build_parser() -> argparse.ArgumentParser:
 
     rbac_cli.register(cmd, group)
 
+    from determined_clone_amd.cli import sso as sso_cli
+
+    sso_cli.register(cmd, group)
+
     from determined_clone_amd.cli import extra as extra_cli
 
     extra_cli.register(cmd, group, groups.__getitem__)
@@ -1041,7 +1045,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         return 1
     try:
         args.func(args)
-    except APIException as e:
+    except (APIException, EnterpriseOnlyError) as e:
         print(f"Error: {e}", file=sys.stderr)
         return 1
     return 0

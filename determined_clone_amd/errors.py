@@ -54,5 +54,9 @@ class UnauthenticatedException(APIException):
         super().__init__(401, message)
 
 
+class EnterpriseOnlyError(Exception):
+    """A feature the master does not serve (reference: det.errors.EnterpriseOnlyError)."""
+
+
 class DeterminedError(Exception):
     """Generic client-side error (reference: det.common.api.errors.DeterminedError-style)."""

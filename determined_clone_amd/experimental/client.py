@@ -792,6 +792,19 @@ class ResourcePool:
 
 
 # ---------------------------------------------------------------------------------- Determined
+class OAuthClient:
+    """An OAuth2 client application registered with the master (reference: Oauth2ScimClient)."""
+
+    def __init__(self, id: str, name: str, domain: str, secret: Optional[str] = None) -> None:  # noqa: A002
+        self.id = id
+        self.name = name
+        self.domain = domain
+        self.secret = secret
+
+    def __repr__(self) -> str:
+        return f"OAuthClient(id={self.id!r}, name={self.name!r}, domain={self.domain!r})"
+
+
 class Determined:
     """Entry point of the SDK bound to one master session."""
 
@@ -979,6 +992,24 @@ class Determined:
                 labels[l] = labels.get(l, 0) + 1
         return sorted(labels, key=lambda k: -labels[k])
 
+    # OAuth clients (reference: common/experimental/determined.py:478-520, oauth2_scim_client.py)
+    def list_oauth_clients(self) -> List["OAuthClient"]:
+        try:
+            return [OAuthClient(c["id"], c["name"], c["domain"])
+                    for c in self._session.get("/oauth2/clients")]
+        except errors.NotFoundException:
+            raise errors.EnterpriseOnlyError("API not found: oauth2/clients")
+
+    def add_oauth_client(self, domain: str, name: str) -> "OAuthClient":
+        try:
+            d = self._session.post("/oauth2/clients", {"domain": domain, "name": name})
+        except errors.NotFoundException:
+            raise errors.EnterpriseOnlyError("API not found: oauth2/clients")
+        return OAuthClient(d["id"], name, domain, secret=d["secret"])
+
+    def remove_oauth_client(self, client_id: str) -> None:
+        self._session.delete(f"/oauth2/clients/{client_id}")
+
     # metrics
     def iter_trials_metrics(self, trial_ids: List[int], group: str) -> Iterable[TrialMetrics]:
         for tid in trial_ids:
@@ -1056,6 +1087,9 @@ get_model_by_id = _export("get_model_by_id")
 get_models = _export("get_models")
 list_models = _export("list_models")
 get_model_labels = _export("get_model_labels")
+list_oauth_clients = _export("list_oauth_clients")
+add_oauth_client = _export("add_oauth_client")
+remove_oauth_client = _export("remove_oauth_client")
 stream_trials_metrics = _export("stream_trials_metrics")
 iter_trials_metrics = _export("iter_trials_metrics")
 stream_trials_training_metrics = _export("stream_trials_training_metrics")

@@ -38,6 +38,8 @@ def main() -> None:
                authz=args.authz or ((cfg.get("security") or {}).get("authz") or {}).get("type", "basic"),
                resource_manager=cfg.get("resource_manager"), resource_pools=cfg.get("resource_pools"),
                logging_config=cfg.get("logging"))
+    m.sso_providers = [{"name": str(p["name"]), "sso_url": str(p["sso_url"])}
+                       for p in cfg.get("sso_providers") or []]
     srv = MasterServer(m, cfg.get("host", args.host), int(cfg.get("port", args.port)))
     if cfg.get("external_url"):  # the address tasks, agents and provisioned instances dial
         m.master_url = str(cfg["external_url"]).rstrip("/")

@@ -138,6 +138,9 @@ class Master:
         self.db.kv_set("cluster_id", self.cluster_id)
         self.cluster_name = cluster_name
         self.master_url = master_url
+        # master.yaml ``sso_providers: [{name, sso_url}]``: advertised on /api/v1/master for
+        # ``det auth login`` (the identity provider redirects to the CLI's localhost listener)
+        self.sso_providers: List[Dict[str, Any]] = []
         self.checkpoint_storage = checkpoint_storage or {
             "type": "shared_fs", "host_path": os.path.join(os.path.expanduser("~"), ".det-clone-ckpts")}
         self.rm = make_resource_manager(resource_manager, scheduler, fit, preemption,
@@ -145,7 +148,9 @@ class Master:
                                         self.container_event, resource_pools)
         self.experiments: Dict[int, Experiment] = {}
         self.allocations: Dict[str, Allocation] = {}
-        self.ports = PortRegistry()
+        # rendezvous ports handed to multi-rank tasks; the range base is overridable for hosts
+        # that run several masters (e.g. parallel test workers) next to each other
+        self.ports = PortRegistry(base=int(os.environ.get("DET_RENDEZVOUS_PORT_BASE", "29400")))
         self.tasks: Dict[str, Dict[str, Any]] = {}
         self.webhooks = Webhooks(self)
         self.lock = threading.RLock()

@@ -179,7 +179,8 @@ def set_password(r: Req) -> Any:
 @route("GET", "/api/v1/master", auth=False)
 def master_info(r: Req) -> Any:
     return {"version": __version__, "master_id": r.m.cluster_id, "cluster_id": r.m.cluster_id,
-            "cluster_name": r.m.cluster_name, "telemetry_enabled": False, "sso_providers": [],
+            "cluster_name": r.m.cluster_name, "telemetry_enabled": False,
+            "sso_providers": list(getattr(r.m, "sso_providers", [])),
             "product": "determined_clone_amd", "uptime_s": time.time() - r.m.start_time}
 
 
@@ -197,6 +198,46 @@ def master_config(r: Req) -> Any:
     return {"config": {"scheduler": {"type": r.m.rm.policy, "fitting_policy": r.m.rm.fit,
                                      "preemption": r.m.rm.preemption},
                        "checkpoint_storage": r.m.checkpoint_storage}}
+
+
+# =========================================================================== OAuth clients
+# The reference's OAuth2 client registry (``/oauth2/clients``, used by SCIM provisioning) is an
+# enterprise add-on: its OSS master answers 404 and the SDK raises EnterpriseOnlyError
+# (harness/determined/common/experimental/determined.py:478-520). Here it is a small admin-only
+# registry in the master's kv store: id + generated secret + redirect domain.
+def _oauth_clients(m: Master) -> List[Dict[str, Any]]:
+    return list(m.db.kv_get("oauth2_clients", []))
+
+
+@route("GET", "/oauth2/clients")
+def oauth_clients(r: Req) -> Any:
+    r.require_admin()
+    return [{"id": c["id"], "name": c["name"], "domain": c["domain"]} for c in _oauth_clients(r.m)]
+
+
+@route("POST", "/oauth2/clients")
+def oauth_client_add(r: Req) -> Any:
+    r.require_admin()
+    name, domain = r.body.get("name"), r.body.get("domain")
+    if not name or not domain:
+        raise HTTPError(400, "name and domain are required")
+    import secrets as _secrets
+
+    c = {"id": _secrets.token_hex(8), "secret": _secrets.token_hex(24), "name": str(name),
+         "domain": str(domain)}
+    r.m.db.kv_set("oauth2_clients", _oauth_clients(r.m) + [c])
+    return {"id": c["id"], "secret": c["secret"]}
+
+
+@route("DELETE", "/oauth2/clients/{cid}")
+def oauth_client_remove(r: Req) -> Any:
+    r.require_admin()
+    cs = _oauth_clients(r.m)
+    keep = [c for c in cs if c["id"] != r.p["cid"]]
+    if len(keep) == len(cs):
+        raise HTTPError(404, "oauth client not found")
+    r.m.db.kv_set("oauth2_clients", keep)
+    return {}
 
 
 # =========================================================================== agents
@@ -1291,7 +1332,7 @@ class _Handler(BaseHTTPRequestHandler):
             ctype, data = (prom.state_metrics(self.master) if parsed.path.startswith("/prom/")
                            else prom.process_metrics())
             return self._send_raw(200, ctype, data)
-        if method == "GET" and not parsed.path.startswith("/api/"):
+        if method == "GET" and not parsed.path.startswith(("/api/", "/oauth2/")):
             return self._static(parsed.path)
         try:
             body = json.loads(raw) if raw else None
