@@ -233,8 +233,19 @@ def main() -> None:
     ap.add_argument("--label", default="")
     ap.add_argument("--slots-per-gpu", type=int, default=1,
                     help="expose each MI355X as this many slots (HP-search trials sharing a GPU)")
+    ap.add_argument("--master-cert-file", default=None,
+                    help="CA / self-signed cert of an HTTPS master, or 'noverify'")
+    ap.add_argument("--master-cert-name", default=None,
+                    help="host name the master's certificate was issued for")
     args = ap.parse_args()
     logging.basicConfig(level=logging.INFO)
+    # the agent's own Session and every task it launches (tasks inherit the agent environment)
+    # verify the master the same way
+    if args.master_cert_file:
+        os.environ["DET_MASTER_CERT_FILE"] = os.path.abspath(args.master_cert_file) \
+            if args.master_cert_file.lower() != "noverify" else "noverify"
+    if args.master_cert_name:
+        os.environ["DET_MASTER_CERT_NAME"] = args.master_cert_name
     Agent(args.master_url, args.agent_id, args.resource_pool, args.artificial_slots, args.label,
           slots_per_gpu=args.slots_per_gpu).run()
 

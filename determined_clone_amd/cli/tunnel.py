@@ -12,6 +12,7 @@ to port N on the task's host, so no WebSocket framing is needed on either side.
 import argparse
 import os
 import socket
+import ssl
 import socketserver
 import sys
 import threading
@@ -25,9 +26,18 @@ def open_tunnel(master_url: str, token: Optional[str], task_id: str,
     """Connect to the master and upgrade to a tunnel; returns the socket and any bytes the
     master's side already sent after the 101 response."""
     u = urllib.parse.urlsplit(master_url if "://" in master_url else "http://" + master_url)
-    if u.scheme != "http":
-        raise ValueError("tunnels need a plain-HTTP master URL")
+    if u.scheme not in ("http", "https"):
+        raise ValueError(f"unsupported master URL scheme {u.scheme!r}")
     sock = socket.create_connection((u.hostname or "127.0.0.1", u.port or 8080), timeout=timeout)
+    if u.scheme == "https":  # verified like the REST session (DET_MASTER_CERT_FILE / _NAME)
+        from determined_clone_amd.common.api import Cert
+
+        cert = Cert.from_env()
+        ctx = ssl.create_default_context(cafile=cert.bundle or None)
+        if cert.bundle is False:
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+        sock = ctx.wrap_socket(sock, server_hostname=cert.name or u.hostname)
     path = f"/tunnel/{urllib.parse.quote(task_id)}" + (f"?port={int(port)}" if port else "")
     req = (f"GET {path} HTTP/1.1\r\nHost: {u.netloc}\r\nConnection: Upgrade\r\nUpgrade: det-tcp\r\n"
            + (f"Authorization: Bearer {token}\r\n" if token else "") + "\r\n")
@@ -59,7 +69,10 @@ def _pump(src: socket.socket, dst: socket.socket) -> None:
         pass
     finally:
         with contextlib.suppress(OSError):
-            dst.shutdown(socket.SHUT_WR)
+            if isinstance(dst, ssl.SSLSocket):
+                dst.close()  # TLS has no half-close
+            else:
+                dst.shutdown(socket.SHUT_WR)
 
 
 def splice(a: socket.socket, b: socket.socket, a_pending: bytes = b"") -> None:

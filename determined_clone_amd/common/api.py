@@ -2,26 +2,70 @@
 `request.py`). JSON in, JSON out; bearer-token auth; bounded retries on connection errors."""
 import json
 import logging
+import os
 import time
 from typing import Any, Dict, Optional
 
 import requests
+import requests.adapters
 
 from determined_clone_amd import errors
 
 logger = logging.getLogger("determined_clone_amd.api")
 
 
+class Cert:
+    """How to verify an HTTPS master (reference: `harness/determined/common/api/certs.py`).
+
+    ``bundle``: a CA / self-signed certificate file to trust, or ``False`` for no verification
+    (``DET_MASTER_CERT_FILE=noverify``), or ``None`` for the system store. ``name``: the host name
+    the certificate was issued for, when it differs from the address dialed
+    (``DET_MASTER_CERT_NAME``)."""
+
+    def __init__(self, bundle: Any = None, name: Optional[str] = None, noverify: bool = False) -> None:
+        self.bundle = False if noverify else bundle
+        self.name = name
+
+    @classmethod
+    def from_env(cls) -> "Cert":
+        f = os.environ.get("DET_MASTER_CERT_FILE")
+        name = os.environ.get("DET_MASTER_CERT_NAME") or None
+        if f and f.lower() == "noverify":
+            return cls(noverify=True, name=name)
+        return cls(bundle=f or None, name=name)
+
+
+class _NamedHostAdapter(requests.adapters.HTTPAdapter):
+    """Checks the master's certificate against ``cert_name`` instead of the dialed host."""
+
+    def __init__(self, cert_name: str, **kw: Any) -> None:
+        self._cert_name = cert_name
+        super().__init__(**kw)
+
+    def init_poolmanager(self, *args: Any, **kw: Any) -> None:
+        kw["assert_hostname"] = self._cert_name
+        kw["server_hostname"] = self._cert_name
+        super().init_poolmanager(*args, **kw)
+
+
 class Session:
     def __init__(self, master_url: str, token: Optional[str] = None, max_retries: int = 5,
-                 timeout: float = 60.0) -> None:
+                 timeout: float = 60.0, cert: Optional[Cert] = None) -> None:
         if not master_url.startswith("http"):
             master_url = "http://" + master_url
         self.master = master_url.rstrip("/")
         self.token = token
         self.max_retries = max_retries
         self.timeout = timeout
+        self.cert = cert if cert is not None else Cert.from_env()
         self._http = requests.Session()
+        # per-request ``verify`` (requests lets REQUESTS_CA_BUNDLE override a session-level one)
+        self._verify: Any = True
+        if self.master.startswith("https://"):
+            if self.cert.bundle is not None:
+                self._verify = self.cert.bundle
+            if self.cert.name:
+                self._http.mount("https://", _NamedHostAdapter(self.cert.name))
 
     def _headers(self) -> Dict[str, str]:
         h = {"Content-Type": "application/json"}
@@ -37,7 +81,7 @@ class Session:
         for attempt in range(self.max_retries + 1):
             try:
                 r = self._http.request(method, url, data=data, params=params, headers=self._headers(),
-                                       timeout=timeout or self.timeout)
+                                       timeout=timeout or self.timeout, verify=self._verify)
             except requests.ConnectionError as e:
                 last = e
                 time.sleep(min(2 ** attempt * 0.2, 5.0))

@@ -40,7 +40,8 @@ def main() -> None:
                logging_config=cfg.get("logging"))
     m.sso_providers = [{"name": str(p["name"]), "sso_url": str(p["sso_url"])}
                        for p in cfg.get("sso_providers") or []]
-    srv = MasterServer(m, cfg.get("host", args.host), int(cfg.get("port", args.port)))
+    srv = MasterServer(m, cfg.get("host", args.host), int(cfg.get("port", args.port)),
+                       tls=(cfg.get("security") or {}).get("tls"))
     if cfg.get("external_url"):  # the address tasks, agents and provisioned instances dial
         m.master_url = str(cfg["external_url"]).rstrip("/")
     srv.start()

@@ -1438,6 +1438,7 @@ class _Handler(BaseHTTPRequestHandler):
         opens (reference: the master's TCP-over-WebSocket proxy, `harness/determined/cli/
         tunnel.py` / `proxy.py`). Authenticated like ``/proxy/``; task owner or admin only."""
         import socket
+        import ssl
 
         task_id = parsed.path.split("/", 3)[2] if parsed.path.count("/") >= 2 else ""
         if self.headers.get("Upgrade", "").lower() != "det-tcp":
@@ -1479,7 +1480,11 @@ class _Handler(BaseHTTPRequestHandler):
                 pass
             finally:
                 try:
-                    dst.shutdown(socket.SHUT_WR)
+                    # TLS has no half-close: end an HTTPS client's connection outright
+                    if isinstance(dst, ssl.SSLSocket):
+                        dst.close()
+                    else:
+                        dst.shutdown(socket.SHUT_WR)
                 except OSError:
                     pass
 
@@ -1559,13 +1564,30 @@ class _Handler(BaseHTTPRequestHandler):
 
 
 class MasterServer:
-    def __init__(self, master: Master, host: str = "127.0.0.1", port: int = 8080) -> None:
+    """The master's HTTP(S) front end. ``tls``: master.yaml ``security.tls`` (``cert``, ``key``
+    PEM files; reference `master/internal/config/config.go` TLSConfig) -- when given, every route,
+    the proxy and the tunnels are served over TLS and ``master_url`` is ``https://``."""
+
+    def __init__(self, master: Master, host: str = "127.0.0.1", port: int = 8080,
+                 tls: Optional[Dict[str, str]] = None) -> None:
         handler = type("H", (_Handler,), {"master": master})
         self.httpd = ThreadingHTTPServer((host, port), handler)
         self.httpd.daemon_threads = True
+        scheme = "http"
+        if tls and (tls.get("cert") or tls.get("key")):
+            if not (tls.get("cert") and tls.get("key")):
+                raise ValueError("security.tls needs both cert and key")
+            import ssl
+
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(tls["cert"], tls["key"])
+            # handshake lazily in the per-connection thread, not in the accept loop
+            self.httpd.socket = ctx.wrap_socket(self.httpd.socket, server_side=True,
+                                                do_handshake_on_connect=False)
+            scheme = "https"
         self.master = master
         self.port = self.httpd.server_address[1]
-        master.master_url = f"http://{host}:{self.port}"
+        master.master_url = f"{scheme}://{host}:{self.port}"
         self._thread: Optional[threading.Thread] = None
 
     def start(self) -> "MasterServer":
