@@ -791,7 +791,8 @@ def list_tasks(r: Req) -> Any:
 def get_task(r: Req) -> Any:
     t = r.m.db.one("SELECT * FROM tasks WHERE task_id=?", [r.p["task_id"]])
     allocs = r.m.db.all("SELECT * FROM allocations WHERE task_id=?", [r.p["task_id"]])
-    if t is None and not allocs:
+    # a trial's task exists from trial creation on (unmanaged trials never get an allocation)
+    if t is None and not allocs and not r.m.db.one("SELECT id FROM trials WHERE task_id=?", [r.p["task_id"]]):
         raise HTTPError(404, "task not found")
     return {"task": {"task_id": r.p["task_id"], "type": (t or {}).get("task_type", "TRIAL"),
                      "allocations": allocs}}
