@@ -5,7 +5,7 @@ timed is the real PyTorchTrial path of this framework: ``pytorch.Trainer.fit`` -
 ``_PyTorchTrialController`` -> ``trial.train_batch`` (forward, ``context.backward`` with bucketed
 RCCL all-reduce overlapped with backward, ``context.step_optimizer`` with the fused HIP SGD) on
 ResNet-50 v1.5 (random init, 25.6M params), bf16 NHWC activations, fp32 master weights, synthetic
-224x224 ImageNet-shaped data resident in HBM. Weak scaling: 512 images per GPU per step.
+224x224 ImageNet-shaped data resident in HBM. Weak scaling: 1024 images per GPU per step.
 
 Usage: ``python bench.py [--gpus N --steps K --warmup W]``; for N>1 launch under
 ``torch.distributed.run`` (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from the env).
@@ -100,7 +100,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=512, help="images per GPU per step (288 GB HBM: 512 is 7%% faster than 256, profiles/round2_resnet50_batch_ab.txt)")
+    ap.add_argument("--batch", type=int, default=1024,
+                    help="images per GPU per step (288 GB HBM: 1024 is 6%% faster than 512 and 13%% "
+                         "faster than 256, profiles/round2_resnet50_batch_ab.txt, round2_resnet50_bs1024_ab.txt)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:

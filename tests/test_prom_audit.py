@@ -59,10 +59,28 @@ def test_process_metrics_count_requests(master):
 def test_audit_log_records_mutations(master, caplog):
     m, url = master
     tok, _ = m.login("admin", "")
-    with caplog.at_level(logging.INFO, logger="determined_clone_amd.master.audit"):
+    # a handler on the audit logger itself: independent of propagation / root-level settings other
+    # tests in the same worker process may have changed
+    records = []
+
+    class _Keep(logging.Handler):
+        def emit(self, record):
+            records.append(record)
+
+    lg = logging.getLogger("determined_clone_amd.master.audit")
+    h = _Keep(level=logging.INFO)
+    old_level, old_disabled = lg.level, lg.disabled
+    lg.addHandler(h)
+    lg.setLevel(logging.INFO)
+    lg.disabled = False
+    try:
         _call(url, "POST", "/api/v1/workspaces", {"name": "audited"}, tok)
         _get(url + "/api/v1/master")  # reads are not audited
-    recs = [json.loads(r.getMessage()) for r in caplog.records if r.name == "determined_clone_amd.master.audit"]
+    finally:
+        lg.removeHandler(h)
+        lg.setLevel(old_level)
+        lg.disabled = old_disabled
+    recs = [json.loads(r.getMessage()) for r in records]
     assert len(recs) == 1
     assert recs[0]["user"] == "admin" and recs[0]["method"] == "POST"
     assert recs[0]["path"] == "/api/v1/workspaces" and recs[0]["status"] == 200
