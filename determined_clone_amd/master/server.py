@@ -6,6 +6,8 @@ import base64
 import json
 import logging
 import re
+import ssl
+import sys
 import threading
 import time
 import http.cookies
@@ -1586,6 +1588,18 @@ class MasterServer:
             self.httpd.socket = ctx.wrap_socket(self.httpd.socket, server_side=True,
                                                 do_handshake_on_connect=False)
             scheme = "https"
+            base_handle_error = self.httpd.handle_error
+
+            def handle_error(request: Any, client_address: Any) -> None:
+                # a client that rejects our certificate (or speaks plain HTTP) ends its
+                # handshake: one log line, not a traceback
+                err = sys.exc_info()[1]
+                if isinstance(err, (ssl.SSLError, ConnectionResetError)):
+                    logger.info(f"TLS handshake with {client_address[0]} failed: {err}")
+                    return
+                base_handle_error(request, client_address)
+
+            self.httpd.handle_error = handle_error
         self.master = master
         self.port = self.httpd.server_address[1]
         master.master_url = f"{scheme}://{host}:{self.port}"
