@@ -323,9 +323,10 @@ class ZeroShardMixin:
                         for n in names:
                             fulls[n][a0:a1].copy_(s[n][o:o + (a1 - a0)])
                         covered[a0:a1] = True
-                for seg in st.buf.segments:
-                    mine = any(a0 < seg.offset + seg.numel and seg.offset < a1 for a0, a1, _ in st.owned)
-                    if mine and not bool(covered[seg.offset:seg.offset + seg.numel].all()):
+                # what this rank reads is exactly its owned ranges (a parameter may straddle two
+                # ranks' partitions: only the owned part of it has to be in the given shards)
+                for a0, a1, _ in st.owned:
+                    if not bool(covered[a0:a1].all()):
                         raise ValueError("optimizer shards do not cover this rank's partition; "
                                          "pass all ranks' shards to load_shard_state_dicts")
                 for a0, a1, o in st.owned:

@@ -226,6 +226,7 @@ class DeepSpeedEngine(torch.nn.Module):
                  device: Optional[torch.device] = None) -> None:
         super().__init__()
         self.group = group
+        self.mp_rank = 0  # tensor-parallel rank (set by initialize() from the mpu): checkpoint names
         self.world_size = dist.get_world_size(group) if dist.is_initialized() else 1
         self.global_rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.config = DeepSpeedConfig(config, self.world_size)
@@ -463,9 +464,10 @@ class DeepSpeedEngine(torch.nn.Module):
     def save_checkpoint(self, save_dir: Union[str, pathlib.Path], tag: Optional[str] = None,
                         client_state: Optional[Dict[str, Any]] = None,
                         save_latest: bool = True) -> bool:
-        """Layout (DeepSpeed-like): ``<dir>/<tag>/mp_rank_00_model_states.pt`` (rank 0: module,
+        """Layout (DeepSpeed-like): ``<dir>/<tag>/mp_rank_<m>_model_states.pt`` (data-parallel rank 0
+        of model-parallel rank m -- 00 without tensor parallelism: module,
         scheduler, counters, client state, stage-0 optimizer) and
-        ``<dir>/<tag>/zero_pp_rank_<r>_mp_rank_00_optim_states.pt`` (every rank's ZeRO shard)."""
+        ``<dir>/<tag>/zero_pp_rank_<r>_mp_rank_<m>_optim_states.pt`` (every rank's ZeRO shard)."""
         tag = tag or f"global_step{self.global_steps}"
         d = self._ckpt_dir(save_dir, tag)
         d.mkdir(parents=True, exist_ok=True)
@@ -482,12 +484,12 @@ class DeepSpeedEngine(torch.nn.Module):
             }
             if self.config.zero_stage == 0:
                 state["optimizer"] = self.optimizer.state_dict()
-            torch.save(state, d / "mp_rank_00_model_states.pt")
+            torch.save(state, d / f"mp_rank_{self.mp_rank:02d}_model_states.pt")
             if save_latest:
                 (pathlib.Path(save_dir) / "latest").write_text(str(tag))
         if self.config.zero_stage >= 1:
             torch.save({"optimizer_state_dict": self.optimizer.state_dict()},
-                       d / f"zero_pp_rank_{self.global_rank}_mp_rank_00_optim_states.pt")
+                       d / f"zero_pp_rank_{self.global_rank}_mp_rank_{self.mp_rank:02d}_optim_states.pt")
         return True
 
     def load_checkpoint(self, load_dir: Union[str, pathlib.Path], tag: Optional[str] = None,
@@ -502,7 +504,7 @@ class DeepSpeedEngine(torch.nn.Module):
                 return None, None
             tag = latest.read_text().strip()
         d = self._ckpt_dir(load_dir, tag)
-        path = d / "mp_rank_00_model_states.pt"
+        path = d / f"mp_rank_{self.mp_rank:02d}_model_states.pt"
         if not path.exists():
             raise FileNotFoundError(f"DeepSpeed-format checkpoint not found at {path}")
         state = torch.load(path, map_location="cpu", weights_only=True)
@@ -519,7 +521,7 @@ class DeepSpeedEngine(torch.nn.Module):
         if self.scaler is not None and state.get("scaler"):
             self.scaler.load_state_dict(state["scaler"])
         if load_optimizer_states:
-            own = d / f"zero_pp_rank_{self.global_rank}_mp_rank_00_optim_states.pt"
+            own = d / f"zero_pp_rank_{self.global_rank}_mp_rank_{self.mp_rank:02d}_optim_states.pt"
             if self._z3 is not None:
                 if int(state.get("dp_world_size", -1)) == self.world_size and own.exists():
                     osd = torch.load(own, map_location="cpu", weights_only=True)["optimizer_state_dict"]
@@ -529,7 +531,7 @@ class DeepSpeedEngine(torch.nn.Module):
                 else:
                     # written at another data-parallel size: re-partition every rank's shards
                     saved_world = int(state.get("dp_world_size", -1))
-                    files = [d / f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt"
+                    files = [d / f"zero_pp_rank_{r}_mp_rank_{self.mp_rank:02d}_optim_states.pt"
                              for r in range(max(saved_world, 0))]
                     if saved_world < 1 or not all(f.exists() for f in files):
                         raise FileNotFoundError(
@@ -543,11 +545,11 @@ class DeepSpeedEngine(torch.nn.Module):
                         self.optimizer.sync_master_from_model()
             elif isinstance(self.optimizer, zero.ZeroShardMixin):
                 saved_world = int(state.get("dp_world_size", self.world_size))
-                own = d / f"zero_pp_rank_{self.global_rank}_mp_rank_00_optim_states.pt"
+                own = d / f"zero_pp_rank_{self.global_rank}_mp_rank_{self.mp_rank:02d}_optim_states.pt"
                 if saved_world == self.world_size and own.exists():
                     shards = [torch.load(own, map_location="cpu", weights_only=True)["optimizer_state_dict"]]
                 else:
-                    shards = [torch.load(d / f"zero_pp_rank_{r}_mp_rank_00_optim_states.pt",
+                    shards = [torch.load(d / f"zero_pp_rank_{r}_mp_rank_{self.mp_rank:02d}_optim_states.pt",
                                          map_location="cpu", weights_only=True)["optimizer_state_dict"]
                               for r in range(saved_world)]
                 self.optimizer.load_shard_state_dicts(shards)
@@ -606,6 +608,19 @@ def initialize(args: Any = None, model: Optional[torch.nn.Module] = None,
             model, cfg, optimizer=optimizer, model_parameters=model_parameters,
             lr_scheduler=lr_scheduler)
     else:
+        mp_size = mpu.get_model_parallel_world_size() if mpu is not None and \
+            hasattr(mpu, "get_model_parallel_world_size") else 1
+        if mpu is not None and group is None and hasattr(mpu, "get_data_parallel_group"):
+            # gradients are averaged over the data-parallel group only (DeepSpeed's mpu contract)
+            group = mpu.get_data_parallel_group()
         engine = DeepSpeedEngine(model, cfg, optimizer=optimizer, model_parameters=model_parameters,
                                  lr_scheduler=lr_scheduler, group=group)
+        if mp_size > 1:
+            from determined_clone_amd.parallel import tensor as tp
+
+            engine.mp_rank = mpu.get_model_parallel_rank()
+
+            # clip norm of the whole model: sharded parameters summed over the TP group,
+            # replicated ones counted once (parallel/tensor.py)
+            tp.tp_norm_setup(engine.optimizer, list(model.parameters()), mpu.get_model_parallel_group())
     return engine, engine.optimizer, None, engine.lr_scheduler

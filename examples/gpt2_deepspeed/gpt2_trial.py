@@ -3,7 +3,10 @@ gpt2_trial.py, which drives GPT-NeoX through DeepSpeed; here ``det_ds.initialize
 MI355X engine: ZeRO-1/2 over RCCL, fused HIP AdamW, MFMA flash attention, fused LN / GELU / CE).
 
 ``hyperparameters.pipe_parallel_size: N`` trains the same GPT as an N-stage pipeline
-(``pipe.yaml``; the reference example's ``pipe_parallel_size: 2``).
+(``pipe.yaml``; the reference example's ``pipe_parallel_size: 2``);
+``hyperparameters.model_parallel_size: M`` shards it Megatron-style over M adjacent ranks
+(``tp.yaml``; the reference example's ``model_parallel_size: 2``): heads / MLP columns / vocab
+split, gradients averaged over the data-parallel group only.
 
 The DeepSpeed JSON config is ``ds_config.json`` overlaid with ``hyperparameters.overwrite_deepspeed_args``
 (same convention as the reference's ``overwrite_deepspeed_config``). Synthetic token data."""
@@ -39,7 +42,17 @@ class GPT2Trial(det_ds.DeepSpeedTrial):
         base = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "ds_config.json")))
         ds_config = det_ds.overwrite_deepspeed_config(base, hp.get("overwrite_deepspeed_args", {}))
         self.pipe = int(hp.get("pipe_parallel_size", 0))
-        if self.pipe >= 1:
+        mp_size = int(hp.get("model_parallel_size", 1))
+        grid = None
+        if mp_size > 1:
+            if self.pipe > 1:
+                raise ValueError("model_parallel_size > 1 is not combined with pipe_parallel_size > 1")
+            from determined_clone_amd.models.gpt2_tp import TPGPT
+            from determined_clone_amd.parallel.tensor import ModelParallelGrid
+
+            grid = ModelParallelGrid(model_parallel_size=mp_size)
+            model = TPGPT(cfg, grid.get_model_parallel_group())
+        elif self.pipe >= 1:
             # GPT-NeoX style pipeline (reference gpt_neox/zero1.yaml: pipe_parallel_size 2):
             # embedding | blocks | final norm | tied LM head over `pipe` stages, 1F1B schedule
             model = det_ds.PipelineModule(gpt2.pipeline_specs(cfg), num_stages=self.pipe,
@@ -48,8 +61,14 @@ class GPT2Trial(det_ds.DeepSpeedTrial):
                                               hp.get("activation_checkpoint_interval", 0)))
         else:
             model = gpt2.GPT(cfg)
-        engine, _, _, _ = det_ds.initialize(model=model, config=ds_config)
+        engine, _, _, _ = det_ds.initialize(model=model, config=ds_config, mpu=grid)
         self.engine = context.wrap_model_engine(engine)
+        if grid is not None:
+            # every TP rank of a data-parallel group reads the same shard of the data
+            context.set_mpu(det_ds.ModelParallelUnit(
+                data_parallel_rank=grid.get_data_parallel_rank(),
+                data_parallel_world_size=grid.get_data_parallel_world_size(),
+                should_report_metrics=True, should_build_data_loader=True))
         self.vocab = cfg.vocab_size
 
     def train_batch(self, it, epoch_idx, batch_idx):

@@ -133,6 +133,29 @@ def test_gpt2_pipeline_example_on_cluster(cluster):
     assert val[-1]["steps_completed"] == 4 and val[-1]["metrics"]["lm_loss"] > 0
 
 
+def test_gpt2_tensor_parallel_example_on_cluster(cluster):
+    """The GPT-2 DeepSpeed example with model_parallel_size 2 over 2 slots (tp.yaml): Megatron
+    TP layers, engine gradient sync over the (size-1) data-parallel group, TP-aware clipping."""
+    s = cluster
+    cfg = yaml.safe_load(open(os.path.join(EX, "gpt2_deepspeed", "tp.yaml")))
+    # the tiny preset's 2 heads of 64 split one per TP rank
+    cfg["hyperparameters"].update({"model": "tiny", "seq_len": 32, "model_parallel_size": 2})
+    cfg["hyperparameters"]["overwrite_deepspeed_args"] = {
+        "train_micro_batch_size_per_gpu": 2, "gradient_clipping": 1.0,
+        "bf16": {"enabled": False}, "zero_optimization": {"stage": 1},
+        "scheduler": {"params": {"warmup_num_steps": 2, "total_num_steps": 10}}}
+    cfg["resources"]["slots_per_trial"] = 2
+    cfg["searcher"]["max_length"] = {"batches": 4}
+    cfg["min_validation_period"] = {"batches": 4}
+    eid, st = _run(s, os.path.join(EX, "gpt2_deepspeed"), cfg)
+    t = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]
+    if st != "COMPLETED":
+        logs = s.get(f"/api/v1/trials/{t['id']}/logs")["logs"]
+        raise AssertionError("\n".join(l["log"] for l in logs[-60:]))
+    val = s.get(f"/api/v1/trials/{t['id']}/metrics", params={"group": "validation"})["metrics"]
+    assert val[-1]["steps_completed"] == 4 and val[-1]["metrics"]["lm_loss"] > 0
+
+
 # ---------------------------------------------------------------- tutorials/core_api_pytorch_mnist
 def test_core_api_pytorch_mnist_tutorial_on_cluster(cluster):
     """Plain PyTorch loop on the Core API: metrics, per-epoch checkpoints, searcher ops."""
