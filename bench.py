@@ -108,7 +108,10 @@ def main() -> None:
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if torch.cuda.is_available():
-        torch.backends.cudnn.benchmark = True
+        # MIOpen: benchmark=True runs miopenFind per conv shape in every process (tuned solvers
+        # come from the shipped perf DB either way); DCA_CONV_BENCHMARK=0 uses immediate mode,
+        # which picks from the shipped find DB without timing candidates
+        torch.backends.cudnn.benchmark = os.environ.get("DCA_CONV_BENCHMARK", "1") != "0"
     hparams = {"global_batch_size": args.batch * world, "warmup": args.warmup, "steps": args.steps}
     # the timed step runs eagerly: optimizations.hip_graph is refused for MIOpen convolutions
     # (pytorch/_graph.py), and train_batch's timestamps must run on every step
