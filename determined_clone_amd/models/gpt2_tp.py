@@ -120,6 +120,7 @@ class TPGPT(nn.Module):
             self.register_buffer("rope_cos", cos, persistent=False)
             self.register_buffer("rope_sin", sin, persistent=False)
         _init_like_gpt(self, cfg)
+        tp_reinit_(self, cfg, group)
 
     def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None):
         B, S = idx.shape
@@ -188,3 +189,115 @@ class TPGPT(nn.Module):
             out[p + "mlp.proj.weight"] = gather(b.mlp.proj.weight, 1)
             out[p + "mlp.proj.bias"] = b.mlp.proj.bias.detach().clone()
         return out
+
+
+def tp_reinit_(module: nn.Module, cfg: GPTConfig, group: Any) -> None:
+    """Re-draw the TP-sharded parameters from a per-TP-rank generator (Megatron's model-parallel
+    RNG): with one global seed every rank would otherwise draw identical shards, i.e. duplicated
+    heads / MLP columns. Replicated parameters keep the global RNG's (identical) values."""
+    if tp._size(group) <= 1 or any(p.is_meta for p in module.parameters()):
+        return  # (meta: PipelineModule sizing its partition without materialising layers)
+    import math
+
+    base = int(torch.randint(0, 2 ** 31 - 1, (1,), device="cpu").item())  # same seed -> same on every rank
+    gen = torch.Generator().manual_seed(base + 7919 * (tp._rank(group) + 1))
+    proj_std = cfg.init_std / math.sqrt(2 * cfg.n_layer)
+    with torch.no_grad():
+        for name, p in module.named_parameters():
+            if not getattr(p, "tensor_model_parallel", False) or p.dim() < 2:
+                continue
+            std = proj_std if name.endswith("proj.weight") else cfg.init_std
+            p.copy_(torch.randn(p.shape, generator=gen) * std)
+
+
+# ---------------------------------------------------------------------------------- pipe x tensor
+class EmbeddingPipeTP(nn.Module):
+    """Vocab-parallel token (+ replicated learned position) embedding for a pipeline stage."""
+
+    def __init__(self, cfg: GPTConfig, group: Any) -> None:
+        super().__init__()
+        self.cfg = cfg
+        self.wte = tp.VocabParallelEmbedding(cfg.padded_vocab, cfg.d_model, group)
+        self.wpe = nn.Embedding(cfg.max_seq_len, cfg.d_model) if cfg.pos_emb == "learned" else None
+        _init_like_gpt(self, cfg)
+        tp_reinit_(self, cfg, group)
+
+    def forward(self, idx: torch.Tensor) -> torch.Tensor:
+        x = self.wte(idx)
+        if self.wpe is not None:
+            x = x + self.wpe.weight[:idx.shape[1]].unsqueeze(0)
+        return x
+
+
+class BlockPipeTP(TPBlock):
+    """Tensor-parallel block on a pipeline activation (residual, or (residual, pending delta))."""
+
+    def __init__(self, cfg: GPTConfig, group: Any) -> None:
+        super().__init__(cfg, group)
+        self.rotary = cfg.pos_emb == "rotary"
+        if self.rotary:
+            cos, sin = T.rope_tables(cfg.max_seq_len, self.attn.rot, cfg.rotary_base)
+            self.register_buffer("rope_cos", cos, persistent=False)
+            self.register_buffer("rope_sin", sin, persistent=False)
+        _init_like_gpt(self, cfg)
+        tp_reinit_(self, cfg, group)
+
+    def forward(self, x):  # type: ignore[override]
+        resid, delta = (x, None) if isinstance(x, torch.Tensor) else x
+        rope = (self.rope_cos, self.rope_sin) if self.rotary else None
+        return super().forward(resid, delta, rope)
+
+
+def _tied_head_tp(module: nn.Module, h: torch.Tensor) -> torch.Tensor:
+    return F.linear(tp.copy_to_tp(h, module.wte.group), module.wte.weight)
+
+
+class PipelineLossTP:
+    """Vocab-parallel cross-entropy on the last stage (the logits are this rank's vocab shard)."""
+
+    def __init__(self, cfg: GPTConfig, group: Any) -> None:
+        self.group = group
+        self.start = tp._rank(group) * (cfg.padded_vocab // tp._size(group))
+
+    def __call__(self, logits: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+        return tp.vocab_parallel_cross_entropy(logits, targets, self.group, self.start)
+
+
+def pipeline_specs_tp(cfg: GPTConfig, group: Any) -> list:
+    """:func:`~determined_clone_amd.models.gpt2.pipeline_specs` with tensor-parallel layers: the
+    reference gpt_neox layout with pipe_parallel_size x model_parallel_size (zero1.yaml: 2 x 2).
+    Use with ``PipelineModule(..., grid=ModelParallelGrid(M, P), loss_fn=PipelineLossTP(cfg,
+    grid.mp_group))``."""
+    from determined_clone_amd.models.gpt2 import FinalNormPipe
+    from determined_clone_amd.parallel.pipeline import LayerSpec, TiedLayerSpec
+
+    if not cfg.tie_embeddings:
+        raise ValueError("the tensor-parallel pipeline uses the tied vocab-parallel embedding as LM head")
+    embed = TiedLayerSpec("embed", EmbeddingPipeTP, cfg, group, tied_weight_attr="wte.weight")
+    head = TiedLayerSpec("embed", EmbeddingPipeTP, cfg, group, forward_fn=_tied_head_tp,
+                         tied_weight_attr="wte.weight")
+    return [embed] + [LayerSpec(BlockPipeTP, cfg, group) for _ in range(cfg.n_layer)] + \
+        [LayerSpec(FinalNormPipe, cfg), head]
+
+
+@torch.no_grad()
+def load_pipeline_from(pipe_module: nn.Module, full: GPT) -> None:
+    """Copy a dense :class:`GPT` into the local stage's layers of a
+    :func:`pipeline_specs_tp` PipelineModule (layer 0 embedding, 1..L blocks, L+1 final norm,
+    L+2 tied head)."""
+    L = full.cfg.n_layer
+    for idx, mod in pipe_module._layer_modules.items():
+        if isinstance(mod, EmbeddingPipeTP):
+            mod.wte.load_full(full.wte.weight)
+            if mod.wpe is not None:
+                mod.wpe.weight.copy_(full.wpe.weight)
+        elif isinstance(mod, TPBlock):
+            fb = full.blocks[idx - 1]
+            mod.ln1.load_state_dict(fb.ln1.state_dict())
+            mod.ln2.load_state_dict(fb.ln2.state_dict())
+            mod.attn.qkv.load_full(fb.attn.qkv.weight, fb.attn.qkv.bias, rows=mod.attn.qkv_rows())
+            mod.attn.proj.load_full(fb.attn.proj.weight, fb.attn.proj.bias)
+            mod.mlp.fc.load_full(fb.mlp.fc.weight, fb.mlp.fc.bias)
+            mod.mlp.proj.load_full(fb.mlp.proj.weight, fb.mlp.proj.bias)
+        elif idx == L + 1:
+            mod.ln_f.load_state_dict(full.ln_f.state_dict())

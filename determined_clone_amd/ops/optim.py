@@ -38,6 +38,13 @@ class _FlatState:
         self.state = {n: torch.zeros(buf.numel, dtype=torch.float32, device=buf.device) for n in names}
 
 
+def _as_groups(g: Any) -> List[Any]:
+    """``norm_group``: None, one process group, or a list of them (pipeline x tensor parallel)."""
+    if g is None:
+        return []
+    return list(g) if isinstance(g, (list, tuple)) else [g]
+
+
 class FusedOptimizerBase(torch.optim.Optimizer):
     state_names: List[str] = []
 
@@ -78,7 +85,7 @@ class FusedOptimizerBase(torch.optim.Optimizer):
         if self.norm_group is not None or self.norm_exclude:
             slices = [st.buf.grad[a:b] for st in self.flat.values()
                       for a, b in self._norm_ranges(st.buf, [(0, st.buf.grad.numel())])]
-            groups = [self.norm_group] if self.norm_group is not None else []
+            groups = _as_groups(self.norm_group)
             self._finish_norm(self._sumsq(slices), max_norm, loss_scale, groups)
             return
         grads = [st.buf.grad for st in self.flat.values()]

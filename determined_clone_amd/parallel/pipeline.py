@@ -168,7 +168,12 @@ class PipelineGrid:
                     if self.global_rank in ranks:
                         self.dp_group = g
 
-    def stage_to_global(self, stage_id: int, data_parallel_id: Optional[int] = None) -> int:
+    model_parallel_size = 1  # no tensor parallelism (parallel.tensor.ModelParallelGrid has it)
+    model_parallel_id = 0
+    mp_group = None
+
+    def stage_to_global(self, stage_id: int, data_parallel_id: Optional[int] = None,
+                        model_parallel_id: Optional[int] = None) -> int:
         d = self.data_parallel_id if data_parallel_id is None else data_parallel_id
         return stage_id * self.data_parallel_size + d
 
@@ -214,7 +219,7 @@ class PipelineModule(nn.Module):
                  loss_fn: Optional[Callable[[Any, Any], torch.Tensor]] = None,
                  partition_method: str = "parameters", activation_checkpoint_interval: int = 0,
                  seed_layers: bool = False, base_seed: int = 1234,
-                 grid: Optional[PipelineGrid] = None) -> None:
+                 grid: Optional[Any] = None) -> None:
         super().__init__()
         self.specs = list(layers)
         self.loss_fn = loss_fn

@@ -84,6 +84,12 @@ class ModelParallelGrid:
                 if r in ranks:
                     self.pp_group = g
 
+    def stage_to_global(self, stage_id: int, data_parallel_id: Optional[int] = None,
+                        model_parallel_id: Optional[int] = None) -> int:
+        d = self.data_parallel_id if data_parallel_id is None else data_parallel_id
+        m = self.model_parallel_id if model_parallel_id is None else model_parallel_id
+        return self.rank_of(stage_id, d, m)
+
     # DeepSpeed / Megatron accessors
     def get_model_parallel_rank(self) -> int:
         return self.model_parallel_id

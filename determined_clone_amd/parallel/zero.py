@@ -231,8 +231,9 @@ class ZeroShardMixin:
         slices = [st.buf.grad[a:b] for st in self._order for a0, a1, _ in st.owned
                   for a, b in self._norm_ranges(st.buf, [(a0, a1)])]
         groups = [self.pg] if self.world > 1 else []
-        if self.norm_group is not None:
-            groups.append(self.norm_group)
+        from determined_clone_amd.ops.optim import _as_groups
+
+        groups += _as_groups(self.norm_group)
         self._finish_norm(self._sumsq(slices), max_norm, loss_scale, groups)
 
     # ------------------------------------------------------------------ step

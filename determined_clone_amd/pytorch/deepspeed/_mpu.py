@@ -28,4 +28,6 @@ def make_deepspeed_mpu(topology: Any) -> ModelParallelUnit:
         data_parallel_rank=topology.get_data_parallel_rank(),
         data_parallel_world_size=topology.get_data_parallel_world_size(),
         should_report_metrics=True,
-        should_build_data_loader=topology.get_slice_parallel_rank() == 0 and (first or last))
+        # every tensor-parallel rank of the first / last stage reads the same batch itself
+        # (instead of Megatron's broadcast from slice rank 0)
+        should_build_data_loader=first or last)

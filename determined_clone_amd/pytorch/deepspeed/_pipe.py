@@ -47,8 +47,19 @@ class PipelineEngine(DeepSpeedEngine):
         self._p2p = _P2P(self.device)
         self._tie_groups: Dict[str, Tuple[Any, List[int]]] = {}
         self._setup_ties()
-        if self.num_stages > 1:
-            self.optimizer.norm_group = grid.pp_group
+        norm_groups = [grid.pp_group] if self.num_stages > 1 else []
+        if grid.model_parallel_size > 1:
+            # tensor parallelism inside each stage (parallel/tensor.py): sharded parameters are
+            # summed over the TP group too, replicated ones counted on TP rank 0 only
+            from determined_clone_amd.parallel import tensor as tp
+
+            norm_groups.append(grid.mp_group)
+            if grid.model_parallel_id != 0:
+                self.optimizer.norm_exclude = list(self.optimizer.norm_exclude) + \
+                    tp.replicated_params(list(model.parameters()))
+            self.mp_rank = grid.model_parallel_id
+        if norm_groups:
+            self.optimizer.norm_group = norm_groups if len(norm_groups) > 1 else norm_groups[0]
         self.agg_train_loss: Optional[torch.Tensor] = None
         self.first_output_send = True
 
@@ -63,10 +74,11 @@ class PipelineEngine(DeepSpeedEngine):
             if len(stages) < 2:
                 continue
             for d in range(self.grid.data_parallel_size):  # collective: same order on every rank
-                ranks = [self.grid.stage_to_global(s, d) for s in stages]
-                g = dist.new_group(ranks)
-                if self.grid.global_rank in ranks:
-                    self._tie_groups[key] = (g, ranks)
+                for m in range(self.grid.model_parallel_size):  # one tie group per TP rank
+                    ranks = [self.grid.stage_to_global(s, d, m) for s in stages]
+                    g = dist.new_group(ranks)
+                    if self.grid.global_rank in ranks:
+                        self._tie_groups[key] = (g, ranks)
             if key in self._tie_groups:
                 g, ranks = self._tie_groups[key]
                 for w in mod.tied_weights(key):
@@ -339,6 +351,10 @@ class PipelineEngine(DeepSpeedEngine):
         return True
 
     # ------------------------------------------------------------------ checkpoint
+    def _mp_tag(self, sep: str) -> str:
+        """File-name part for the TP rank (DeepSpeed's ``-model_XX``); empty without TP."""
+        return f"{sep}{self.grid.model_parallel_id:02d}" if self.grid.model_parallel_size > 1 else ""
+
     def save_checkpoint(self, save_dir: Union[str, pathlib.Path], tag: Optional[str] = None,
                         client_state: Optional[Dict[str, Any]] = None,
                         save_latest: bool = True) -> bool:
@@ -352,12 +368,12 @@ class PipelineEngine(DeepSpeedEngine):
         dp = self.grid.data_parallel_id
         if dp == 0:
             for idx, sd in self.module.layer_state_dicts().items():
-                torch.save(sd, d / f"layer_{idx:02d}-model_states.pt")
+                torch.save(sd, d / f"layer_{idx:02d}{self._mp_tag('-model_')}-model_states.pt")
         if self.config.zero_stage >= 1 or dp == 0:
             torch.save({"optimizer_state_dict": self.optimizer.state_dict(),
                         "parts": list(self.module.parts),
                         "dp_world_size": self.grid.data_parallel_size},
-                       d / f"pipe_stage_{self.stage_id:02d}_dp_{dp:02d}_optim_states.pt")
+                       d / f"pipe_stage_{self.stage_id:02d}_dp_{dp:02d}{self._mp_tag('_mp_')}_optim_states.pt")
         if self.grid.global_rank == 0:
             torch.save({
                 "module": None,
@@ -388,7 +404,7 @@ class PipelineEngine(DeepSpeedEngine):
         start, stop = self.module.stage_layers()
         layers = {}
         for idx in range(start, stop):
-            p = d / f"layer_{idx:02d}-model_states.pt"
+            p = d / f"layer_{idx:02d}{self._mp_tag('-model_')}-model_states.pt"
             if p.exists():
                 layers[idx] = torch.load(p, map_location="cpu", weights_only=True)
         self.module.load_layer_state_dicts(layers, strict=load_module_strict)
@@ -401,7 +417,7 @@ class PipelineEngine(DeepSpeedEngine):
         same_layout = list(state.get("parts", [])) == list(self.module.parts) and \
             int(state.get("dp_world_size", -1)) == self.grid.data_parallel_size
         dp = self.grid.data_parallel_id if self.config.zero_stage >= 1 else 0
-        opt_path = d / f"pipe_stage_{self.stage_id:02d}_dp_{dp:02d}_optim_states.pt"
+        opt_path = d / f"pipe_stage_{self.stage_id:02d}_dp_{dp:02d}{self._mp_tag('_mp_')}_optim_states.pt"
         if load_optimizer_states and same_layout and opt_path.exists():
             osd = torch.load(opt_path, map_location="cpu", weights_only=True)["optimizer_state_dict"]
             from determined_clone_amd.parallel import zero

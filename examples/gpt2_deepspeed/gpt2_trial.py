@@ -6,7 +6,8 @@ MI355X engine: ZeRO-1/2 over RCCL, fused HIP AdamW, MFMA flash attention, fused 
 (``pipe.yaml``; the reference example's ``pipe_parallel_size: 2``);
 ``hyperparameters.model_parallel_size: M`` shards it Megatron-style over M adjacent ranks
 (``tp.yaml``; the reference example's ``model_parallel_size: 2``): heads / MLP columns / vocab
-split, gradients averaged over the data-parallel group only.
+split, gradients averaged over the data-parallel group only; both together (``pipe_tp.yaml``) is
+the reference's ``zero1.yaml`` layout: a pipeline of tensor-parallel stages.
 
 The DeepSpeed JSON config is ``ds_config.json`` overlaid with ``hyperparameters.overwrite_deepspeed_args``
 (same convention as the reference's ``overwrite_deepspeed_config``). Synthetic token data."""
@@ -44,9 +45,18 @@ class GPT2Trial(det_ds.DeepSpeedTrial):
         self.pipe = int(hp.get("pipe_parallel_size", 0))
         mp_size = int(hp.get("model_parallel_size", 1))
         grid = None
-        if mp_size > 1:
-            if self.pipe > 1:
-                raise ValueError("model_parallel_size > 1 is not combined with pipe_parallel_size > 1")
+        if mp_size > 1 and self.pipe >= 1:
+            # the reference's gpt_neox zero1.yaml layout: pipe_parallel_size x model_parallel_size
+            from determined_clone_amd.models import gpt2_tp
+            from determined_clone_amd.parallel.tensor import ModelParallelGrid
+
+            g = ModelParallelGrid(model_parallel_size=mp_size, pipe_parallel_size=self.pipe)
+            model = det_ds.PipelineModule(gpt2_tp.pipeline_specs_tp(cfg, g.mp_group),
+                                          num_stages=self.pipe, grid=g,
+                                          loss_fn=gpt2_tp.PipelineLossTP(cfg, g.mp_group),
+                                          activation_checkpoint_interval=int(
+                                              hp.get("activation_checkpoint_interval", 0)))
+        elif mp_size > 1:
             from determined_clone_amd.models.gpt2_tp import TPGPT
             from determined_clone_amd.parallel.tensor import ModelParallelGrid
 

@@ -156,6 +156,28 @@ def test_gpt2_tensor_parallel_example_on_cluster(cluster):
     assert val[-1]["steps_completed"] == 4 and val[-1]["metrics"]["lm_loss"] > 0
 
 
+def test_gpt2_pipe_tp_example_on_cluster(cluster):
+    """pipe_tp.yaml (the reference gpt_neox zero1.yaml layout) shrunk to 4 slots: 2 pipeline
+    stages of 2-way tensor-parallel layers."""
+    s = cluster
+    cfg = yaml.safe_load(open(os.path.join(EX, "gpt2_deepspeed", "pipe_tp.yaml")))
+    cfg["hyperparameters"].update({"model": "tiny", "seq_len": 32})
+    cfg["hyperparameters"]["overwrite_deepspeed_args"] = {
+        "train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2,
+        "bf16": {"enabled": False}, "zero_optimization": {"stage": 1},
+        "scheduler": {"params": {"warmup_num_steps": 2, "total_num_steps": 10}}}
+    cfg["resources"]["slots_per_trial"] = 4
+    cfg["searcher"]["max_length"] = {"batches": 2}
+    cfg["min_validation_period"] = {"batches": 2}
+    eid, st = _run(s, os.path.join(EX, "gpt2_deepspeed"), cfg)
+    t = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]
+    if st != "COMPLETED":
+        logs = s.get(f"/api/v1/trials/{t['id']}/logs")["logs"]
+        raise AssertionError("\n".join(l["log"] for l in logs[-60:]))
+    val = s.get(f"/api/v1/trials/{t['id']}/metrics", params={"group": "validation"})["metrics"]
+    assert val[-1]["steps_completed"] == 2 and val[-1]["metrics"]["lm_loss"] > 0
+
+
 # ---------------------------------------------------------------- tutorials/core_api_pytorch_mnist
 def test_core_api_pytorch_mnist_tutorial_on_cluster(cluster):
     """Plain PyTorch loop on the Core API: metrics, per-epoch checkpoints, searcher ops."""

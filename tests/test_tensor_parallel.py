@@ -188,3 +188,42 @@ def _gpu_tp(rank, world, d):
 @pytest.mark.gpu
 def test_tp2_bf16_hip_path_matches_dense():
     _run(2, _gpu_tp)
+
+
+# ---------------------------------------------------------------------------- pipe x tensor
+def _pipe_tp(rank, world, d):
+    """pipe 2 x model 2 (the reference gpt_neox zero1.yaml layout): the 1F1B pipeline of
+    tensor-parallel stages reproduces the dense model's loss and clip norm, and checkpoints per
+    (stage, TP rank)."""
+    from determined_clone_amd.models import gpt2_tp
+    from determined_clone_amd.pytorch import deepspeed as det_ds
+
+    torch.manual_seed(0)
+    cfg = _cfg()
+    full = gpt2.GPT(cfg)
+    grid = tp.ModelParallelGrid(model_parallel_size=2, pipe_parallel_size=2)
+    mod = det_ds.PipelineModule(gpt2_tp.pipeline_specs_tp(cfg, grid.mp_group), num_stages=2,
+                                loss_fn=gpt2_tp.PipelineLossTP(cfg, grid.mp_group), grid=grid)
+    gpt2_tp.load_pipeline_from(mod, full)
+    ds = {"train_micro_batch_size_per_gpu": 2, "gradient_accumulation_steps": 2,
+          "gradient_clipping": 1e-3, "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}},
+          "zero_optimization": {"stage": 1}}
+    eng, _, _, _ = det_ds.initialize(model=mod, config=ds)
+    g = torch.Generator().manual_seed(5)
+    micro = [(torch.randint(0, cfg.vocab_size, (2, 32), generator=g),
+              torch.randint(0, cfg.vocab_size, (2, 32), generator=g)) for _ in range(2)]
+    loss = eng.train_batch(iter(micro))
+    ref = sum(full(x, y)[1] for x, y in micro) / 2
+    ref.backward()
+    torch.testing.assert_close(loss.float(), ref.detach(), rtol=1e-5, atol=1e-5)
+    dense_norm = float(torch.sqrt(sum(p.grad.double().pow(2).sum() for p in full.parameters())))
+    assert abs(float(eng._last_grad_norm) - dense_norm) < 1e-4 * dense_norm, (float(eng._last_grad_norm), dense_norm)
+    eng.save_checkpoint(os.path.join(d, "ck"))
+    dist.barrier()
+    names = sorted(os.listdir(os.path.join(d, "ck", "global_step1")))
+    assert "layer_00-model_00-model_states.pt" in names and "layer_00-model_01-model_states.pt" in names
+    assert "pipe_stage_01_dp_00_mp_01_optim_states.pt" in names
+
+
+def test_pipe2_tp2_matches_dense():
+    _run(4, _pipe_tp)
