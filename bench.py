@@ -108,10 +108,11 @@ def main() -> None:
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if torch.cuda.is_available():
-        # MIOpen: benchmark=True runs miopenFind per conv shape in every process (tuned solvers
-        # come from the shipped perf DB either way); DCA_CONV_BENCHMARK=0 uses immediate mode,
-        # which picks from the shipped find DB without timing candidates
-        torch.backends.cudnn.benchmark = os.environ.get("DCA_CONV_BENCHMARK", "1") != "0"
+        # MIOpen immediate mode (benchmark=False) picks each conv's solver from the shipped find /
+        # perf DB (tools/miopen) without timing candidates: same kernels and step time as
+        # per-process miopenFind, but a 12 s instead of a 4 min process at bs 1024
+        # (profiles/round2_miopen_immediate_mode_ab.txt); DCA_CONV_BENCHMARK=1 runs the find
+        torch.backends.cudnn.benchmark = os.environ.get("DCA_CONV_BENCHMARK", "0") == "1"
     hparams = {"global_batch_size": args.batch * world, "warmup": args.warmup, "steps": args.steps}
     # the timed step runs eagerly: optimizations.hip_graph is refused for MIOpen convolutions
     # (pytorch/_graph.py), and train_batch's timestamps must run on every step
