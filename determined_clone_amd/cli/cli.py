@@ -760,6 +760,24 @@ def shell_open(args):
     state["closed"] = True
 
 
+def shell_show_ssh_command(args):
+    """det shell show-ssh-command ID [SSH_OPTS...]: the ssh command (e.g. for an IDE's remote
+    interpreter) that reaches the shell task through the master's TCP tunnel as ProxyCommand
+    (reference: cli/shell.py show_ssh_command). It needs an sshd serving the task's port in its
+    container image; without one use ``det shell open`` / ``det shell run``."""
+    import shlex
+
+    s = session(args)
+    t = s.get(f"/api/v1/shells/{args.task_id}")
+    shell = t.get("shell", t)
+    proxy = (f"{shlex.quote(sys.executable)} -m determined_clone_amd.cli.tunnel {s.master} %h"
+             f" --token {s.token}")
+    user = (shell.get("agent_user_group") or {}).get("agent_user") or os.environ.get("USER", "root")
+    opts = " ".join(shlex.quote(o) for o in (args.ssh_opts or []))
+    print(f"ssh -o {shlex.quote('ProxyCommand=' + proxy)} -o StrictHostKeyChecking=no "
+          f"-o IdentitiesOnly=yes {opts + ' ' if opts else ''}{user}@{args.task_id}")
+
+
 def shell_run(args):
     """det shell run ID -- CMD...: one command in the shell task's container."""
     s = session(args)
@@ -991,6 +1009,9 @@ def build_parser() -> argparse.ArgumentParser:
             sp.add_argument("--no-browser", action="store_true")
         if kind == "SHELL":
             sp = cmd(g, "open", shell_open); sp.add_argument("task_id")
+            for name in ("show-ssh-command", "show_ssh_command"):
+                sp = cmd(g, name, shell_show_ssh_command); sp.add_argument("task_id")
+                sp.add_argument("ssh_opts", nargs="*", help="additional ssh options")
             sp = cmd(g, "run", shell_run); sp.add_argument("task_id")
             sp.add_argument("command", nargs=argparse.REMAINDER)
 

@@ -41,7 +41,12 @@ def _run(s, ctx_dir, cfg, timeout=300):
         if st in ("COMPLETED", "CANCELED", "ERROR"):
             return eid, st
         time.sleep(0.5)
-    raise TimeoutError(st)
+    # diagnose a stuck run: the trial logs and allocation states
+    lines = []
+    for t in s.get(f"/api/v1/experiments/{eid}/trials")["trials"]:
+        lines.append(f"trial {t['id']} state={t.get('state')} restarts={t.get('restarts')}")
+        lines += [l["log"].rstrip() for l in s.get(f"/api/v1/trials/{t['id']}/logs")["logs"][-80:]]
+    raise TimeoutError(f"experiment {eid} still {st} after {timeout}s\n" + "\n".join(lines))
 
 
 def test_mnist_tutorial_on_cluster(cluster):

@@ -106,6 +106,13 @@ def test_shell_session_and_cli(cluster, monkeypatch):
     with redirect_stdout(buf), pytest.raises(SystemExit) as ex:
         cli.main(["-m", m.master_url, "-u", "admin", "shell", "run", tid, "--", "echo", "from-run;", "exit", "3"])
     assert ex.value.code == 3 and "from-run" in buf.getvalue()
+    # det shell show-ssh-command: ssh through the master's tunnel as ProxyCommand
+    buf = io.StringIO()
+    with redirect_stdout(buf):
+        assert cli.main(["-m", m.master_url, "-u", "admin", "shell", "show-ssh-command", tid, "--", "-p", "22"]) == 0
+    line = buf.getvalue().strip()
+    assert line.startswith("ssh -o ") and "determined_clone_amd.cli.tunnel " + m.master_url + " %h" in line
+    assert line.endswith(f"-p 22 {line.split()[-1]}") and line.split()[-1].endswith("@" + tid)
     s.post(base + "/input", {"data": "exit\n"})
     t0 = time.time()
     while s.get(f"/api/v1/shells/{tid}")["shell"].get("state") != "TERMINATED":
