@@ -610,6 +610,14 @@ def initialize(args: Any = None, model: Optional[torch.nn.Module] = None,
     else:
         mp_size = mpu.get_model_parallel_world_size() if mpu is not None and \
             hasattr(mpu, "get_model_parallel_world_size") else 1
+        raw = cfg
+        if isinstance(raw, (str, os.PathLike)):
+            with open(raw) as f:
+                raw = json.load(f)
+        if mp_size > 1 and int((raw.get("zero_optimization") or {}).get("stage", 0)) >= 3:
+            # ZeRO-3 flattens parameters into cross-parameter shards: the TP-aware clip norm
+            # (which tells sharded from replicated parameters) cannot see them
+            raise ValueError("tensor parallelism (model_parallel_size > 1) supports ZeRO stages 0-2")
         if mpu is not None and group is None and hasattr(mpu, "get_data_parallel_group"):
             # gradients are averaged over the data-parallel group only (DeepSpeed's mpu contract)
             group = mpu.get_data_parallel_group()

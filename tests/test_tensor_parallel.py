@@ -227,3 +227,18 @@ def _pipe_tp(rank, world, d):
 
 def test_pipe2_tp2_matches_dense():
     _run(4, _pipe_tp)
+
+
+def _z3_refused(rank, world, d):
+    from determined_clone_amd.pytorch import deepspeed as det_ds
+
+    grid = tp.ModelParallelGrid(model_parallel_size=2)
+    m = TPGPT(_cfg(), grid.get_model_parallel_group())
+    with pytest.raises(ValueError, match="ZeRO stages 0-2"):
+        det_ds.initialize(model=m, mpu=grid, config={
+            "train_micro_batch_size_per_gpu": 1, "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}},
+            "zero_optimization": {"stage": 3}})
+
+
+def test_tp_refuses_zero3():
+    _run(2, _z3_refused)
