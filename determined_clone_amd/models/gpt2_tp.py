@@ -83,6 +83,10 @@ class TPMLP(nn.Module):
 class TPBlock(nn.Module):
     def __init__(self, cfg: GPTConfig, group: Any) -> None:
         super().__init__()
+        if cfg.dropout and tp._size(group) > 1:
+            # dropout on the replicated residual stream must draw the same mask on every TP rank
+            # (Megatron's model-parallel RNG tracker); not provided here
+            raise NotImplementedError("dropout > 0 with tensor parallelism is not supported")
         self.ln1 = FusedLayerNorm(cfg.d_model, cfg.ln_eps)
         self.attn = TPAttention(cfg, group)
         self.ln2 = FusedLayerNorm(cfg.d_model, cfg.ln_eps)
