@@ -3,7 +3,10 @@ Determined (Core API, PyTorchTrial/Trainer, DeepSpeed-style ZeRO, hyperparameter
 agent / CLI), built on PyTorch-ROCm, hand-written HIP kernels for gfx950 and RCCL over xGMI."""
 __version__ = "0.1.0"
 
-from determined_clone_amd._info import ClusterInfo, RendezvousInfo, TrialInfo, get_cluster_info
+from determined_clone_amd._info import (ClusterInfo, RendezvousInfo, ResourcesInfo, TrialInfo,
+                                        get_cluster_info)
+from determined_clone_amd._experiment_config import ExperimentConfig
+from determined_clone_amd._import import import_from_path
 from determined_clone_amd.errors import InvalidHP
 from determined_clone_amd import errors, util
 

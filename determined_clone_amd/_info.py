@@ -6,6 +6,7 @@ inline in ``DET_CLUSTER_INFO``; off-cluster both are absent and ``get_cluster_in
 """
 import json
 import os
+import subprocess
 from typing import Any, Dict, List, Optional
 
 DEFAULT_CLUSTER_INFO_PATH = "/run/determined/info/cluster_info.json"
@@ -158,3 +159,29 @@ def get_cluster_info() -> Optional[ClusterInfo]:
         with open(path) as f:
             return ClusterInfo.from_dict(json.load(f))
     return None
+
+
+class ResourcesInfo:
+    """GPUs assigned to this container (reference: `_info.py` ResourcesInfo): the ROCm device
+    UUIDs from the cluster info, or from ``rocm-smi`` when off-cluster."""
+
+    def __init__(self, gpu_uuids: List[str]) -> None:
+        self._gpu_uuids = list(gpu_uuids)
+
+    @property
+    def gpu_uuids(self) -> List[str]:
+        return self._gpu_uuids
+
+    @classmethod
+    def _by_inspection(cls) -> "ResourcesInfo":
+        info = get_cluster_info()
+        if info is not None and info.gpu_uuids:
+            return cls(info.gpu_uuids)
+        try:
+            out = subprocess.run(["rocm-smi", "--showuniqueid", "--json"], capture_output=True,
+                                 text=True, timeout=20).stdout
+            d = json.loads(out or "{}")
+            return cls([str(v.get("Unique ID")) for k, v in sorted(d.items())
+                        if k.startswith("card") and v.get("Unique ID")])
+        except (OSError, ValueError, subprocess.SubprocessError):
+            return cls([])
