@@ -7,7 +7,7 @@ mkdir -p gpurun_out/bn_pmc
 cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $ROOT/gpurun_out/bn_pmc/fetch -o run --output-format csv -- python3 $ROOT/bench.py --batch 256 --steps 2 --warmup 1 > $ROOT/gpurun_out/bn_pmc/fetch.log 2>&1 && \
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $ROOT/gpurun_out/bn_pmc/write -o run --output-format csv -- python3 $ROOT/bench.py --batch 256 --steps 2 --warmup 1 > $ROOT/gpurun_out/bn_pmc/write.log 2>&1 && \
 cd $ROOT && python3 - > gpurun_out/bn_pmc/summary.txt <<'PY'
-import csv, glob, collections
+import csv, glob, collections, re
 def load(kind):
     f = glob.glob(f"gpurun_out/bn_pmc/{kind}/**/run_counter_collection.csv", recursive=True)[0]
     agg = collections.defaultdict(list)
@@ -15,7 +15,8 @@ def load(kind):
         name = r["Kernel_Name"]
         if "bn_" not in name:
             continue
-        short = name.split("(")[0].replace("void dca::(anonymous namespace)::", "")
+        m = re.search(r"(bn_[a-z_]+_kernel<[^>(]*>?)", name)
+        short = m.group(1) if m else name[:60]
         agg[(short, r.get("Grid_Size", ""))].append(float(r["Counter_Value"]))
     return agg
 fe, wr = load("fetch"), load("write")
