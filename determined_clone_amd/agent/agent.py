@@ -136,7 +136,14 @@ class Agent:
         runtime.fetch_context(self.session, spec["task_id"], ctx_dir)
         cmd, env = runtime.build_task(spec, self.master_url, self.id, self.devices, ctx_dir)
         proc = None
-        if self.zygote is not None and len(cmd) >= 3 and cmd[0] == sys.executable and cmd[1] == "-m":
+        why = None
+        if self.zygote is not None:
+            from determined_clone_amd.exec.zygote import incompatible_reason
+
+            why = incompatible_reason(env, skip_paths=[runtime.FRAMEWORK_ROOT])
+            if why:
+                logger.info(f"task {spec['task_id']}: plain subprocess, not the zygote ({why})")
+        if self.zygote is not None and not why and len(cmd) >= 3 and cmd[0] == sys.executable and cmd[1] == "-m":
             try:
                 proc = self.zygote.spawn(cmd[2], cmd[3:], env, ctx_dir)
             except Exception as e:

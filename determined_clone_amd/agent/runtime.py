@@ -74,6 +74,8 @@ def build_task(spec: Dict[str, Any], master_url: str, agent_id: str,
     env["DET_AGENT_ID"] = agent_id
     env["DET_ALLOCATION_ID"] = alloc
     env["DET_TASK_ID"] = task_id
+    if spec.get("proxy_secret"):
+        env["DET_TASK_PROXY_SECRET"] = str(spec["proxy_secret"])
     env["PYTHONUNBUFFERED"] = "1"
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env["PYTHONPATH"] = os.pathsep.join([ctx_dir, FRAMEWORK_ROOT] + ([env["PYTHONPATH"]] if env.get("PYTHONPATH") else []))

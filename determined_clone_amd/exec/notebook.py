@@ -35,7 +35,7 @@ from contextlib import redirect_stderr, redirect_stdout
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional
 
-from determined_clone_amd.util import routable_address
+from determined_clone_amd.util import proxy_secret_ok, routable_address
 
 PAGE = """<!doctype html><html><head><meta charset="utf-8"><title>notebook</title>
 <style>body{font-family:monospace;margin:2em}textarea{width:100%;height:6em}pre{background:#f4f4f4;padding:.5em}</style>
@@ -142,7 +142,7 @@ class Kernel:
 
 # ----------------------------------------------------------------------------- server
 class NotebookServer:
-    def __init__(self, root: str, host: str = "0.0.0.0", port: int = 0) -> None:
+    def __init__(self, root: str, host: Optional[str] = None, port: int = 0) -> None:
         self.root = os.path.abspath(root)
         self.kernels: Dict[str, Kernel] = {}
         self.last_activity = time.time()
@@ -167,6 +167,11 @@ class NotebookServer:
                 return json.loads(self.rfile.read(n)) if n else {}
 
             def _go(self, method: str) -> None:
+                # kernels run arbitrary code: on a cluster only the master's owner-checked
+                # /proxy/ route (which attaches the task's secret) may reach them
+                if not proxy_secret_ok(self.headers):
+                    self._body()
+                    return self._send(403, {"message": "requests must come through the master's /proxy/ route"})
                 srv.last_activity = time.time()
                 try:
                     code, obj, *ct = srv.handle(method, self.path.split("?")[0], self._body())
@@ -188,7 +193,7 @@ class NotebookServer:
             def do_DELETE(self) -> None:
                 self._go("DELETE")
 
-        self.httpd = ThreadingHTTPServer((host, port), H)
+        self.httpd = ThreadingHTTPServer((routable_address() if host is None else host, port), H)
         self.httpd.daemon_threads = True
 
     def _nb_path(self, name: str) -> str:
@@ -267,7 +272,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     if a.kernel:
         return kernel_main()
     srv = NotebookServer(a.root, port=a.port)
-    addr = f"http://{routable_address()}:{srv.httpd.server_address[1]}"
+    addr = f"http://{srv.httpd.server_address[0]}:{srv.httpd.server_address[1]}"
     print(f"notebook server at {addr} (root {a.root})", flush=True)
     from determined_clone_amd import _info
 

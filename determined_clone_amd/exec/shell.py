@@ -27,7 +27,7 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, List, Optional
 from urllib.parse import parse_qs, urlparse
 
-from determined_clone_amd.util import routable_address
+from determined_clone_amd.util import proxy_secret_ok, routable_address
 
 
 class ShellSession:
@@ -82,7 +82,10 @@ class ShellSession:
                 self.proc.kill()
 
 
-def make_server(session: ShellSession, cwd: str, host: str = "0.0.0.0", port: int = 0) -> ThreadingHTTPServer:
+def make_server(session: ShellSession, cwd: str, host: Optional[str] = None, port: int = 0) -> ThreadingHTTPServer:
+    """The shell's HTTP service, bound to ``host`` (default: the routable address registered with
+    the master). On a cluster every request must carry the task's proxy secret
+    (``util.proxy_secret_ok``), which only the master's owner-checked ``/proxy/`` route attaches."""
     class H(BaseHTTPRequestHandler):
         protocol_version = "HTTP/1.1"
         last = [time.time()]
@@ -102,7 +105,15 @@ def make_server(session: ShellSession, cwd: str, host: str = "0.0.0.0", port: in
             n = int(self.headers.get("Content-Length") or 0)
             return json.loads(self.rfile.read(n)) if n else {}
 
+        def _authorized(self) -> bool:
+            if proxy_secret_ok(self.headers):
+                return True
+            self._send(403, {"error": "requests must come through the master's /proxy/ route"})
+            return False
+
         def do_GET(self) -> None:
+            if not self._authorized():
+                return
             H.last[0] = time.time()
             u = urlparse(self.path)
             q = parse_qs(u.query)
@@ -112,6 +123,8 @@ def make_server(session: ShellSession, cwd: str, host: str = "0.0.0.0", port: in
                 self._send(200, {"service": "shell", "closed": session.closed})
 
         def do_POST(self) -> None:
+            if not self._authorized():
+                return
             H.last[0] = time.time()
             u = urlparse(self.path)
             b = self._body()
@@ -128,7 +141,7 @@ def make_server(session: ShellSession, cwd: str, host: str = "0.0.0.0", port: in
             else:
                 self._send(404, {"error": "no route"})
 
-    srv = ThreadingHTTPServer((host, port), H)
+    srv = ThreadingHTTPServer((routable_address() if host is None else host, port), H)
     srv.daemon_threads = True
     srv.last_activity = H.last  # type: ignore[attr-defined]
     return srv
@@ -142,7 +155,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     cwd = os.environ.get("DET_CONTEXT_DIR") or os.getcwd()
     session = ShellSession(cwd)
     srv = make_server(session, cwd, port=a.port)
-    addr = f"http://{routable_address()}:{srv.server_address[1]}"
+    addr = f"http://{srv.server_address[0]}:{srv.server_address[1]}"
     print(f"shell service at {addr}", flush=True)
     from determined_clone_amd import _info
 

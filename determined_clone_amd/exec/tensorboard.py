@@ -21,7 +21,7 @@ from urllib.parse import parse_qs, urlparse
 
 from determined_clone_amd import _info
 from determined_clone_amd.tensorboard import read_scalars
-from determined_clone_amd.util import routable_address
+from determined_clone_amd.util import proxy_secret_ok, routable_address
 
 
 def collect(logdirs: Dict[str, str]) -> Dict[str, Dict[str, list]]:
@@ -32,7 +32,7 @@ def collect(logdirs: Dict[str, str]) -> Dict[str, Dict[str, list]]:
     return runs
 
 
-def make_server(logdirs: Dict[str, str], host: str = "0.0.0.0", port: int = 0) -> ThreadingHTTPServer:
+def make_server(logdirs: Dict[str, str], host: Optional[str] = None, port: int = 0) -> ThreadingHTTPServer:
     class H(BaseHTTPRequestHandler):
         def log_message(self, *a):  # quiet
             pass
@@ -45,6 +45,9 @@ def make_server(logdirs: Dict[str, str], host: str = "0.0.0.0", port: int = 0) -
             self.wfile.write(body)
 
         def do_GET(self) -> None:
+            if not proxy_secret_ok(self.headers):
+                return self._send(403, b'{"error": "requests must come through the master proxy"}',
+                                  "application/json")
             u = urlparse(self.path)
             q = {k: v[0] for k, v in parse_qs(u.query).items()}
             runs = collect(logdirs)
@@ -66,7 +69,7 @@ def make_server(logdirs: Dict[str, str], host: str = "0.0.0.0", port: int = 0) -
                     "<th>last step</th><th>last value</th></tr>" + "".join(rows) + "</table></body></html>")
             return self._send(200, page.encode(), "text/html")
 
-    return ThreadingHTTPServer((host, port), H)
+    return ThreadingHTTPServer((routable_address() if host is None else host, port), H)
 
 
 def _experiment_logdirs(exp_ids: List[str]) -> Dict[str, str]:
@@ -99,7 +102,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     if a.experiment_ids:
         logdirs.update(_experiment_logdirs(a.experiment_ids))
     srv = make_server(logdirs, port=a.port)
-    addr = f"http://{routable_address()}:{srv.server_address[1]}"
+    addr = f"http://{srv.server_address[0]}:{srv.server_address[1]}"
     print(f"serving tensorboard scalars at {addr}", flush=True)
     info = _info.get_cluster_info()
     if info is not None:

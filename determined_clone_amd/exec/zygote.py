@@ -18,7 +18,10 @@ initialised here, so forking is safe -- and asks it to fork each task process:
 
 Only this framework's modules are imported fresh in each child (they read ``DCA_*`` / ``DET_*``
 environment variables at import time). The agent falls back to a plain subprocess when the zygote
-is unavailable or ``DET_ZYGOTE=0``.
+is unavailable or ``DET_ZYGOTE=0``, and when the task's environment asks for something a forked,
+already-initialised interpreter cannot honour (``incompatible_reason``): a different
+``LD_PRELOAD`` / ``LD_LIBRARY_PATH`` (or any ``LD_*``), ``PYTHONHASHSEED``, a virtualenv, or a
+``PYTHONPATH`` entry that would shadow one of the pre-imported ``WARM_MODULES``.
 """
 import json
 import os
@@ -34,6 +37,30 @@ from typing import Any, Dict, List, Optional
 
 WARM_MODULES = ("numpy", "torch", "torch.nn", "torch.nn.functional", "torch.utils.data",
                 "torch.distributed", "yaml", "requests")
+
+
+# variables the dynamic loader / interpreter only read at process start
+_START_ONLY = ("PYTHONHASHSEED", "VIRTUAL_ENV", "PYTHONHOME", "PYTHONNOUSERSITE", "PYTHONSTARTUP")
+
+
+def incompatible_reason(env: Dict[str, str], base_env: Optional[Dict[str, str]] = None,
+                        skip_paths: Optional[List[str]] = None) -> Optional[str]:
+    """Why a task with environment ``env`` must not be forked from a zygote started under
+    ``base_env`` (default: this process's environment), or None if forking is equivalent to a
+    fresh interpreter. ``skip_paths``: PYTHONPATH entries known not to shadow anything (the
+    task's context directory is checked, the framework root is not)."""
+    base = dict(os.environ if base_env is None else base_env)
+    for k in sorted(set(env) | set(base)):
+        if (k.startswith("LD_") or k in _START_ONLY) and env.get(k) != base.get(k):
+            return f"{k} differs from the agent's environment"
+    skip = set(skip_paths or ())
+    for entry in (env.get("PYTHONPATH") or "").split(os.pathsep):
+        if not entry or entry in skip or not os.path.isdir(entry):
+            continue
+        for mod in {m.split(".")[0] for m in WARM_MODULES}:
+            if os.path.exists(os.path.join(entry, mod)) or os.path.exists(os.path.join(entry, mod + ".py")):
+                return f"PYTHONPATH entry {entry} shadows pre-imported module {mod}"
+    return None
 
 
 def _send(conn: socket.socket, obj: Dict[str, Any]) -> None:

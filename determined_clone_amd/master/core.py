@@ -424,7 +424,13 @@ class Master:
                        name: Optional[str] = None) -> Dict[str, Any]:
         task_id = str(uuid.uuid4())
         alloc_id = f"{task_id}.0"
+        # per-task secret the service (shell / notebook / tensorboard) demands on every request:
+        # only the master's /proxy/ route, which checks the owner, can attach it (the reference
+        # gets the same property from a per-shell ssh keypair held by the owner)
+        secret = secrets.token_urlsafe(24)
+        self.db.kv_set(f"proxy_secret:{task_id}", secret)
         spec = {"kind": kind, "entrypoint": entrypoint, "environment": {"environment_variables": env or {}},
+                "proxy_secret": secret,
                 "cluster_info": {"master_url": self.master_url, "cluster_id": self.cluster_id,
                                  "agent_id": "", "slot_ids": [], "task_id": task_id,
                                  "allocation_id": alloc_id, "session_token": self._task_token(),
@@ -446,6 +452,20 @@ class Master:
         """Owner user id of an NTSC task (None for trials / unknown tasks)."""
         row = self.db.one("SELECT owner_id FROM tasks WHERE task_id=?", [task_id])
         return row["owner_id"] if row else None
+
+    def task_experiment(self, task_id: str) -> Optional[Dict[str, Any]]:
+        """``{"id", "owner_id", "project_id", "config"}`` of the experiment whose trial runs as
+        ``task_id`` (trial task ids are ``<experiment id>.<request id>``), else None."""
+        for e in list(self.experiments.values()):
+            if any(t.task_id == task_id for t in list(e.trials.values())):
+                row = self.db.one("SELECT owner_id, project_id FROM experiments WHERE id=?", [e.id]) or {}
+                return {"id": e.id, "owner_id": row.get("owner_id"), "project_id": row.get("project_id"),
+                        "config": e.config}
+        return None
+
+    def task_proxy_secret(self, task_id: str) -> Optional[str]:
+        """The secret an NTSC task's service expects in ``X-Det-Proxy-Secret`` (None for trials)."""
+        return self.db.kv_get(f"proxy_secret:{task_id}")
 
     # ------------------------------------------------------------------ agents
     def register_agent(self, body: Dict[str, Any]) -> None:

@@ -23,6 +23,7 @@ from determined_clone_amd.errors import InvalidConfigurationException
 from determined_clone_amd.master.core import Master, hash_password
 from determined_clone_amd.master.db import dec, now
 from determined_clone_amd.master.experiment import TERMINAL, experiment_row_to_api, trial_row_to_api
+from determined_clone_amd.util import PROXY_SECRET_HEADER
 
 logger = logging.getLogger("determined_clone_amd.master.api")
 audit_logger = logging.getLogger("determined_clone_amd.master.audit")
@@ -1417,10 +1418,46 @@ class _Handler(BaseHTTPRequestHandler):
         self.end_headers()
         self.wfile.write(body)
 
+    # ------------------------------------------------------------------ task access
+    def _task_access(self, user: Dict[str, Any], task_id: str) -> Optional[str]:
+        """None when ``user`` may reach ``task_id``'s services through /proxy/ or /tunnel/, else
+        why not. NTSC tasks: their owner (or an admin). Trials: the experiment's owner, an admin,
+        or (``security.authz.type: rbac``) a holder of UPDATE_EXPERIMENT in its workspace -- a
+        tunnel is a raw socket into the trial's container, so viewing rights are not enough
+        (reference: `master/internal/proxy` + `ExperimentAuthZ.CanEditExperiment` under RBAC)."""
+        if user.get("admin"):
+            return None
+        owner = self.master.task_owner(task_id)
+        if owner is not None:
+            return None if owner == user["id"] else "not the task owner"
+        exp = self.master.task_experiment(task_id)
+        if exp is None:
+            return "not the task owner"
+        if exp["owner_id"] == user["id"]:
+            return None
+        ws = _project_workspace(self.master, exp["project_id"])
+        if self.master.authz.mode != "basic" and self.master.authz.permitted(user, "UPDATE_EXPERIMENT", ws):
+            return None
+        return f"not permitted on experiment {exp['id']}"
+
+    def _task_ports(self, task_id: str, svc_port: Optional[int]) -> set:
+        """Ports a tunnel may reach on a task's host: the service port it registered plus the
+        ``environment.proxy_ports`` its config declares (reference: allocation.go registerProxies
+        over ``req.ProxyPorts``)."""
+        allowed = {svc_port} if svc_port else set()
+        exp = self.master.task_experiment(task_id)
+        cfg = exp["config"] if exp is not None else (self.master.tasks.get(task_id) or {}).get("config") or {}
+        for pp in ((cfg.get("environment") or {}).get("proxy_ports") or []):
+            try:
+                allowed.add(int(pp["proxy_port"] if isinstance(pp, dict) else pp))
+            except (KeyError, TypeError, ValueError):
+                continue
+        return allowed
+
     # ------------------------------------------------------------------ TCP tunnel
     def _task_host(self, task_id: str) -> Optional[Tuple[str, Optional[int]]]:
         """(host, service port) of a live task: its registered proxy address, else the first
-        address of the agent running its first container."""
+        address of the agent running its first container; None when neither is known."""
         allocs = [a for a in list(self.master.allocations.values()) if a.task_id == task_id and not a.exited]
         if not allocs:
             return None
@@ -1432,14 +1469,15 @@ class _Handler(BaseHTTPRequestHandler):
             agent = self.master.rm.agents.get(p.get("agent_id"))
             if agent is not None and agent.addresses:
                 return agent.addresses[0], None
-        return "127.0.0.1", None
+        return None
 
     def _tunnel(self, parsed: Any, query: Dict[str, List[str]]) -> None:
         """``GET /tunnel/{task_id}?port=N`` with ``Upgrade: det-tcp``: after ``101 Switching
         Protocols`` the connection is a raw byte pipe to port N (default: the task's service port)
         on the task's host -- ssh into a shell, or ``det task tunnel -p`` to any port a trial
         opens (reference: the master's TCP-over-WebSocket proxy, `harness/determined/cli/
-        tunnel.py` / `proxy.py`). Authenticated like ``/proxy/``; task owner or admin only."""
+        tunnel.py` / `proxy.py`). Authenticated like ``/proxy/`` (``_task_access``); only the
+        task's service port and its declared ``proxy_ports`` are reachable."""
         import socket
         import ssl
 
@@ -1449,15 +1487,22 @@ class _Handler(BaseHTTPRequestHandler):
         user = self._proxy_user(query)
         if user is None:
             return self._send(401, {"error": "unauthenticated"})
-        if not (user["admin"] or self.master.task_owner(task_id) in (None, user["id"])):
-            return self._send(403, {"error": "not the task owner"})
         target = self._task_host(task_id)
         if target is None:
             return self._send(404, {"error": f"no running task {task_id}"})
+        denied = self._task_access(user, task_id)
+        if denied:
+            return self._send(403, {"error": denied})
         host, svc_port = target
-        port = int(query["port"][0]) if query.get("port") else svc_port
+        try:
+            port = int(query["port"][0]) if query.get("port") else svc_port
+        except ValueError:
+            return self._send(400, {"error": "port must be an integer"})
         if not port:
             return self._send(400, {"error": "task has no service port; pass ?port="})
+        if port not in self._task_ports(task_id, svc_port):
+            return self._send(403, {"error": f"port {port} is neither the task's service port nor "
+                                             "one of its environment.proxy_ports"})
         try:
             upstream = socket.create_connection((host, port), timeout=10)
         except OSError as e:
@@ -1523,13 +1568,18 @@ class _Handler(BaseHTTPRequestHandler):
                       if a.task_id == task_id and not a.exited and a.proxy_address), None)
         if alloc is None:
             return self._send(404, {"error": f"no running service for task {task_id}"})
-        if not (user["admin"] or self.master.task_owner(task_id) in (None, user["id"])):
-            return self._send(403, {"error": "not the task owner"})
+        denied = self._task_access(user, task_id)
+        if denied:
+            return self._send(403, {"error": denied})
         q = [(k, v) for k, vs in query.items() if k != "token" for v in vs]
         url = alloc.proxy_address.rstrip("/") + rest + ("?" + urllib.parse.urlencode(q) if q else "")
         fwd = {k: v for k, v in self.headers.items()
-               if k.lower() not in ("host", "authorization", "cookie", "content-length", "connection")}
+               if k.lower() not in ("host", "authorization", "cookie", "content-length", "connection",
+                                    PROXY_SECRET_HEADER.lower())}
         fwd["X-Forwarded-Prefix"] = f"/proxy/{task_id}"
+        secret = self.master.task_proxy_secret(task_id)
+        if secret:
+            fwd[PROXY_SECRET_HEADER] = secret
         try:
             req = urllib.request.Request(url, data=raw or None, method=method, headers=fwd)
             try:

@@ -26,8 +26,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 64;   // query rows per forward block / keys per backward block
-constexpr int kPad = 8;
-constexpr bool FWD_ONE_COPY = true;     // LDS row padding (elements) to break power-of-two bank strides
+constexpr int kPad = 8;     // LDS row padding (elements) to break power-of-two bank strides
 
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);

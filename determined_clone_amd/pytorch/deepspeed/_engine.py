@@ -36,6 +36,7 @@ from typing import Any, Dict, Iterable, List, Optional, Tuple, Union
 import torch
 import torch.distributed as dist
 
+from determined_clone_amd.ops import _grad
 from determined_clone_amd.ops import optim as fopt
 from determined_clone_amd.parallel import ddp, zero
 
@@ -415,6 +416,10 @@ class DeepSpeedEngine(torch.nn.Module):
         scaled.backward(retain_graph=retain_graph)
         if self._z3 is not None:
             self._z3.finish_backward()
+        if loss.is_cuda:
+            # conv / linear weight gradients run on a side stream (ops/_grad.py): .grad is
+            # complete for any reader (custom clipping, logging, step) once this returns
+            _grad.join()
         return loss
 
     def step(self, lr_kwargs: Optional[Dict[str, Any]] = None) -> None:

@@ -10,6 +10,7 @@ from typing import Any, Dict, Iterator, List, Optional, Tuple, Union
 import torch
 import torch.distributed as dist
 
+from determined_clone_amd.ops import _grad
 from determined_clone_amd.parallel.pipeline import (_META_LEN, Activation, PipelineModule, _flatten,
                                                     _Meta, _P2P)
 from determined_clone_amd.pytorch.deepspeed._engine import DeepSpeedEngine
@@ -106,6 +107,8 @@ class PipelineEngine(DeepSpeedEngine):
             dist.all_reduce(t, group=group)
 
     def _reduce_tied_grads(self) -> None:
+        if self.device.type == "cuda":
+            _grad.join()  # tied weights' side-stream gradients (ops/_grad.py) land before the reduce
         self.optimizer.space.ensure_views()
         for key, (g, _) in self._tie_groups.items():
             for w in self.module.tied_weights(key):

@@ -158,3 +158,20 @@ def routable_address() -> str:
             return s.getsockname()[0]
     except OSError:
         return "127.0.0.1"
+
+
+# Header the master's /proxy/ route attaches when it forwards to an NTSC task's service; the
+# service (exec/shell.py, notebook.py, tensorboard.py) refuses requests without it.
+PROXY_SECRET_HEADER = "X-Det-Proxy-Secret"
+
+
+def proxy_secret_ok(headers: Any) -> bool:
+    """True when ``headers`` carry this task's ``DET_TASK_PROXY_SECRET`` (always true off-cluster,
+    where no secret is set)."""
+    import hmac
+
+    secret = os.environ.get("DET_TASK_PROXY_SECRET")
+    if not secret:
+        return True
+    return hmac.compare_digest(str(headers.get(PROXY_SECRET_HEADER) or ""), secret)
+

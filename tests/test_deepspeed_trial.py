@@ -202,3 +202,36 @@ def test_engine_zero_two_ranks_matches_single_process(stage):
         rsd = ref.optimizer.state_dict()
         for i, st in rsd["state"].items():
             torch.testing.assert_close(full["state"][i]["exp_avg"], st["exp_avg"], atol=1e-6, rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_engine_grads_readable_right_after_backward_gpu():
+    """Weight gradients run on a side stream (ops/_grad.py); ``engine.backward`` joins it, so a
+    reader of ``.grad`` between ``backward`` and ``step`` (custom clipping, logging) sees the
+    finished gradient: same values as with the side stream off (``DCA_WGRAD_STREAM=0``)."""
+    from determined_clone_amd.ops import _grad
+
+    def grads(side: bool):
+        old = _grad.SIDE_STREAM
+        _grad.SIDE_STREAM = side
+        try:
+            torch.manual_seed(0)
+            model = gpt2.cast_for_mi355x(gpt2.gpt2("tiny", n_layer=2, max_seq_len=256)).cuda()
+            cfg = dict(DS_CONFIG, gradient_accumulation_steps=1, gradient_clipping=0.0)
+            eng, _, _, _ = det_ds.initialize(model=model, config=cfg)
+            g = torch.Generator(device="cpu").manual_seed(1)
+            x = torch.randint(0, 512, (4, 256), generator=g).cuda()
+            _, loss = eng(x, x)
+            eng.backward(loss)
+            # read on the current stream immediately (no synchronize in between)
+            out = [p.grad.float().clone() for p in eng.module.parameters() if p.grad is not None]
+            assert not _grad.pending()
+            torch.cuda.synchronize()
+            return out
+        finally:
+            _grad.SIDE_STREAM = old
+
+    ref, got = grads(False), grads(True)
+    assert len(ref) == len(got) and len(ref) > 0
+    for a, b in zip(ref, got):
+        torch.testing.assert_close(b, a, rtol=1e-3, atol=1e-5)

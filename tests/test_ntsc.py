@@ -98,6 +98,20 @@ def test_shell_session_and_cli(cluster, monkeypatch):
         seen += out["data"]
         nxt = out["next"]
         assert time.time() - t0 < 30, seen
+    # the shell's own HTTP service refuses anyone who bypasses the master's proxy (no secret) ...
+    addr = next(a.proxy_address for a in m.allocations.values() if a.task_id == tid and a.proxy_address)
+    assert requests.post(addr + "/run", json={"cmd": "true"}, timeout=30).status_code == 403
+    assert requests.get(addr + "/output", timeout=30).status_code == 403
+    # ... and the proxy refuses users other than the owner
+    from determined_clone_amd.master.core import hash_password
+
+    if not m.db.one("SELECT id FROM users WHERE username='mallory'"):
+        m.db.insert("users", {"username": "mallory", "admin": 0, "active": 1,
+                              "password_hash": hash_password(""), "created": 0})
+    mallory, _ = m.login("mallory", "")
+    r = requests.post(f"{m.master_url}{base}/run", json={"cmd": "id"}, timeout=30,
+                      headers={"Authorization": f"Bearer {mallory}"})
+    assert r.status_code == 403
     # det shell run
     from determined_clone_amd.cli import cli
 

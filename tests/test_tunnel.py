@@ -69,22 +69,67 @@ def test_tunnel_refusals(cluster):
         tunnel.open_tunnel(url, None, "t1")
     with pytest.raises(ConnectionError, match="404"):
         tunnel.open_tunnel(url, tok, "nope")
-    with pytest.raises(ConnectionError, match="502"):
+    # only the service port and declared proxy_ports are reachable, even for an admin
+    with pytest.raises(ConnectionError, match="403"):
         tunnel.open_tunnel(url, tok, "t1", port=1)
     # another (non-admin) user may not tunnel into someone else's task
     from determined_clone_amd.master.core import hash_password
 
     m.db.insert("users", {"username": "eve", "admin": 0, "active": 1, "password_hash": hash_password(""),
                           "created": 0})
+    eve_tok, eve = m.login("eve", "")
+    with pytest.raises(ConnectionError, match="403"):  # a task nobody owns is not public
+        tunnel.open_tunnel(url, eve_tok, "t1")
     m.task_owner = lambda task_id: 1  # owned by admin
-    eve_tok, _ = m.login("eve", "")
     with pytest.raises(ConnectionError, match="403"):
         tunnel.open_tunnel(url, eve_tok, "t1")
+    m.task_owner = lambda task_id: eve["id"]
+    s, _ = tunnel.open_tunnel(url, eve_tok, "t1")
+    s.close()
     # a plain GET without the upgrade header is rejected
     import requests
 
     r = requests.get(url + "/tunnel/t1", headers={"Authorization": f"Bearer {tok}"})
     assert r.status_code == 400
+
+
+def test_trial_tunnel_needs_experiment_rights(cluster):
+    """A trial task has no NTSC owner: the tunnel checks the experiment (owner / admin / RBAC
+    UPDATE_EXPERIMENT) and reaches only the ports the experiment declares in proxy_ports."""
+    from determined_clone_amd.master.core import hash_password
+
+    m, url, tok, echo_port = cluster
+    a = Allocation("9.1.0", "9.1", "TRIAL")
+    a.placements = [{"agent_id": "agent-x"}]
+    m.allocations[a.id] = a
+
+    class _Agent:
+        addresses = ["127.0.0.1"]
+
+    m.rm.agents["agent-x"] = _Agent()
+    for name in ("alice", "bob"):
+        m.db.insert("users", {"username": name, "admin": 0, "active": 1, "password_hash": hash_password(""),
+                              "created": 0})
+    alice_tok, alice = m.login("alice", "")
+    bob_tok, _ = m.login("bob", "")
+    exp = {"id": 9, "owner_id": alice["id"], "project_id": None,
+           "config": {"environment": {"proxy_ports": [{"proxy_port": echo_port, "proxy_tcp": True}]}}}
+    m.task_experiment = lambda task_id: exp if task_id == "9.1" else None
+    with pytest.raises(ConnectionError, match="403"):
+        tunnel.open_tunnel(url, bob_tok, "9.1", port=echo_port)
+    with pytest.raises(ConnectionError, match="403"):  # not a declared port
+        tunnel.open_tunnel(url, alice_tok, "9.1", port=echo_port + 1)
+    for t in (alice_tok, tok):
+        s, _ = tunnel.open_tunnel(url, t, "9.1", port=echo_port)
+        with s:
+            assert _roundtrip(s, b"ok") == b"OK"
+    # with RBAC, an editor role in the experiment's workspace grants access too
+    m.authz.mode = "rbac"
+    with pytest.raises(ConnectionError, match="403"):
+        tunnel.open_tunnel(url, bob_tok, "9.1", port=echo_port)
+    m.authz.permitted = lambda user, perm, ws=None: perm == "UPDATE_EXPERIMENT"
+    s, _ = tunnel.open_tunnel(url, bob_tok, "9.1", port=echo_port)
+    s.close()
 
 
 def test_listeners_port_map(cluster):

@@ -40,3 +40,19 @@ def test_zygote_spawn_exit_and_kill():
         assert p2.wait() == -signal.SIGTERM
     finally:
         z.close()
+
+
+def test_incompatible_env_falls_back(tmp_path):
+    """Variables a forked interpreter cannot honour route the task to a plain subprocess."""
+    from determined_clone_amd.exec.zygote import incompatible_reason
+
+    base = {"PATH": "/bin", "LD_LIBRARY_PATH": "/opt/rocm/lib"}
+    assert incompatible_reason(dict(base, DET_X="1"), base) is None
+    assert "LD_PRELOAD" in incompatible_reason(dict(base, LD_PRELOAD="/x.so"), base)
+    assert "LD_LIBRARY_PATH" in incompatible_reason(dict(base, LD_LIBRARY_PATH="/other"), base)
+    assert "PYTHONHASHSEED" in incompatible_reason(dict(base, PYTHONHASHSEED="0"), base)
+    shadow = tmp_path / "venv_site"
+    (shadow / "numpy").mkdir(parents=True)
+    why = incompatible_reason(dict(base, PYTHONPATH=str(shadow)), base)
+    assert why and "numpy" in why
+    assert incompatible_reason(dict(base, PYTHONPATH=str(shadow)), base, skip_paths=[str(shadow)]) is None
