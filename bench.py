@@ -46,6 +46,7 @@ class ResNet50BenchTrial(pytorch.PyTorchTrial):
         opt = torch.optim.SGD(self.model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5)
         self.opt = context.wrap_optimizer(opt)
         self.t0 = self.t1 = None
+        self.events = []
 
     def _mark(self) -> float:
         if torch.cuda.is_available():
@@ -61,12 +62,21 @@ class ResNet50BenchTrial(pytorch.PyTorchTrial):
     def train_batch(self, batch, epoch_idx: int, batch_idx: int):
         if batch_idx == self.warmup:
             self.t0 = self._mark()
+        if torch.cuda.is_available() and batch_idx >= self.warmup:
+            # per-step GPU timestamps (no synchronisation) for the stderr diagnostics
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.events.append(ev)
         images, labels = batch
         logits = self.model(images)
         loss = F.cross_entropy(logits.float(), labels)
         self.context.backward(loss)
         self.context.step_optimizer(self.opt)
         if batch_idx == self.warmup + self.steps - 1:
+            if torch.cuda.is_available():
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                self.events.append(ev)
             self.t1 = self._mark()
         return {"loss": loss}
 
@@ -128,6 +138,15 @@ def main() -> None:
         if ctx.distributed.size > 1:
             ms = max(ctx.distributed.allgather(ms))
         imgs = args.batch * world * args.steps / (ms * args.steps / 1000.0)
+        if torch.cuda.is_available():
+            ev = trial.events
+            step_ms = [round(a.elapsed_time(b), 2) for a, b in zip(ev[:-1], ev[1:])]
+            ms_stats = torch.cuda.memory_stats()
+            print(json.dumps({"rank": ctx.distributed.rank, "step_ms": step_ms,
+                              "max_reserved_gb": round(torch.cuda.max_memory_reserved() / 2**30, 1),
+                              "alloc_retries": ms_stats.get("num_alloc_retries", 0),
+                              "device_free_gb": round(torch.cuda.mem_get_info()[0] / 2**30, 1)}),
+                  file=sys.stderr, flush=True)
         if ctx.distributed.rank == 0:
             out = {
                 "metric": METRIC, "value": round(imgs, 1), "unit": "images/sec",

@@ -17,6 +17,7 @@ forward/dgrad by 1.3-2.4x, so the end-to-end step is slower (7.8k vs 9.2k img/s)
 BatchNorm statistics pass removed. The model therefore keeps MIOpen by default.
 """
 import os
+import sys
 from typing import Optional, Tuple
 
 import torch
@@ -100,6 +101,9 @@ def _choose(key, candidates) -> int:
     times = [_time_us(fn) for fn in candidates]
     best = min(range(len(times)), key=times.__getitem__)
     _CHOICE[key] = best
+    if os.environ.get("DCA_CONV_DEBUG") == "1":
+        print(f"[conv chooser] {key[0]} {key[1:]} us={[round(t, 1) for t in times]} -> {best}",
+              file=sys.stderr, flush=True)
     return best
 
 

@@ -12,6 +12,7 @@
 #include "common.h"
 #include "transformer_api.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace dca {
@@ -232,36 +233,82 @@ __global__ __launch_bounds__(kColWaves * 64) void column_reduce_kernel(const flo
   if (w == 0 && j < ncols) column_store(out, j, red[0][lane]);
 }
 
-// Per-block column partial sums of dy [rows][N] (bias gradient of a linear layer): block = 256
-// threads x 8 columns, rows strided by gridDim.y with 4 independent 16-B loads in flight.
+// Per-block column partial sums of dy [rows][N] (bias gradient of a linear layer). Block = 4 waves;
+// a wave's 64 lanes cover 512 consecutive columns (8 per lane, one 16-B load per row) and the 4
+// waves take interleaved rows, so every lane is busy whatever N is (the previous 2048-column block
+// left half the block idle at N = 1024). Rows stride by gridDim.y * 4 with 4 independent loads in
+// flight; the waves combine through LDS and the block writes one partial row (grid.y partial rows,
+// summed by column_reduce_kernel).
+constexpr int kRsWaves = 4;
+constexpr int kRsCols = 512;
 template <typename T>
-__global__ __launch_bounds__(256) void row_sum_kernel(const void* __restrict__ dy,
-                                                      float* __restrict__ partial, int64_t rows,
-                                                      int N) {
-  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
-  if (c >= N) return;
+__global__ __launch_bounds__(kRsWaves * 64) void row_sum_kernel(const void* __restrict__ dy,
+                                                                float* __restrict__ partial,
+                                                                int64_t rows, int N) {
+  __shared__ __attribute__((aligned(16))) float red[kRsWaves][kRsCols];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * kRsCols + lane * 8;
+  const bool ok = c < N;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int64_t step = gridDim.y;
-  int64_t r = blockIdx.y;
-  for (; r + 3 * step < rows; r += 4 * step) {
-    float g[4][8];
+  if (ok) {
+    const int64_t step = static_cast<int64_t>(gridDim.y) * kRsWaves;
+    int64_t r = static_cast<int64_t>(blockIdx.y) * kRsWaves + w;
+    for (; r + 3 * step < rows; r += 4 * step) {
+      float g[4][8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      Vec8<T>::load(reinterpret_cast<const char*>(dy) + ((r + u * step) * N + c) * Vec8<T>::bytes, g[u]);
+      for (int u = 0; u < 4; ++u)
+        Vec8<T>::load(reinterpret_cast<const char*>(dy) + ((r + u * step) * N + c) * Vec8<T>::bytes, g[u]);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += g[u][k];
+        for (int k = 0; k < 8; ++k) acc[k] += g[u][k];
+    }
+    for (; r < rows; r += step) {
+      float g[8];
+      Vec8<T>::load(reinterpret_cast<const char*>(dy) + (r * N + c) * Vec8<T>::bytes, g);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += g[k];
+    }
   }
-  for (; r < rows; r += step) {
-    float g[8];
-    Vec8<T>::load(reinterpret_cast<const char*>(dy) + (r * N + c) * Vec8<T>::bytes, g);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] += g[k];
+  for (int k = 0; k < 8; ++k) red[w][lane * 8 + k] = acc[k];
+  __syncthreads();
+  // 256 threads x 2 columns each: sum the 4 waves' rows in fixed order
+  for (int j = threadIdx.x; j < kRsCols; j += kRsWaves * 64) {
+    const int col = blockIdx.x * kRsCols + j;
+    if (col < N)
+      partial[static_cast<int64_t>(blockIdx.y) * N + col] = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
   }
-  float4* out = reinterpret_cast<float4*>(partial + static_cast<int64_t>(blockIdx.y) * N + c);
-  out[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-  out[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+
+// acc[i] (+)= sum_s part[s][i] for the split-K weight gradients of ops/transformer.py: the
+// per-slice fp32 GEMM outputs are summed in a fixed order and added into the parameter's
+// persistent .grad view (bf16 or fp32) in one pass -- replaces a torch reduce over the slices plus
+// a mixed-dtype add (two kernels, ~95 us per GPT-2-medium weight at 32k tokens).
+template <typename A>
+__global__ __launch_bounds__(256) void splitk_accumulate_kernel(const float* __restrict__ part,
+                                                                void* __restrict__ acc, int64_t n,
+                                                                int splits, bool accumulate) {
+  const int64_t nv = n / 8;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < nv;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    float s[8];
+    Vec8<F32>::load(part + i * 8, s);
+    for (int p = 1; p < splits; ++p) {
+      float t[8];
+      Vec8<F32>::load(part + static_cast<int64_t>(p) * n + i * 8, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += t[k];
+    }
+    char* dst = reinterpret_cast<char*>(acc) + i * 8 * Vec8<A>::bytes;
+    if (accumulate) {
+      float a[8];
+      Vec8<A>::load(dst, a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += a[k];
+    }
+    Vec8<A>::store(dst, s);
+  }
 }
 
 // 8 bias values starting at column c, fp32 or bf16 storage (nullptr -> zeros).
@@ -433,8 +480,25 @@ inline int ln_grid(int64_t rows) {
 }  // namespace
 
 int ln_bwd_blocks(int64_t rows) {
+  // 512 blocks (2048 waves, 2 per SIMD) left the kernel latency-bound at 1.3 TB/s on GPT-2-medium
+  // rows; DCA_LN_BWD_BLOCKS overrides for tuning
+  static const int cap = [] {
+    const char* e = std::getenv("DCA_LN_BWD_BLOCKS");
+    return e ? std::atoi(e) : 2048;
+  }();
   int64_t g = (rows + kWaves - 1) / kWaves;
-  return static_cast<int>(g < 512 ? (g < 1 ? 1 : g) : 512);
+  return static_cast<int>(g < cap ? (g < 1 ? 1 : g) : cap);
+}
+
+void splitk_accumulate(bool acc_bf16, const float* part, void* acc, int64_t n, int splits,
+                       bool accumulate, hipStream_t st) {
+  const int grid = stream_grid(n / 8, 256);
+  if (acc_bf16)
+    hipLaunchKernelGGL(splitk_accumulate_kernel<BF16>, dim3(grid), dim3(256), 0, st, part, acc, n,
+                       splits, accumulate);
+  else
+    hipLaunchKernelGGL(splitk_accumulate_kernel<F32>, dim3(grid), dim3(256), 0, st, part, acc, n,
+                       splits, accumulate);
 }
 
 void layernorm_fwd(TDtype dt, const void* x, const void* res, void* sum_out, void* y,
@@ -497,19 +561,22 @@ void bias_gelu_bwd(TDtype dt, const void* dy, const void* x, const void* bias, b
                        partial, rb, static_cast<int64_t>(N), *dbias);
 }
 
-int row_sum_blocks(int64_t rows) {
-  // ~64 rows per block-row, at most 256 slabs (partials stay small for the column pass).
-  int64_t b = (rows + 63) / 64;
-  return static_cast<int>(b < 1 ? 1 : (b > 256 ? 256 : b));
+int row_sum_blocks(int64_t rows, int N) {
+  // ~4096 waves over the whole chip (16 per CU): grid.y row slabs of >= 16 rows per wave
+  const int cb = (N + kRsCols - 1) / kRsCols;
+  int64_t b = 1024 / cb;
+  const int64_t cap = (rows + 16 * kRsWaves - 1) / (16 * kRsWaves);
+  if (b > cap) b = cap;
+  return static_cast<int>(b < 1 ? 1 : b);
 }
 
 void row_sum(TDtype dt, const void* dy, float* partial, const ColumnOut& out, int64_t rows, int N,
              hipStream_t st) {
-  const int rb = row_sum_blocks(rows);
-  dim3 grid((N / 8 + 255) / 256, rb);
+  const int rb = row_sum_blocks(rows, N);
+  dim3 grid((N + kRsCols - 1) / kRsCols, rb);
   dispatch_t(dt, [&](auto t) {
     using T = decltype(t);
-    hipLaunchKernelGGL(row_sum_kernel<T>, grid, dim3(256), 0, st, dy, partial, rows, N);
+    hipLaunchKernelGGL(row_sum_kernel<T>, grid, dim3(kRsWaves * 64), 0, st, dy, partial, rows, N);
   });
   hipLaunchKernelGGL(column_reduce_kernel, dim3((N + 63) / 64), dim3(kColWaves * 64), 0, st,
                      partial, rb, static_cast<int64_t>(N), out);

@@ -32,7 +32,10 @@ void bias_gelu_bwd(TDtype dt, const void* dy, const void* x, const void* bias, b
                    void* dx, float* partial, const ColumnOut* dbias, int64_t rows, int N,
                    hipStream_t st);
 // Bias gradient of a linear layer: out[j] (+)= sum_r dy[r][j], dy [rows][N] (N % 8 == 0).
-int row_sum_blocks(int64_t rows);
+int row_sum_blocks(int64_t rows, int N);
+// acc[i] (+)= sum_s part[s][i], part fp32 [splits][n], acc bf16 or fp32 [n] (n % 8 == 0).
+void splitk_accumulate(bool acc_bf16, const float* part, void* acc, int64_t n, int splits,
+                       bool accumulate, hipStream_t st);
 void row_sum(TDtype dt, const void* dy, float* partial, const ColumnOut& out, int64_t rows, int N,
              hipStream_t st);
 void rope(TDtype dt, const void* x, void* y, const float* cosT, const float* sinT, int64_t rows,

@@ -144,7 +144,7 @@ Tensor bias_grad(const Tensor& dy_in, const OptT& acc) {
   TORCH_CHECK(N % 8 == 0, "bias_grad: last dim must be a multiple of 8");
   const int64_t rows = dy.numel() / N;
   auto fo = dy.options().dtype(at::kFloat);
-  Tensor partial = torch::empty({static_cast<int64_t>(dca::row_sum_blocks(rows)) * N}, fo);
+  Tensor partial = torch::empty({static_cast<int64_t>(dca::row_sum_blocks(rows, N)) * N}, fo);
   Tensor db;
   dca::ColumnOut out;
   if (want_acc(acc)) {
@@ -156,6 +156,23 @@ Tensor bias_grad(const Tensor& dy_in, const OptT& acc) {
   }
   dca::row_sum(tdt(dy), dy.data_ptr(), partial.data_ptr<float>(), out, rows, N, stream());
   return db;
+}
+
+// acc (+)= part.sum(0) for part fp32 [splits, *acc.shape]; acc bf16/fp32 contiguous.
+void splitk_accumulate(const Tensor& part, Tensor& acc, bool accumulate) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous(),
+              "splitk_accumulate: part must be a contiguous fp32 GPU tensor");
+  TORCH_CHECK(acc.is_contiguous() && (acc.scalar_type() == at::kBFloat16 || acc.scalar_type() == at::kFloat),
+              "splitk_accumulate: acc must be contiguous bf16/fp32");
+  TORCH_CHECK(part.dim() >= 1 && part.numel() == part.size(0) * acc.numel(),
+              "splitk_accumulate: part must be [splits, *acc.shape]");
+  TORCH_CHECK(acc.numel() % 8 == 0, "splitk_accumulate: numel must be a multiple of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(acc.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(part.data_ptr()) % 16 == 0,
+              "splitk_accumulate: 16-byte aligned buffers required");
+  const c10::DeviceGuard g(acc.device());
+  dca::splitk_accumulate(acc.scalar_type() == at::kBFloat16, part.data_ptr<float>(), acc.data_ptr(),
+                         acc.numel(), static_cast<int>(part.size(0)), accumulate, stream());
 }
 
 Tensor rope_apply(const Tensor& x, const Tensor& cosT, const Tensor& sinT, int64_t H, int64_t S,
@@ -269,6 +286,8 @@ void register_transformer_ops(pybind11::module& m) {
         pybind11::arg("dbeta_acc") = pybind11::none());
   m.def("bias_grad", &bias_grad, pybind11::arg("dy"), pybind11::arg("acc") = pybind11::none());
   m.def("bias_gelu", &bias_gelu);
+  m.def("splitk_accumulate", &splitk_accumulate, pybind11::arg("part"), pybind11::arg("acc"),
+        pybind11::arg("accumulate") = true);
   m.def("bias_gelu_bwd", &bias_gelu_bwd, pybind11::arg("dy"), pybind11::arg("x"),
         pybind11::arg("bias"), pybind11::arg("need_db") = true,
         pybind11::arg("dbias_acc") = pybind11::none());

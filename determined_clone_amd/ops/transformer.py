@@ -174,11 +174,13 @@ def _wgrad_splits(tokens: int, m: int, n: int) -> int:
 
 
 def _wgrad_split_k(acc: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, s: int) -> None:
-    """``acc += dy2^T x2`` as ``s`` K-slices in one batched GEMM, summed in fp32."""
+    """``acc += dy2^T x2`` as ``s`` K-slices in one batched GEMM with fp32 outputs, summed and
+    added into ``acc`` by one fused kernel (``splitk_accumulate``: fixed-order fp32 sum of the
+    slices, then the bf16/fp32 accumulate)."""
     t, m = dy2.shape
     a = dy2.reshape(s, t // s, m).transpose(1, 2)
     b = x2.reshape(s, t // s, x2.shape[1])
-    acc.add_(torch.bmm(a, b).sum(0, dtype=torch.float32))
+    _ext.load().splitk_accumulate(torch.bmm(a, b, out_dtype=torch.float32), acc)
 
 
 class _Linear(torch.autograd.Function):

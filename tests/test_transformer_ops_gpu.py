@@ -180,7 +180,7 @@ def test_fused_cross_entropy(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("rows,N", [(1, 8), (333, 1024), (8192, 3072), (4097, 4096)])
+@pytest.mark.parametrize("rows,N", [(1, 8), (333, 1024), (100, 520), (8192, 3072), (4097, 4096), (65536, 1024)])
 def test_bias_grad_column_sum(dtype, rows, N):
     C = _C()
     torch.manual_seed(0)
@@ -193,6 +193,23 @@ def test_bias_grad_column_sum(dtype, rows, N):
     want = (acc.float() + ref).to(dtype)
     assert C.bias_grad(dy, acc) is None
     torch.testing.assert_close(acc.float(), want.float(), atol=1e-3 * math.sqrt(rows) + (0.02 if dtype == torch.bfloat16 else 0), rtol=1e-2)
+
+
+@pytest.mark.parametrize("acc_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("splits,shape", [(4, (1024, 1024)), (1, (8,)), (3, (3072, 1024)), (4, (24, 40))])
+def test_splitk_accumulate(acc_dtype, splits, shape):
+    """acc += part.sum(0) in one kernel (fp32 slice sum, then the bf16/fp32 accumulate)."""
+    C = _C()
+    torch.manual_seed(0)
+    part = torch.randn(splits, *shape, device="cuda")
+    acc = torch.randn(*shape, device="cuda").to(acc_dtype)
+    want = (acc.float() + part.sum(0)).to(acc_dtype)
+    C.splitk_accumulate(part, acc)
+    torch.testing.assert_close(acc, want, atol=1e-5 if acc_dtype == torch.float32 else 0.05, rtol=1e-5 if acc_dtype == torch.float32 else 1e-2)
+    C.splitk_accumulate(part, acc, accumulate=False)
+    torch.testing.assert_close(acc.float(), part.sum(0).to(acc_dtype).float(), atol=1e-5 if acc_dtype == torch.float32 else 0.05, rtol=1e-2)
+    with pytest.raises(RuntimeError):
+        C.splitk_accumulate(part[:, :1], acc)
 
 
 def _flat(params):
