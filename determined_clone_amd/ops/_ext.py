@@ -32,6 +32,13 @@ def load() -> Any:
                 "determined_clone_amd.ops._C is not built; run "
                 "`python -m determined_clone_amd.ops.build`"
             ) from e
+    import torch
+
+    if torch.cuda.is_available():
+        # replay the shipped tuned hipBLASLt/rocBLAS GEMM solutions (ops/gemm_tuning.py)
+        from determined_clone_amd.ops import gemm_tuning
+
+        gemm_tuning.enable()
     return _C
 
 

@@ -27,6 +27,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 64;   // query rows per forward block / keys per backward block
 constexpr int kPad = 8;     // LDS row padding (elements) to break power-of-two bank strides
+constexpr float kRescaleLog2 = 8.f;  // forward: deferred-max threshold (log2 units)
 
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -231,9 +232,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         mx = fmaxf(mx, sc[i]);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx * scale_log2);
+      // deferred max (T13): the running max m moves only when a score exceeds it by more than
+      // kRescaleLog2 (p <= 2^kRescaleLog2 meanwhile: exact in the fp32 accumulators, 8 bits of
+      // headroom in the bf16 P), so the D/2-multiply rescale of O and l runs on a few sub-tiles
+      // per row instead of on every max increase. Per lane (= query row): the factor that scales
+      // this lane's l is the one that scales its O accumulators.
+      const float mcand = mx * scale_log2;
+      const bool upd = mcand > m + kRescaleLog2;
+      const float mnew = upd ? mcand : m;
       const float mref = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = fast_exp2(m - mref);
+      const float alpha = upd ? fast_exp2(m - mref) : 1.f;
       float rs = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -244,9 +252,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       rs += __shfl_xor(rs, 32, 64);
       l = l * alpha + rs;
       m = mnew;
-      // rescale the output accumulators only when some row's max moved (rare after the first
-      // tiles): skips D/2 multiplies per lane per sub-tile
-      if (__any(alpha != 1.f)) {
+      if (__any(upd)) {
 #pragma unroll
         for (int n = 0; n < D / 32; ++n) oacc[n] *= alpha;
       }

@@ -9,3 +9,5 @@ for b in 512 1024 2048 4096; do
 done
 timeout -k 10 300 python tools/bench_gpt2.py --steps 10 --warmup 4 > $O/gpt2.txt 2>&1 || exit $?
 tail -3 $O/pytest.log; cat $O/micro_2048.txt; grep -h ln_bwd $O/micro_*.txt; tail -2 $O/gpt2.txt
+timeout -k 10 200 python tools/bench_attn.py > $O/attn.txt 2>&1 || exit $?
+cat $O/attn.txt | tail -8
