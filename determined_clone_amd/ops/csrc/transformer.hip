@@ -480,11 +480,11 @@ inline int ln_grid(int64_t rows) {
 }  // namespace
 
 int ln_bwd_blocks(int64_t rows) {
-  // 512 blocks (2048 waves, 2 per SIMD) left the kernel latency-bound at 1.3 TB/s on GPT-2-medium
-  // rows; DCA_LN_BWD_BLOCKS overrides for tuning
+  // 512-4096 blocks measure within 15% of each other at GPT-2-medium rows (2.7-3.1 TB/s,
+  // tools/bench_tx_bwd.py); DCA_LN_BWD_BLOCKS overrides for tuning
   static const int cap = [] {
     const char* e = std::getenv("DCA_LN_BWD_BLOCKS");
-    return e ? std::atoi(e) : 2048;
+    return e ? std::atoi(e) : 1024;
   }();
   int64_t g = (rows + kWaves - 1) / kWaves;
   return static_cast<int>(g < cap ? (g < 1 ? 1 : g) : cap);
