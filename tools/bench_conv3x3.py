@@ -18,6 +18,9 @@ import torch.nn.functional as F  # noqa: E402
 # (H_in, Cin, Cout, k, stride, pad, count per ResNet-50 step)
 SHAPES = [
     (224, 3, 64, 7, 2, 3, 1),
+    # stem variants with the same math: input channels zero-padded to 4 / 8, and space-to-depth
+    # (7x7/2 on 230x230x3 == 4x4/1 on 115x115x12 with a re-packed weight)
+    (224, 4, 64, 7, 2, 3, 0), (224, 8, 64, 7, 2, 3, 0), (115, 12, 64, 4, 1, 0, 0),
     (56, 64, 64, 3, 1, 1, 3),
     (56, 128, 128, 3, 2, 1, 1), (28, 128, 128, 3, 1, 1, 3),
     (28, 256, 256, 3, 2, 1, 1), (14, 256, 256, 3, 1, 1, 5),
@@ -41,11 +44,16 @@ def timed(fn, it=10):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--find", action="store_true", help="MIOpen find (cudnn.benchmark) instead of "
+                    "immediate mode: needed for shapes the shipped find DB does not hold")
+    ap.add_argument("--only-stem", action="store_true")
     a = ap.parse_args()
-    torch.backends.cudnn.benchmark = False
+    torch.backends.cudnn.benchmark = a.find
     n = a.batch
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     for H, ci, co, k, st, pad, cnt in SHAPES:
+        if a.only_stem and H < 100:
+            continue
         x = torch.randn(n, ci, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
         w = (torch.randn(co, ci, k, k, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
         y = F.conv2d(x, w, stride=st, padding=pad)
