@@ -109,10 +109,12 @@ class Agent:
         self.devices = detect_devices(artificial_slots, slots_per_gpu)
         self.tasks: Dict[str, _Task] = {}
         self.workdir = workdir or tempfile.mkdtemp(prefix="det-clone-agent-")
+        os.makedirs(self.workdir, exist_ok=True)  # the zygote binds its socket here right away
         self._stop = threading.Event()
         self._lock = threading.Lock()
         # pre-warmed fork server for task processes (exec/zygote.py), started in the background
         self.zygote = None
+        self._zygote_done = threading.Event()
         threading.Thread(target=self._start_zygote, daemon=True).start()
 
     def _start_zygote(self) -> None:
@@ -122,6 +124,8 @@ class Agent:
             self.zygote = ZygoteClient.start(self.workdir)
         except Exception as e:  # plain subprocesses still work
             logger.warning(f"zygote unavailable: {e}")
+        finally:
+            self._zygote_done.set()
 
     def register(self) -> None:
         self.session.post("/api/v1/agents/register", {
@@ -136,6 +140,9 @@ class Agent:
         runtime.fetch_context(self.session, spec["task_id"], ctx_dir)
         cmd, env = runtime.build_task(spec, self.master_url, self.id, self.devices, ctx_dir)
         proc = None
+        # a task that arrives while the zygote is still importing waits for it: a cold
+        # subprocess would pay the same imports (and compete with the zygote for the CPU)
+        self._zygote_done.wait(timeout=60)
         why = None
         if self.zygote is not None:
             from determined_clone_amd.exec.zygote import incompatible_reason
@@ -149,6 +156,7 @@ class Agent:
             except Exception as e:
                 logger.warning(f"zygote spawn failed ({e}); starting {cmd[2]} as a subprocess")
         if proc is None:
+            env["DET_SPAWN_TIME"] = repr(time.time())
             proc = subprocess.Popen(cmd, cwd=ctx_dir, env=env, stdout=subprocess.PIPE,
                                     stderr=subprocess.STDOUT, start_new_session=True)
         t = _Task(spec, proc, wd)

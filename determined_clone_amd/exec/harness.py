@@ -36,8 +36,29 @@ def load_trial_class(spec: str):
     return obj
 
 
+def _since_start() -> float:
+    """Seconds since the agent spawned this task process (``DET_SPAWN_TIME``, set at the zygote
+    fork / before Popen), else since the process's creation; for DET_STARTUP_TRACE=1."""
+    import time
+
+    if os.environ.get("DET_SPAWN_TIME"):
+        return time.time() - float(os.environ["DET_SPAWN_TIME"])
+    try:
+        import psutil
+
+        return time.time() - psutil.Process().create_time()
+    except Exception:  # pragma: no cover - psutil missing
+        return float("nan")
+
+
+def _trace(what: str) -> None:
+    if os.environ.get("DET_STARTUP_TRACE") == "1":
+        logging.getLogger("determined_clone_amd.startup").info(f"{what} at +{_since_start():.3f}s")
+
+
 def main(spec: str) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    _trace("harness main")
     from determined_clone_amd import pytorch
 
     info = _info.get_cluster_info()
@@ -50,8 +71,24 @@ def main(spec: str) -> int:
     gbs = info.trial.hparams.get("global_batch_size")
     rpe = int(cfg.get("records_per_epoch") or 0)
     opts = cfg.get("optimizations") or {}
+    prof = None
+    if os.environ.get("DET_STARTUP_PROFILE") == "1":
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     with pytorch.init(aggregation_frequency=int(opts.get("aggregation_frequency", 1))) as ctx:
+        _trace("pytorch.init")
+        if prof is not None:
+            import io
+            import pstats
+
+            prof.disable()
+            buf = io.StringIO()
+            pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(25)
+            logging.getLogger("determined_clone_amd.startup").info(buf.getvalue())
         trial = trial_cls(ctx)
+        _trace("trial constructed")
         trainer = pytorch.Trainer(trial, ctx)
         if (cfg.get("profiling") or {}).get("enabled"):
             p = cfg["profiling"]
@@ -65,6 +102,8 @@ def main(spec: str) -> int:
             latest_checkpoint=info.latest_checkpoint,
             step_zero_validation=bool(cfg.get("perform_initial_validation")),
         )
+        _trace("fit done")
+    _trace("context closed")
     return 0
 
 

@@ -35,8 +35,27 @@ import time
 import traceback
 from typing import Any, Dict, List, Optional
 
+# torch.optim's first Optimizer() imports torch._dynamo (+ sympy, torch.fx, torch._inductor):
+# 2.1 s of every trial's start-up on this image unless the zygote has it warm
 WARM_MODULES = ("numpy", "torch", "torch.nn", "torch.nn.functional", "torch.utils.data",
-                "torch.distributed", "yaml", "requests")
+                "torch.distributed", "torch.optim", "torch._dynamo", "yaml", "requests")
+
+
+def gpu_touched() -> bool:
+    """True if this process holds the KFD / DRM render device open -- i.e. some import initialised
+    the HIP runtime. A process in that state must not fork task processes (whatever module did it,
+    not only torch.cuda)."""
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                target = os.readlink(f"/proc/self/fd/{fd}")
+            except OSError:
+                continue
+            if target == "/dev/kfd" or target.startswith("/dev/dri/renderD"):
+                return True
+    except OSError:
+        pass
+    return False
 
 
 # variables the dynamic loader / interpreter only read at process start
@@ -82,6 +101,7 @@ def _child(req: Dict[str, Any], out_fd: int) -> None:
         os.chdir(req.get("cwd") or "/")
         os.environ.clear()
         os.environ.update(req["env"])
+        os.environ["DET_SPAWN_TIME"] = repr(time.time())  # start-up trace origin (exec/harness.py)
         extra = [p for p in req["env"].get("PYTHONPATH", "").split(os.pathsep) if p]
         sys.path[:0] = [p for p in extra if p not in sys.path]
         random.seed()
@@ -111,7 +131,7 @@ def _child(req: Dict[str, Any], out_fd: int) -> None:
 def _handle(conn: socket.socket, srv: socket.socket) -> None:
     msg, fds, _, _ = socket.recv_fds(conn, 1 << 20, 4)
     req = json.loads(msg.decode())
-    if "torch" in sys.modules and sys.modules["torch"].cuda.is_initialized():
+    if ("torch" in sys.modules and sys.modules["torch"].cuda.is_initialized()) or gpu_touched():
         _send(conn, {"error": "zygote has initialised the GPU; refusing to fork"})
         return
     pid = os.fork()
@@ -140,6 +160,9 @@ def serve(path: str) -> None:
             __import__(m)
         except Exception:  # pragma: no cover - optional module
             pass
+    if gpu_touched():  # the agent then starts plain subprocesses
+        print("zygote: an import opened the GPU device; not serving", flush=True)
+        return
     srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
     if os.path.exists(path):
         os.unlink(path)

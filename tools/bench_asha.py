@@ -53,6 +53,23 @@ def search_config(args: argparse.Namespace) -> dict:
     return cfg
 
 
+def _print_trace(s: Session, trials: list) -> None:
+    """Mean seconds-since-process-start of each start-up mark (exec/harness.py DET_STARTUP_TRACE)
+    over the trials, plus the mean allocation wall time."""
+    import re
+    import statistics
+
+    marks: dict = {}
+    for t in trials:
+        for line in s.get(f"/api/v1/trials/{t['id']}/logs")["logs"]:
+            m = re.search(r"startup: (.+) at \+([0-9.]+)s", line["log"])
+            if m:
+                marks.setdefault(m.group(1), []).append(float(m.group(2)))
+    for k, v in sorted(marks.items(), key=lambda kv: statistics.mean(kv[1])):
+        print(f"[bench_asha] startup '{k}': mean +{statistics.mean(v):.3f}s over {len(v)} trials",
+              file=sys.stderr, flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--slots-per-gpu", type=int, default=8)
@@ -63,6 +80,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--timeout", type=float, default=1500.0)
     ap.add_argument("--cpu", action="store_true", help="artificial CPU slots (plumbing check)")
+    ap.add_argument("--trace", action="store_true",
+                    help="DET_STARTUP_TRACE=1 in the trials; print mean start-up phase times to stderr")
     args = ap.parse_args()
 
     tmp = tempfile.mkdtemp(prefix="det-asha-bench-")
@@ -75,7 +94,13 @@ def main() -> None:
     s = Session(m.master_url)
     s.token = s.post("/api/v1/auth/login", {"username": "admin", "password": ""})["token"]
     try:
-        body = {"config": search_config(args), "model_definition": base64.b64encode(
+        cfg = search_config(args)
+        if args.trace:
+            env = cfg.setdefault("environment", {}).setdefault("environment_variables", [])
+            env.append("DET_STARTUP_TRACE=1")
+            if os.environ.get("DET_STARTUP_PROFILE"):
+                env.append("DET_STARTUP_PROFILE=1")
+        body = {"config": cfg, "model_definition": base64.b64encode(
             tar_directory(os.path.join(ROOT, "examples", "cifar10_asha"))).decode()}
         t0 = time.time()
         eid = s.post("/api/v1/experiments", body)["experiment"]["id"]
@@ -100,6 +125,8 @@ def main() -> None:
             v = t.get("best_validation")
             if v is not None and (best is None or v < best):
                 best = v
+        if args.trace:
+            _print_trace(s, trials)
         if state != "COMPLETED":
             errs = [t["id"] for t in trials if t["state"] == "ERROR"]
             print(f"[bench_asha] experiment ended {state!r}; errored trials {errs}", file=sys.stderr)
