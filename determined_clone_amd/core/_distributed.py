@@ -33,6 +33,7 @@ class DistributedContext:
         self._group = _group  # torch.distributed ProcessGroup (gloo) or None
         self._local_group = None
         self._closed = False
+        self._owns_pg = False
         if size > 1 and _group is None:
             self._group = _new_object_group()
         if size > 1 and local_size < size:
@@ -52,6 +53,7 @@ class DistributedContext:
         local_size = int(os.environ.get("LOCAL_WORLD_SIZE", size))
         cross_rank = int(os.environ.get("GROUP_RANK", rank // max(local_size, 1)))
         cross_size = size // max(local_size, 1)
+        owns = False
         if not dist.is_initialized():
             import torch
 
@@ -59,9 +61,12 @@ class DistributedContext:
             if backend == "nccl":
                 torch.cuda.set_device(local_rank)
             dist.init_process_group(backend=backend)
-        return cls(rank=rank, size=size, local_rank=local_rank, local_size=local_size,
-                   cross_rank=cross_rank, cross_size=cross_size,
-                   chief_ip=chief_ip or os.environ.get("MASTER_ADDR"))
+            owns = True
+        ctx = cls(rank=rank, size=size, local_rank=local_rank, local_size=local_size,
+                  cross_rank=cross_rank, cross_size=cross_size,
+                  chief_ip=chief_ip or os.environ.get("MASTER_ADDR"))
+        ctx._owns_pg = owns
+        return ctx
 
     @classmethod
     def from_deepspeed(cls, chief_ip: Optional[str] = None) -> "DistributedContext":
@@ -96,7 +101,31 @@ class DistributedContext:
         return self.cross_size
 
     def close(self) -> None:
+        """Release the process groups this context created (its gloo object groups, and the
+        default group when ``from_torch_distributed`` initialised it): a worker that exits with a
+        live gloo group can abort in the group's destructor ("terminate called without an active
+        exception") while a peer is still tearing down."""
+        if self._closed:
+            return
         self._closed = True
+        if self.size <= 1:
+            return
+        import torch.distributed as dist
+
+        if not (dist.is_available() and dist.is_initialized()):
+            return
+        for g in (self._local_group, self._group):
+            if g is not None:
+                try:
+                    dist.destroy_process_group(g)
+                except Exception:  # noqa: BLE001 - teardown is best effort
+                    pass
+        self._local_group = self._group = None
+        if getattr(self, "_owns_pg", False):
+            try:
+                dist.destroy_process_group()
+            except Exception:  # noqa: BLE001
+                pass
 
     # ------------------------------------------------------------------ collectives
     def _objs(self, obj: Any, group: Any) -> List[Any]:
