@@ -105,6 +105,36 @@ class ResNet50BenchTrial(pytorch.PyTorchTrial):
         return self._data(1, 1)
 
 
+def _gpu_state() -> dict:
+    """sclk level in use, power draw / cap and junction temperature of the visible amdgpu cards
+    (sysfs; for the stderr diagnostics: a throttled or power-capped device shows here)."""
+    import glob
+
+    out = {}
+    for dev in sorted(glob.glob("/sys/class/drm/card[0-9]*/device"))[:8]:
+        def rd(name: str) -> str:
+            try:
+                with open(os.path.join(dev, name)) as f:
+                    return f.read().strip()
+            except OSError:
+                return ""
+        sclk = next((ln.split(":", 1)[1].strip().rstrip("*").strip() for ln in rd("pp_dpm_sclk").splitlines()
+                     if ln.endswith("*")), "")
+        hw = sorted(glob.glob(os.path.join(dev, "hwmon", "hwmon*")))
+        def hwrd(name: str) -> str:
+            try:
+                with open(os.path.join(hw[0], name)) as f:
+                    return f.read().strip()
+            except (OSError, IndexError):
+                return ""
+        pw = hwrd("power1_average") or hwrd("power1_input")
+        card = os.path.basename(os.path.dirname(dev))
+        out[card] = {"sclk": sclk, "power_w": round(int(pw) / 1e6, 1) if pw.isdigit() else None,
+                     "cap_w": round(int(hwrd("power1_cap")) / 1e6, 1) if hwrd("power1_cap").isdigit() else None,
+                     "temp_c": round(int(hwrd("temp1_input")) / 1e3, 1) if hwrd("temp1_input").isdigit() else None}
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -142,6 +172,7 @@ def main() -> None:
             ev = trial.events
             step_ms = [round(a.elapsed_time(b), 2) for a, b in zip(ev[:-1], ev[1:])]
             ms_stats = torch.cuda.memory_stats()
+            print(json.dumps({"rank": ctx.distributed.rank, "gpu_state_end": _gpu_state()}), file=sys.stderr)
             print(json.dumps({"rank": ctx.distributed.rank, "step_ms": step_ms,
                               "max_reserved_gb": round(torch.cuda.max_memory_reserved() / 2**30, 1),
                               "alloc_retries": ms_stats.get("num_alloc_retries", 0),

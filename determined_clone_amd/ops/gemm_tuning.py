@@ -60,7 +60,8 @@ def enable(path: Optional[str] = None, tune: bool = False) -> bool:
     if tune:
         # time each candidate on rotated operand copies (L2/MALL-cold, as in the training step)
         tunable.set_rotating_buffer_size(256)
-        tunable.set_max_tuning_duration(20)
+        tunable.set_max_tuning_duration(8)
+        tunable.set_max_tuning_iterations(30)
     tunable.enable(True)
     _state["path"] = target
     return True
