@@ -13,3 +13,5 @@ cp determined_clone_amd/ops/tuned/gemm_gfx950.csv $O/merged.csv
 DCA_GEMM_TUNED=0 timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/rn_default.txt 2>&1 || exit $?
 timeout -k 10 240 python bench.py --steps 20 --warmup 5 > $O/rn_tuned.txt 2>&1 || exit $?
 grep -h '"metric"' $O/rn_default.txt $O/rn_tuned.txt | cut -c1-150
+timeout -k 10 400 python tools/bench_conv3x3.py --find --only-stem > $O/stem_find.txt 2>&1 || exit $?
+cat $O/stem_find.txt
