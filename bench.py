@@ -128,6 +128,8 @@ def _gpu_state() -> dict:
             except (OSError, IndexError):
                 return ""
         pw = hwrd("power1_average") or hwrd("power1_input")
+        if not sclk and not pw:
+            continue  # not an amdgpu device with power management
         card = os.path.basename(os.path.dirname(dev))
         out[card] = {"sclk": sclk, "power_w": round(int(pw) / 1e6, 1) if pw.isdigit() else None,
                      "cap_w": round(int(hwrd("power1_cap")) / 1e6, 1) if hwrd("power1_cap").isdigit() else None,

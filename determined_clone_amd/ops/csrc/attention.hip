@@ -14,6 +14,7 @@
 // Backward (FlashAttention-2 ordering), one workgroup = 64 keys; dK/dV accumulate in VGPRs while
 //   the workgroup sweeps the query tiles; recomputed P^T = exp2(S^T - LSE), dP^T = V dO^T,
 //   dS^T = P^T (dP^T - rowsum(dO*O)); dQ partials are added into an fp32 buffer with float atomics.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -126,10 +127,10 @@ __device__ __forceinline__ void stage_rows(const uint16_t* __restrict__ src, Str
 
 // Register double buffer for a pair of [64 rows][D] tiles (K and V): fetch() issues the HBM loads of
 // the NEXT tile before the current tile's MFMAs, store() writes them to LDS after the barrier.
-template <int D>
+template <int D, int ROWS = 64>
 struct KVPrefetch {
   static constexpr int CPR = D / 8;
-  static constexpr int N = 2 * 64 * CPR / 256;
+  static constexpr int N = 2 * ROWS * CPR / 256;
   uint4 reg[N];
   __device__ __forceinline__ void fetch(const uint16_t* __restrict__ kb, Strides ks,
                                         const uint16_t* __restrict__ vb, Strides vs, int r0,
@@ -137,8 +138,8 @@ struct KVPrefetch {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const int c = threadIdx.x + 256 * j;
-      const int which = c / (64 * CPR);
-      const int cc = c % (64 * CPR);
+      const int which = c / (ROWS * CPR);
+      const int cc = c % (ROWS * CPR);
       const int rr = cc / CPR, d0 = (cc % CPR) * 8;
       reg[j] = make_uint4(0, 0, 0, 0);
       if (r0 + rr < n_rows) {
@@ -152,8 +153,8 @@ struct KVPrefetch {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const int c = threadIdx.x + 256 * j;
-      const int which = c / (64 * CPR);
-      const int cc = c % (64 * CPR);
+      const int which = c / (ROWS * CPR);
+      const int cc = c % (ROWS * CPR);
       *reinterpret_cast<uint4*>((which ? Vs : Ks) + (cc / CPR) * (D + kPad) + (cc % CPR) * 8) = reg[j];
     }
   }
@@ -166,12 +167,12 @@ struct KVPrefetch {
 // + one exchange with lane^32), and P^T -- still in registers -- is directly the B operand of
 // O^T += V^T P^T (no LDS round trip for P). V^T fragments come from the row-major V tile through
 // ds_read_b64_tr_b16 (hardware transpose), so K and V are staged exactly as they arrive from HBM.
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int KT>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
     Strides ks, Strides vs, Strides os, float scale_log2) {
-  constexpr int KT = 64;       // keys per LDS tile
+  // KT = keys per LDS tile (one barrier pair per tile), consumed in 32-key MFMA sub-tiles
   constexpr int QB = 128;      // queries per workgroup
   constexpr int RS = D + kPad; // LDS row stride (elements)
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   // tr-read lane address pieces (see T10: lane 4q+p of a 16-lane group -> row q, cols 4p..4p+3)
   const int tr_row = (r & 15) >> 2;
   const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
-  KVPrefetch<D> pf;
+  KVPrefetch<D, KT> pf;
   pf.fetch(kb, ks, vb, vs, 0, Sk);
   for (int kt = 0; kt < k_end; kt += KT) {
     __syncthreads();
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     __syncthreads();
     if (kt + KT < k_end) pf.fetch(kb, ks, vb, vs, kt + KT, Sk);
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
+    for (int sub = 0; sub < KT / 32; ++sub) {
       const int kb0 = kt + 32 * sub;
       if (kb0 >= k_end) break;
       if (CAUSAL && kb0 > q0 + 31) break;  // wave-uniform: the rest of this tile is masked
@@ -415,14 +416,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   }
 }
 
-template <int D, bool CAUSAL>
+// QT = queries staged per LDS tile (one barrier pair per tile); each wave consumes it in 32-query
+// MFMA sub-tiles, so QT = 64 halves the barriers and staging passes per MFMA of QT = 32.
+template <int D, bool CAUSAL, int QT>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     const uint16_t* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
     uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int Sq, int Sk, int H, Strides qs,
     Strides ks, Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale) {
   constexpr int KB = 128;
-  constexpr int QT = 32;
+  static_assert(QT == 32 || QT == 64, "query tile");
   constexpr int RS = D + kPad;
   constexpr int CPR = D / 8;                 // 16-byte chunks per row
   constexpr int NPF = 2 * QT * CPR / 256;    // prefetched chunks per thread (Q and dO tiles)
@@ -499,24 +502,26 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     }
     __syncthreads();
     if (qt + QT < Sq) fetch(qt + QT);
-    const bool active = !(CAUSAL && kw0 > qt + QT - 1) && kw0 < Sk;  // wave-uniform
-    if (!active) continue;
-    auto tile = [&](auto masked) {
+    // one 32-query MFMA sub-tile at LDS row offset 32*half (queries qs0 .. qs0+31)
+    auto tile = [&](auto masked, const int half) {
+      const int qs0 = qt + 32 * half;
+      const uint16_t* Qh = Qs + 32 * half * RS;
+      const uint16_t* dOh = dOs + 32 * half * RS;
       // this lane's 16 queries are 4 runs of 4 consecutive rows: their LSE / delta come in as
       // four 16-B LDS reads each instead of sixteen 4-B reads
       float4 l4[4], d4[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        l4[g] = *reinterpret_cast<const float4*>(lse_s + 8 * g + 4 * hf);
-        d4[g] = *reinterpret_cast<const float4*>(del_s + 8 * g + 4 * hf);
+        l4[g] = *reinterpret_cast<const float4*>(lse_s + 32 * half + 8 * g + 4 * hf);
+        d4[g] = *reinterpret_cast<const float4*>(del_s + 32 * half + 8 * g + 4 * hf);
       }
       f32x16 sacc = zero16(), dpacc = zero16();
       if constexpr (D == 64) {  // fragments preloaded (see the forward)
         bf16x8 qfr[D / 16], dofr[D / 16];
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          qfr[s] = load8(Qs + r * RS + 16 * s + 8 * hf);
-          dofr[s] = load8(dOs + r * RS + 16 * s + 8 * hf);
+          qfr[s] = load8(Qh + r * RS + 16 * s + 8 * hf);
+          dofr[s] = load8(dOh + r * RS + 16 * s + 8 * hf);
         }
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
@@ -526,8 +531,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
       } else {
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          sacc = mfma32(load8(Qs + r * RS + 16 * s + 8 * hf), kf[s], sacc);
-          dpacc = mfma32(load8(dOs + r * RS + 16 * s + 8 * hf), vf[s], dpacc);
+          sacc = mfma32(load8(Qh + r * RS + 16 * s + 8 * hf), kf[s], sacc);
+          dpacc = mfma32(load8(dOh + r * RS + 16 * s + 8 * hf), vf[s], dpacc);
         }
       }
 #pragma unroll
@@ -536,7 +541,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
         const float dl = reinterpret_cast<const float*>(&d4[i >> 2])[i & 3];
         float p = fast_exp2(fmaf(sacc[i], scale_log2, -lq));
         if constexpr (decltype(masked)::value) {
-          const int qi = qt + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          const int qi = qs0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
           p = (qi >= Sq || my_key >= Sk || (CAUSAL && my_key > qi)) ? 0.f : p;
         }
         sacc[i] = p;
@@ -549,16 +554,22 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int off = (16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
-          dvacc[n] = mfma32(cat8(tr_read(dOs + off), tr_read(dOs + off + 8 * RS)), s2 ? p1 : p0, dvacc[n]);
-          dkacc[n] = mfma32(cat8(tr_read(Qs + off), tr_read(Qs + off + 8 * RS)), s2 ? s1 : s0, dkacc[n]);
+          dvacc[n] = mfma32(cat8(tr_read(dOh + off), tr_read(dOh + off + 8 * RS)), s2 ? p1 : p0, dvacc[n]);
+          dkacc[n] = mfma32(cat8(tr_read(Qh + off), tr_read(Qh + off + 8 * RS)), s2 ? s1 : s0, dkacc[n]);
         }
       }
     };
-    // wave-uniform (a key block straddling Sk only exists in the last workgroup)
-    if (D == 128 || (qt + QT > Sq) || (kw0 + 32 > Sk) || (CAUSAL && kw0 + 31 > qt))
-      tile(std::true_type{});
-    else
-      tile(std::false_type{});
+#pragma unroll
+    for (int half = 0; half < QT / 32; ++half) {
+      const int qs0 = qt + 32 * half;
+      // wave-uniform: causal (keys after every query of the sub-tile), past Sq / Sk
+      if (qs0 >= Sq || (CAUSAL && kw0 > qs0 + 31) || kw0 >= Sk) continue;
+      // a key block straddling Sk only exists in the last workgroup
+      if (D == 128 || (qs0 + 32 > Sq) || (kw0 + 32 > Sk) || (CAUSAL && kw0 + 31 > qs0))
+        tile(std::true_type{}, half);
+      else
+        tile(std::false_type{}, half);
+    }
   }
   if (my_key < Sk) {
     uint16_t* dkrow = dk + b * dks.b + h * dks.h + static_cast<int64_t>(my_key) * dks.s;
@@ -578,20 +589,50 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   }
 }
 
-size_t fwd_lds(int D) { return 2 * static_cast<size_t>(64) * (D + kPad) * 2; }
+size_t fwd_lds(int D, int KT = 64) { return 2 * static_cast<size_t>(KT) * (D + kPad) * 2; }
 size_t bwd_dq_lds(int D) { return fwd_lds(D); }
-size_t bwd_dkdv_lds(int D) { return 2 * 32 * static_cast<size_t>(D + kPad) * 2 + 2 * 32 * sizeof(float); }
+
+// keys per LDS tile of the forward kernel (DCA_ATTN_FWD_KT=128: half the barriers per MFMA)
+int fwd_kt() {
+  static const int kt = [] {
+    const char* e = std::getenv("DCA_ATTN_FWD_KT");
+    return (e && std::atoi(e) == 128) ? 128 : 64;
+  }();
+  return kt;
+}
+size_t bwd_dkdv_lds(int D, int QT) {
+  return 2 * static_cast<size_t>(QT) * (D + kPad) * 2 + 2 * static_cast<size_t>(QT) * sizeof(float);
+}
+
+// queries per LDS tile of the dK/dV kernel (DCA_ATTN_DKDV_QT=32 restores the 32-query tiles)
+int dkdv_qt() {
+  static const int qt = [] {
+    const char* e = std::getenv("DCA_ATTN_DKDV_QT");
+    return (e && std::atoi(e) == 32) ? 32 : 64;
+  }();
+  return qt;
+}
 
 template <int D, bool C>
 void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse,
                 int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs, Strides os,
                 float scale_log2, hipStream_t st) {
   dim3 grid((Sq + 127) / 128, H, B);
-  const size_t lds = fwd_lds(D);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_fwd_kernel<D, C>),
-                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-  hipLaunchKernelGGL((attn_fwd_kernel<D, C>), grid, dim3(256), lds, st, q, k, v, o, lse, Sq, Sk, H,
-                     qs, ks, vs, os, scale_log2);
+  auto go = [&](auto ktag) {
+    constexpr int KT = decltype(ktag)::value;
+    const size_t lds = fwd_lds(D, KT);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_fwd_kernel<D, C, KT>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    hipLaunchKernelGGL((attn_fwd_kernel<D, C, KT>), grid, dim3(256), lds, st, q, k, v, o, lse, Sq,
+                       Sk, H, qs, ks, vs, os, scale_log2);
+  };
+  if constexpr (D == 64) {  // D = 128 at KT = 128 exceeds the register file (spills)
+    if (fwd_kt() == 128) {
+      go(std::integral_constant<int, 128>{});
+      return;
+    }
+  }
+  go(std::integral_constant<int, 64>{});
 }
 
 template <int D, bool C>
@@ -606,10 +647,15 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C>), dim3((Sq + 127) / 128, H, B), dim3(256), l1, st, q,
                      k, v, o, dO, lse, delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2,
                      scale);
-  const size_t l2 = bwd_dkdv_lds(D);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C>), dim3((Sk + 127) / 128, H, B), dim3(256), l2, st,
-                     q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks, vs, dos, dks, dvs,
-                     scale_log2, scale);
+  if (dkdv_qt() == 64) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H, B), dim3(256),
+                       bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
+                       vs, dos, dks, dvs, scale_log2, scale);
+  } else {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 32>), dim3((Sk + 127) / 128, H, B), dim3(256),
+                       bwd_dkdv_lds(D, 32), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
+                       vs, dos, dks, dvs, scale_log2, scale);
+  }
 }
 
 }  // namespace
