@@ -278,6 +278,82 @@ def _bgrad(dy: torch.Tensor, bias: torch.Tensor) -> Optional[torch.Tensor]:
     return None
 
 
+# ----------------------------------------------------------------------------- ResNet stem
+# The 7x7 / stride-2 stem on a 3-channel image is MIOpen's least efficient convolution of the model
+# (140 TFLOP/s forward, 175 weight gradient at bs 1024: 3-channel pixels are 6-byte rows). Rewritten
+# by space-to-depth -- pad the image by 3, fold each 2x2 pixel block into 12 channels, pad the
+# kernel to 8x8 and fold it the same way -- it is exactly a 4x4 / stride-1 convolution on a
+# 115x115x12 image: 1119 us forward + 934 us weight gradient instead of 1716 + 1381
+# (profiles/round3_stem_conv_variants_find.txt). Opt-in (DCA_STEM_S2D=1) until measured end to end.
+STEM_S2D = os.environ.get("DCA_STEM_S2D", "0") == "1"
+
+
+def _s2d_input(x: torch.Tensor) -> torch.Tensor:
+    """[N, 3, H, W] (NHWC memory) -> [N, 12, (H+6)/2, (W+6)/2] channels_last, channel (dy, dx, c)."""
+    n, c, h, w = x.shape
+    xn = F.pad(x.permute(0, 2, 3, 1), (0, 0, 3, 3, 3, 3))  # [N, H+6, W+6, C]
+    hh, ww = (h + 6) // 2, (w + 6) // 2
+    xs = xn.view(n, hh, 2, ww, 2, c).permute(0, 1, 3, 2, 4, 5).reshape(n, hh, ww, 4 * c)
+    return xs.permute(0, 3, 1, 2)
+
+
+def _s2d_weight(w: torch.Tensor) -> torch.Tensor:
+    """[K, C, 7, 7] -> [K, 4C, 4, 4] (channels_last), channel (dy, dx, c), tap (i, j) = (2i+dy, 2j+dx)."""
+    k, c = w.shape[:2]
+    wp = F.pad(w, (0, 1, 0, 1)).view(k, c, 4, 2, 4, 2).permute(0, 3, 5, 1, 2, 4)
+    return wp.reshape(k, 4 * c, 4, 4).contiguous(memory_format=torch.channels_last)
+
+
+def _s2d_weight_grad(dw2: torch.Tensor, c: int) -> torch.Tensor:
+    """Inverse of :func:`_s2d_weight` for the gradient: [K, 4C, 4, 4] -> [K, C, 7, 7]."""
+    k = dw2.shape[0]
+    d = dw2.reshape(k, 2, 2, c, 4, 4).permute(0, 3, 4, 1, 5, 2).reshape(k, c, 8, 8)
+    return d[:, :, :7, :7]
+
+
+class _StemS2D(torch.autograd.Function):
+    """7x7/2 (padding 3) convolution of a 3-channel image as the space-to-depth 4x4/1 convolution;
+    the weight gradient is folded back to 7x7 and, on a GPU, runs on the side stream into the
+    parameter's ``.grad`` view (``ops/_grad.py``). The image gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        xs = _s2d_input(x)
+        w2 = _s2d_weight(weight)
+        ctx.save_for_backward(xs, w2)
+        ctx.weight = weight
+        return F.conv2d(xs, w2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, w2 = ctx.saved_tensors
+        weight = ctx.weight
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        args = (dy, xs, w2, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+        bwd = torch.ops.aten.convolution_backward
+        s = _grad.side_stream_for(weight)
+        if s is None:
+            dw2 = bwd(*args, [False, True, False])[1]
+            return None, _s2d_weight_grad(dw2, weight.shape[1]).to(weight.dtype)
+        _grad.fork(s, (dy, xs))
+        with torch.cuda.stream(s):
+            dw2 = bwd(*args, [False, True, False])[1]
+            _grad.target(weight).add_(_s2d_weight_grad(dw2, weight.shape[1]))
+        return None, None
+
+
+def stem_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """The ResNet stem convolution: space-to-depth form on a GPU when it applies (7x7, stride 2,
+    padding 3, 3 input channels, no bias, even H and W, image without gradient), else
+    :func:`spatial_conv`."""
+    if (STEM_S2D and x.is_cuda and not x.requires_grad and conv.kernel_size == (7, 7)
+            and conv.stride == (2, 2) and conv.padding == (3, 3) and conv.in_channels == 3
+            and conv.groups == 1 and conv.bias is None and conv.dilation == (1, 1)
+            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0):
+        return _StemS2D.apply(x.contiguous(memory_format=torch.channels_last), conv.weight)
+    return spatial_conv(conv, x)
+
+
 def spatial_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """``conv(x)``; on a GPU its weight (and bias) gradient runs on the side stream
     (``ops/_grad.py``)."""

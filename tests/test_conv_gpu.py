@@ -222,3 +222,28 @@ def test_side_stream_weight_gradients_match_inline(monkeypatch, model_fn):
     F.cross_entropy(model(x).float(), y).backward()
     opt.step()
     assert not _grad.pending()
+
+
+@pytest.mark.parametrize("side", [True, False])
+@pytest.mark.parametrize("hw", [(224, 224), (64, 48)])
+def test_stem_space_to_depth_matches_fp32(monkeypatch, side, hw):
+    """The space-to-depth stem (7x7/2 as a 4x4/1 conv on 12 channels) equals the fp32 7x7
+    convolution forward and weight gradient, inline and on the side stream."""
+    from determined_clone_amd.ops import _grad
+    from determined_clone_amd.parallel.flat import FlatParamSpace
+
+    monkeypatch.setattr(_grad, "SIDE_STREAM", side)
+    monkeypatch.setattr(conv, "STEM_S2D", True)
+    torch.manual_seed(0)
+    c = nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    FlatParamSpace([[c.weight]])  # persistent .grad view (side-stream accumulation target)
+    x = torch.randn(4, 3, *hw, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = conv.stem_conv(c, x)
+    ref = F.conv2d(x.float(), c.weight.float(), stride=2, padding=3)
+    _close(y, ref, 2e-2, "stem fwd")
+    g = torch.randn_like(ref)
+    y.backward(g.to(y.dtype))
+    _grad.join()
+    dw_ref = torch.ops.aten.convolution_backward(g, x.float(), c.weight.float(), None, [2, 2], [3, 3], [1, 1],
+                                                 False, [0, 0], 1, [False, True, False])[1]
+    _close(c.weight.grad, dw_ref, 3e-2, "stem wgrad")
