@@ -18,8 +18,8 @@ arch): on a different software stack TunableOp rejects the file and everything r
 * ``DCA_GEMM_TUNE=<file>`` -- tuning run: every new shape is timed and the results are written to
   ``<file>`` at exit; ``tools/tune_gemms.py`` merges such files into the shipped one.
 
-Each process replays from its own copy of the file (TunableOp may write its database back at
-exit; 8 ranks must not write one shared file).
+Each process replays from its own temporary copy of the file (removed at exit), so no rank ever
+opens the shipped file for writing.
 """
 import os
 import shutil
@@ -53,6 +53,11 @@ def enable(path: Optional[str] = None, tune: bool = False) -> bool:
         fd, target = tempfile.mkstemp(prefix="dca_gemm_tuned_", suffix=".csv")
         os.close(fd)
         shutil.copyfile(src, target)
+        # replay never writes the database back (results are written as tunings complete), so
+        # the copy can go when the process ends
+        import atexit
+
+        atexit.register(lambda p=target: os.path.exists(p) and os.remove(p))
     import torch.cuda.tunable as tunable
 
     tunable.set_filename(target, False)
