@@ -91,6 +91,24 @@ struct Strides {
   int64_t b, h, s;  // element strides; d stride is 1
 };
 
+// XCD-aware workgroup order (guide T1). Consecutive workgroup ids are dealt round-robin to the 8
+// XCDs, each with its own L2, so the query (or key) blocks of one (batch, head) -- which all stream
+// the same K/V (or Q/dO) tiles -- would be spread over 8 L2s and every tile fetched 8 times from
+// HBM / MALL. With remap, each XCD gets a contiguous range of grid positions (the bijective form,
+// valid for any grid size): the blocks of a (batch, head) share one L2. DCA_ATTN_XCD_REMAP=0 off.
+struct Blk {
+  int x, y, z;
+};
+__device__ __forceinline__ Blk xcd_block(bool remap) {
+  if (!remap) return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y), static_cast<int>(blockIdx.z)};
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int n = nx * ny * gridDim.z;
+  const int l = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const int xcd = l % 8, q = n / 8, r = n % 8;
+  const int v = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + l / 8;
+  return {v % nx, (v / nx) % ny, v / (nx * ny)};
+}
+
 // Stage a [64 rows][D] tile (rows r0.., clamped to n_rows, zero-filled beyond) into LDS,
 // row-major (dst[r][d], row stride D + kPad) and/or transposed (dstT[d][r], row stride 64 + kPad).
 template <int D>
@@ -171,7 +189,7 @@ template <int D, bool CAUSAL, int KT>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
-    Strides ks, Strides vs, Strides os, float scale_log2) {
+    Strides ks, Strides vs, Strides os, float scale_log2, bool remap) {
   // KT = keys per LDS tile (one barrier pair per tile), consumed in 32-key MFMA sub-tiles
   constexpr int QB = 128;      // queries per workgroup
   constexpr int RS = D + kPad; // LDS row stride (elements)
@@ -182,9 +200,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   // wave index in an SGPR: the causal extent checks below are uniform branches
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hf = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
+  const Blk blk = xcd_block(remap);
+  const int b = blk.z, h = blk.y;
   // heaviest (largest causal extent) query blocks first
-  const int q_blk = (CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * QB;
+  const int q_blk = (CAUSAL ? (gridDim.x - 1 - blk.x) : blk.x) * QB;
   const int q0 = q_blk + w * 32;
   const int my_q = q0 + r;
   const uint16_t* qb = q + b * qs.b + h * qs.h;
@@ -301,7 +320,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     const uint16_t* __restrict__ o, const uint16_t* __restrict__ dO, const float* __restrict__ lse,
     float* __restrict__ delta, uint16_t* __restrict__ dq, int Sq, int Sk, int H, Strides qs,
-    Strides ks, Strides vs, Strides os, Strides dos, Strides dqs, float scale_log2, float scale) {
+    Strides ks, Strides vs, Strides os, Strides dos, Strides dqs, float scale_log2, float scale,
+    bool remap) {
   constexpr int KT = 64;
   constexpr int QB = 128;
   constexpr int RS = D + kPad;
@@ -313,8 +333,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   // uniform branch instead of per-lane exec masking
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hf = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int q_blk = (CAUSAL ? (gridDim.x - 1 - blockIdx.x) : blockIdx.x) * QB;
+  const Blk blk = xcd_block(remap);
+  const int b = blk.z, h = blk.y;
+  const int q_blk = (CAUSAL ? (gridDim.x - 1 - blk.x) : blk.x) * QB;
   const int q0 = q_blk + w * 32;
   const int my_q = q0 + r;
   const bool q_ok = my_q < Sq;
@@ -423,7 +444,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     const uint16_t* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
     uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int Sq, int Sk, int H, Strides qs,
-    Strides ks, Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale) {
+    Strides ks, Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale,
+    bool remap) {
   constexpr int KB = 128;
   static_assert(QT == 32 || QT == 64, "query tile");
   constexpr int RS = D + kPad;
@@ -439,8 +461,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   // uniform branch instead of per-lane exec masking
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hf = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int k_blk = blockIdx.x * KB;
+  const Blk blk = xcd_block(remap);
+  const int b = blk.z, h = blk.y;
+  const int k_blk = blk.x * KB;
   const int kw0 = k_blk + 32 * w;
   const int my_key = kw0 + r;
   const uint16_t* qb = q + b * qs.b + h * qs.h;
@@ -592,6 +615,14 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
 size_t fwd_lds(int D, int KT = 64) { return 2 * static_cast<size_t>(KT) * (D + kPad) * 2; }
 size_t bwd_dq_lds(int D) { return fwd_lds(D); }
 
+bool xcd_remap() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCA_ATTN_XCD_REMAP");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 // keys per LDS tile of the forward kernel (DCA_ATTN_FWD_KT=128: half the barriers per MFMA)
 int fwd_kt() {
   static const int kt = [] {
@@ -624,7 +655,7 @@ void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_fwd_kernel<D, C, KT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     hipLaunchKernelGGL((attn_fwd_kernel<D, C, KT>), grid, dim3(256), lds, st, q, k, v, o, lse, Sq,
-                       Sk, H, qs, ks, vs, os, scale_log2);
+                       Sk, H, qs, ks, vs, os, scale_log2, xcd_remap());
   };
   if constexpr (D == 64) {  // D = 128 at KT = 128 exceeds the register file (spills)
     if (fwd_kt() == 128) {
@@ -646,15 +677,15 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
                       hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l1));
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C>), dim3((Sq + 127) / 128, H, B), dim3(256), l1, st, q,
                      k, v, o, dO, lse, delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2,
-                     scale);
+                     scale, xcd_remap());
   if (dkdv_qt() == 64) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H, B), dim3(256),
                        bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
-                       vs, dos, dks, dvs, scale_log2, scale);
+                       vs, dos, dks, dvs, scale_log2, scale, xcd_remap());
   } else {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 32>), dim3((Sk + 127) / 128, H, B), dim3(256),
                        bwd_dkdv_lds(D, 32), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
-                       vs, dos, dks, dvs, scale_log2, scale);
+                       vs, dos, dks, dvs, scale_log2, scale, xcd_remap());
   }
 }
 
