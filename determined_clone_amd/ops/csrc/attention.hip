@@ -185,7 +185,7 @@ struct KVPrefetch {
 // + one exchange with lane^32), and P^T -- still in registers -- is directly the B operand of
 // O^T += V^T P^T (no LDS round trip for P). V^T fragments come from the row-major V tile through
 // ds_read_b64_tr_b16 (hardware transpose), so K and V are staged exactly as they arrive from HBM.
-template <int D, bool CAUSAL, int KT>
+template <int D, bool CAUSAL, int KT, bool PIPE>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
@@ -229,6 +229,78 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     pf.store(Ks, Vs);
     __syncthreads();
     if (kt + KT < k_end) pf.fetch(kb, ks, vb, vs, kt + KT, Sk);
+    if constexpr (PIPE) {
+      // S^T = K Q^T for the 32-key sub-tile `sub` of the staged tile
+      auto scores = [&](const int sub) {
+        f32x16 sc = zero16();
+  #pragma unroll
+        for (int s = 0; s < D / 16; ++s)
+          sc = mfma32(load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf), qf[s], sc);
+        return sc;
+      };
+      // online softmax of one sub-tile's scores and O^T += V^T P^T
+      auto softmax_pv = [&](f32x16 sc, const int sub, const int kb0, const bool need_mask) {
+        // sc[i]: key = kb0 + (i&3) + 8(i>>2) + 4hf, query = my_q
+        // row max on the RAW scores (scale > 0 commutes with max); the scale is folded into the
+        // exponent's FMA below -- one VALU op per score instead of a multiply and a subtract
+        float mx = -INFINITY;
+  #pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (need_mask) {
+            const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+            if (key >= Sk || (CAUSAL && key > my_q)) sc[i] = -INFINITY;
+          }
+          mx = fmaxf(mx, sc[i]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        // deferred max (T13): the running max m moves only when a score exceeds it by more than
+        // kRescaleLog2 (p <= 2^kRescaleLog2 meanwhile: exact in the fp32 accumulators, 8 bits of
+        // headroom in the bf16 P), so the D/2-multiply rescale of O and l runs on a few sub-tiles
+        // per row instead of on every max increase. Per lane (= query row): the factor that scales
+        // this lane's l is the one that scales its O accumulators.
+        const float mcand = mx * scale_log2;
+        const bool upd = mcand > m + kRescaleLog2;
+        const float mnew = upd ? mcand : m;
+        const float mref = mnew == -INFINITY ? 0.f : mnew;
+        const float alpha = upd ? fast_exp2(m - mref) : 1.f;
+        float rs = 0.f;
+  #pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = fast_exp2(fmaf(sc[i], scale_log2, -mref));
+          sc[i] = p;
+          rs += p;
+        }
+        rs += __shfl_xor(rs, 32, 64);
+        l = l * alpha + rs;
+        m = mnew;
+        if (__any(upd)) {
+  #pragma unroll
+          for (int n = 0; n < D / 32; ++n) oacc[n] *= alpha;
+        }
+        const bf16x8 p0 = pack8(sc, 0), p1 = pack8(sc, 8);
+  #pragma unroll
+        for (int n = 0; n < D / 32; ++n) {
+  #pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
+            oacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RS)), s2 ? p1 : p0, oacc[n]);
+          }
+        }
+      };
+      // wave-uniform: every key of the tile exists and precedes every query of this wave
+      if (kt + KT <= Sk && (!CAUSAL || kt + KT - 1 <= q0)) {
+        // pairs of sub-tiles: both score products are issued before the first softmax, so the
+        // second one's MFMAs run in the matrix pipe under the first softmax's VALU work
+#pragma unroll
+        for (int sub = 0; sub < KT / 32; sub += 2) {
+          const f32x16 sa = scores(sub);
+          const f32x16 sb = scores(sub + 1);
+          softmax_pv(sa, sub, kt + 32 * sub, false);
+          softmax_pv(sb, sub + 1, kt + 32 * sub + 32, false);
+        }
+        continue;
+      }
+    }
 #pragma unroll
     for (int sub = 0; sub < KT / 32; ++sub) {
       const int kb0 = kt + 32 * sub;
@@ -623,6 +695,15 @@ bool xcd_remap() {
   return on;
 }
 
+// forward: issue a sub-tile pair's score MFMAs before its softmaxes (DCA_ATTN_FWD_PIPE=1)
+bool fwd_pipe() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCA_ATTN_FWD_PIPE");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
 // keys per LDS tile of the forward kernel (DCA_ATTN_FWD_KT=128: half the barriers per MFMA)
 int fwd_kt() {
   static const int kt = [] {
@@ -652,10 +733,19 @@ void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
   auto go = [&](auto ktag) {
     constexpr int KT = decltype(ktag)::value;
     const size_t lds = fwd_lds(D, KT);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_fwd_kernel<D, C, KT>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    hipLaunchKernelGGL((attn_fwd_kernel<D, C, KT>), grid, dim3(256), lds, st, q, k, v, o, lse, Sq,
-                       Sk, H, qs, ks, vs, os, scale_log2, xcd_remap());
+    auto launch = [&](auto kern) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
+                         scale_log2, xcd_remap());
+    };
+    if constexpr (D == 64) {  // D = 128 with two live score tiles spills
+      if (fwd_pipe()) {
+        launch(attn_fwd_kernel<D, C, KT, true>);
+        return;
+      }
+    }
+    launch(attn_fwd_kernel<D, C, KT, false>);
   };
   if constexpr (D == 64) {  // D = 128 at KT = 128 exceeds the register file (spills)
     if (fwd_kt() == 128) {
