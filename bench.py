@@ -150,6 +150,17 @@ def main() -> None:
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if torch.cuda.is_available():
+        # A process that just ended on this GPU may still be returning its ~200 GB of HBM: starting
+        # the bs-1024 step in the remainder makes the caching allocator free and re-map blocks every
+        # step (alloc retries). Wait (bounded) for the device's memory to come back first.
+        free0, total = torch.cuda.mem_get_info()
+        t_wait = time.time()
+        while free0 < 0.8 * total and time.time() - t_wait < 60:
+            time.sleep(2)
+            free0, total = torch.cuda.mem_get_info()
+        print(json.dumps({"device_free_gb_at_start": round(free0 / 2**30, 1),
+                          "device_total_gb": round(total / 2**30, 1),
+                          "waited_s": round(time.time() - t_wait, 1)}), file=sys.stderr, flush=True)
         # MIOpen immediate mode (benchmark=False) picks each conv's solver from the shipped find /
         # perf DB (tools/miopen) without timing candidates: same kernels and step time as
         # per-process miopenFind, but a 12 s instead of a 4 min process at bs 1024
