@@ -284,8 +284,9 @@ def _bgrad(dy: torch.Tensor, bias: torch.Tensor) -> Optional[torch.Tensor]:
 # by space-to-depth -- pad the image by 3, fold each 2x2 pixel block into 12 channels, pad the
 # kernel to 8x8 and fold it the same way -- it is exactly a 4x4 / stride-1 convolution on a
 # 115x115x12 image: 1119 us forward + 934 us weight gradient instead of 1716 + 1381
-# (profiles/round3_stem_conv_variants_find.txt). Opt-in (DCA_STEM_S2D=1) until measured end to end.
-STEM_S2D = os.environ.get("DCA_STEM_S2D", "0") == "1"
+# (profiles/round3_stem_conv_variants_find.txt); +0.5% end to end with its find-DB entries shipped
+# (profiles/round3_stem_s2d_ab.txt). DCA_STEM_S2D=0 runs the plain 7x7 convolution.
+STEM_S2D = os.environ.get("DCA_STEM_S2D", "1") != "0"
 
 
 def _s2d_input(x: torch.Tensor) -> torch.Tensor:

@@ -695,11 +695,12 @@ bool xcd_remap() {
   return on;
 }
 
-// forward: issue a sub-tile pair's score MFMAs before its softmaxes (DCA_ATTN_FWD_PIPE=1)
+// forward (D = 64): issue a sub-tile pair's score MFMAs before its softmaxes -- 377/477 ->
+// 395/523 TFLOP/s at S = 1024/2048 (profiles/round3_attention_ab.txt); DCA_ATTN_FWD_PIPE=0 off
 bool fwd_pipe() {
   static const bool on = [] {
     const char* e = std::getenv("DCA_ATTN_FWD_PIPE");
-    return e && std::atoi(e) == 1;
+    return !(e && std::atoi(e) == 0);
   }();
   return on;
 }

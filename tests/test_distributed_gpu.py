@@ -203,8 +203,20 @@ def test_gpt_zero2_two_ranks_matches_reference():
         mp.spawn(_gpt_worker, args=(world, _free_port(), d), nprocs=world, join=True)
         outs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
     before, ref = _gpt_reference()
-    ref_delta = {n: ref[n] - before[n] for n in ref}
+
+    def delta(p):
+        out = {n: p[n] - before[n] for n in p}
+        for n in out:
+            # the key bias's gradient is exactly zero (softmax is invariant to adding q.b_k to a
+            # whole row of scores): its AdamW "update" g / (|g| + eps) is rounding noise of the
+            # attention kernels, not a property of the gradient reduction under test
+            if n.endswith("attn.qkv.bias"):
+                e = out[n].numel() // 3
+                out[n] = torch.cat([out[n][:e], out[n][2 * e:]])
+        return out
+
+    ref_delta = delta(ref)
     for r, o in enumerate(outs):
-        _close({n: o[n] - before[n] for n in o}, ref_delta, f"rank{r} update", rtol=5e-2)
+        _close(delta(o), ref_delta, f"rank{r} update", rtol=5e-2)
     for n in outs[0]:
         torch.testing.assert_close(outs[0][n], outs[1][n], atol=0, rtol=0)
