@@ -36,24 +36,10 @@ def load_trial_class(spec: str):
     return obj
 
 
-def _since_start() -> float:
-    """Seconds since the agent spawned this task process (``DET_SPAWN_TIME``, set at the zygote
-    fork / before Popen), else since the process's creation; for DET_STARTUP_TRACE=1."""
-    import time
-
-    if os.environ.get("DET_SPAWN_TIME"):
-        return time.time() - float(os.environ["DET_SPAWN_TIME"])
-    try:
-        import psutil
-
-        return time.time() - psutil.Process().create_time()
-    except Exception:  # pragma: no cover - psutil missing
-        return float("nan")
-
-
 def _trace(what: str) -> None:
-    if os.environ.get("DET_STARTUP_TRACE") == "1":
-        logging.getLogger("determined_clone_amd.startup").info(f"{what} at +{_since_start():.3f}s")
+    from determined_clone_amd.util import startup_mark
+
+    startup_mark(what)
 
 
 def main(spec: str) -> int:

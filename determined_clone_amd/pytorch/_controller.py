@@ -443,6 +443,7 @@ class _PyTorchTrialController:
         if self.context._scaler is not None and self.context.experimental._auto_amp \
                 and self.context._should_communicate_and_update():
             self.context._scaler.update()
+        util.startup_mark("first train batch")
         if isinstance(out, torch.Tensor):
             out = {"loss": out}
         if not isinstance(out, dict):
@@ -481,6 +482,7 @@ class _PyTorchTrialController:
         for cb in self.callbacks.values():
             cb.on_validation_start()
         metrics = self._compute_validation_metrics()
+        util.startup_mark("first validation")
         metrics.update(self.context.reduce_metrics(for_training=False))
         metrics = {k: util.to_python(v) for k, v in metrics.items()}
         if self.context.distributed.size > 1:
@@ -580,6 +582,7 @@ class _PyTorchTrialController:
                     self._save(path)
                     uuid = storage_id
             uuid = self.context.distributed.broadcast(uuid)
+            util.startup_mark("first checkpoint")
             for cb in self.callbacks.values():
                 cb.on_checkpoint_upload_end(uuid=uuid)
         except errors.InvalidHP:

@@ -175,3 +175,34 @@ def proxy_secret_ok(headers: Any) -> bool:
         return True
     return hmac.compare_digest(str(headers.get(PROXY_SECRET_HEADER) or ""), secret)
 
+
+
+_marked = set()
+
+
+def startup_mark(what: str, once: bool = True) -> None:
+    """With ``DET_STARTUP_TRACE=1``: log ``what`` with the seconds since the agent spawned this task
+    process (``DET_SPAWN_TIME``; else since process creation). The task's start-up timeline
+    (``tools/bench_asha.py --trace`` averages the marks over a search's trials). GPU work queued
+    so far is synchronised first, so a mark includes the device time of what precedes it."""
+    if os.environ.get("DET_STARTUP_TRACE") != "1" or (once and what in _marked):
+        return
+    _marked.add(what)
+    import logging
+    import time
+
+    import sys as _sys
+
+    torch = _sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+    if os.environ.get("DET_SPAWN_TIME"):
+        since = time.time() - float(os.environ["DET_SPAWN_TIME"])
+    else:
+        try:
+            import psutil
+
+            since = time.time() - psutil.Process().create_time()
+        except Exception:  # pragma: no cover - psutil missing
+            since = float("nan")
+    logging.getLogger("determined_clone_amd.startup").info(f"{what} at +{since:.3f}s")
