@@ -387,14 +387,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
 //    next tile's HBM loads overlap the current tile's MFMAs). S and dP have the key on the lane, so
 //    P and dS are directly the B operands of dV^T += dO^T P and dK^T += Q^T dS (A operands by
 //    transposed LDS reads of the row-major Q / dO tiles).
-template <int D, bool CAUSAL>
+template <int D, bool CAUSAL, int KT>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     const uint16_t* __restrict__ o, const uint16_t* __restrict__ dO, const float* __restrict__ lse,
     float* __restrict__ delta, uint16_t* __restrict__ dq, int Sq, int Sk, int H, Strides qs,
     Strides ks, Strides vs, Strides os, Strides dos, Strides dqs, float scale_log2, float scale,
     bool remap) {
-  constexpr int KT = 64;
+  // KT = keys per LDS tile (one barrier pair per tile), consumed in 32-key MFMA sub-tiles
   constexpr int QB = 128;
   constexpr int RS = D + kPad;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   const int tr_row = (r & 15) >> 2;
   const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
   const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
-  KVPrefetch<D> pf;
+  KVPrefetch<D, KT> pf;
   pf.fetch(kb, ks, vb, vs, 0, Sk);
   for (int kt = 0; kt < k_end; kt += KT) {
     __syncthreads();
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
         }
     };
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
+    for (int sub = 0; sub < KT / 32; ++sub) {
       const int kb0 = kt + 32 * sub;
       if (kb0 >= k_end) break;
       if (CAUSAL && kb0 > q0 + 31) break;
@@ -685,7 +685,16 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
 }
 
 size_t fwd_lds(int D, int KT = 64) { return 2 * static_cast<size_t>(KT) * (D + kPad) * 2; }
-size_t bwd_dq_lds(int D) { return fwd_lds(D); }
+size_t bwd_dq_lds(int D, int KT = 64) { return fwd_lds(D, KT); }
+
+// keys per LDS tile of the dQ kernel (DCA_ATTN_DQ_KT=128: half the barriers per MFMA, D = 64)
+int dq_kt() {
+  static const int kt = [] {
+    const char* e = std::getenv("DCA_ATTN_DQ_KT");
+    return (e && std::atoi(e) == 128) ? 128 : 64;
+  }();
+  return kt;
+}
 
 bool xcd_remap() {
   static const bool on = [] {
@@ -763,12 +772,20 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
                 uint16_t* dv, int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs,
                 Strides os, Strides dos, Strides dqs, Strides dks, Strides dvs, float scale_log2,
                 float scale, hipStream_t st) {
-  const size_t l1 = bwd_dq_lds(D);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(attn_bwd_dq_kernel<D, C>),
-                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l1));
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C>), dim3((Sq + 127) / 128, H, B), dim3(256), l1, st, q,
-                     k, v, o, dO, lse, delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2,
-                     scale, xcd_remap());
+  auto dq_go = [&](auto kern, size_t l1) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l1));
+    hipLaunchKernelGGL(kern, dim3((Sq + 127) / 128, H, B), dim3(256), l1, st, q, k, v, o, dO, lse,
+                       delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2, scale, xcd_remap());
+  };
+  bool dq_done = false;
+  if constexpr (D == 64) {
+    if (dq_kt() == 128) {
+      dq_go(attn_bwd_dq_kernel<D, C, 128>, bwd_dq_lds(D, 128));
+      dq_done = true;
+    }
+  }
+  if (!dq_done) dq_go(attn_bwd_dq_kernel<D, C, 64>, bwd_dq_lds(D, 64));
   if (dkdv_qt() == 64) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H, B), dim3(256),
                        bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,

@@ -186,10 +186,11 @@ def _gpt_reference():
         b = idx[h * 2:(h + 1) * 2]
         _, loss = model(b, b)
         (loss / 2).backward()
+    grads = {n: p.grad.detach().float().cpu().clone() for n, p in model.named_parameters()}
     opt.prepare_grads(max_norm=1.0)
     opt.step()
     torch.cuda.synchronize()
-    return before, _params(model)
+    return before, _params(model), grads
 
 
 def test_gpt_zero2_two_ranks_matches_reference():
@@ -202,18 +203,16 @@ def test_gpt_zero2_two_ranks_matches_reference():
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_gpt_worker, args=(world, _free_port(), d), nprocs=world, join=True)
         outs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
-    before, ref = _gpt_reference()
+    before, ref, ref_grads = _gpt_reference()
+    # AdamW's first step moves each element by ~lr * g / (|g| + eps): where |g| is at the level of
+    # bf16 rounding noise (the key bias's gradient is exactly zero -- softmax ignores a constant
+    # added to a row of scores -- and a few other elements are near it) the "update" is the sign
+    # of that noise, not a property of the gradient reduction under test. Compare the elements
+    # whose reference gradient is above 1% of the parameter's RMS gradient.
+    keep = {n: g.abs() > 1e-2 * g.pow(2).mean().sqrt() for n, g in ref_grads.items()}
 
     def delta(p):
-        out = {n: p[n] - before[n] for n in p}
-        for n in out:
-            # the key bias's gradient is exactly zero (softmax is invariant to adding q.b_k to a
-            # whole row of scores): its AdamW "update" g / (|g| + eps) is rounding noise of the
-            # attention kernels, not a property of the gradient reduction under test
-            if n.endswith("attn.qkv.bias"):
-                e = out[n].numel() // 3
-                out[n] = torch.cat([out[n][:e], out[n][2 * e:]])
-        return out
+        return {n: (p[n] - before[n])[keep[n]] for n in p}
 
     ref_delta = delta(ref)
     for r, o in enumerate(outs):
