@@ -19,9 +19,13 @@ import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
-# Ship MIOpen's find/perf databases with the repo so a fresh box skips convolution tuning.
-os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(HERE, "tools", "miopen", "db"))
-os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(HERE, "tools", "miopen", "cache"))
+# MIOpen's find/perf databases and kernel cache ship in-tree (ops/miopen_db.py): a fresh box
+# neither tunes nor compiles the convolutions. The library GEMMs replay the shipped TunableOp
+# results (ops/gemm_tuning.py: +5% on this step, profiles/round3_resnet50_gemm_tuning_ab.txt).
+_MIOPEN = os.path.join(HERE, "determined_clone_amd", "ops", "tuned", "miopen")
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_MIOPEN, "db"))
+os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_MIOPEN, "cache"))
+os.environ.setdefault("DCA_GEMM_TUNED", "1")
 
 import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
@@ -162,7 +166,7 @@ def main() -> None:
                           "device_total_gb": round(total / 2**30, 1),
                           "waited_s": round(time.time() - t_wait, 1)}), file=sys.stderr, flush=True)
         # MIOpen immediate mode (benchmark=False) picks each conv's solver from the shipped find /
-        # perf DB (tools/miopen) without timing candidates: same kernels and step time as
+        # perf DB (ops/tuned/miopen) without timing candidates: same kernels and step time as
         # per-process miopenFind, but a 12 s instead of a 4 min process at bs 1024
         # (profiles/round2_miopen_immediate_mode_ab.txt); DCA_CONV_BENCHMARK=1 runs the find
         torch.backends.cudnn.benchmark = os.environ.get("DCA_CONV_BENCHMARK", "0") == "1"

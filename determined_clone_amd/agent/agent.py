@@ -139,6 +139,13 @@ class Agent:
         ctx_dir = os.path.join(wd, "context")
         runtime.fetch_context(self.session, spec["task_id"], ctx_dir)
         cmd, env = runtime.build_task(spec, self.master_url, self.id, self.devices, ctx_dir)
+        if "MIOPEN_USER_DB_PATH" not in env:
+            # one writable MIOpen find DB + kernel cache per agent, seeded from the shipped MI355X
+            # files: what one trial compiles or finds, every later trial of the agent reuses
+            from determined_clone_amd.ops import miopen_db
+
+            db, cache = miopen_db.task_dirs(self.workdir)
+            miopen_db.configure(env, db, cache)
         proc = None
         # a task that arrives while the zygote is still importing waits for it: a cold
         # subprocess would pay the same imports (and compete with the zygote for the CPU)

@@ -13,8 +13,11 @@ tuned fall back to the default heuristic.
 The CSV starts with TunableOp's validator lines (PyTorch / ROCm / hipBLASLt / rocBLAS versions, GPU
 arch): on a different software stack TunableOp rejects the file and everything runs untuned.
 
-* ``enable()`` -- replay the shipped results (called once the HIP extension loads on a GPU
-  process); ``DCA_GEMM_TUNED=0`` turns it off.
+* ``enable()`` -- replay the shipped results; called when the HIP extension loads on a GPU
+  process, effective with ``DCA_GEMM_TUNED=1`` (set by the benchmarks and the ResNet-50 / GPT-2
+  example configs). Opt-in because switching TunableOp on costs a process ~0.8 s at its first GEMMs
+  (library / validator loading, tools/probe_trial_startup.py): worth it for a long training job,
+  20% of a short ASHA trial.
 * ``DCA_GEMM_TUNE=<file>`` -- tuning run: every new shape is timed and the results are written to
   ``<file>`` at exit; ``tools/tune_gemms.py`` merges such files into the shipped one.
 
@@ -38,7 +41,7 @@ def enable(path: Optional[str] = None, tune: bool = False) -> bool:
         return True
     if os.environ.get("DCA_GEMM_TUNE"):  # tuning run (tools/tune_gemms.py): write results there
         path, tune = os.environ["DCA_GEMM_TUNE"], True
-    if os.environ.get("DCA_GEMM_TUNED", "1") == "0" and not tune:
+    if os.environ.get("DCA_GEMM_TUNED", "0") != "1" and not tune:
         return False
     import torch
 

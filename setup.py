@@ -12,7 +12,8 @@ setup(
     python_requires=">=3.10",
     packages=find_packages(include=["determined_clone_amd", "determined_clone_amd.*"]),
     package_data={
-        "determined_clone_amd.ops": ["csrc/*", "*.so"],
+        "determined_clone_amd.ops": ["csrc/*", "*.so", "tuned/*.csv", "tuned/miopen/db/*",
+                                     "tuned/miopen/cache/*"],
         "determined_clone_amd.native": ["*.cpp", "*.so", "bin/*"],
         "determined_clone_amd.webui": ["static/*"],
     },

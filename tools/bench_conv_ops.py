@@ -12,8 +12,8 @@ import sys
 
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, HERE)
-os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(HERE, "tools", "miopen", "db"))
-os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(HERE, "tools", "miopen", "cache"))
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(HERE, "determined_clone_amd", "ops", "tuned", "miopen", "db"))
+os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(HERE, "determined_clone_amd", "ops", "tuned", "miopen", "cache"))
 
 import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402

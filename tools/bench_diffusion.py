@@ -11,6 +11,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("DCA_GEMM_TUNED", "1")  # replay the shipped tuned GEMMs (ops/gemm_tuning.py)
 
 import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402

@@ -20,7 +20,16 @@ import torch.nn.functional as F  # noqa: E402
 
 
 def main() -> None:
-    out = {"import_torch_s": round(time.time() - t_start, 3)}
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=32)
+    ap.add_argument("--hidden", type=int, default=512)
+    ap.add_argument("--find", action="store_true",
+                    help="MIOpen find (cudnn.benchmark): record the shapes' best solvers in the DB")
+    a = ap.parse_args()
+    torch.backends.cudnn.benchmark = a.find
+    out = {"import_torch_s": round(time.time() - t_start, 3), "width": a.width, "find": a.find}
 
     def mark(name: str, t0: float) -> float:
         torch.cuda.synchronize()
@@ -36,13 +45,13 @@ def main() -> None:
 
     _ext.load()
     t = mark("ext_load_s", t)
-    hp = {"learning_rate": 0.05, "momentum": 0.9, "weight_decay": 5e-4, "n_filters1": 32,
-          "n_filters2": 64, "dropout1": 0.25, "dropout2": 0.5, "global_batch_size": 128}
+    hp = {"width": a.width, "hidden": a.hidden, "dropout": 0.25, "dropout2": 0.5}
     model = cifar.CifarCNN(hp).cuda().to(memory_format=torch.channels_last)
     opt = torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.9)
     x = torch.randn(128, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (128,), device="cuda")
     t = mark("model_build_s", t)
+    # training and evaluation (validation runs the forward at the evaluation batch too)
     for i in range(2):
         with torch.autocast("cuda", dtype=torch.bfloat16):
             logits = model(x)
@@ -53,6 +62,10 @@ def main() -> None:
         opt.step()
         opt.zero_grad()
         t = mark(f"opt{i}_s", t)
+    model.eval()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        model(x)
+    t = mark("eval_fwd_s", t)
     out["total_s"] = round(time.time() - t_start, 3)
     out["env"] = {k: os.environ.get(k) for k in ("MIOPEN_CUSTOM_CACHE_DIR", "MIOPEN_USER_DB_PATH",
                                                    "DCA_GEMM_TUNED")}
