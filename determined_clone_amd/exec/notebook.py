@@ -150,6 +150,7 @@ class NotebookServer:
 
         class H(BaseHTTPRequestHandler):
             protocol_version = "HTTP/1.1"
+            disable_nagle_algorithm = True  # headers + body writes: no delayed-ACK stall
 
             def log_message(self, *a: Any) -> None:
                 pass

@@ -88,6 +88,7 @@ def make_server(session: ShellSession, cwd: str, host: Optional[str] = None, por
     (``util.proxy_secret_ok``), which only the master's owner-checked ``/proxy/`` route attaches."""
     class H(BaseHTTPRequestHandler):
         protocol_version = "HTTP/1.1"
+        disable_nagle_algorithm = True  # headers + body writes: no delayed-ACK stall
         last = [time.time()]
 
         def log_message(self, *a: Any) -> None:

@@ -1306,6 +1306,9 @@ def delete_webhook(r: Req) -> Any:
 class _Handler(BaseHTTPRequestHandler):
     master: Master = None  # type: ignore[assignment]
     protocol_version = "HTTP/1.1"
+    # headers and body leave in separate writes on a kept-alive connection: with Nagle on, the
+    # body waits for the client's delayed ACK of the headers (~40 ms per request on Linux)
+    disable_nagle_algorithm = True
 
     def log_message(self, fmt: str, *args: Any) -> None:  # quiet
         logger.debug(fmt % args)

@@ -21,6 +21,7 @@ lr_schedulers_state_dict, callbacks, rng_state, scaler_state_dict), ``load_data.
 import contextlib
 import json
 import logging
+import os
 import pathlib
 import random
 import sys
@@ -562,6 +563,22 @@ class _PyTorchTrialController:
 
     # ------------------------------------------------------------------ checkpoint
     def _checkpoint(self, already_exiting: bool) -> None:
+        if os.environ.get("DET_STARTUP_PROFILE") == "checkpoint" and not getattr(self, "_ckpt_profiled", False):
+            # start-up investigation: cProfile of the first checkpoint, into the task log
+            import cProfile
+            import io
+            import pstats
+
+            self._ckpt_profiled = True
+            prof = cProfile.Profile()
+            prof.enable()
+            try:
+                return self._checkpoint(already_exiting)
+            finally:
+                prof.disable()
+                buf = io.StringIO()
+                pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(30)
+                logging.getLogger("determined_clone_amd.startup").info(buf.getvalue())
         if self.is_chief:
             self.core_context.train.set_status("checkpointing")
         self.state.last_ckpt = self.state.batches_trained
