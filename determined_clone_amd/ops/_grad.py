@@ -103,3 +103,34 @@ def comm_stream() -> Optional["torch.cuda.Stream"]:
     s = next(iter(_pending))
     fork(s)
     return s
+
+
+# ----------------------------------------------------------------------------- step stream
+# The training step's critical path (forward, data gradients, optimizer) runs on the current
+# stream while the weight gradients queue on the side stream: when both have work ready the
+# hardware dispatches their workgroups in queue-priority order. With DCA_STEP_STREAM_PRIORITY=high
+# the controllers run the step on a high-priority stream, so side-stream work fills the CUs the
+# critical path leaves idle instead of delaying it.
+import contextlib  # noqa: E402
+
+STEP_PRIORITY = os.environ.get("DCA_STEP_STREAM_PRIORITY", "normal")
+
+
+@contextlib.contextmanager
+def step_stream(device: Optional[torch.device] = None):
+    """Run the enclosed training loop on a high-priority stream (``DCA_STEP_STREAM_PRIORITY=high``
+    on a GPU), ordered after the work queued so far and joined back at the end."""
+    if STEP_PRIORITY != "high" or not torch.cuda.is_available() or \
+            (device is not None and device.type != "cuda"):
+        yield None
+        return
+    _, greatest = torch.cuda.Stream.priority_range()
+    prev = torch.cuda.current_stream()
+    s = torch.cuda.Stream(priority=greatest)
+    s.wait_stream(prev)
+    with torch.cuda.stream(s):
+        try:
+            yield s
+        finally:
+            join()
+    prev.wait_stream(s)
