@@ -45,11 +45,19 @@ def _trace(what: str) -> None:
 def main(spec: str) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     _trace("harness main")
+    prof = None
+    if os.environ.get("DET_STARTUP_PROFILE") == "1":
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     from determined_clone_amd import pytorch
 
     info = _info.get_cluster_info()
     cfg = info.trial._config
+    _trace("framework imported")
     trial_cls = load_trial_class(spec)
+    _trace("trial class loaded")
     if getattr(trial_cls, "_is_deepspeed_trial", False):
         from determined_clone_amd.pytorch import deepspeed as ds
 
@@ -57,12 +65,6 @@ def main(spec: str) -> int:
     gbs = info.trial.hparams.get("global_batch_size")
     rpe = int(cfg.get("records_per_epoch") or 0)
     opts = cfg.get("optimizations") or {}
-    prof = None
-    if os.environ.get("DET_STARTUP_PROFILE") == "1":
-        import cProfile
-
-        prof = cProfile.Profile()
-        prof.enable()
     with pytorch.init(aggregation_frequency=int(opts.get("aggregation_frequency", 1))) as ctx:
         _trace("pytorch.init")
         if prof is not None:
