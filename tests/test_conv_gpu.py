@@ -202,7 +202,9 @@ def test_side_stream_weight_gradients_match_inline(monkeypatch, model_fn):
     x = torch.randn(16, 3, 64, 64, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (16,), device=dev)
     grads = []
-    for side in (False, True):
+    # warm-up pass first: the convolution choosers (ops/conv.py _choose) time their candidates on
+    # first use; the compared passes then run the same kernels. Inline twice gives the noise floor.
+    for side in (False, False, False, True):
         monkeypatch.setattr(_grad, "SIDE_STREAM", side)
         opt.zero_grad()
         loss = F.cross_entropy(model(x).float(), y)
@@ -211,11 +213,13 @@ def test_side_stream_weight_gradients_match_inline(monkeypatch, model_fn):
             assert _grad.pending()
         _grad.join()
         torch.cuda.synchronize()
-        grads.append([p.grad.clone() for p in model.parameters()])
-    for a, b in zip(*grads):
-        # MIOpen's split-K weight-gradient solvers reduce with atomics: compare in norm
-        a, b = a.float(), b.float()
-        assert (a - b).norm() <= 2e-2 * a.norm() + 1e-6
+        grads.append([p.grad.float().clone() for p in model.parameters()])
+    names = [n for n, _ in model.named_parameters()]
+    for name, a, a2, b in zip(names, grads[1], grads[2], grads[3]):
+        # MIOpen's split-K weight-gradient solvers reduce with atomics: compare in norm, above the
+        # inline-vs-inline noise (bias gradients are sums with heavy cancellation)
+        err, floor = (a - b).norm().item(), (a - a2).norm().item()
+        assert err <= 2e-2 * a.norm().item() + 4 * floor + 1e-6, (name, err, floor, a.norm().item())
     # the optimizer step joins by itself when the caller did not
     monkeypatch.setattr(_grad, "SIDE_STREAM", True)
     opt.zero_grad()
