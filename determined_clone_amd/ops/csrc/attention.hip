@@ -15,6 +15,7 @@
 //   the workgroup sweeps the query tiles; recomputed P^T = exp2(S^T - LSE), dP^T = V dO^T,
 //   dS^T = P^T (dP^T - rowsum(dO*O)); dQ partials are added into an fp32 buffer with float atomics.
 #include <cstdlib>
+#include <string>
 #include <type_traits>
 
 #include "common.h"
@@ -87,6 +88,22 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int base) {
 // v_exp_f32 directly (inputs are finite or -inf; no denormal range fix-up needed)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// max / sum of a value with the same value in lane i^32 (the other half-wave): one
+// v_permlane32_swap (a VALU lane exchange) instead of a ds_bpermute round trip through the LDS
+// unit and its lgkmcnt wait (guide T12). The swap leaves lanes 0-31 with (own, partner) and lanes
+// 32-63 with (partner, own): either order gives the same max / sum. fmax via asm: fmaxf would add
+// two canonicalising v_max on the swap results.
+__device__ __forceinline__ float half_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  float o;
+  asm("v_max_f32 %0, %1, %2" : "=v"(o) : "v"(__uint_as_float(r[0])), "v"(__uint_as_float(r[1])));
+  return o;
+}
+__device__ __forceinline__ float half_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 struct Strides {
   int64_t b, h, s;  // element strides; d stride is 1
 };
@@ -96,14 +113,28 @@ struct Strides {
 // the same K/V (or Q/dO) tiles -- would be spread over 8 L2s and every tile fetched 8 times from
 // HBM / MALL. With remap, each XCD gets a contiguous range of grid positions (the bijective form,
 // valid for any grid size): the blocks of a (batch, head) share one L2. DCA_ATTN_XCD_REMAP=0 off.
+//
+// order 2 (heaviest first, causal): additionally, each XCD walks its (batch, head) pairs
+// x-slowest -- every pair's x = 0 block (the largest causal extent: the last query block of the
+// forward / dQ pass, the first key block of the dK/dV pass) before any pair's x = 1 -- so the
+// light blocks fill the tail of the launch instead of heavy ones (longest-processing-time-first).
+// A pair's blocks then no longer run together; the K/V (Q/dO) re-reads come from the Infinity
+// Cache. Needs (batch * heads) % 8 == 0, else order 1.
 struct Blk {
   int x, y, z;
 };
-__device__ __forceinline__ Blk xcd_block(bool remap) {
-  if (!remap) return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y), static_cast<int>(blockIdx.z)};
+__device__ __forceinline__ Blk xcd_block(int order) {
+  if (order == 0) return {static_cast<int>(blockIdx.x), static_cast<int>(blockIdx.y), static_cast<int>(blockIdx.z)};
   const int nx = gridDim.x, ny = gridDim.y;
   const int n = nx * ny * gridDim.z;
   const int l = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const int nbh = ny * static_cast<int>(gridDim.z);
+  if (order == 2 && nbh % 8 == 0) {
+    const int per = nbh / 8;          // (batch, head) pairs per XCD
+    const int p = l / 8;              // dispatch position within this XCD's stream
+    const int bh = (l % 8) * per + p % per;
+    return {p / per, bh % ny, bh / ny};
+  }
   const int xcd = l % 8, q = n / 8, r = n % 8;
   const int v = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + l / 8;
   return {v % nx, (v / nx) % ny, v / (nx * ny)};
@@ -189,7 +220,7 @@ template <int D, bool CAUSAL, int KT, bool PIPE>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
-    Strides ks, Strides vs, Strides os, float scale_log2, bool remap) {
+    Strides ks, Strides vs, Strides os, float scale_log2, int order) {
   // KT = keys per LDS tile (one barrier pair per tile), consumed in 32-key MFMA sub-tiles
   constexpr int QB = 128;      // queries per workgroup
   constexpr int RS = D + kPad; // LDS row stride (elements)
@@ -200,7 +231,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   // wave index in an SGPR: the causal extent checks below are uniform branches
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hf = lane >> 5;
-  const Blk blk = xcd_block(remap);
+  const Blk blk = xcd_block(order);
   const int b = blk.z, h = blk.y;
   // heaviest (largest causal extent) query blocks first
   const int q_blk = (CAUSAL ? (gridDim.x - 1 - blk.x) : blk.x) * QB;
@@ -230,14 +261,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     __syncthreads();
     if (kt + KT < k_end) pf.fetch(kb, ks, vb, vs, kt + KT, Sk);
     if constexpr (PIPE) {
-      // S^T = K Q^T for the 32-key sub-tile `sub` of the staged tile
-      auto scores = [&](const int sub) {
-        f32x16 sc = zero16();
-  #pragma unroll
-        for (int s = 0; s < D / 16; ++s)
-          sc = mfma32(load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf), qf[s], sc);
-        return sc;
-      };
       // online softmax of one sub-tile's scores and O^T += V^T P^T
       auto softmax_pv = [&](f32x16 sc, const int sub, const int kb0, const bool need_mask) {
         // sc[i]: key = kb0 + (i&3) + 8(i>>2) + 4hf, query = my_q
@@ -252,7 +275,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
           }
           mx = fmaxf(mx, sc[i]);
         }
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx = half_max(mx);
         // deferred max (T13): the running max m moves only when a score exceeds it by more than
         // kRescaleLog2 (p <= 2^kRescaleLog2 meanwhile: exact in the fp32 accumulators, 8 bits of
         // headroom in the bf16 P), so the D/2-multiply rescale of O and l runs on a few sub-tiles
@@ -270,7 +293,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
           sc[i] = p;
           rs += p;
         }
-        rs += __shfl_xor(rs, 32, 64);
+        rs = half_sum(rs);
         l = l * alpha + rs;
         m = mnew;
         if (__any(upd)) {
@@ -293,8 +316,23 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         // second one's MFMAs run in the matrix pipe under the first softmax's VALU work
 #pragma unroll
         for (int sub = 0; sub < KT / 32; sub += 2) {
-          const f32x16 sa = scores(sub);
-          const f32x16 sb = scores(sub + 1);
+          // both sub-tiles' K fragments read up front, their two independent MFMA chains
+          // interleaved (back-to-back MFMAs without waiting on each other's results)
+          bf16x8 ka[D / 16], kb2[D / 16];
+  #pragma unroll
+          for (int s = 0; s < D / 16; ++s) {
+            ka[s] = load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf);
+            kb2[s] = load8(Ks + (32 * sub + 32 + r) * RS + 16 * s + 8 * hf);
+          }
+          f32x16 sa = zero16(), sb = zero16();
+  #pragma unroll
+          for (int s = 0; s < D / 16; ++s) {
+            sa = mfma32(ka[s], qf[s], sa);
+            sb = mfma32(kb2[s], qf[s], sb);
+          }
+          // schedule: every fragment read issued before the first MFMA (one LDS wait)
+          __builtin_amdgcn_sched_group_barrier(0x100, D / 8, 0);
+          __builtin_amdgcn_sched_group_barrier(0x8, D / 8, 0);
           softmax_pv(sa, sub, kt + 32 * sub, false);
           softmax_pv(sb, sub + 1, kt + 32 * sub + 32, false);
         }
@@ -323,7 +361,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         }
         mx = fmaxf(mx, sc[i]);
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = half_max(mx);
       // deferred max (T13): the running max m moves only when a score exceeds it by more than
       // kRescaleLog2 (p <= 2^kRescaleLog2 meanwhile: exact in the fp32 accumulators, 8 bits of
       // headroom in the bf16 P), so the D/2-multiply rescale of O and l runs on a few sub-tiles
@@ -341,7 +379,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         sc[i] = p;
         rs += p;
       }
-      rs += __shfl_xor(rs, 32, 64);
+      rs = half_sum(rs);
       l = l * alpha + rs;
       m = mnew;
       if (__any(upd)) {
@@ -393,7 +431,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const uint16_t* __restrict__ o, const uint16_t* __restrict__ dO, const float* __restrict__ lse,
     float* __restrict__ delta, uint16_t* __restrict__ dq, int Sq, int Sk, int H, Strides qs,
     Strides ks, Strides vs, Strides os, Strides dos, Strides dqs, float scale_log2, float scale,
-    bool remap) {
+    int order) {
   // KT = keys per LDS tile (one barrier pair per tile), consumed in 32-key MFMA sub-tiles
   constexpr int QB = 128;
   constexpr int RS = D + kPad;
@@ -405,7 +443,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   // uniform branch instead of per-lane exec masking
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hf = lane >> 5;
-  const Blk blk = xcd_block(remap);
+  const Blk blk = xcd_block(order);
   const int b = blk.z, h = blk.y;
   const int q_blk = (CAUSAL ? (gridDim.x - 1 - blk.x) : blk.x) * QB;
   const int q0 = q_blk + w * 32;
@@ -428,7 +466,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
       for (int j = 0; j < 8; ++j) dsum += static_cast<float>(of[j]) * static_cast<float>(dof[s][j]);
     }
   }
-  dsum += __shfl_xor(dsum, 32, 64);
+  dsum = half_sum(dsum);
   if (q_ok && hf == 0) delta[bh * Sq + my_q] = dsum;
   const float lq = q_ok ? lse[bh * Sq + my_q] : INFINITY;
   f32x16 dqacc[D / 32];
@@ -517,7 +555,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     const uint16_t* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
     uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int Sq, int Sk, int H, Strides qs,
     Strides ks, Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale,
-    bool remap) {
+    int order) {
   constexpr int KB = 128;
   static_assert(QT == 32 || QT == 64, "query tile");
   constexpr int RS = D + kPad;
@@ -533,7 +571,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   // uniform branch instead of per-lane exec masking
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hf = lane >> 5;
-  const Blk blk = xcd_block(remap);
+  const Blk blk = xcd_block(order);
   const int b = blk.z, h = blk.y;
   const int k_blk = blk.x * KB;
   const int kw0 = k_blk + 32 * w;
@@ -696,12 +734,17 @@ int dq_kt() {
   return kt;
 }
 
-bool xcd_remap() {
-  static const bool on = [] {
+// workgroup order (see xcd_block): causal launches heaviest-first (2) -- fwd +12-38%, bwd
+// +10-23% over XCD remap alone at S 1024-4096 (profiles/round3_attention_lpt_order.txt);
+// DCA_ATTN_ORDER=xcd -> 1; DCA_ATTN_XCD_REMAP=0 -> 0 (hardware order)
+int attn_order(bool causal) {
+  static const int base = [] {
     const char* e = std::getenv("DCA_ATTN_XCD_REMAP");
-    return !(e && std::atoi(e) == 0);
+    if (e && std::atoi(e) == 0) return 0;
+    const char* o = std::getenv("DCA_ATTN_ORDER");
+    return (o && std::string(o) == "xcd") ? 1 : 2;
   }();
-  return on;
+  return (base == 2 && !causal) ? 1 : base;
 }
 
 // forward (D = 64): issue a sub-tile pair's score MFMAs before its softmaxes -- 377/477 ->
@@ -747,7 +790,7 @@ void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
       hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
-                         scale_log2, xcd_remap());
+                         scale_log2, attn_order(C));
     };
     if constexpr (D == 64) {  // D = 128 with two live score tiles spills
       if (fwd_pipe()) {
@@ -776,7 +819,7 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l1));
     hipLaunchKernelGGL(kern, dim3((Sq + 127) / 128, H, B), dim3(256), l1, st, q, k, v, o, dO, lse,
-                       delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2, scale, xcd_remap());
+                       delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2, scale, attn_order(C));
   };
   bool dq_done = false;
   if constexpr (D == 64) {
@@ -789,11 +832,11 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
   if (dkdv_qt() == 64) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H, B), dim3(256),
                        bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
-                       vs, dos, dks, dvs, scale_log2, scale, xcd_remap());
+                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C));
   } else {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 32>), dim3((Sk + 127) / 128, H, B), dim3(256),
                        bwd_dkdv_lds(D, 32), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
-                       vs, dos, dks, dvs, scale_log2, scale, xcd_remap());
+                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C));
   }
 }
 

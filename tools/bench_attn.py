@@ -30,21 +30,26 @@ def main():
     p.add_argument("--iters", type=int, default=30)
     p.add_argument("--only", default="")
     p.add_argument("--gpt2", action="store_true", help="only the GPT-2-medium shape (16x1024x16x64)")
+    p.add_argument("--shapes", default="", help="B,S,H,D[;B,S,H,D...] instead of the defaults")
+    p.add_argument("--noncausal", action="store_true")
     a = p.parse_args()
     shapes = ((16, 1024, 16, 64), (8, 2048, 16, 64), (4, 4096, 8, 128))
+    if a.shapes:
+        shapes = tuple(tuple(int(v) for v in t.split(",")) for t in a.shapes.split(";"))
+    causal = not a.noncausal
     for B, S, H, D in shapes[:1] if a.gpt2 else shapes:
         q, k, v = (torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
                    for _ in range(3))
         g = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
-        flops = 4 * B * H * S * S * D / 2
+        flops = 4 * B * H * S * S * D / (2 if causal else 1)
         if a.only in ("", "fwd"):
-            ms = timeit(lambda: T.flash_attention(q, k, v, causal=True), a.iters)
-            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "pass": "fwd", "ms": round(ms, 4),
+            ms = timeit(lambda: T.flash_attention(q, k, v, causal=causal), a.iters)
+            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "causal": causal, "pass": "fwd", "ms": round(ms, 4),
                               "tflops": round(flops / ms / 1e9, 1)}), flush=True)
         if a.only in ("", "bwd"):
-            o = T.flash_attention(q, k, v, causal=True)
+            o = T.flash_attention(q, k, v, causal=causal)
             ms = timeit(lambda: torch.autograd.grad(o, (q, k, v), g, retain_graph=True), a.iters)
-            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "pass": "bwd", "ms": round(ms, 4),
+            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "causal": causal, "pass": "bwd", "ms": round(ms, 4),
                               "tflops": round(2.5 * flops / ms / 1e9, 1)}), flush=True)
 
 
