@@ -5,7 +5,10 @@ the op raises (no silent eager fallback). CPU tensors use the PyTorch reference 
 that the GPU numerics tests compare against.
 """
 import importlib
+import importlib.machinery
+import importlib.util
 import os
+import sys
 from typing import Any, Optional
 
 _C: Optional[Any] = None
@@ -18,8 +21,16 @@ def load() -> Any:
         return _C
     import torch  # noqa: F401  (loads libc10_hip / libamdhip64 before the extension)
 
+    alt = os.environ.get("DCA_OPS_SO")
+    if alt:  # A/B builds: load this file as the extension (e.g. a variant built with other flags)
+        loader = importlib.machinery.ExtensionFileLoader("determined_clone_amd.ops._C", alt)
+        spec = importlib.util.spec_from_file_location("determined_clone_amd.ops._C", alt, loader=loader)
+        _C = importlib.util.module_from_spec(spec)
+        loader.exec_module(_C)
+        sys.modules["determined_clone_amd.ops._C"] = _C
     try:
-        _C = importlib.import_module("determined_clone_amd.ops._C")
+        if _C is None:
+            _C = importlib.import_module("determined_clone_amd.ops._C")
     except ImportError as e:  # pragma: no cover - exercised only when the build is missing
         _err = e
         if os.environ.get("DCA_AUTOBUILD", "1") == "1":

@@ -41,6 +41,12 @@ def _common_flags(abi: int) -> List[str]:
             "-D__HIP_PLATFORM_AMD__=1", "-Wno-unused-result", "-Wno-deprecated-declarations"]
 
 
+# per-source extra flags. attention.hip: no SLP vectorizer -- it packs the softmax-gradient
+# subtract/multiply pairs into v_pk_add_f32 / v_pk_mul_f32, which cost ~24 extra cycles each beside
+# MFMAs on gfx950 (cdna guide: packed f32 VALU is an anti-lever in MFMA loops)
+_FILE_FLAGS = {"attention": [] if os.environ.get("DCA_BUILD_SLP") else ["-fno-slp-vectorize"]}
+
+
 def _newer(src: pathlib.Path, obj: pathlib.Path, headers: List[pathlib.Path]) -> bool:
     if not obj.exists():
         return True
@@ -64,7 +70,8 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> pathlib.
         objs.append(obj)
         if force or _newer(src, obj, headers):
             cmds.append([_hipcc(), "-c", str(src), "-o", str(obj), f"--offload-arch={ARCH}",
-                         "-munsafe-fp-atomics", f"-I{CSRC}"] + _common_flags(abi))
+                         "-munsafe-fp-atomics", f"-I{CSRC}"] + _common_flags(abi)
+                        + _FILE_FLAGS.get(src.stem, []))
     py_inc = sysconfig.get_paths()["include"]
     for src in sorted(CSRC.glob("*.cpp")):
         obj = BUILD / (src.stem + ".cpp.o")
