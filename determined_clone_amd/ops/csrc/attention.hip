@@ -425,7 +425,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
 //    next tile's HBM loads overlap the current tile's MFMAs). S and dP have the key on the lane, so
 //    P and dS are directly the B operands of dV^T += dO^T P and dK^T += Q^T dS (A operands by
 //    transposed LDS reads of the row-major Q / dO tiles).
-template <int D, bool CAUSAL, int KT>
+template <int D, bool CAUSAL, int KT, bool PIPE>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     const uint16_t* __restrict__ o, const uint16_t* __restrict__ dO, const float* __restrict__ lse,
@@ -482,8 +482,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     pf.store(Ks, Vs);
     __syncthreads();
     if (kt + KT < k_end) pf.fetch(kb, ks, vb, vs, kt + KT, Sk);
-    auto sub_tile = [&](auto masked, const int sub, const int kb0) {
-      f32x16 sc = zero16(), dp = zero16();
+    // S^T = K Q^T and dP^T = V dO^T for the 32-key sub-tile `sub` of the staged tile
+    auto sdp = [&](const int sub, f32x16& sc, f32x16& dp) {
+      sc = zero16();
+      dp = zero16();
       if constexpr (D == 64) {  // fragments preloaded (see the forward)
         bf16x8 kfr[D / 16], vfr[D / 16];
 #pragma unroll
@@ -503,6 +505,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
           dp = mfma32(load8(Vs + (32 * sub + r) * RS + 16 * s + 8 * hf), dof[s], dp);
         }
       }
+    };
+    // dS^T = P^T (dP^T - delta) and dQ^T += K^T dS^T
+    auto finish = [&](auto masked, f32x16 sc, f32x16 dp, const int sub, const int kb0) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         float p = fast_exp2(fmaf(sc[i], scale_log2, -lq));
@@ -521,6 +526,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
           dqacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RS)), s2 ? s1 : s0, dqacc[n]);
         }
     };
+    auto sub_tile = [&](auto masked, const int sub, const int kb0) {
+      f32x16 sc, dp;
+      sdp(sub, sc, dp);
+      finish(masked, sc, dp, sub, kb0);
+    };
+    if constexpr (PIPE) {
+      // wave-uniform: every key of the tile exists and precedes every query of this wave. Both
+      // sub-tiles' score / dP products are issued before the first softmax gradient, so the
+      // second pair's MFMAs run in the matrix pipe under the first one's VALU work.
+      if (kt + KT <= Sk && (!CAUSAL || kt + KT - 1 <= q0)) {
+#pragma unroll
+        for (int sub = 0; sub < KT / 32; sub += 2) {
+          f32x16 sa, da, sb, db;
+          sdp(sub, sa, da);
+          sdp(sub + 1, sb, db);
+          finish(std::false_type{}, sa, da, sub, kt + 32 * sub);
+          finish(std::false_type{}, sb, db, sub + 1, kt + 32 * sub + 32);
+        }
+        continue;
+      }
+    }
 #pragma unroll
     for (int sub = 0; sub < KT / 32; ++sub) {
       const int kb0 = kt + 32 * sub;
@@ -596,6 +622,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   // register double buffer for the next query tile
   uint4 pf[NPF];
   float pl = 0.f, pd = 0.f;
+  constexpr bool ROWC = D == 128;
+  const float inv_sl2 = 1.f / scale_log2;
   auto fetch = [&](int qt) {
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {
@@ -612,8 +640,14 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     }
     if (threadIdx.x < QT) {
       const int qi = qt + threadIdx.x;
-      pl = qi < Sq ? lse[bh * Sq + qi] : INFINITY;
-      pd = qi < Sq ? delta[bh * Sq + qi] : 0.f;
+      if constexpr (ROWC) {
+        // staged as the accumulators' initial values (see the tile below): -LSE/scale_log2, -delta
+        pl = qi < Sq ? -lse[bh * Sq + qi] * inv_sl2 : -INFINITY;
+        pd = qi < Sq ? -delta[bh * Sq + qi] : 0.f;
+      } else {
+        pl = qi < Sq ? lse[bh * Sq + qi] : INFINITY;
+        pd = qi < Sq ? delta[bh * Sq + qi] : 0.f;
+      }
     }
   };
   const int tr_row = (r & 15) >> 2;
@@ -640,15 +674,25 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
       const int qs0 = qt + 32 * half;
       const uint16_t* Qh = Qs + 32 * half * RS;
       const uint16_t* dOh = dOs + 32 * half * RS;
-      // this lane's 16 queries are 4 runs of 4 consecutive rows: their LSE / delta come in as
-      // four 16-B LDS reads each instead of sixteen 4-B reads
-      float4 l4[4], d4[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        l4[g] = *reinterpret_cast<const float4*>(lse_s + 32 * half + 8 * g + 4 * hf);
-        d4[g] = *reinterpret_cast<const float4*>(del_s + 32 * half + 8 * g + 4 * hf);
+      // ROWC (D = 128): row constants as the initial accumulators (guide: attention backward):
+      // S' = Q K^T - LSE/scale_log2 and dP' = dO V^T - delta come out of the MFMA chains, so
+      // p = exp2(S' * scale_log2) and dS = p * dP' need no per-element subtraction and no
+      // registers for the constants (D = 128: +6%; D = 64: neutral, so off there --
+      // profiles/round3_attention_bwd_ab.txt). This lane's 16 queries are 4 runs of 4 consecutive
+      // rows: 16-B LDS reads straight into the accumulator registers.
+      auto rows16 = [&](const float* base) {
+        const f32x4* b4 = reinterpret_cast<const f32x4*>(base + 32 * half + 4 * hf);
+        const f32x4 a0 = b4[0], a1 = b4[2], a2 = b4[4], a3 = b4[6];  // rows +0, +8, +16, +24
+        return __builtin_shufflevector(__builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7),
+                                       __builtin_shufflevector(a2, a3, 0, 1, 2, 3, 4, 5, 6, 7),
+                                       0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+      };
+      f32x16 sacc = ROWC ? rows16(lse_s) : zero16(), dpacc = ROWC ? rows16(del_s) : zero16();
+      f32x16 lrow, drow;  // !ROWC: the same constants, subtracted per element below
+      if constexpr (!ROWC) {
+        lrow = rows16(lse_s);
+        drow = rows16(del_s);
       }
-      f32x16 sacc = zero16(), dpacc = zero16();
       if constexpr (D == 64) {  // fragments preloaded (see the forward)
         bf16x8 qfr[D / 16], dofr[D / 16];
 #pragma unroll
@@ -670,15 +714,13 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float lq = reinterpret_cast<const float*>(&l4[i >> 2])[i & 3];
-        const float dl = reinterpret_cast<const float*>(&d4[i >> 2])[i & 3];
-        float p = fast_exp2(fmaf(sacc[i], scale_log2, -lq));
+        float p = ROWC ? fast_exp2(sacc[i] * scale_log2) : fast_exp2(fmaf(sacc[i], scale_log2, -lrow[i]));
         if constexpr (decltype(masked)::value) {
           const int qi = qs0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
           p = (qi >= Sq || my_key >= Sk || (CAUSAL && my_key > qi)) ? 0.f : p;
         }
         sacc[i] = p;
-        dpacc[i] = p * (dpacc[i] - dl);  // scale applied once to dK at the end
+        dpacc[i] = ROWC ? p * dpacc[i] : p * (dpacc[i] - drow[i]);  // scale applied once to dK at the end
       }
       const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8);
       const bf16x8 s0 = pack8(dpacc, 0), s1 = pack8(dpacc, 8);
@@ -757,6 +799,16 @@ bool fwd_pipe() {
   return on;
 }
 
+// dQ kernel (D = 64): issue a sub-tile pair's S / dP products before their softmax gradients
+// (DCA_ATTN_DQ_PIPE=1)
+bool dq_pipe() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCA_ATTN_DQ_PIPE");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
 // keys per LDS tile of the forward kernel (DCA_ATTN_FWD_KT=128: half the barriers per MFMA)
 int fwd_kt() {
   static const int kt = [] {
@@ -824,11 +876,14 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
   bool dq_done = false;
   if constexpr (D == 64) {
     if (dq_kt() == 128) {
-      dq_go(attn_bwd_dq_kernel<D, C, 128>, bwd_dq_lds(D, 128));
+      dq_go(attn_bwd_dq_kernel<D, C, 128, false>, bwd_dq_lds(D, 128));
+      dq_done = true;
+    } else if (dq_pipe()) {
+      dq_go(attn_bwd_dq_kernel<D, C, 64, true>, bwd_dq_lds(D, 64));
       dq_done = true;
     }
   }
-  if (!dq_done) dq_go(attn_bwd_dq_kernel<D, C, 64>, bwd_dq_lds(D, 64));
+  if (!dq_done) dq_go(attn_bwd_dq_kernel<D, C, 64, false>, bwd_dq_lds(D, 64));
   if (dkdv_qt() == 64) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H, B), dim3(256),
                        bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
