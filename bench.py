@@ -154,6 +154,8 @@ def main() -> None:
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if torch.cuda.is_available():
+        # this rank's GPU first: a bare torch.cuda call would open a context on device 0 in every rank
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
         # A process that just ended on this GPU may still be returning its ~200 GB of HBM: starting
         # the bs-1024 step in the remainder makes the caching allocator free and re-map blocks every
         # step (alloc retries). Wait (bounded) for the device's memory to come back first.
