@@ -104,6 +104,28 @@ __device__ __forceinline__ float half_sum(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// Epilogue store of one row-per-lane-pair accumulator set (T21): lane r holds columns 8k..8k+3 and
+// lane r+32 columns 8k+4..8k+7 of group k. One v_permlane32_swap per dword of the group pair
+// (k, k+1) leaves the lower lane with all of group k and the upper lane with all of group k+1, so
+// each lane writes 16 contiguous bytes: half the store instructions of the 8-byte form. Every lane
+// must execute the swaps (all 64 active); `ok` guards only the stores (same for both lanes of a row).
+template <int D>
+__device__ __forceinline__ void store_rows(uint16_t* row, const f32x16 (&acc)[D / 32], float mul,
+                                           int hf, bool ok) {
+#pragma unroll
+  for (int n = 0; n < D / 32; ++n)
+#pragma unroll
+    for (int g = 0; g < 4; g += 2) {
+      uint32_t ax = pack_bf16x2(acc[n][4 * g] * mul, acc[n][4 * g + 1] * mul);
+      uint32_t ay = pack_bf16x2(acc[n][4 * g + 2] * mul, acc[n][4 * g + 3] * mul);
+      uint32_t bx = pack_bf16x2(acc[n][4 * g + 4] * mul, acc[n][4 * g + 5] * mul);
+      uint32_t by = pack_bf16x2(acc[n][4 * g + 6] * mul, acc[n][4 * g + 7] * mul);
+      const auto rx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+      const auto ry = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+      if (ok) *reinterpret_cast<uint4*>(row + 32 * n + 8 * g + 8 * hf) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    }
+}
+
 struct Strides {
   int64_t b, h, s;  // element strides; d stride is 1
 };
@@ -397,6 +419,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       }
     }
   }
+  // 8-byte stores here: the widened form (store_rows) measured -2..-3% on this kernel at S >= 2048
+  // (+1.5% at S 1024), +2.5-4% on the backward kernels (profiles/round3_attention_epilogue_ab.txt)
   if (my_q < Sq) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     uint16_t* orow = o + b * os.b + h * os.h + static_cast<int64_t>(my_q) * os.s;
@@ -559,18 +583,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
         sub_tile(std::false_type{}, sub, kb0);
     }
   }
-  if (q_ok) {
-    uint16_t* row = dq + b * dqs.b + h * dqs.h + static_cast<int64_t>(my_q) * dqs.s;
-#pragma unroll
-    for (int n = 0; n < D / 32; ++n)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint2 pk;
-        pk.x = pack_bf16x2(dqacc[n][4 * g] * scale, dqacc[n][4 * g + 1] * scale);
-        pk.y = pack_bf16x2(dqacc[n][4 * g + 2] * scale, dqacc[n][4 * g + 3] * scale);
-        *reinterpret_cast<uint2*>(row + 32 * n + 8 * g + 4 * hf) = pk;
-      }
-  }
+  store_rows<D>(dq + b * dqs.b + h * dqs.h + static_cast<int64_t>(my_q) * dqs.s, dqacc, scale, hf, q_ok);
 }
 
 // QT = queries staged per LDS tile (one barrier pair per tile); each wave consumes it in 32-query
@@ -746,22 +759,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
         tile(std::false_type{}, half);
     }
   }
-  if (my_key < Sk) {
-    uint16_t* dkrow = dk + b * dks.b + h * dks.h + static_cast<int64_t>(my_key) * dks.s;
-    uint16_t* dvrow = dv + b * dvs.b + h * dvs.h + static_cast<int64_t>(my_key) * dvs.s;
-#pragma unroll
-    for (int n = 0; n < D / 32; ++n)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint2 pk;
-        pk.x = pack_bf16x2(dkacc[n][4 * g] * scale, dkacc[n][4 * g + 1] * scale);
-        pk.y = pack_bf16x2(dkacc[n][4 * g + 2] * scale, dkacc[n][4 * g + 3] * scale);
-        *reinterpret_cast<uint2*>(dkrow + 32 * n + 8 * g + 4 * hf) = pk;
-        pk.x = pack_bf16x2(dvacc[n][4 * g], dvacc[n][4 * g + 1]);
-        pk.y = pack_bf16x2(dvacc[n][4 * g + 2], dvacc[n][4 * g + 3]);
-        *reinterpret_cast<uint2*>(dvrow + 32 * n + 8 * g + 4 * hf) = pk;
-      }
-  }
+  store_rows<D>(dk + b * dks.b + h * dks.h + static_cast<int64_t>(my_key) * dks.s, dkacc, scale, hf, my_key < Sk);
+  store_rows<D>(dv + b * dvs.b + h * dvs.h + static_cast<int64_t>(my_key) * dvs.s, dvacc, 1.f, hf, my_key < Sk);
 }
 
 size_t fwd_lds(int D, int KT = 64) { return 2 * static_cast<size_t>(KT) * (D + kPad) * 2; }

@@ -79,42 +79,6 @@ __device__ __forceinline__ RowRange chunk_rows(int64_t M, int rpi, int bx, int n
   return {b, e};
 }
 
-// Raw 8-element vectors: loads are issued into these (no conversion in between), so the U loads
-// of an unrolled iteration are all in flight before the first use; unpacked afterwards.
-template <typename T> struct Raw8;
-template <> struct Raw8<BF16> { uint4 q; };
-template <> struct Raw8<F16> { uint4 q; };
-template <> struct Raw8<F32> { float4 a, b; };
-
-template <typename T>
-__device__ __forceinline__ Raw8<T> ld8(const void* base, int64_t elem_off) {
-  Raw8<T> r;
-  if constexpr (std::is_same<T, F32>::value) {
-    const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(base) + elem_off);
-    r.a = p[0];
-    r.b = p[1];
-  } else {
-    r.q = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(base) + elem_off);
-  }
-  return r;
-}
-template <typename T>
-__device__ __forceinline__ void unpack8(const Raw8<T>& r, float (&v)[8]) {
-  if constexpr (std::is_same<T, F32>::value) {
-    v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w;
-    v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
-  } else if constexpr (std::is_same<T, BF16>::value) {
-    v[0] = bf16_lo(r.q.x); v[1] = bf16_hi(r.q.x); v[2] = bf16_lo(r.q.y); v[3] = bf16_hi(r.q.y);
-    v[4] = bf16_lo(r.q.z); v[5] = bf16_hi(r.q.z); v[6] = bf16_lo(r.q.w); v[7] = bf16_hi(r.q.w);
-  } else {
-    const uint32_t w[4] = {r.q.x, r.q.y, r.q.z, r.q.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[2 * i] = h2f(w[i] & 0xffffu);
-      v[2 * i + 1] = h2f(w[i] >> 16);
-    }
-  }
-}
 template <typename T>
 __device__ __forceinline__ void st8(void* base, int64_t elem_off, const float (&v)[8]) {
   Vec8<T>::store(reinterpret_cast<char*>(base) + elem_off * Vec8<T>::bytes, v);

@@ -124,20 +124,48 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_kernel(
     const int c = (lane + i * 64) * 8;
     load_affine8(gamma, c, c < D, 1.f, gam[i]);
   }
-  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wid; row < rows;
-       row += static_cast<int64_t>(gridDim.x) * kWaves) {
+  // One row per wave per iteration, with the NEXT row's x / dy / dsum / mean / rstd loads issued
+  // before this row's math and wave reduction: two rows of loads in flight per wave, so the kernel
+  // keeps HBM busy even when a concurrent side-stream GEMM leaves it few waves per CU.
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kWaves;
+  Raw8<T> nx[NV], ng[NV], nr[NV];
+  float nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](int64_t row) {
     const int64_t base = row * D;
-    const float mean = mean_in[row], rstd = rstd_in[row];
+    nmu = mean_in[row];
+    nrs = rstd_in[row];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nvec) {
+        nx[i] = ld8<T>(x, base + vi * 8);
+        ng[i] = ld8<T>(dy, base + vi * 8);
+        if (dsum) nr[i] = ld8<T>(dsum, base + vi * 8);
+      }
+    }
+  };
+  int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wid;
+  if (row < rows) fetch(row);
+  for (; row < rows; row += stride) {
+    const int64_t base = row * D;
+    const float mean = nmu, rstd = nrs;
+    Raw8<T> cx[NV], cg[NV], cr[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      cx[i] = nx[i];
+      cg[i] = ng[i];
+      cr[i] = nr[i];
+    }
+    if (row + stride < rows) fetch(row + stride);
     float xh[NV][8], g[NV][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int vi = lane + i * 64;
       if (vi < nvec) {
-        const int c = vi * 8;
         float xv[8];
-        Vec8<T>::load(reinterpret_cast<const char*>(x) + (base + c) * Vec8<T>::bytes, xv);
-        Vec8<T>::load(reinterpret_cast<const char*>(dy) + (base + c) * Vec8<T>::bytes, g[i]);
+        unpack8<T>(cx[i], xv);
+        unpack8<T>(cg[i], g[i]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           xh[i][k] = (xv[k] - mean) * rstd;
@@ -161,7 +189,7 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_kernel(
         for (int k = 0; k < 8; ++k) o[k] = rstd * (g[i][k] - m1 - xh[i][k] * m2);
         if (dsum) {
           float r[8];
-          Vec8<T>::load(reinterpret_cast<const char*>(dsum) + (base + c) * Vec8<T>::bytes, r);
+          unpack8<T>(cr[i], r);
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] += r[k];
         }
