@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_kernel(
   // before this row's math and wave reduction: two rows of loads in flight per wave, so the kernel
   // keeps HBM busy even when a concurrent side-stream GEMM leaves it few waves per CU.
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kWaves;
-  Raw8<T> nx[NV], ng[NV], nr[NV];
+  Raw8<T> nx[NV] = {}, ng[NV] = {}, nr[NV] = {};  // zero: lanes past D and nr without dsum
   float nmu = 0.f, nrs = 0.f;
   auto fetch = [&](int64_t row) {
     const int64_t base = row * D;
