@@ -39,6 +39,7 @@ import torch.distributed as dist
 from determined_clone_amd.ops import _grad
 from determined_clone_amd.ops import optim as fopt
 from determined_clone_amd.parallel import ddp, zero
+from determined_clone_amd.pytorch.deepspeed._autotune import AutotuneHook
 
 logger = logging.getLogger("determined_clone_amd.pytorch.deepspeed")
 
@@ -238,6 +239,9 @@ class DeepSpeedEngine(torch.nn.Module):
         self.device = device
         self.module = model
         self._z3: Any = None  # ZeRO-3 partitioner (stage 3 only)
+        # parameter counts before any ZeRO-3 partitioning (the autotuning model profile)
+        n_params = sum(p.numel() for p in model.parameters())
+        n_trainable = sum(p.numel() for p in model.parameters() if p.requires_grad)
         if cfg.bf16:
             _cast_module(model, torch.bfloat16)
         elif cfg.fp16:
@@ -265,6 +269,8 @@ class DeepSpeedEngine(torch.nn.Module):
         self.global_samples = 0
         self.skipped_steps = 0
         self._last_grad_norm: Optional[torch.Tensor] = None
+        # dsat measurements ("autotuning" section of the config): pytorch/deepspeed/_autotune.py
+        self._autotune = AutotuneHook(self, cfg.raw, n_params, n_trainable)
 
     # ------------------------------------------------------------------ construction
     def _param_groups(self, model_parameters: Optional[List[Any]]) -> List[Dict[str, Any]]:
@@ -396,6 +402,8 @@ class DeepSpeedEngine(torch.nn.Module):
 
     # ------------------------------------------------------------------ training
     def forward(self, *args: Any, **kwargs: Any) -> Any:
+        if self._autotune.enabled:
+            self._autotune.on_forward()
         return self.module(*args, **kwargs)
 
     def _set_sync(self, enabled: bool) -> None:
@@ -420,6 +428,8 @@ class DeepSpeedEngine(torch.nn.Module):
             # conv / linear weight gradients run on a side stream (ops/_grad.py): .grad is
             # complete for any reader (custom clipping, logging, step) once this returns
             _grad.join()
+        if self._autotune.enabled:
+            self._autotune.after_backward()
         return loss
 
     def step(self, lr_kwargs: Optional[Dict[str, Any]] = None) -> None:
@@ -452,6 +462,8 @@ class DeepSpeedEngine(torch.nn.Module):
             self.lr_scheduler.step(**(lr_kwargs or {}))
         opt.zero_grad()
         self.global_steps += 1
+        if self._autotune.enabled:
+            self._autotune.on_step()  # may end a dsat measurement run (SystemExit)
 
     def zero_grad(self) -> None:
         self.optimizer.zero_grad()

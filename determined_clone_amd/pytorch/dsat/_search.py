@@ -12,7 +12,15 @@ INVALID_HP, which the search treats as "micro batch too large".
 * ``binary``: per stage, double the micro batch from 1 until OOM (or ``max_mbs``), then bisect
   between the largest success and the smallest failure.
 * ``random``: random (stage, micro batch) pairs from the allowed space, never repeating a pair and
-  never trying a micro batch at or above a known OOM for that stage.
+  never trying a micro batch at or above a known OOM for that stage; ``early_stopping`` ends the
+  search after that many completed trials without a new best.
+* ``_test``: micro batches 1, 2, ... ``max_trials`` over the stages in turn (for testing).
+
+(``asha`` -- lineages of random DeepSpeed configurations, each binary-searching its micro batch, under
+successive halving -- is :class:`._asha.ASHADSATSearchMethod`.)
+Trials also carry an ``autotuning`` section in their overwrite, so the native engine measures the
+profiled steps itself (``pytorch/deepspeed/_autotune.py``) for DeepSpeedTrials and Core API
+scripts alike; a metric reported as the engine's dict is read by name.
 """
 import json
 import pathlib
@@ -38,9 +46,12 @@ class DSATSearchMethod(searcher.SearchMethod):
                  metric: str = "throughput", zero_stages: Tuple[int, ...] = (1, 2),
                  max_trials: int = 32, max_concurrent_trials: int = 4,
                  start_profile_step: int = 3, end_profile_step: int = 5, max_mbs: int = 1024,
-                 seed: int = 42) -> None:
-        if search not in _defaults.SEARCH_METHODS:
+                 seed: int = 42, early_stopping: Optional[int] = None) -> None:
+        if search not in ("binary", "random", "_test"):
             raise ValueError(f"unknown dsat search {search!r}")
+        self.early_stopping = early_stopping
+        self._since_best = 0
+        self._best_val: Optional[float] = None
         self.base = dict(base_hparams)
         self.search = search
         self.metric = metric
@@ -61,7 +72,12 @@ class DSATSearchMethod(searcher.SearchMethod):
         return any(c.stage == stage and c.mbs == mbs for c in self.cands.values())
 
     def _propose(self) -> Optional[Tuple[int, int]]:
+        if self.search == "_test":
+            m = len(self.cands) + 1
+            return (self.stages[(m - 1) % len(self.stages)], m) if m <= self.max_mbs else None
         if self.search == "random":
+            if self.early_stopping is not None and self._since_best >= self.early_stopping:
+                return None
             for _ in range(64):
                 s = int(self.rng.choice(self.stages))
                 cap = min(self.hi[s] - 1, self.max_mbs)
@@ -102,6 +118,8 @@ class DSATSearchMethod(searcher.SearchMethod):
             ow["train_micro_batch_size_per_gpu"] = mbs
             ow.pop("train_batch_size", None)
             ow["zero_optimization"] = dict(ow.get("zero_optimization") or {}, stage=stage)
+            ow["autotuning"] = {"enabled": True, "start_profile_step": self.profile[0],
+                                "end_profile_step": self.profile[1]}
             hp[_defaults.OVERWRITE_KEY] = ow
             hp[_defaults.USE_DSAT_MODE_KEY] = True
             hp[_defaults.PROFILE_KEY] = list(self.profile)
@@ -117,8 +135,13 @@ class DSATSearchMethod(searcher.SearchMethod):
 
     def on_validation_completed(self, state, request_id, metric: Any, train_length: int):
         c = self.cands[str(request_id)]
-        c.metric = float(metric)
+        c.metric = self._value(metric)
         c.done = True
+        if c.metric is not None:
+            better = self._best_val is None or (c.metric < self._best_val if self.smaller_is_better
+                                                else c.metric > self._best_val)
+            self._best_val = c.metric if better else self._best_val
+            self._since_best = 0 if better else self._since_best + 1
         self.lo[c.stage] = max(self.lo[c.stage], c.mbs)
         return [searcher.Close(request_id)] + self._create() + self._maybe_shutdown()
 
@@ -132,6 +155,14 @@ class DSATSearchMethod(searcher.SearchMethod):
 
     def on_trial_closed(self, state, request_id):
         return self._maybe_shutdown()
+
+    def _value(self, metric: Any) -> Optional[float]:
+        if isinstance(metric, dict):  # the engine's autotuning measurements
+            for name in (self.metric, "latency" if self.smaller_is_better else "throughput"):
+                if metric.get(name) is not None:
+                    return float(metric[name])
+            return None
+        return None if metric is None else float(metric)
 
     def _maybe_shutdown(self) -> List[searcher.Operation]:
         if self.cands and all(c.done for c in self.cands.values()) and self._propose_peek() is None:
