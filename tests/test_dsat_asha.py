@@ -331,3 +331,34 @@ def test_binary_on_core_api_example(cluster, capsys):
     # every trial reported the engine's measurements through dsat_reporting_context
     assert [t["mbs"] for t in out["trials"]] == [1, 2, 4] and all(t["metric"] for t in out["trials"])
     assert out["best"]["train_micro_batch_size_per_gpu"] in (1, 2, 4)
+
+
+@pytest.mark.gpu
+def test_engine_autotuning_hook_on_gpu(tmp_path, monkeypatch):
+    """CUDA branch of the hook: activation bytes from the device allocator's peak, device memory
+    from the MI355X's properties, bf16 ZeRO-2 engine."""
+    from determined_clone_amd.models import resnet
+    from determined_clone_amd.pytorch import deepspeed as det_ds
+
+    monkeypatch.chdir(tmp_path)
+    cfg = {"train_micro_batch_size_per_gpu": 8, "bf16": {"enabled": True},
+           "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "zero_optimization": {"stage": 2},
+           "autotuning": {"enabled": True, "model_info": {"profile": True}}}
+    model = resnet.to_mi355x_layout(resnet.resnet18_bottleneck_tiny(num_classes=10))
+    eng, _, _, _ = det_ds.initialize(model=model, config=cfg)
+    x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device="cuda")
+    with pytest.raises(SystemExit):
+        eng.backward(torch.nn.functional.cross_entropy(eng(x).float(), y))
+        eng.step()
+    info = json.loads((tmp_path / _defaults.MODEL_INFO_PROFILING_PATH).read_text())
+    assert info["gpu_mem"] == torch.cuda.get_device_properties(0).total_memory
+    assert info["activation_mem_per_gpu"] > 8 * 3 * 64 * 64 * 2  # at least the input images
+    cfg["autotuning"] = {"enabled": True, "start_profile_step": 1, "end_profile_step": 3}
+    eng, _, _, _ = det_ds.initialize(model=model, config=cfg)
+    with pytest.raises(SystemExit):
+        for _ in range(10):
+            eng.backward(torch.nn.functional.cross_entropy(eng(x).float(), y))
+            eng.step()
+    res = json.loads((tmp_path / _defaults.AUTOTUNING_RESULTS_PATH).read_text())
+    assert res["throughput"] > 0 and res["zero_stage"] == 2
