@@ -127,7 +127,8 @@ def test_asha_search_runs_concurrent_trials(cluster):
 
 def test_pause_activate_and_kill(cluster):
     m, s, ctx, _ = cluster
-    eid = _create(s, ctx, BASE + "searcher: {name: single, metric: val_loss, max_length: {batches: 400}}\n")
+    # long enough that the resumed trial cannot finish inside the activate -> kill window
+    eid = _create(s, ctx, BASE + "searcher: {name: single, metric: val_loss, max_length: {batches: 200000}}\n")
     time.sleep(4)
     s.post(f"/api/v1/experiments/{eid}/pause")
     assert _wait(s, eid, states=("PAUSED",)) == "PAUSED"
