@@ -119,6 +119,12 @@ def _from_rows(m: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
     return m.view(n, h, w, m.shape[1]).permute(0, 3, 1, 2)  # channels_last NCHW view
 
 
+# backward-data GEMM of a 1x1 conv accumulates into its input's deposited identity-shortcut
+# gradient (see _PointwiseLib); DCA_PW_ACC_RESIDUAL=0 keeps the two gradients separate
+ACC_RESIDUAL = os.environ.get("DCA_PW_ACC_RESIDUAL", "1") != "0"
+ACC_HITS = 0  # backward passes that took the accumulate path (tests)
+
+
 def _pw_forward(x: torch.Tensor, weight: torch.Tensor, stride: int) -> torch.Tensor:
     n, cin, h, w = x.shape
     cout = weight.shape[0]
@@ -142,6 +148,9 @@ class _PointwiseLib(torch.autograd.Function):
         y = _pw_forward(x, weight, stride)
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
+        # x is a fused BN output whose identity-shortcut gradient arrives through a sink
+        # (ops/batchnorm.py ResidualGradSink): the backward-data GEMM can accumulate into it
+        ctx.sink = getattr(x, "_dca_grad_sink", None) if ACC_RESIDUAL else None
         return y
 
     @staticmethod
@@ -167,7 +176,22 @@ class _PointwiseLib(torch.autograd.Function):
                     return _from_rows(torch.mm(_rows(dy, 1), W), n, h, w)
 
                 cands = (lib, gemm)
-                dx = cands[_choose(("dgrad", tuple(x.shape), cout, st, x.dtype), cands)]()
+                pick = _choose(("dgrad", tuple(x.shape), cout, st, x.dtype), cands)
+                acc = ctx.sink.grad if ctx.sink is not None else None
+                if pick == 1 and acc is not None and acc.shape == x.shape and acc.dtype == dy.dtype \
+                        and acc.is_contiguous(memory_format=torch.channels_last):
+                    # dx = d(shortcut) + dy W as ONE GEMM with beta = 1 into the deposited
+                    # shortcut gradient: the producing BN then reads one gradient tensor instead
+                    # of two in both of its backward passes (one full-tensor pass saved per
+                    # identity block)
+                    rows = _rows(acc, 1)
+                    rows.addmm_(_rows(dy, 1), W)
+                    ctx.sink.grad = None
+                    dx = acc
+                    global ACC_HITS
+                    ACC_HITS += 1
+                else:
+                    dx = cands[pick]()
             else:
                 dx = lib()
         return dx, dw, None
