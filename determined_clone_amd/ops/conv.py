@@ -234,7 +234,11 @@ class _PointwiseDual(torch.autograd.Function):
             if st == 1:
                 c2 = (lambda: bwd(*a2, [True, False, False])[0],
                       lambda: _from_rows(torch.mm(_rows(dy2, 1), W2), n, h, w))
-                dx.add_(c2[_choose(("dgrad", tuple(x.shape), w2.shape[0], 1, x.dtype), c2)]())
+                pick = _choose(("dgrad", tuple(x.shape), w2.shape[0], 1, x.dtype), c2)
+                if pick == 1 and ACC_RESIDUAL and dx.is_contiguous(memory_format=torch.channels_last):
+                    _rows(dx, 1).addmm_(_rows(dy2, 1), W2)  # beta = 1: no separate full-size add
+                else:
+                    dx.add_(c2[pick]())
             else:
                 ho, wo = dy2.shape[2], dy2.shape[3]
                 small = torch.mm(_rows(dy2, 1), W2).view(n, ho, wo, cin)

@@ -164,19 +164,29 @@ def test_pointwise_library_choice_matches_fp32(shape, stride, choice):
         conv._CHOICE.clear()
 
 
+@pytest.mark.parametrize("dgrad_choice", [None, 0, 1])
 @pytest.mark.parametrize("stride", [1, 2])
-def test_pointwise_dual_matches_two_convs(stride):
+def test_pointwise_dual_matches_two_convs(stride, dgrad_choice):
     """conv1(x) and the projection shortcut proj(x) through ops.conv.pointwise_dual (one input
-    gradient, the strided shortcut's dgrad accumulated in place) against fp32 autograd."""
+    gradient, the strided shortcut's dgrad accumulated in place -- for stride 1 on the GEMM path
+    as one beta = 1 GEMM into conv1's gradient) against fp32 autograd; backward-data library
+    chosen by the chooser, or forced to MIOpen (0) / the GEMM (1)."""
     torch.manual_seed(0)
     N, ci, H = 4, 256, 28
     c1 = nn.Conv2d(ci, 128, 1, bias=False).cuda().bfloat16().to(memory_format=torch.channels_last)
     cp = nn.Conv2d(ci, 512, 1, stride=stride, bias=False).cuda().bfloat16().to(memory_format=torch.channels_last)
     x = torch.randn(N, ci, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     x1 = x.clone().requires_grad_(True)
-    y1, yp = conv.pointwise_dual(c1, cp, x1)
-    g1, gp = torch.randn_like(y1), torch.randn_like(yp)
-    torch.autograd.backward([y1, yp], [g1, gp])
+    conv._CHOICE.clear()
+    if dgrad_choice is not None:
+        for co in (128, 512):
+            conv._CHOICE[("dgrad", tuple(x.shape), co, 1, x.dtype)] = dgrad_choice
+    try:
+        y1, yp = conv.pointwise_dual(c1, cp, x1)
+        g1, gp = torch.randn_like(y1), torch.randn_like(yp)
+        torch.autograd.backward([y1, yp], [g1, gp])
+    finally:
+        conv._CHOICE.clear()
     x2 = x.float().clone().requires_grad_(True)
     w1 = c1.weight.detach().float().clone().requires_grad_(True)
     wp = cp.weight.detach().float().clone().requires_grad_(True)
