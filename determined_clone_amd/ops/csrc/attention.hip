@@ -29,6 +29,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 64;   // query rows per forward block / keys per backward block
 constexpr int kPad = 8;     // LDS row padding (elements) to break power-of-two bank strides
+// Row padding of tiles that are only read transposed (ds_read_b64_tr_b16: per 32-lane group, 4 rows
+// x 64 B): rows D + 32 elements apart sit 16 banks apart mod 64, so the 4 rows never share a bank
+// (with kPad two of them do: 2-way conflicts). Tiles read row-wise by ds_read_b128 keep kPad (its
+// lane groups span rows 0-3, 12-15, 20-27, conflict-free at a 144-B stride but not at this one).
+constexpr int kTrPad = 32;
 constexpr float kRescaleLog2 = 8.f;  // forward: deferred-max threshold (log2 units)
 
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -162,43 +167,9 @@ __device__ __forceinline__ Blk xcd_block(int order) {
   return {v % nx, (v / nx) % ny, v / (nx * ny)};
 }
 
-// Stage a [64 rows][D] tile (rows r0.., clamped to n_rows, zero-filled beyond) into LDS,
-// row-major (dst[r][d], row stride D + kPad) and/or transposed (dstT[d][r], row stride 64 + kPad).
-template <int D>
-__device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ src, Strides st, int r0,
-                                           int n_rows, uint16_t* dst, uint16_t* dstT) {
-  constexpr int chunks_per_row = D / 8;
-  constexpr int total = kTile * chunks_per_row;
-  for (int c = threadIdx.x; c < total; c += blockDim.x) {
-    const int r = c / chunks_per_row;
-    const int d0 = (c % chunks_per_row) * 8;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + r < n_rows) v = *reinterpret_cast<const uint4*>(src + static_cast<int64_t>(r0 + r) * st.s + d0);
-    if (dst) *reinterpret_cast<uint4*>(dst + r * (D + kPad) + d0) = v;
-    if (dstT) {
-      const uint16_t* e = reinterpret_cast<const uint16_t*>(&v);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) dstT[(d0 + i) * (kTile + kPad) + r] = e[i];
-    }
-  }
-}
-
-// Stage ROWS consecutive rows (from r0, zero-filled beyond n_rows) row-major into LDS.
-template <int D, int ROWS>
-__device__ __forceinline__ void stage_rows(const uint16_t* __restrict__ src, Strides st, int r0,
-                                           int n_rows, uint16_t* dst) {
-  constexpr int cpr = D / 8;
-  for (int c = threadIdx.x; c < ROWS * cpr; c += blockDim.x) {
-    const int rr = c / cpr, d0 = (c % cpr) * 8;
-    uint4 val = make_uint4(0, 0, 0, 0);
-    if (r0 + rr < n_rows) val = *reinterpret_cast<const uint4*>(src + static_cast<int64_t>(r0 + rr) * st.s + d0);
-    *reinterpret_cast<uint4*>(dst + rr * (D + kPad) + d0) = val;
-  }
-}
-
 // Register double buffer for a pair of [64 rows][D] tiles (K and V): fetch() issues the HBM loads of
 // the NEXT tile before the current tile's MFMAs, store() writes them to LDS after the barrier.
-template <int D, int ROWS = 64>
+template <int D, int ROWS = 64, int VPAD = kPad>
 struct KVPrefetch {
   static constexpr int CPR = D / 8;
   static constexpr int N = 2 * ROWS * CPR / 256;
@@ -226,7 +197,8 @@ struct KVPrefetch {
       const int c = threadIdx.x + 256 * j;
       const int which = c / (ROWS * CPR);
       const int cc = c % (ROWS * CPR);
-      *reinterpret_cast<uint4*>((which ? Vs : Ks) + (cc / CPR) * (D + kPad) + (cc % CPR) * 8) = reg[j];
+      const int rr = cc / CPR, d0 = (cc % CPR) * 8;
+      *reinterpret_cast<uint4*>(which ? Vs + rr * (D + VPAD) + d0 : Ks + rr * (D + kPad) + d0) = reg[j];
     }
   }
 };
@@ -248,7 +220,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   constexpr int RS = D + kPad; // LDS row stride (elements)
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Ks = smem;           // [KT][RS]
-  uint16_t* Vs = Ks + KT * RS;   // [KT][RS]
+  // V tile: read only transposed -- the conflict-free kTrPad stride for D = 128 (+5-14%); D = 64
+  // measured 1-3% slower with it at S 1024-2048 (profiles/round3_attention_vtile_pad_ab.txt)
+  constexpr int VPAD = D == 128 ? kTrPad : kPad;
+  constexpr int RSV = D + VPAD;
+  uint16_t* Vs = Ks + KT * RS;   // [KT][RSV]
   const int lane = threadIdx.x & 63;
   // wave index in an SGPR: the causal extent checks below are uniform branches
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -275,7 +251,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   // tr-read lane address pieces (see T10: lane 4q+p of a 16-lane group -> row q, cols 4p..4p+3)
   const int tr_row = (r & 15) >> 2;
   const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
-  KVPrefetch<D, KT> pf;
+  KVPrefetch<D, KT, VPAD> pf;
   pf.fetch(kb, ks, vb, vs, 0, Sk);
   for (int kt = 0; kt < k_end; kt += KT) {
     __syncthreads();
@@ -327,8 +303,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         for (int n = 0; n < D / 32; ++n) {
   #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
-            const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
-            oacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RS)), s2 ? p1 : p0, oacc[n]);
+            const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RSV + 32 * n + tr_col;
+            oacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RSV)), s2 ? p1 : p0, oacc[n]);
           }
         }
       };
@@ -413,8 +389,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       for (int n = 0; n < D / 32; ++n) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
-          oacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RS)), s2 ? p1 : p0, oacc[n]);
+          const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RSV + 32 * n + tr_col;
+          oacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RSV)), s2 ? p1 : p0, oacc[n]);
         }
       }
     }
@@ -763,8 +739,10 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   store_rows<D>(dv + b * dvs.b + h * dvs.h + static_cast<int64_t>(my_key) * dvs.s, dvacc, 1.f, hf, my_key < Sk);
 }
 
-size_t fwd_lds(int D, int KT = 64) { return 2 * static_cast<size_t>(KT) * (D + kPad) * 2; }
-size_t bwd_dq_lds(int D, int KT = 64) { return fwd_lds(D, KT); }
+size_t fwd_lds(int D, int KT = 64) {  // K tile + V tile (see attn_fwd_kernel's VPAD)
+  return static_cast<size_t>(KT) * ((D + kPad) + (D + (D == 128 ? kTrPad : kPad))) * 2;
+}
+size_t bwd_dq_lds(int D, int KT = 64) { return 2 * static_cast<size_t>(KT) * (D + kPad) * 2; }
 
 // keys per LDS tile of the dQ kernel (DCA_ATTN_DQ_KT=128: half the barriers per MFMA, D = 64)
 int dq_kt() {
