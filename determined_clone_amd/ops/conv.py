@@ -178,13 +178,17 @@ class _PointwiseLib(torch.autograd.Function):
                 cands = (lib, gemm)
                 pick = _choose(("dgrad", tuple(x.shape), cout, st, x.dtype), cands)
                 acc = ctx.sink.grad if ctx.sink is not None else None
+                rows = None
                 if pick == 1 and acc is not None and acc.shape == x.shape and acc.dtype == dy.dtype \
                         and acc.is_contiguous(memory_format=torch.channels_last):
+                    rows = _rows(acc, 1)
+                    if rows.data_ptr() != acc.data_ptr():  # not a view: would accumulate into a copy
+                        rows = None
+                if rows is not None:
                     # dx = d(shortcut) + dy W as ONE GEMM with beta = 1 into the deposited
                     # shortcut gradient: the producing BN then reads one gradient tensor instead
                     # of two in both of its backward passes (one full-tensor pass saved per
                     # identity block)
-                    rows = _rows(acc, 1)
                     rows.addmm_(_rows(dy, 1), W)
                     ctx.sink.grad = None
                     dx = acc
@@ -235,8 +239,10 @@ class _PointwiseDual(torch.autograd.Function):
                 c2 = (lambda: bwd(*a2, [True, False, False])[0],
                       lambda: _from_rows(torch.mm(_rows(dy2, 1), W2), n, h, w))
                 pick = _choose(("dgrad", tuple(x.shape), w2.shape[0], 1, x.dtype), c2)
-                if pick == 1 and ACC_RESIDUAL and dx.is_contiguous(memory_format=torch.channels_last):
-                    _rows(dx, 1).addmm_(_rows(dy2, 1), W2)  # beta = 1: no separate full-size add
+                rows = _rows(dx, 1) if pick == 1 and ACC_RESIDUAL and \
+                    dx.is_contiguous(memory_format=torch.channels_last) else None
+                if rows is not None and rows.data_ptr() == dx.data_ptr():
+                    rows.addmm_(_rows(dy2, 1), W2)  # beta = 1: no separate full-size add
                 else:
                     dx.add_(c2[pick]())
             else:

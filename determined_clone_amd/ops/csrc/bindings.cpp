@@ -120,7 +120,12 @@ std::vector<Tensor> bn_fwd_train(const Tensor& x, const OptT& residual, const Op
   const c10::DeviceGuard guard(x.device());
   auto [M, C] = rows_channels(x);
   if (residual.has_value()) {
-    TORCH_CHECK(residual->sizes() == x.sizes() && residual->strides() == x.strides() &&
+    // same element order as x (NHWC / row-major contiguity), not identical strides: size-1 dims
+    // (e.g. 1x1 spatial maps) may carry any stride in a channels_last-contiguous tensor
+    const bool same_layout = x.dim() == 4
+                                 ? residual->is_contiguous(at::MemoryFormat::ChannelsLast)
+                                 : residual->is_contiguous();
+    TORCH_CHECK(residual->sizes() == x.sizes() && same_layout &&
                     residual->scalar_type() == x.scalar_type(),
                 "batchnorm: residual must match input shape/layout/dtype");
   }
