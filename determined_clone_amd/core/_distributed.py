@@ -121,11 +121,10 @@ class DistributedContext:
                 except Exception:  # noqa: BLE001 - teardown is best effort
                     pass
         self._local_group = self._group = None
-        if getattr(self, "_owns_pg", False):
-            try:
-                dist.destroy_process_group()
-            except Exception:  # noqa: BLE001
-                pass
+        # The default process group stays up even when from_torch_distributed() created it (as the
+        # reference's close() never tears torch.distributed down): user code may still run
+        # collectives after the Core API context exits (a final barrier, DDP / engine teardown).
+        # The process's exit releases it.
 
     # ------------------------------------------------------------------ collectives
     def _objs(self, obj: Any, group: Any) -> List[Any]:

@@ -133,6 +133,31 @@ def get_gpus() -> Tuple[List[GPU], str]:
     return (gpus, "rocm") if gpus else ([], "")
 
 
+class GPUStats(NamedTuple):
+    uuid: str
+    util_percent: float  # amdgpu gpu_busy_percent
+    free_memory_gb: float  # VRAM total - used, in 1e9 bytes (the reference's pynvml unit)
+
+
+def get_gpu_stats() -> List[GPUStats]:
+    """Utilisation and free VRAM of the visible devices from the amdgpu sysfs files (no HIP
+    initialisation, no CLI tool): what the profiler's system-metrics thread samples."""
+    out: List[GPUStats] = []
+    nodes = _kfd_nodes()
+    for i in _visible(len(nodes)):
+        d = _drm_device(nodes[i]["render_minor"])
+        if d is None:
+            continue
+        busy = _read(os.path.join(d, "gpu_busy_percent"))
+        used = _read(os.path.join(d, "mem_info_vram_used"))
+        total = _read(os.path.join(d, "mem_info_vram_total"))
+        if not (busy and busy.isdigit()):
+            continue
+        free = (int(total) - int(used)) / 1e9 if used and total and used.isdigit() and total.isdigit() else 0.0
+        out.append(GPUStats(uuid=nodes[i]["uuid"], util_percent=float(busy), free_memory_gb=free))
+    return out
+
+
 def get_gpu_uuids() -> List[str]:
     gpus, _ = get_gpus()
     return [g.uuid for g in sorted(gpus, key=lambda g: g.id)]

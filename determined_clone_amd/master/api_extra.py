@@ -548,17 +548,49 @@ def metrics_by_checkpoint(r: Req) -> Any:
 
 @route("GET", "/api/v1/trials/{tid}/profiler/available_series")
 def profiler_series(r: Req) -> Any:
-    rows = r.m.db.all("SELECT DISTINCT name FROM profiler_metrics WHERE trial_id=?", [_int(r.p["tid"])])
-    return {"labels": [{"trial_id": _int(r.p["tid"]), "name": x["name"]} for x in rows]}
+    """GetTrialProfilerAvailableSeries: the distinct label sets of the trial's profiler data."""
+    tid = _int(r.p["tid"])
+    rows = r.m.db.all("SELECT DISTINCT name, agent_id, gpu_uuid, metric_type FROM profiler_metrics "
+                      "WHERE trial_id=? ORDER BY metric_type, name, gpu_uuid", [tid])
+    return {"labels": [{"trialId": tid, "name": x["name"], "agentId": x["agent_id"] or "",
+                        "gpuUuid": x["gpu_uuid"] or "",
+                        "metricType": x["metric_type"] or "PROFILER_METRIC_TYPE_UNSPECIFIED"}
+                       for x in rows]}
 
 
-@route("POST", "/api/v1/trials/profiler/metrics")
+def _label(labels: Dict[str, Any], snake: str, camel: str, default: Any = "") -> Any:
+    v = labels.get(camel, labels.get(snake))
+    return default if v is None else v
+
+
+@route("POST", "/api/v1/trials/profiler/metrics", first=True)
 def profiler_metrics_batch(r: Req) -> Any:
+    """PostTrialProfilerMetricsBatch: ``{"batches": [TrialProfilerMetricsBatch]}`` with labels in
+    either JSON spelling (``trialId`` / ``trial_id``, ...); one row per reading."""
+    import datetime as _dt
+
     for batch in r.body.get("batches", []):
-        tid = (batch.get("labels") or {}).get("trial_id")
-        for ts, vals in zip(batch.get("timestamps", []), batch.get("values", [])):
-            r.m.db.insert("profiler_metrics", {"trial_id": tid, "name": (batch.get("labels") or {}).get("name", "system"),
-                                               "ts": ts, "value": {"time": ts, "value": vals}})
+        labels = batch.get("labels") or {}
+        tid = _int(_label(labels, "trial_id", "trialId", 0))
+        if not r.m.db.one("SELECT id FROM trials WHERE id=?", [tid]):
+            raise HTTPError(404, f"trial {tid} not found")
+        name = _label(labels, "name", "name", "")
+        if not name:
+            raise HTTPError(400, "profiler batch labels need a name")
+        mtype = _label(labels, "metric_type", "metricType", "PROFILER_METRIC_TYPE_UNSPECIFIED")
+        agent, uuid = _label(labels, "agent_id", "agentId"), _label(labels, "gpu_uuid", "gpuUuid")
+        vals, bats, tss = batch.get("values", []), batch.get("batches", []), batch.get("timestamps", [])
+        if not (len(vals) == len(bats) == len(tss)):
+            raise HTTPError(400, "values, batches and timestamps must have equal lengths")
+        for v, b, t in zip(vals, bats, tss):
+            try:
+                ts = _dt.datetime.fromisoformat(str(t).replace("Z", "+00:00")).timestamp()
+            except ValueError:
+                ts = float(t) if isinstance(t, (int, float)) else time.time()
+            r.m.db.insert("profiler_metrics", {"trial_id": tid, "name": name, "ts": ts,
+                                               "agent_id": agent, "gpu_uuid": uuid,
+                                               "metric_type": mtype, "batch": int(b),
+                                               "value": {"time": t, "value": float(v)}})
     return {}
 
 

@@ -77,6 +77,11 @@ CREATE TABLE IF NOT EXISTS kv (key TEXT PRIMARY KEY, value TEXT);
 MIGRATIONS = [
     ("experiments", "external_experiment_id", "TEXT"),
     ("trials", "external_trial_id", "TEXT"),
+    # profiler series labels (trial/v1 TrialProfilerMetricLabels) and the batch of each reading
+    ("profiler_metrics", "agent_id", "TEXT"),
+    ("profiler_metrics", "gpu_uuid", "TEXT"),
+    ("profiler_metrics", "metric_type", "TEXT"),
+    ("profiler_metrics", "batch", "INTEGER"),
 ]
 
 

@@ -699,18 +699,32 @@ def trial_logs(r: Req) -> Any:
     return _logs(r, row["task_id"])
 
 
-@route("POST", "/api/v1/trials/{tid}/profiler/metrics")
-def post_profiler(r: Req) -> Any:
-    for s in r.body.get("samples", []):
-        r.m.db.insert("profiler_metrics", {"trial_id": _int(r.p["tid"]), "name": s.get("name", "system"),
-                                           "ts": s.get("time", now()), "value": s})
-    return {}
-
-
 @route("GET", "/api/v1/trials/{tid}/profiler/metrics")
 def get_profiler(r: Req) -> Any:
-    rows = r.m.db.all("SELECT * FROM profiler_metrics WHERE trial_id=? ORDER BY ts", [_int(r.p["tid"])])
-    return {"samples": [dec(x["value"], {}) for x in rows]}
+    """GetTrialProfilerMetrics: the trial's profiler series as TrialProfilerMetricsBatch objects
+    (one per series), filtered by ``labels.name`` / ``labels.agent_id`` / ``labels.gpu_uuid`` /
+    ``labels.metric_type``; ``follow`` is accepted and answered with what exists now."""
+    where, args = ["trial_id=?"], [_int(r.p["tid"])]
+    for q, col in (("labels.name", "name"), ("labels.agent_id", "agent_id"),
+                   ("labels.gpu_uuid", "gpu_uuid"), ("labels.metric_type", "metric_type")):
+        v = r.qget(q)
+        if v not in (None, ""):
+            where.append(f"COALESCE({col}, '')=?")
+            args.append(v)
+    rows = r.m.db.all(f"SELECT * FROM profiler_metrics WHERE {' AND '.join(where)} ORDER BY ts, id", args)
+    series: Dict[Any, Dict[str, Any]] = {}
+    for x in rows:
+        key = (x["name"], x["agent_id"] or "", x["gpu_uuid"] or "", x["metric_type"] or "")
+        b = series.get(key)
+        if b is None:
+            b = series[key] = {"values": [], "batches": [], "timestamps": [], "labels": {
+                "trialId": _int(r.p["tid"]), "name": key[0], "agentId": key[1], "gpuUuid": key[2],
+                "metricType": key[3] or "PROFILER_METRIC_TYPE_UNSPECIFIED"}}
+        v = dec(x["value"], None)
+        b["values"].append(v["value"] if isinstance(v, dict) else v)
+        b["batches"].append(x["batch"] if x["batch"] is not None else 0)
+        b["timestamps"].append(v.get("time") if isinstance(v, dict) else x["ts"])
+    return {"batches": list(series.values())}
 
 
 # =========================================================================== allocations
@@ -1383,7 +1397,7 @@ class _Handler(BaseHTTPRequestHandler):
 
     # task-plumbing endpoints polled/posted by every running task or agent: not audited
     _UNAUDITED = ("agent_events", "post_task_logs", "post_metrics", "trial_progress", "trial_heartbeat",
-                  "post_profiler", "runner_metadata", "agent_register", "alloc_allgather", "ack_preemption",
+                  "profiler_metrics_batch", "runner_metadata", "agent_register", "alloc_allgather", "ack_preemption",
                   "alloc_ready", "alloc_proxy", "report_checkpoint", "trial_completed_op")
 
     def _account(self, handler: str, method: str, path: str, code: int, started: float,

@@ -380,8 +380,11 @@ class _StemS2D(torch.autograd.Function):
 def stem_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     """The ResNet stem convolution: space-to-depth form on a GPU when it applies (7x7, stride 2,
     padding 3, 3 input channels, no bias, even H and W, image without gradient), else
-    :func:`spatial_conv`."""
+    :func:`spatial_conv`. The S2D form is pinned to the 7x7 path only for zero padding, matching
+    input / weight dtypes and no autocast (its saved tensors keep their own dtype)."""
     if (STEM_S2D and x.is_cuda and not x.requires_grad and conv.kernel_size == (7, 7)
+            and conv.padding_mode == "zeros" and x.dtype == conv.weight.dtype
+            and not torch.is_autocast_enabled()
             and conv.stride == (2, 2) and conv.padding == (3, 3) and conv.in_channels == 3
             and conv.groups == 1 and conv.bias is None and conv.dilation == (1, 1)
             and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0):

@@ -38,6 +38,22 @@ def configure(env: Optional[MutableMapping[str, str]] = None, db_dir: Optional[s
             "MIOPEN_CUSTOM_CACHE_DIR": env["MIOPEN_CUSTOM_CACHE_DIR"]}
 
 
+def use_private_copy(tag: str = "proc", env: Optional[MutableMapping[str, str]] = None) -> Dict[str, str]:
+    """Point MIOpen at a writable copy of the shipped files private to ``tag`` (e.g. one per rank)
+    under the temp dir, unless the environment already chose a location. Benchmarks and tools use
+    this so that find results / compiled kernels never land in the git-tracked shipped directory
+    and no two processes of one job share one sqlite DB; only an explicit tuning run writes the
+    shipped files."""
+    import tempfile
+
+    env = os.environ if env is None else env
+    if "MIOPEN_USER_DB_PATH" in env:
+        return configure(env)
+    root = os.path.join(tempfile.gettempdir(), f"dca_miopen_{os.getuid()}", tag)
+    db, cache = task_dirs(root)
+    return configure(env, db, cache)
+
+
 def task_dirs(root: str) -> Tuple[str, str]:
     """``(db_dir, cache_dir)`` under ``root``: created from the shipped files the first time,
     reused afterwards (files a task added are kept)."""

@@ -170,6 +170,8 @@ def _wgrad_splits(tokens: int, m: int, n: int) -> int:
     3072x1024 166 -> 115 us, 4096x1024 166 -> 145 us, 1024x4096 161 -> 143 us."""
     if not _WGRAD_SPLITK or tokens < 8192 or tokens % 4 or m * n > 16 * 2 ** 20:
         return 1
+    if (m * n) % 8:  # splitk_accumulate streams 8 elements per thread (16-B aligned buffers)
+        return 1
     return 4
 
 

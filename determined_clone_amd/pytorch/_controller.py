@@ -31,6 +31,7 @@ from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 import numpy as np
 import torch
 
+from determined_clone_amd import profiler as profiler_mod
 from determined_clone_amd import core, errors, util
 from determined_clone_amd.ops import _grad
 from determined_clone_amd.pytorch import _data, _reducer
@@ -135,7 +136,12 @@ class _PyTorchTrialController:
         self.trial = trial_inst
         self.context = context
         self.core_context = context._core
-        self.prof = profiler
+        # Determined profiler (system metrics + loop timings, profiler.py); a no-op agent when
+        # profiling is off. Timings end at a device synchronisation (reference
+        # _pytorch_trial.py:200-209, 257).
+        self.prof = profiler if profiler is not None else profiler_mod.DummyProfilerAgent()
+        if torch.cuda.is_available():
+            self.prof._set_sync_device(torch.cuda.synchronize)
         self.local_training = local_training
         self.is_chief = context.distributed.rank == 0
         self.max_length = max_length
@@ -246,11 +252,42 @@ class _PyTorchTrialController:
         return (now < before) if self.smaller_is_better else (now > before)
 
     # ------------------------------------------------------------------ run
+    @contextlib.contextmanager
+    def _profiling(self) -> Iterator[None]:
+        """The Determined profiler and the user's torch profiler (``context.set_profiler``) are
+        entered ONCE around the training loop; the torch profiler's schedule advances with one
+        ``step()`` per batch (``_train_batch``)."""
+        with contextlib.ExitStack() as stack:
+            stack.enter_context(self.prof)
+            if self.context.profiler:
+                stack.enter_context(self.context.profiler)
+            yield
+
+    def _timed_callback(self, name: str, fn: Any) -> Any:
+        def call(*a: Any, **kw: Any) -> Any:
+            with self.prof.record_timing(name):
+                return fn(*a, **kw)
+        return call
+
+    def _timed_iter(self, it: Iterator[Any]) -> Iterator[Any]:
+        """``next()`` of the training loader timed as ``dataloader_next`` (reference
+        _pytorch_trial.py:34-40)."""
+        while True:
+            with self.prof.record_timing("dataloader_next", requires_sync=False):
+                try:
+                    item = next(it)
+                except StopIteration:
+                    return
+            yield item
+
     def run(self) -> None:
         with contextlib.ExitStack() as stack:
             for name, cb in self.callbacks.items():
-                cb.on_trial_startup(self.start_from_batch, self.latest_checkpoint)
-                stack.callback(cb.on_trial_shutdown)
+                cls = type(cb).__name__
+                self._timed_callback(f"callbacks.{cls}.on_trial_startup", cb.on_trial_startup)(
+                    self.start_from_batch, self.latest_checkpoint)
+                stack.callback(self._timed_callback(f"callbacks.{cls}.on_trial_shutdown",
+                                                    cb.on_trial_shutdown))
             if self.local_training and self.latest_checkpoint is not None:
                 # Off-cluster there is no master to tell us steps_completed: take it from the
                 # checkpoint so data loading resumes at the right batch.
@@ -263,7 +300,7 @@ class _PyTorchTrialController:
             if self.context.experimental._auto_to_device and self.context.device.type == "cuda":
                 it = _data.DevicePrefetcher(it, self.context.device)
             self.training_iterator = it
-            self.training_enumerator = enumerate(it, start=self.start_from_batch)
+            self.training_enumerator = enumerate(self._timed_iter(it), start=self.start_from_batch)
 
             def cleanup() -> None:
                 del self.training_iterator
@@ -278,7 +315,7 @@ class _PyTorchTrialController:
                 self.state = _TrialState(trial_id=self.trial_id)
             for cb in self.callbacks.values():
                 cb.on_training_start()
-            with _grad.step_stream(self.context.device):
+            with _grad.step_stream(self.context.device), self._profiling():
                 self._run()
 
     def _run(self) -> None:
@@ -310,6 +347,7 @@ class _PyTorchTrialController:
         metrics: List[Dict[str, Any]] = []
         if self.is_chief:
             self.core_context.train.set_status("training")
+        self.prof.set_training(True)
         for m in self.context.models:
             m.train()
         self.context.reset_reducers()
@@ -433,16 +471,18 @@ class _PyTorchTrialController:
     def _train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, Any]:
         self.context._loss_ids = {}
         t0 = time.time()
+        self.prof.update_batch_idx(batch_idx)
         if self.context.experimental._auto_to_device and not isinstance(self.training_iterator, _data.DevicePrefetcher):
-            batch = self.context.to_device(batch)
-        if self.context.profiler:
-            with self.context.profiler:
+            with self.prof.record_timing("to_device", accumulate=True):
+                batch = self.context.to_device(batch)
+        with self.prof.record_timing("train_batch", requires_sync=False):
+            if self.context.profiler:
                 out = self.trial.train_batch(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
                 self.context.profiler.step()
-        elif self._graph_step() is not None:
-            out = self._graphed(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
-        else:
-            out = self.trial.train_batch(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
+            elif self._graph_step() is not None:
+                out = self._graphed(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
+            else:
+                out = self.trial.train_batch(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
         if self.context._scaler is not None and self.context.experimental._auto_amp \
                 and self.context._should_communicate_and_update():
             self.context._scaler.update()
@@ -452,19 +492,26 @@ class _PyTorchTrialController:
         if not isinstance(out, dict):
             raise TypeError("train_batch() must return a dictionary mapping string names to Tensor "
                             f"metrics, got {type(out).__name__}")
-        for sched in self.context.lr_schedulers:
-            self._auto_step_lr_scheduler_per_batch(batch_idx, sched)
-        metrics = {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}
+        with self.prof.record_timing("step_lr_schedulers"):
+            for sched in self.context.lr_schedulers:
+                self._auto_step_lr_scheduler_per_batch(batch_idx, sched)
+        # metrics stay on the device until the workload's reduction (no per-batch host sync)
+        with self.prof.record_timing("from_device"):
+            metrics = {k: (v.detach() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}
         dt = time.time() - t0
         self.last_step_time_s = dt
         if dt > 0:
-            self.samples_per_second.append(self.trial.get_batch_length(batch) * self.context.distributed.size / dt)
+            sps = self.trial.get_batch_length(batch) * self.context.distributed.size / dt
+            self.samples_per_second.append(sps)
+            self.prof.record_metric("samples_per_second", sps)
         return metrics
 
     def _aggregate_training_metrics(self, batch_metrics: List[Dict[str, Any]]) -> Dict[str, Any]:
-        agg = _reducer.average_training_metrics(self.context.distributed, batch_metrics,
-                                                self.context._average_training_metrics)
-        extra = self.context.reduce_metrics(for_training=True)
+        with self.prof.record_timing("average_training_metrics"):
+            agg = _reducer.average_training_metrics(self.context.distributed, batch_metrics,
+                                                    self.context._average_training_metrics)
+        with self.prof.record_timing("reduce_metrics"):
+            extra = self.context.reduce_metrics(for_training=True)
         agg["avg_metrics"].update({k: util.to_python(v) for k, v in extra.items()})
         if not self.is_chief:
             return {"avg_metrics": agg["avg_metrics"], "batch_metrics": agg["batch_metrics"]}

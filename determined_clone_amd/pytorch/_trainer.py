@@ -28,10 +28,23 @@ class Trainer:
 
     def configure_profiler(self, enabled: bool = False, sync_timings: bool = True,
                            begin_on_batch: int = 0, end_after_batch: Optional[int] = None) -> None:
+        """Configure the Determined profiler (reference pytorch/_trainer.py:36-84): on-cluster
+        only; in local training it is a no-op. Samples system metrics (GPU utilisation / free
+        VRAM from amdgpu sysfs, CPU, memory, network, disk) and the loop's timings between
+        ``begin_on_batch`` and ``end_after_batch`` (at most 5 minutes) and ships them to the
+        master's ``/api/v1/trials/profiler/metrics``."""
         from determined_clone_amd import profiler
 
-        if enabled:
-            self._profiler = profiler.ProfilerAgent(begin_on_batch, end_after_batch, sync_timings)
+        if self._local_training or self._info is None:
+            self._profiler = profiler.DummyProfilerAgent()
+            return
+        session = getattr(self._core.train, "_session", None)
+        self._profiler = profiler.ProfilerAgent.from_config(
+            {"enabled": enabled, "sync_timings": sync_timings, "begin_on_batch": begin_on_batch,
+             "end_after_batch": end_after_batch},
+            trial_id=self._info.trial.trial_id, agent_id=self._info.agent_id,
+            global_rank=self._core.distributed.get_rank(),
+            local_rank=self._core.distributed.get_local_rank(), session=session)
 
     def fit(self, checkpoint_period: Optional[TrainUnit] = None,
             validation_period: Optional[TrainUnit] = None, max_length: Optional[TrainUnit] = None,

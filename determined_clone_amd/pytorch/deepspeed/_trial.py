@@ -279,7 +279,7 @@ class DeepSpeedTrialController(_PyTorchTrialController):
                 self.state = _TrialState(trial_id=self.trial_id)
             for cb in self.callbacks.values():
                 cb.on_training_start()
-            with _grad.step_stream(self.context.device):
+            with _grad.step_stream(self.context.device), self._profiling():
                 self._run()
 
     # ------------------------------------------------------------------ DeepSpeed autotune mode
@@ -368,6 +368,7 @@ class DeepSpeedTrialController(_PyTorchTrialController):
         metrics: List[Dict[str, Any]] = []
         if self.is_chief:
             self.core_context.train.set_status("training")
+        self.prof.set_training(True)
         for m in ctx.models:
             m.train()
         ctx.reset_reducers()
@@ -382,13 +383,14 @@ class DeepSpeedTrialController(_PyTorchTrialController):
                 for cb in self.callbacks.values():
                     cb.on_training_epoch_start(epoch_idx)
             ctx._loss_ids = {}
+            self.prof.update_batch_idx(batch_idx)
+            t0 = time.time()
             for _ in range(calls):
-                if ctx.profiler:
-                    with ctx.profiler:
-                        out = self.trial.train_batch(self.training_iterator, epoch_idx, batch_idx)
-                        ctx.profiler.step()
-                else:
+                # the torch profiler (set_profiler) was entered once around the loop (_profiling)
+                with self.prof.record_timing("train_batch", requires_sync=False, accumulate=True):
                     out = self.trial.train_batch(self.training_iterator, epoch_idx, batch_idx)
+                if ctx.profiler:
+                    ctx.profiler.step()
                 if ctx._mpu.should_report_metrics:
                     if isinstance(out, torch.Tensor):
                         out = {"loss": out}
@@ -401,6 +403,11 @@ class DeepSpeedTrialController(_PyTorchTrialController):
             if isinstance(m0, DeepSpeedEngine) and not ctx._manual_grad_accumulation and \
                     m0.micro_steps % ctx.num_micro_batches_per_slot != 0:
                 raise RuntimeError("did not train for gradient accumulation steps")
+            dt = time.time() - t0
+            if dt > 0:
+                self.prof.record_metric("samples_per_second",
+                                        ctx.train_micro_batch_size_per_gpu * ctx.num_micro_batches_per_slot
+                                        * ctx.distributed.size / dt)
             self._step_batch()
             for b in boundaries:
                 if isinstance(b.unit, Batch) and b.unit.should_stop(batch_idx + 1):

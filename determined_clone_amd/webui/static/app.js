@@ -337,13 +337,36 @@ async function pageTrial(params, id) {
   } else if (tab === "checkpoints") {
     body = checkpointTable((await api.get(`/api/v1/trials/${id}/checkpoints`)).checkpoints);
   } else if (tab === "profiler") {
-    const { samples } = await api.get(`/api/v1/trials/${id}/profiler/metrics`);
-    const rows = samples.map((s, i) => ({ steps_completed: s.time !== undefined ? s.time - (samples[0].time || 0) : i, metrics: s.metrics || s }));
-    body = rows.length ? metricCharts([{ name: "system", rows }]) : h("div", { class: "muted" }, "no profiler samples (enable profiling in the experiment config)");
+    body = await profilerView(id);
   } else {
     body = logView(`/api/v1/trials/${id}/logs`);
   }
   return h("div", {}, head, body);
+}
+
+// Profiler tab (reference TrialDetailsProfiles): system metrics vs seconds since the first
+// sample, one line per GPU / agent; loop timings and samples/s vs batch, one line per timing.
+async function profilerView(id) {
+  const [{ labels }, { batches }] = await Promise.all([
+    api.get(`/api/v1/trials/${id}/profiler/available_series`), api.get(`/api/v1/trials/${id}/profiler/metrics`)]);
+  if (!batches.length) return h("div", { class: "muted" }, "no profiler data (set profiling.enabled in the experiment config)");
+  const t0 = Math.min(...batches.flatMap((b) => b.timestamps.map((t) => Date.parse(t))));
+  const byType = (ty) => batches.filter((b) => b.labels.metricType === ty);
+  const sys = byType("PROFILER_METRIC_TYPE_SYSTEM");
+  const names = [...new Set(sys.map((b) => b.labels.name))].sort();
+  const sysCharts = names.map((n) => lineChart(n, sys.filter((b) => b.labels.name === n).map((b) => ({
+    name: b.labels.gpuUuid ? `gpu ${b.labels.gpuUuid}` : (b.labels.agentId || "agent"),
+    points: b.values.map((v, i) => [(Date.parse(b.timestamps[i]) - t0) / 1000, v]),
+  })), "seconds"));
+  const timing = byType("PROFILER_METRIC_TYPE_TIMING");
+  const timingChart = lineChart("timings (s)", timing.map((b) => ({
+    name: b.labels.name, points: b.values.map((v, i) => [b.batches[i], v]) })), "batch");
+  const misc = byType("PROFILER_METRIC_TYPE_MISC").map((b) => lineChart(b.labels.name, [{
+    name: b.labels.name, points: b.values.map((v, i) => [b.batches[i], v]) }], "batch"));
+  const summary = table([{ key: "metricType", label: "Type" }, { key: "name", label: "Series" },
+    { key: "gpuUuid", label: "GPU" }, { key: "agentId", label: "Agent" }], labels, { sortKey: "metricType", desc: false });
+  return h("div", {}, h("h2", {}, "Timings"), h("div", { class: "charts" }, timingChart, ...misc),
+    h("h2", {}, "System metrics"), h("div", { class: "charts" }, ...sysCharts), h("h2", {}, "Series"), summary);
 }
 
 // incremental log tail with follow; stops when the page changes

@@ -33,3 +33,22 @@ def test_bench_two_ranks_prints_one_aggregate_json_line():
     assert r["config"]["parallelism"] == "dp2"
     # whole-job images/s from the slowest rank's step time
     assert abs(r["value"] - 4 / (r["ms_per_step"] / 1000.0)) / r["value"] < 0.01
+
+
+def test_bench_gpus_flag_launches_ranks_itself():
+    """``python bench.py --gpus 2`` with NO launcher around it (the driver's BENCH command shape)
+    starts the two ranks itself and reports what torch.distributed formed."""
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--batch", "2"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["world_size"] == 2
+    assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 4
+    assert r["backend"] == "gloo"  # CPU here; "nccl" (RCCL) on the GPU box
+    assert r["device"] == "cpu" and "host memory" in r["data"]

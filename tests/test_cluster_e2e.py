@@ -233,3 +233,26 @@ def test_cli_against_cluster(cluster, tmp_path, capsys, monkeypatch):
     assert cli.main(base + ["model", "describe", "mymodel"]) == 0
     out = capsys.readouterr().out
     assert "mymodel" in out and cks[0]["uuid"] in out
+
+
+def test_profiler_ships_timings_and_system_metrics(cluster):
+    """profiling.enabled: the trial's ProfilerAgent samples system metrics and the loop timings
+    and the master serves them back by series (reference profiler.py + _pytorch_trial.py:883-932)."""
+    m, s, ctx, _ = cluster
+    eid = _create(s, ctx, BASE + "searcher: {name: single, metric: val_loss, max_length: {batches: 48}}\n"
+                  "profiling: {enabled: true, begin_on_batch: 0}\n")
+    assert _wait(s, eid) == "COMPLETED"
+    tid = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]["id"]
+    labels = s.get(f"/api/v1/trials/{tid}/profiler/available_series")["labels"]
+    by_type = {}
+    for lab in labels:
+        by_type.setdefault(lab["metricType"], set()).add(lab["name"])
+    assert {"train_batch", "dataloader_next", "step_lr_schedulers", "from_device"} <= by_type["PROFILER_METRIC_TYPE_TIMING"]
+    assert "samples_per_second" in by_type["PROFILER_METRIC_TYPE_MISC"]
+    assert {"cpu_util_simple", "free_memory"} <= by_type["PROFILER_METRIC_TYPE_SYSTEM"]
+    tb = s.get(f"/api/v1/trials/{tid}/profiler/metrics",
+               params={"labels.name": "train_batch", "labels.metric_type": "PROFILER_METRIC_TYPE_TIMING"})["batches"]
+    assert len(tb) == 1 and tb[0]["labels"]["trialId"] == tid
+    assert tb[0]["batches"] == list(range(48)) and all(v >= 0 for v in tb[0]["values"])
+    sysb = s.get(f"/api/v1/trials/{tid}/profiler/metrics", params={"labels.name": "cpu_util_simple"})["batches"]
+    assert sysb and len(sysb[0]["values"]) == len(sysb[0]["timestamps"]) >= 1

@@ -149,3 +149,28 @@ def test_core_distributed_context_collectives():
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_worker_core, args=(2, _free_port(), d), nprocs=2, start_method="spawn")
         assert os.path.exists(os.path.join(d, "ok0")) and os.path.exists(os.path.join(d, "ok1"))
+
+
+def _worker_dist_after_close(rank: int, world: int, port: int, out_dir: str) -> None:
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "LOCAL_WORLD_SIZE": str(world)})
+    from determined_clone_amd import core
+
+    # from_torch_distributed() initialises the default group itself here
+    with core.init(distributed=core.DistributedContext.from_torch_distributed()) as ctx:
+        assert ctx.distributed.allgather(rank) == list(range(world))
+    # user code keeps using torch.distributed after the Core API context closed
+    t = torch.tensor([rank + 1.0])
+    torch.distributed.all_reduce(t)
+    torch.distributed.barrier()
+    assert t.item() == sum(range(1, world + 1))
+    open(os.path.join(out_dir, f"ok{rank}"), "w").close()
+    torch.distributed.destroy_process_group()
+
+
+def test_default_group_survives_core_context_close():
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_dist_after_close, args=(2, port, d), nprocs=2, join=True)
+        assert sorted(os.listdir(d)) == ["ok0", "ok1"]

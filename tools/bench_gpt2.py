@@ -108,7 +108,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     a = ap.parse_args()
+    from determined_clone_amd.launch import ranks
+
+    if ranks.needs_launch(a.gpus):  # --gpus N without a launcher: start the N ranks as a child
+        raise SystemExit(ranks.run_as_ranks(__file__, sys.argv[1:], a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        raise SystemExit(f"bench_gpt2.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     hp = {"model": a.model, "micro": a.micro, "gas": a.gas, "seq": a.seq, "stage": a.stage,
           "warmup": a.warmup, "steps": a.steps}
     with det_ds.init(hparams=hp, exp_conf={}) as ctx:
@@ -119,8 +125,13 @@ def main():
         if trial.t1 is None:
             trial.t1 = trial._mark()
         ms = (trial.t1 - trial.t0) / a.steps * 1000.0
+        backend, pg_size = "none", 1
         if ctx.distributed.size > 1:
             ms = max(ctx.distributed.allgather(ms))
+            backend, pg_size = str(torch.distributed.get_backend()), torch.distributed.get_world_size()
+        wdt = next(p.dtype for p in trial.model.parameters())
+        dtype = {torch.bfloat16: "bf16", torch.float16: "fp16", torch.float32: "fp32"}.get(wdt, str(wdt))
+        where = "resident in HBM" if torch.cuda.is_available() else "in host memory (CPU run)"
         tokens = a.micro * a.gas * a.seq * world
         tps = tokens / (ms / 1000.0)
         fpt = trial.model.flops_per_token(a.seq)
@@ -129,8 +140,9 @@ def main():
                 "metric": f"tokens/sec {a.model} DeepSpeedTrial ZeRO-{a.stage}", "value": round(tps, 1),
                 "unit": "tokens/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                 "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-                "vs_baseline": None, "dtype": "bf16",
-                "data": "synthetic (random tokens resident in HBM, random-init weights)",
+                "vs_baseline": None, "dtype": dtype,
+                "data": f"synthetic (random tokens {where}, random-init weights)",
+                "world_size": pg_size, "backend": backend,
                 "tflops_per_gpu": round(tps * fpt / world / 1e12, 1),
                 "config": {"model": a.model, "global_batch": a.micro * a.gas * world, "seq_len": a.seq,
                            "parallelism": f"zero{a.stage}-dp{world}", "micro_batch": a.micro,
