@@ -10,6 +10,9 @@ architecture is defined here. It is laid out for MI355X rather than copied:
   GPU runs the hand-written NHWC HIP kernels in ``ops/csrc/batchnorm.hip`` (stats + apply + add +
   ReLU in two passes over HBM instead of four separate PyTorch ops); BN affine params and running
   stats stay fp32 while activations are bf16;
+* 3x3 convolutions run on the hand-written implicit-GEMM MFMA kernel (``ops/csrc/conv_igemm.hip``,
+  forward + stride-1 data gradient), whose forward epilogue also reduces the following
+  BatchNorm's statistics;
 * 1x1/stride-1 convolutions go through ``ops.conv.pointwise_conv``: MIOpen by default (measured
   faster), or with ``DCA_CONV1X1=1`` hand-written MFMA GEMM kernels (``ops/csrc/conv1x1.hip``)
   whose forward epilogue also reduces the next BatchNorm's statistics;
@@ -95,7 +98,8 @@ class Bottleneck(nn.Module):
                 y1, yd = pointwise_dual(self.conv1, ds_conv, x)
             identity = ds_bn(yd)
             out = self.bn1(y1)
-        out = self.bn2(conv_ops.spatial_conv(self.conv2, out))
+        # 3x3: implicit-GEMM MFMA kernel whose epilogue also reduces bn2's statistics
+        out = self.bn2(conv_ops.spatial_conv(self.conv2, out, self.bn2.training))
         # identity shortcut: x also feeds conv1, so its gradient can be summed inside the
         # producer's BN backward (no separate autograd add)
         return self.bn3(pointwise_conv(self.conv3, out, self.bn3.training), residual=identity,

@@ -392,9 +392,74 @@ def stem_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
     return spatial_conv(conv, x)
 
 
-def spatial_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
-    """``conv(x)``; on a GPU its weight (and bias) gradient runs on the side stream
-    (``ops/_grad.py``)."""
+# ----------------------------------------------------------------------------- k x k implicit GEMM
+# ResNet-50's 3x3 convolutions on the hand-written MFMA implicit-GEMM kernel (csrc/conv_igemm.hip):
+# the forward also emits the following BatchNorm's per-block statistics (its reduce pass over HBM
+# is skipped), the stride-1 data gradient runs on the same kernel (flipped, transposed weight).
+# Measured at bs 1024 against MIOpen (tools/bench_igemm.py, profiles/round4_igemm_v2_stages.txt):
+# forward at parity (5.23 vs 5.18 ms per step, before counting the statistics pass it removes),
+# stride-1 data gradient 4.16 vs 5.56 ms. Stride-2 data gradients and every weight gradient stay
+# on MIOpen (the latter on the side stream). DCA_IGEMM=0 routes everything back to MIOpen.
+IGEMM = os.environ.get("DCA_IGEMM", "1") != "0"
+
+
+def igemm_supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    if not (IGEMM and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16):
+        return False
+    w = conv.weight
+    k = conv.kernel_size
+    if k[0] != k[1] or k[0] < 2 or conv.stride[0] != conv.stride[1] or conv.groups != 1:
+        return False
+    if conv.dilation != (1, 1) or conv.bias is not None or conv.padding_mode != "zeros":
+        return False
+    if not isinstance(conv.padding, tuple) or conv.padding[0] != conv.padding[1] or conv.padding[0] >= k[0]:
+        return False
+    if conv.in_channels % 64 or conv.out_channels % 64 or w.dtype != torch.bfloat16:
+        return False
+    if not w.is_contiguous(memory_format=torch.channels_last) or torch.is_autocast_enabled():
+        return False
+    n, c, h, ww = x.shape
+    return n * c * h * ww < 2 ** 31 and n * conv.out_channels * h * ww < 2 ** 31
+
+
+class _IgemmConv(torch.autograd.Function):
+    """k x k convolution on conv_igemm.hip; returns ``(y, bn_partials)``."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad, stats):
+        y, partial = _ext.load().conv_igemm_fwd(x, weight, stride, pad, stats)
+        ctx.save_for_backward(x, weight)
+        ctx.stride, ctx.pad = stride, pad
+        if partial is not None:
+            ctx.mark_non_differentiable(partial)
+        return y, partial
+
+    @staticmethod
+    def backward(ctx, dy, _dpartial):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        st, pad = ctx.stride, ctx.pad
+        args = (dy, x, w, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1)
+        dw = _wgrad(args, w) if ctx.needs_input_grad[1] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if st == 1:
+                dx = _ext.load().conv_igemm_dgrad(dy, w, pad)
+            else:
+                dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
+        return dx, dw, None, None, None
+
+
+def spatial_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> torch.Tensor:
+    """``conv(x)``; on a GPU, k x k bf16 convolutions run on the implicit-GEMM kernel (with
+    ``bn_stats`` the output carries the following BatchNorm's partial statistics), others on
+    MIOpen with the weight (and bias) gradient on the side stream (``ops/_grad.py``)."""
+    if igemm_supported(conv, x):
+        x = x.contiguous(memory_format=torch.channels_last)
+        y, partial = _IgemmConv.apply(x, conv.weight, conv.stride[0], conv.padding[0], bool(bn_stats))
+        if partial is not None:
+            y._dca_bn_partials = partial
+        return y
     if (_grad.SIDE_STREAM and x.is_cuda and conv.groups == 1 and conv.dilation == (1, 1)
             and isinstance(conv.padding, tuple) and conv.training and conv.weight.requires_grad
             and conv.padding_mode == "zeros"):

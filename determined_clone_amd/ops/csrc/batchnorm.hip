@@ -464,26 +464,32 @@ inline int reduce_blocks(int64_t M, int C, const ReduceGeom& g) {
   return static_cast<int>(b);
 }
 
-// Apply-pass tuning (A/B sweeps only): DCA_BN_APPLY="U,max_blocks" -- rows in flight per lane
-// (2 | 4 | 8) and the workgroup cap.
+// Apply-pass geometry. Large tensors (>= 32M elements) run as an almost one-shot grid: 2 rows
+// in flight per lane and no workgroup cap (each workgroup does 2 unrolled iterations), which
+// streams at 5.4-5.7 TB/s on the bs-1024 ResNet-50 shapes against 4.9-5.3 for the old 8-per-CU
+// grid with 4 rows per lane (tools/bench_bn.py, profiles/round4_bn_apply_oneshot_ab.txt; the
+// one-shot copy ceiling of this box is 6.16 TB/s, profiles/round4_hbm_streaming_ceilings.txt);
+// smaller tensors keep 4 rows per lane and the 2048-workgroup cap.
+// DCA_BN_APPLY="U,max_blocks" (U in 2 | 4 | 8) forces one geometry (A/B sweeps only).
 struct ApplyTuning {
   int u, max_blocks;
 };
-inline const ApplyTuning& apply_tuning() {
-  static const ApplyTuning t = [] {
-    ApplyTuning r{kUApply, 2048};
+inline ApplyTuning apply_tuning(int64_t elems) {
+  static const ApplyTuning forced = [] {
+    ApplyTuning r{0, 0};
     if (const char* e = std::getenv("DCA_BN_APPLY")) {
       int u = 0, mb = 0;
       if (std::sscanf(e, "%d,%d", &u, &mb) == 2 && (u == 2 || u == 4 || u == 8) && mb > 0) r = {u, mb};
     }
     return r;
   }();
-  return t;
+  if (forced.u) return forced;
+  if (elems >= (int64_t{1} << 25)) return {2, 1 << 30};
+  return {kUApply, 2048};
 }
 
-// Workgroups (in x) for the apply passes: up to 8 per CU, each with >= 2 unrolled iterations.
-inline int apply_blocks(int64_t M, const RowGeom& g) {
-  const ApplyTuning& t = apply_tuning();
+// Workgroups (in x) for the apply passes, each with >= 2 unrolled iterations.
+inline int apply_blocks(int64_t M, const RowGeom& g, const ApplyTuning& t) {
   int64_t b = (M + static_cast<int64_t>(g.rpi) * t.u * 2 - 1) / (static_cast<int64_t>(g.rpi) * t.u * 2);
   if (b > t.max_blocks) b = t.max_blocks;
   if (b < 1) b = 1;
@@ -510,8 +516,9 @@ void launch_apply_fwd(const void* x, const void* res, void* y, const float* scal
                       const float* shift, int64_t M, int C, bool relu, uint8_t* mask,
                       hipStream_t st) {
   const RowGeom g = row_geom(C);
-  dim3 grid(apply_blocks(M, g), g.cgroups);
-  switch (apply_tuning().u) {
+  const ApplyTuning t = apply_tuning(M * C);
+  dim3 grid(apply_blocks(M, g, t), g.cgroups);
+  switch (t.u) {
     case 2: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, 2>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
     case 8: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, 8>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
     default: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
@@ -523,8 +530,9 @@ void launch_apply_bwd(const void* dy, const void* dy2, const uint8_t* mask, cons
                       const float* coef, void* dx, void* dres, int64_t M, int C, bool relu,
                       hipStream_t st) {
   const RowGeom g = row_geom(C);
-  dim3 grid(apply_blocks(M, g), g.cgroups);
-  switch (apply_tuning().u) {
+  const ApplyTuning t = apply_tuning(M * C);
+  dim3 grid(apply_blocks(M, g, t), g.cgroups);
+  switch (t.u) {
     case 2: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 2>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
     case 8: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 8>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
     default: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
@@ -875,7 +883,7 @@ void bn_relu_pool_backward(BnDtype dt, const void* dyp, const uint8_t* idx, cons
   }
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
                      C, M, gamma, save_mean, save_invstd, dgamma, dbeta, false, coef);
-  dim3 ag(apply_blocks(M, rg), rg.cgroups);
+  dim3 ag(apply_blocks(M, rg, ApplyTuning{kUApply, 2048}), rg.cgroups);
   switch (dt) {
     case BnDtype::kBF16: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<BF16, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;
     case BnDtype::kF16: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<F16, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;

@@ -18,4 +18,16 @@ void conv1x1_dgrad(const void* dy, const void* w, void* wt, void* dx, int64_t M,
 int64_t conv1x1_wgrad_ws_floats(int64_t M, int Cin, int Cout);
 void conv1x1_wgrad(const void* dy, const void* x, float* ws, void* dw, bool dw_f32,
                    bool accumulate, int64_t M, int Cin, int Cout, hipStream_t st);
+
+// ---- k x k implicit-GEMM convolutions (conv_igemm.hip). x [N][H][W][C], w [K][R][S][C],
+// y [N][P][Q][K], all bf16; C and K multiples of 64; N*H*W*C and N*P*Q*K below 2^31.
+struct ConvGeom {
+  int N, H, W, C, K, P, Q, R, S, stride, pad, M;  // M = N*P*Q
+};
+// Row blocks of the forward = first dimension of its [blocks][2][K] BatchNorm partial statistics.
+int conv_igemm_row_blocks(const ConvGeom& g);
+void conv_igemm_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
+                    hipStream_t st);
+// w [K][RS][C] -> wt [C][RS][K] with the taps reversed (stride-1 data-gradient weight).
+void conv_flip_transpose(const void* w, void* wt, int K, int C, int RS, hipStream_t st);
 }  // namespace dca

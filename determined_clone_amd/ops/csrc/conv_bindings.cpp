@@ -97,9 +97,82 @@ Tensor conv1x1_wgrad(const Tensor& dy_in, const Tensor& x, const Tensor& w, cons
   return out;
 }
 
+// ---------------------------------------------------------------- k x k implicit GEMM
+void check_nhwc(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4, what,
+              ": bf16 4-D GPU tensor required");
+  TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), what, ": channels_last layout required");
+  TORCH_CHECK(t.size(1) % 64 == 0, what, ": channels must be a multiple of 64");
+  TORCH_CHECK(t.numel() < (int64_t{1} << 31), what, ": tensor too large for 32-bit offsets");
+}
+
+dca::ConvGeom geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(1) == x.size(1),
+              "conv_igemm: weight must be bf16 [K, C, R, S] matching the input channels");
+  TORCH_CHECK(w.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_igemm: weight must be channels_last");
+  TORCH_CHECK(w.size(0) % 64 == 0, "conv_igemm: output channels must be a multiple of 64");
+  TORCH_CHECK(stride >= 1 && pad >= 0, "conv_igemm: bad stride / padding");
+  dca::ConvGeom g;
+  g.N = static_cast<int>(x.size(0));
+  g.C = static_cast<int>(x.size(1));
+  g.H = static_cast<int>(x.size(2));
+  g.W = static_cast<int>(x.size(3));
+  g.K = static_cast<int>(w.size(0));
+  g.R = static_cast<int>(w.size(2));
+  g.S = static_cast<int>(w.size(3));
+  g.stride = static_cast<int>(stride);
+  g.pad = static_cast<int>(pad);
+  g.P = static_cast<int>((g.H + 2 * pad - g.R) / stride + 1);
+  g.Q = static_cast<int>((g.W + 2 * pad - g.S) / stride + 1);
+  TORCH_CHECK(g.P > 0 && g.Q > 0, "conv_igemm: empty output");
+  const int64_t M = static_cast<int64_t>(g.N) * g.P * g.Q;
+  TORCH_CHECK(M * g.K < (int64_t{1} << 31), "conv_igemm: output too large for 32-bit offsets");
+  g.M = static_cast<int>(M);
+  return g;
+}
+
+// y = conv2d(x, w, stride, pad) (no bias); with `stats` also the [blocks, 2, K] BatchNorm partial
+// statistics of y.
+std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad,
+                                   bool stats) {
+  const c10::DeviceGuard dg(x.device());
+  check_nhwc(x, "conv_igemm_fwd");
+  const dca::ConvGeom g = geom(x, w, stride, pad);
+  Tensor y = torch::empty({g.N, g.K, g.P, g.Q}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor partial;
+  if (stats) partial = torch::empty({dca::conv_igemm_row_blocks(g), 2, g.K}, x.options().dtype(at::kFloat));
+  dca::conv_igemm_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                      stats ? partial.data_ptr<float>() : nullptr, g, stream());
+  return {y, partial};
+}
+
+// dx of a stride-1 convolution: the forward kernel on dy with the flipped, transposed weight.
+Tensor conv_igemm_dgrad(const Tensor& dy_in, const Tensor& w, int64_t pad) {
+  const Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const c10::DeviceGuard dg(dy.device());
+  check_nhwc(dy, "conv_igemm_dgrad");
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == dy.size(1) && w.size(1) % 64 == 0 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.scalar_type() == at::kBFloat16,
+              "conv_igemm_dgrad: weight must be bf16 channels_last [K, C, R, S], C a multiple of 64");
+  const int64_t K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(R == S && pad <= R - 1, "conv_igemm_dgrad: square kernels, padding < kernel");
+  // [C, K, R, S] channels_last == physical [C][R][S][K]
+  Tensor wt = torch::empty({C, K, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dca::conv_flip_transpose(w.data_ptr(), wt.data_ptr(), static_cast<int>(K), static_cast<int>(C),
+                           static_cast<int>(R * S), stream());
+  const dca::ConvGeom g = geom(dy, wt, 1, R - 1 - pad);
+  Tensor dx = torch::empty({g.N, g.K, g.P, g.Q}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dca::conv_igemm_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), nullptr, g, stream());
+  return dx;
+}
+
 }  // namespace
 
 void register_conv_ops(pybind11::module& m) {
+  m.def("conv_igemm_fwd", &conv_igemm_fwd, pybind11::arg("x"), pybind11::arg("w"),
+        pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stats"));
+  m.def("conv_igemm_dgrad", &conv_igemm_dgrad, pybind11::arg("dy"), pybind11::arg("w"),
+        pybind11::arg("pad"));
   m.def("conv1x1_fwd", &conv1x1_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stats"));
   m.def("conv1x1_dgrad", &conv1x1_dgrad);
   m.def("conv1x1_wgrad", &conv1x1_wgrad, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"),

@@ -1,0 +1,383 @@
+// k x k NHWC convolutions of the ResNet-50 bottleneck (3x3, stride 1 or 2, padding 1) as implicit
+// GEMMs on gfx950 MFMA, with the following BatchNorm's statistics fused into the forward epilogue.
+//
+// The reference trains torchvision's resnet50 through cuDNN (examples/deepspeed_autotune/
+// torchvision, harness/determined/pytorch/_pytorch_trial.py); on MI355X MIOpen's NHWC solvers run
+// the 3x3 convolutions at 360-900 TFLOP/s (profiles/round3_conv3x3_miopen_bs1024.txt, 28% of the
+// bs-1024 step). GEMM view, NHWC activations and [K][R][S][C] (channels_last) weights:
+//   y[m = (n, p, q)][k] = sum_{(r, s, c)} x[n][p*str + r - pad][q*str + s - pad][c] * w[k][r][s][c]
+// i.e. M = N*P*Q output pixels, Ngemm = K, Kgemm = R*S*C, visited as R*S*C/64 stages of one tap and
+// 64 channels. The stride-1 data gradient is the same kernel on dy with the flipped, transposed
+// weight w'[c][r][s][k] = w[k][R-1-r][S-1-s][c] and padding R-1-pad.
+//
+// Kernel structure (cdna_hip_programming.md §5: 2-phase glds pipeline):
+//  * 256 threads = 4 waves in a WM x WN grid; block tile BM pixels x BN channels; LDS holds two
+//    stages of [BM rows][64] (pixels) + [BN rows][64] (weights), 128-B rows;
+//  * every stage is loaded by global_load_lds_dwordx4 (16 B per lane, 8 rows per wave
+//    instruction, no VGPR staging); the im2col gather is the per-lane SOURCE address: a padding
+//    tap reads a 16-B block of zeros in device memory, so the LDS image stays lane-linear;
+//  * rows are XOR-swizzled in 16-B chunks by (row >> 1) & 7 -- applied to the source chunk a lane
+//    fetches and to the ds_read_b128 fragment address (guide rule 21: both sides or neither), which
+//    makes the 16-lane groups of the MFMA fragment reads conflict-free on 128-B rows;
+//  * v_mfma_f32_32x32x16_bf16 computes the TRANSPOSED tile (rows = output channels, cols = pixels)
+//    so every lane holds 4 consecutive channels of one pixel: the epilogue packs 8-B LDS writes,
+//    streams the tile out with 16-B coalesced stores and -- forward -- reduces per-channel
+//    (sum, sum^2) of the bf16-rounded outputs into batchnorm.hip's partial-statistics layout;
+//  * one barrier per stage: issue the NEXT stage's loads, compute the current one, then
+//    vmcnt(0) + barrier (the "minimum 2-phase" loop of guide T3/T4);
+//  * tiles are dealt XCD-contiguously (neighbouring pixel tiles share input rows in an XCD's L2).
+#include <cstdlib>
+
+#include "common.h"
+#include "conv_api.h"
+
+namespace dca {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kThreads = 256;
+constexpr int kBK = 64;  // k elements (channels of one tap) per stage
+
+// 16-B block of zeros that padding taps read (static device memory is zero-initialised).
+__device__ __attribute__((aligned(64))) uint16_t g_zero_block[32];
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_dst), 16, 0, 0);
+}
+
+__device__ __forceinline__ int xcd_swizzle(int id, int G) {
+  // bijective for any G: block ids that share an XCD (id % 8) get one contiguous range of tiles
+  const int q = G >> 3, r = G & 7, xcd = id & 7, k = id >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Workgroup barrier that does not drain the vector-memory counter; the empty asm keeps the
+// compiler from moving LDS accesses across it.
+__device__ __forceinline__ void barrier_raw() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int NSTAGE, bool STATS>
+__global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+    float* __restrict__ partial, ConvGeom g) {
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int TM = BM / WM, TN = BN / WN;  // wave tile: pixels x channels
+  constexpr int FM = TM / 32, FN = TN / 32;
+  static_assert(FM >= 1 && FN >= 1, "wave tile below one 32x32 MFMA tile");
+  constexpr int A_INS = BM / 32;  // glds per wave per stage (8 rows x 128 B each, 4 waves)
+  constexpr int B_INS = BN / 32;
+  constexpr int STAGE = (BM + BN) * kBK;  // elements per LDS stage
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int NT = g.K / BN;
+  const int t = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int mt = t / NT, nt = t - mt * NT;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int PQ = g.P * g.Q;
+  const int KT = g.R * g.S * (g.C / kBK);
+  const int CT = g.C / kBK;
+
+  // ---- per-lane gather state: for each A instruction, the output pixel's input origin
+  int a_off[A_INS];    // element offset of x[n][ih0][iw0][0] (may be "negative" for pad rows)
+  int a_ih[A_INS], a_iw[A_INS];
+  int a_chunk[A_INS];  // source 16-B chunk (0..7) this lane fetches (swizzle inverse)
+#pragma unroll
+  for (int i = 0; i < A_INS; ++i) {
+    const int j = wv + 4 * i;
+    const int row = 8 * j + (lane >> 3);
+    const int m = m0 + row;
+    a_chunk[i] = (lane & 7) ^ swz(row);
+    if (m < g.M) {
+      const int n = m / PQ, rem = m - n * PQ, p = rem / g.Q, q = rem - p * g.Q;
+      a_ih[i] = p * g.stride - g.pad;
+      a_iw[i] = q * g.stride - g.pad;
+      a_off[i] = ((n * g.H + a_ih[i]) * g.W + a_iw[i]) * g.C;
+    } else {
+      a_ih[i] = -(1 << 20);  // never valid
+      a_iw[i] = 0;
+      a_off[i] = 0;
+    }
+  }
+  const int RSC = g.R * g.S * g.C;
+  int b_off[B_INS];
+#pragma unroll
+  for (int i = 0; i < B_INS; ++i) {
+    const int j = wv + 4 * i;
+    const int row = 8 * j + (lane >> 3);
+    b_off[i] = (n0 + row) * RSC + ((lane & 7) ^ swz(row)) * 8;
+  }
+
+  auto stage = [&](int kt, int buf) {
+    const int tap = kt / CT, cc = kt - tap * CT;
+    const int r = tap / g.S, s = tap - r * g.S;
+    const int tap_off = (r * g.W + s) * g.C + cc * kBK;
+    uint16_t* As = lds + buf * STAGE;
+    uint16_t* Bs = As + BM * kBK;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+      const int j = wv + 4 * i;
+      const bool ok = static_cast<unsigned>(a_ih[i] + r) < static_cast<unsigned>(g.H) &&
+                      static_cast<unsigned>(a_iw[i] + s) < static_cast<unsigned>(g.W);
+      const uint16_t* src = ok ? x + (a_off[i] + tap_off + a_chunk[i] * 8) : g_zero_block;
+      glds16(src, As + j * 8 * kBK);
+    }
+    const int wk = tap * g.C + cc * kBK;
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) {
+      const int j = wv + 4 * i;
+      glds16(w + b_off[i] + wk, Bs + j * 8 * kBK);
+    }
+  };
+
+  const int wm = wv % WM, wn = wv / WM;
+  const int r32 = lane & 31, h = lane >> 5;
+
+  f32x16 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // NSTAGE-deep LDS ring: stages kt+1 .. kt+NSTAGE-1 are in flight while stage kt is computed.
+  // Every wave issues LPS loads per stage, so "stage kt+1 landed" is vmcnt(LPS * (stages issued
+  // after it)); raw s_barrier (not __syncthreads, which would drain vmcnt to 0) publishes it.
+  constexpr int LPS = A_INS + B_INS;
+#pragma unroll
+  for (int p = 0; p < NSTAGE - 1; ++p)
+    if (p < KT) stage(p, p);
+  if constexpr (NSTAGE == 3) {
+    if (KT > 1) wait_vmcnt<LPS>();
+    else wait_vmcnt<0>();
+  } else {
+    wait_vmcnt<0>();
+  }
+  barrier_raw();
+  int buf = 0;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int ahead = kt + NSTAGE - 1;
+    if (ahead < KT) {
+      int nb = buf + NSTAGE - 1;
+      if (nb >= NSTAGE) nb -= NSTAGE;
+      stage(ahead, nb);
+    }
+    const uint16_t* As = lds + buf * STAGE;
+    const uint16_t* Bs = As + BM * kBK;
+#pragma unroll
+    for (int ks = 0; ks < kBK / 16; ++ks) {
+      const int cidx = 2 * ks + h;
+      bf16x8 a[FN], b[FM];
+#pragma unroll
+      for (int i = 0; i < FN; ++i) {
+        const int row = wn * TN + i * 32 + r32;
+        a[i] = *reinterpret_cast<const bf16x8*>(Bs + row * kBK + ((cidx ^ swz(row)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int row = wm * TM + j * 32 + r32;
+        b[j] = *reinterpret_cast<const bf16x8*>(As + row * kBK + ((cidx ^ swz(row)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+    }
+    // stage kt+1 must have landed; later stages may stay in flight
+    if constexpr (NSTAGE == 3) {
+      if (kt + 2 < KT) wait_vmcnt<LPS>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    barrier_raw();
+    buf = buf + 1 == NSTAGE ? 0 : buf + 1;
+  }
+
+  // ---- epilogue: bf16 tile -> LDS [BM][BN + 8] -> 16-B coalesced stores (+ BN statistics)
+  constexpr int CS = BN + 8;
+  uint16_t* Cs = lds;
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int m = wm * TM + j * 32 + r32;
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const int n = wn * TN + i * 32 + 8 * q4 + 4 * h;
+        uint2 pk;
+        pk.x = pack_bf16x2(acc[i][j][4 * q4 + 0], acc[i][j][4 * q4 + 1]);
+        pk.y = pack_bf16x2(acc[i][j][4 * q4 + 2], acc[i][j][4 * q4 + 3]);
+        *reinterpret_cast<uint2*>(Cs + m * CS + n) = pk;
+      }
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;          // 16-B chunks per output row
+  constexpr int RPP = kThreads / CPR;  // rows per pass
+  const int cc = tid % CPR, rr = tid / CPR;
+  float s8[8], q8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
+  for (int row = rr; row < BM; row += RPP) {
+    if (m0 + row >= g.M) break;
+    const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CS + cc * 8);
+    *reinterpret_cast<uint4*>(y + static_cast<int64_t>(m0 + row) * g.K + n0 + cc * 8) = v;
+    if (STATS) {
+      const float f[8] = {bf16_lo(v.x), bf16_hi(v.x), bf16_lo(v.y), bf16_hi(v.y),
+                          bf16_lo(v.z), bf16_hi(v.z), bf16_lo(v.w), bf16_hi(v.w)};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] = fmaf(f[k], f[k], q8[k]); }
+    }
+  }
+  if (STATS) {
+    // partial[mt][0][k] = sum, partial[mt][1][k] = sum of squares (batchnorm.hip layout)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);  // [RPP][CPR * 16]
+    constexpr int width = CPR * 16;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[rr * width + cc * 16 + k] = s8[k];
+      red[rr * width + cc * 16 + 8 + k] = q8[k];
+    }
+    __syncthreads();
+    for (int o = tid; o < width; o += kThreads) {
+      float a = 0.f;
+      for (int j = 0; j < RPP; ++j) a += red[j * width + o];
+      const int ch = n0 + (o >> 4) * 8 + (o & 7);
+      partial[(static_cast<int64_t>(mt) * 2 + ((o >> 3) & 1)) * g.K + ch] = a;
+    }
+  }
+}
+
+// w [K][R][S][C] -> wt [C][R][S][K] with the taps flipped (the stride-1 data-gradient weight).
+__global__ __launch_bounds__(kThreads) void flip_transpose_kernel(const uint16_t* __restrict__ w,
+                                                                  uint16_t* __restrict__ wt, int K,
+                                                                  int C, int RS) {
+  __shared__ uint16_t tile[64][65];
+  const int tap = blockIdx.z;
+  const int k0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += kThreads) {
+    const int kk = i / 64, c = i % 64;
+    if (k0 + kk < K && c0 + c < C)
+      tile[kk][c] = w[(static_cast<int64_t>(k0 + kk) * RS + tap) * C + c0 + c];
+  }
+  __syncthreads();
+  const int ftap = RS - 1 - tap;
+  for (int i = threadIdx.x; i < 64 * 64; i += kThreads) {
+    const int c = i / 64, kk = i % 64;
+    if (k0 + kk < K && c0 + c < C)
+      wt[(static_cast<int64_t>(c0 + c) * RS + ftap) * K + k0 + kk] = tile[kk][c];
+  }
+}
+
+struct Cfg {
+  int bm, bn;
+};
+
+Cfg pick(const ConvGeom& g) {
+  static const int force_bm = [] {
+    const char* e = std::getenv("DCA_IGEMM_BM");  // tuning sweeps only
+    return e ? std::atoi(e) : 0;
+  }();
+  static const int force_bn = [] {
+    const char* e = std::getenv("DCA_IGEMM_BN");
+    return e ? std::atoi(e) : 0;
+  }();
+  Cfg c;
+  c.bn = g.K % 128 == 0 ? 128 : 64;
+  if (force_bn == 64 || (force_bn == 128 && g.K % 128 == 0)) c.bn = force_bn;
+  // 256 x 64 (80 KB of stages) and 128 x 128 (64 KB) both keep two workgroups per CU; 256 x 128
+  // (96 KB) would keep one and measured 10-20% slower (profiles/round4_igemm_v2_stages.txt)
+  c.bm = c.bn == 64 ? 256 : 128;
+  if (force_bm == 128 || force_bm == 256) c.bm = force_bm;
+  return c;
+}
+
+// LDS ring depth: 2 (two workgroups per CU fit for tiles up to 80 KB of stages, which measured
+// faster than a 3-deep ring at one workgroup per CU: profiles/round4_igemm_v2_stages.txt);
+// DCA_IGEMM_STAGES=3 for sweeps.
+int stages() {
+  static const int v = [] {
+    const char* e = std::getenv("DCA_IGEMM_STAGES");
+    return e && std::atoi(e) == 3 ? 3 : 2;
+  }();
+  return v;
+}
+
+template <int BM, int BN, int NSTAGE, bool STATS>
+void launch_fwd_n(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
+                  hipStream_t st) {
+  constexpr int WM = BN >= 128 ? 2 : 4, WN = 4 / WM;
+  constexpr size_t stage = static_cast<size_t>(BM + BN) * kBK * 2 * NSTAGE;
+  constexpr size_t epi = static_cast<size_t>(BM) * (BN + 8) * 2;
+  constexpr size_t lds = stage > epi ? stage : epi;
+  const int grid = static_cast<int>((static_cast<int64_t>(g.M) + BM - 1) / BM * (g.K / BN));
+  auto kern = conv_fwd_kernel<BM, BN, WM, WN, NSTAGE, STATS>;
+  static const bool attr = [&] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, st,
+                     static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w),
+                     static_cast<uint16_t*>(y), partial, g);
+}
+
+template <int BM, int BN, bool STATS>
+void launch_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
+                hipStream_t st) {
+  if (stages() == 3) launch_fwd_n<BM, BN, 3, STATS>(x, w, y, partial, g, st);
+  else launch_fwd_n<BM, BN, 2, STATS>(x, w, y, partial, g, st);
+}
+
+template <bool STATS>
+void fwd_dispatch(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
+                  hipStream_t st) {
+  const Cfg c = pick(g);
+  if (c.bn == 128) {
+    if (c.bm == 256) launch_fwd<256, 128, STATS>(x, w, y, partial, g, st);
+    else launch_fwd<128, 128, STATS>(x, w, y, partial, g, st);
+  } else {
+    if (c.bm == 256) launch_fwd<256, 64, STATS>(x, w, y, partial, g, st);
+    else launch_fwd<128, 64, STATS>(x, w, y, partial, g, st);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ host API
+int conv_igemm_row_blocks(const ConvGeom& g) {
+  const Cfg c = pick(g);
+  return static_cast<int>((static_cast<int64_t>(g.M) + c.bm - 1) / c.bm);
+}
+
+void conv_igemm_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
+                    hipStream_t st) {
+  if (partial) fwd_dispatch<true>(x, w, y, partial, g, st);
+  else fwd_dispatch<false>(x, w, y, nullptr, g, st);
+}
+
+void conv_flip_transpose(const void* w, void* wt, int K, int C, int RS, hipStream_t st) {
+  hipLaunchKernelGGL(flip_transpose_kernel, dim3((C + 63) / 64, (K + 63) / 64, RS), dim3(kThreads),
+                     0, st, static_cast<const uint16_t*>(w), static_cast<uint16_t*>(wt), K, C, RS);
+}
+
+}  // namespace dca

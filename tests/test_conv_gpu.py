@@ -298,3 +298,91 @@ def test_pointwise_dgrad_accumulates_into_shortcut_gradient(monkeypatch):
     rel = [((a - b).norm() / (a.norm() + 1e-12)).item() for a, b in zip(*grads)]
     assert max(rel) < 0.1, max(zip(rel, names))
     assert sorted(rel)[len(rel) // 2] < 0.02, sorted(rel)[len(rel) // 2]
+
+
+# ----------------------------------------------------------------------------- implicit GEMM (3x3)
+IGEMM_SHAPES = [
+    # (N, C, H, K, stride): ResNet-50 3x3 shapes (small batch) + ragged pixel counts
+    (2, 64, 56, 64, 1), (2, 128, 56, 128, 2), (3, 128, 28, 128, 1), (2, 256, 28, 256, 2),
+    (4, 256, 14, 256, 1), (3, 512, 14, 512, 2), (5, 512, 7, 512, 1), (1, 64, 5, 128, 1),
+    (1, 192, 9, 64, 2),
+]
+
+
+def _igemm_inputs(n, c, h, k, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(n, c, h, h, generator=g).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(k, c, 3, 3, generator=g) / (9 * c) ** 0.5).cuda().bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    return x, w
+
+
+@pytest.mark.parametrize("shape", IGEMM_SHAPES)
+def test_conv_igemm_forward_stats_and_dgrad(shape):
+    """Forward + fused BN statistics + stride-1 data gradient vs fp32 convolutions."""
+    C = _ext.load()
+    n, c, h, k, st = shape
+    x, w = _igemm_inputs(n, c, h, k)
+    y, partial = C.conv_igemm_fwd(x, w, st, 1, True)
+    ref = F.conv2d(x.float(), w.float(), stride=st, padding=1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    _close(y, ref, 1e-2, "y")
+    yc = y.float().permute(0, 2, 3, 1).reshape(-1, k)
+    got = partial.sum(0)
+    torch.testing.assert_close(got[0], yc.sum(0), atol=1e-2 * yc.shape[0] ** 0.5, rtol=1e-3)
+    torch.testing.assert_close(got[1], (yc * yc).sum(0), atol=1e-2, rtol=1e-3)
+    y2, p2 = C.conv_igemm_fwd(x, w, st, 1, False)
+    assert p2 is None
+    torch.testing.assert_close(y2, y, atol=0, rtol=0)
+    if st == 1:
+        g = torch.Generator(device="cpu").manual_seed(1)
+        dy = torch.randn(ref.shape, generator=g).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+        dref = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [1, 1], [1, 1],
+                                                   [1, 1], False, [0, 0], 1, [True, False, False])[0]
+        _close(C.conv_igemm_dgrad(dy, w, 1), dref, 1e-2, "dx")
+
+
+def test_conv_igemm_asymmetric_weight_orientation():
+    """A weight that is non-zero at ONE tap and ONE (k, c) pair: catches transposed taps /
+    swapped channel maps that random data can hide."""
+    C = _ext.load()
+    x, w = _igemm_inputs(2, 64, 9, 64)
+    w = torch.zeros_like(w)
+    w[5, 17, 0, 2] = 1.0  # k=5 reads channel 17 at tap (r=0, s=2)
+    y, _ = C.conv_igemm_fwd(x, w, 1, 1, False)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    torch.testing.assert_close(y.float(), ref, atol=0, rtol=0)
+    dy = torch.zeros_like(y)
+    dy[0, 5, 4, 4] = 1.0
+    dx = C.conv_igemm_dgrad(dy, w, 1)
+    dref = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [1, 1], [1, 1],
+                                               [1, 1], False, [0, 0], 1, [True, False, False])[0]
+    torch.testing.assert_close(dx.float(), dref, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_spatial_conv_igemm_autograd_and_bn(stride):
+    """conv3x3 -> fused BN through the model path: output, BN statistics source, input and weight
+    gradients against the fp32 PyTorch composition."""
+    torch.manual_seed(0)
+    conv_m = nn.Conv2d(128, 128, 3, stride=stride, padding=1, bias=False).cuda().bfloat16().to(
+        memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(128).cuda()
+    x = torch.randn(4, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    assert conv.igemm_supported(conv_m, x)
+    y = conv.spatial_conv(conv_m, x, bn_stats=True)
+    assert getattr(y, "_dca_bn_partials", None) is not None
+    out = batchnorm.batch_norm_act(y, bn.weight, bn.bias, bn.running_mean.clone(), bn.running_var.clone(),
+                                   training=True, momentum=0.1, eps=1e-5, relu=True)
+    g = torch.randn_like(out)
+    out.backward(g)
+    x32 = x.detach().float().requires_grad_(True)
+    w32 = conv_m.weight.detach().float().requires_grad_(True)
+    ref = F.relu(F.batch_norm(F.conv2d(x32, w32, stride=stride, padding=1), None, None, bn.weight.float(),
+                              bn.bias.float(), training=True, eps=1e-5))
+    ref.backward(g.float())
+    _close(out, ref.detach(), 3e-2, "bn(conv(x))")
+    _close(x.grad, x32.grad, 5e-2, "dx")
+    wg = conv_m.weight.grad
+    _close(wg, w32.grad, 5e-2, "dw")
