@@ -34,6 +34,19 @@ class StorageManager:
     def list_files(self, storage_id: str) -> Dict[str, int]:
         raise NotImplementedError
 
+    def store_path_is_direct_access(self) -> bool:
+        """True when ``store_path`` yields the storage location itself (files written there ARE
+        the checkpoint; sharded writers share it). Object stores stage locally and upload."""
+        return False
+
+    def pre_store_path(self, dst: str) -> pathlib.Path:
+        """A fresh local staging directory for one writer of checkpoint ``dst``."""
+        return pathlib.Path(tempfile.mkdtemp(prefix=f"dca-ckpt-{dst[:8]}-"))
+
+    def post_store_path(self, path: Union[str, os.PathLike]) -> None:
+        """Remove a staging directory from :meth:`pre_store_path` (after its upload)."""
+        shutil.rmtree(path, ignore_errors=True)
+
     @contextlib.contextmanager
     def store_path(self, dst: str) -> Iterator[pathlib.Path]:
         tmp = tempfile.mkdtemp(prefix="dca-ckpt-")
@@ -71,6 +84,17 @@ class SharedFSStorageManager(StorageManager):
     def __init__(self, base_path: str) -> None:
         super().__init__(base_path)
         os.makedirs(self._base_path, exist_ok=True)
+
+    def store_path_is_direct_access(self) -> bool:
+        return True
+
+    def pre_store_path(self, dst: str) -> pathlib.Path:
+        p = self.path(dst)
+        p.mkdir(parents=True, exist_ok=True)
+        return p
+
+    def post_store_path(self, path: Union[str, os.PathLike]) -> None:
+        pass  # the checkpoint directory itself
 
     def path(self, storage_id: str) -> pathlib.Path:
         return pathlib.Path(self._base_path) / storage_id

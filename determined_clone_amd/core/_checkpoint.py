@@ -7,6 +7,7 @@ own files into the same checkpoint (ZeRO optimizer shards, per-rank RNG), merged
 """
 import contextlib
 import enum
+import hashlib
 import json
 import logging
 import os
@@ -24,32 +25,56 @@ class DownloadMode(enum.Enum):
     NoSharedDownload = "NO_SHARED_DOWNLOAD"
 
 
-def merge_metadata(base: Dict[str, Any], other: Dict[str, Any]) -> Tuple[Dict[str, Any], List[str]]:
-    """Merge two metadata dicts; returns (merged, conflicting_keys)."""
-    out = dict(base)
-    conflicts = []
-    for k, v in other.items():
-        if k in out and out[k] != v:
-            if isinstance(out[k], dict) and isinstance(v, dict):
-                sub, c = merge_metadata(out[k], v)
-                out[k] = sub
-                conflicts += [f"{k}.{x}" for x in c]
+def _merge_md(merged: Dict[str, Any], md: Dict[str, Any], rank: int, owners: Dict[str, Any],
+              conflicts: Dict[str, List[int]], prefix: str) -> None:
+    for k, v in md.items():
+        full = f"{prefix}{k}"
+        if k not in merged:
+            if isinstance(v, dict):
+                merged[k], owners[k] = {}, {}
+                _merge_md(merged[k], v, rank, owners[k], conflicts, full + ".")
             else:
-                conflicts.append(k)
+                merged[k], owners[k] = v, [rank]
+            continue
+        cur = merged[k]
+        if isinstance(cur, dict) and isinstance(v, dict):
+            _merge_md(cur, v, rank, owners[k], conflicts, full + ".")
+        elif isinstance(cur, dict) or isinstance(v, dict) or cur != v:
+            prev = owners[k] if isinstance(owners[k], list) else []
+            conflicts[full] = sorted(set(conflicts.get(full, prev) + [rank]))
         else:
-            out[k] = v
-    return out, conflicts
+            owners[k].append(rank)
 
 
-def merge_resources(all_resources: List[Dict[str, int]]) -> Tuple[Dict[str, int], List[str]]:
-    out: Dict[str, int] = {}
-    conflicts = []
-    for res in all_resources:
-        for k, v in res.items():
-            if k in out and not k.endswith("/") and out[k] != v:
-                conflicts.append(k)
-            out[k] = v
-    return out, conflicts
+def merge_metadata(all_metadata: List[Dict[str, Any]]) -> Tuple[Dict[str, Any], Dict[str, List[int]]]:
+    """Merge every rank's metadata (reference core/_checkpoint.py:84-124): dictionaries under one
+    key merge recursively, equal repeated values are fine, anything else is a conflict. Returns
+    ``(merged, {dotted key: ranks that reported it})``."""
+    merged: Dict[str, Any] = {}
+    owners: Dict[str, Any] = {}
+    conflicts: Dict[str, List[int]] = {}
+    for rank, md in enumerate(all_metadata):
+        _merge_md(merged, md or {}, rank, owners, conflicts, "")
+    return merged, conflicts
+
+
+def merge_resources(all_resources: List[Dict[str, int]]) -> Tuple[Dict[str, int], Dict[str, List[int]]]:
+    """Merge every rank's ``{path: size}`` (directories end in ``/``; reference :127-167). Two
+    ranks may both create a directory; a FILE name that more than one rank writes (or that one
+    rank writes as a file and another as a directory) is a conflict: ``{name: ranks}``."""
+    files = set()
+    uploaders: Dict[str, List[int]] = {}
+    merged: Dict[str, int] = {}
+    for rank, rscs in enumerate(all_resources):
+        for name, size in rscs.items():
+            if name.endswith("/") or name.endswith(os.sep):
+                uploaders.setdefault(name.rstrip("/").rstrip(os.sep), []).append(rank)
+            else:
+                files.add(name)
+                uploaders.setdefault(name, []).append(rank)
+            merged[name] = size
+    conflicts = {n: uploaders[n] for n in sorted(files) if len(uploaders[n]) > 1}
+    return merged, conflicts
 
 
 class CheckpointContext:
@@ -66,7 +91,8 @@ class CheckpointContext:
 
     # ------------------------------------------------------------------ writing
     def upload(self, ckpt_dir: Optional[os.PathLike], metadata: Optional[Dict[str, Any]] = None, *,
-               shard: bool = False, selector: Optional[Callable[[str], bool]] = None) -> str:
+               shard: bool = False, selector: Optional[Callable[[str], bool]] = None,
+               _storage_id: Optional[str] = None) -> str:
         if not shard:
             if self._dist.rank != 0:
                 raise RuntimeError("upload(shard=False) may only be called on the chief")
@@ -76,26 +102,31 @@ class CheckpointContext:
             self._storage_manager.upload(ckpt_dir, storage_id, self._selected(ckpt_dir, selector))
             resources = self._storage_manager.list_files(storage_id) if isinstance(
                 self._storage_manager, storage.SharedFSStorageManager) else _local_resources(ckpt_dir)
-            md = self._merge_metadata(metadata)
+            md = dict(metadata or {})
             self._write_metadata(storage_id, md)
             self._report_checkpoint(storage_id, resources, md)
             return storage_id
-        storage_id = self._dist.broadcast(str(uuid.uuid4()) if self._dist.rank == 0 else None)
+        storage_id = _storage_id or self._dist.broadcast(str(uuid.uuid4()) if self._dist.rank == 0 else None)
+        # a directory several local ranks share is uploaded once, by the lowest of them
+        want_upload = ckpt_dir is not None
         if ckpt_dir is not None:
-            self._storage_manager.upload(ckpt_dir, storage_id, self._selected(ckpt_dir, selector))
-        res = _local_resources(ckpt_dir) if ckpt_dir is not None else {}
-        all_res = self._dist.gather(res)
-        all_md = self._dist.gather(metadata or {})
+            st = os.stat(ckpt_dir)
+            uids = self._dist.allgather((os.uname().nodename, st.st_dev, st.st_ino))
+            want_upload = uids.index(uids[self._dist.rank]) == self._dist.rank
+        else:
+            self._dist.allgather(None)
+        res = {}
+        if want_upload:
+            res = _local_resources(ckpt_dir)
+            if selector is not None:
+                res = {k: v for k, v in res.items() if selector(k.rstrip("/"))}
+        merged_res, conflicts = merge_resources(self._dist.allgather(res))
+        res = self._resolve_conflicts(res, conflicts, ckpt_dir)
+        md = self._merge_metadata(metadata)
+        if want_upload and res:
+            self._storage_manager.upload(ckpt_dir, storage_id, [k for k in res if not k.endswith("/")])
+        self._dist.allgather(None)  # every shard is in storage before the chief reports
         if self._dist.rank == 0:
-            merged_res, rc = merge_resources(all_res)
-            if rc:
-                raise RuntimeError(f"sharded checkpoint: ranks wrote conflicting files {rc}")
-            md: Dict[str, Any] = {}
-            for m in all_md:
-                md, mc = merge_metadata(md, m)
-                if mc:
-                    raise RuntimeError(f"sharded checkpoint: conflicting metadata keys {mc}")
-            md = self._merge_metadata(md)
             self._write_metadata(storage_id, md)
             self._report_checkpoint(storage_id, merged_res, md)
         return storage_id
@@ -103,47 +134,113 @@ class CheckpointContext:
     @contextlib.contextmanager
     def store_path(self, metadata: Optional[Dict[str, Any]] = None, *,
                    shard: bool = False) -> Iterator[Tuple[pathlib.Path, str]]:
-        """Yields ``(path, storage_id)``; files written under ``path`` become the checkpoint."""
-        if not shard and self._dist.rank != 0:
-            raise RuntimeError("store_path(shard=False) may only be called on the chief")
-        if shard:
-            storage_id = self._dist.broadcast(str(uuid.uuid4()) if self._dist.rank == 0 else None)
-        else:
-            storage_id = str(uuid.uuid4())
-        with self._storage_manager.store_path(storage_id) as path:
-            yield path, storage_id
-            res = _local_resources(path)
-        if shard:
-            all_res = self._dist.gather(res)
-            all_md = self._dist.gather(metadata or {})
+        """Yields ``(path, storage_id)``; files written under ``path`` become the checkpoint.
+
+        ``shard=False``: chief only. ``shard=True`` (reference core/_checkpoint.py:526-590): every
+        rank must enter; ranks' metadata are merged and a conflicting key raises. On a storage
+        whose ``store_path`` is the storage itself (shared_fs / directory) every rank writes
+        straight into the one checkpoint directory; otherwise each rank writes a local staging
+        directory, a directory shared by several local ranks is uploaded once (lowest rank), a
+        file written by more than one rank raises unless every copy has the same content (then
+        the lowest rank uploads it), exactly as :meth:`upload` with ``shard=True``."""
+        if not shard:
             if self._dist.rank != 0:
-                return
-            res, _ = merge_resources(all_res)
-            md: Dict[str, Any] = {}
-            for m in all_md:
-                md, _ = merge_metadata(md, m)
-            metadata = md
-        md = self._merge_metadata(metadata)
-        self._write_metadata(storage_id, md)
-        if isinstance(self._storage_manager, storage.SharedFSStorageManager):
-            res = self._storage_manager.list_files(storage_id)
-        self._report_checkpoint(storage_id, res, md)
+                raise RuntimeError("store_path(shard=False) may only be called on the chief "
+                                   f"(rank={self._dist.rank})")
+            storage_id = str(uuid.uuid4())
+            with self._storage_manager.store_path(storage_id) as path:
+                yield path, storage_id
+                res = _local_resources(path)
+            md = dict(metadata or {})
+            self._write_metadata(storage_id, md)
+            if isinstance(self._storage_manager, storage.SharedFSStorageManager):
+                res = self._storage_manager.list_files(storage_id)
+            self._report_checkpoint(storage_id, res, md)
+            return
+        storage_id = self._dist.broadcast(str(uuid.uuid4()) if self._dist.rank == 0 else None)
+        if self._storage_manager.store_path_is_direct_access():
+            with self._storage_manager.store_path(storage_id) as path:
+                yield path, storage_id
+            md = self._merge_metadata(metadata)
+            self._dist.allgather(None)  # every rank's files are written
+            if self._dist.rank == 0:
+                self._write_metadata(storage_id, md)
+                self._report_checkpoint(storage_id, self._storage_manager.list_files(storage_id), md)
+            return
+        path = self._storage_manager.pre_store_path(storage_id)
+        try:
+            yield path, storage_id
+            self.upload(path, metadata, shard=True, _storage_id=storage_id)
+        finally:
+            self._storage_manager.post_store_path(path)
 
     # ------------------------------------------------------------------ reading
+    def _coordinated_selector(self, selector: Optional[Callable[[str], bool]]) -> Optional[Callable[[str], bool]]:
+        """On the local chief: a selector that asks every local rank about each file (functions
+        do not serialise, file names do) and keeps a file if any rank wants it (reference
+        core/_checkpoint.py:429-460)."""
+        def sel(path: str) -> bool:
+            self._dist.broadcast_local(path)
+            votes = self._dist.gather_local(selector(path) if selector is not None else True)
+            return any(votes or [True])
+        return sel
+
+    def _serve_local_chief(self, selector: Optional[Callable[[str], bool]]) -> None:
+        """Non-chief local ranks: answer the chief's per-file questions until it says done."""
+        while True:
+            name = self._dist.broadcast_local(None)
+            if name is None:
+                return
+            self._dist.gather_local(selector(name) if selector is not None else True)
+
     def download(self, storage_id: str, ckpt_dir: os.PathLike,
                  download_mode: DownloadMode = DownloadMode.LocalWorkersShareDownload,
                  selector: Optional[Callable[[str], bool]] = None) -> None:
-        if download_mode == DownloadMode.NoSharedDownload or self._dist.local_rank == 0:
+        """Download a checkpoint into ``ckpt_dir``. ``LocalWorkersShareDownload`` (default): every
+        rank calls, only the local chief of each node downloads (the union of the local ranks'
+        selectors); ``NoSharedDownload``: each caller downloads for itself."""
+        download_mode = DownloadMode(download_mode)
+        if download_mode == DownloadMode.NoSharedDownload:
             self._storage_manager.download(storage_id, ckpt_dir, selector)
-        if download_mode == DownloadMode.LocalWorkersShareDownload:
-            self._dist.allgather_local(None)
+            return
+        want_filter = any(self._dist.allgather(selector is not None))
+        if self._dist.local_rank == 0:
+            self._storage_manager.download(storage_id, ckpt_dir,
+                                           self._coordinated_selector(selector) if want_filter else None)
+            self._dist.broadcast_local(None)
+        else:
+            self._serve_local_chief(selector)
 
     @contextlib.contextmanager
     def restore_path(self, storage_id: str,
                      download_mode: DownloadMode = DownloadMode.LocalWorkersShareDownload,
                      selector: Optional[Callable[[str], bool]] = None) -> Iterator[pathlib.Path]:
-        with self._storage_manager.restore_path(storage_id, selector) as p:
-            yield p
+        """Context manager yielding a local path holding the checkpoint (reference :599-675).
+        ``LocalWorkersShareDownload``: all ranks must call; only the local chief of each node
+        downloads (cloud storage) and the others receive its path; the download is removed when
+        every local rank has left the context. ``NoSharedDownload``: each rank for itself."""
+        download_mode = DownloadMode(download_mode)
+        if download_mode == DownloadMode.NoSharedDownload:
+            with self._storage_manager.restore_path(storage_id, selector) as p:
+                yield p
+            return
+        want_filter = any(self._dist.allgather(selector is not None))
+        if self._dist.local_rank == 0:
+            sel = self._coordinated_selector(selector) if want_filter else None
+            with self._storage_manager.restore_path(storage_id, sel) as p:
+                self._dist.broadcast_local(None)  # download finished
+                self._dist.broadcast_local(str(p))
+                try:
+                    yield p
+                finally:
+                    self._dist.gather_local(None)  # local ranks are done with it
+        else:
+            self._serve_local_chief(selector)
+            p = pathlib.Path(self._dist.broadcast_local(None))
+            try:
+                yield p
+            finally:
+                self._dist.gather_local(None)
 
     def get_metadata(self, storage_id: str) -> Dict[str, Any]:
         if isinstance(self._storage_manager, storage.SharedFSStorageManager):
@@ -169,7 +266,38 @@ class CheckpointContext:
         return [str(p.relative_to(root)) for p in root.rglob("*") if selector(str(p.relative_to(root)))]
 
     def _merge_metadata(self, metadata: Optional[Dict[str, Any]]) -> Dict[str, Any]:
-        return dict(metadata or {})
+        merged, conflicts = merge_metadata(self._dist.allgather(metadata or {}))
+        if conflicts:
+            self._raise_conflict_error(conflicts, "metadata")
+        return merged
+
+    def _resolve_conflicts(self, resources: Dict[str, int], conflicts: Dict[str, List[int]],
+                           ckpt_dir: Optional[os.PathLike]) -> Dict[str, int]:
+        """Files written by several ranks are fine when every copy is byte-identical (md5,
+        compared across ranks in sorted name order); the lowest such rank uploads it. Anything
+        else raises (reference core/_checkpoint.py:353-402)."""
+        remaining = dict(conflicts)
+        for fname in sorted(conflicts):
+            digest = None
+            if self._dist.rank in conflicts[fname]:
+                fpath = os.path.join(os.fspath(ckpt_dir), fname)
+                if os.path.isdir(fpath):
+                    digest = "this is a directory"
+                else:
+                    with open(fpath, "rb") as f:
+                        digest = hashlib.md5(f.read()).hexdigest()
+            if len({d for d in self._dist.allgather(digest) if d is not None}) == 1:
+                remaining.pop(fname)
+        if remaining:
+            self._raise_conflict_error(remaining, "files")
+        return {k: v for k, v in resources.items()
+                if k not in conflicts or min(conflicts[k]) == self._dist.rank}
+
+    def _raise_conflict_error(self, conflicts: Dict[str, List[int]], what: str) -> None:
+        if self._dist.rank > 0:
+            raise RuntimeError(f"refusing to upload with {what} conflicts: {conflicts}")
+        lines = [f"    {k} uploaded by ranks {r}" for k, r in sorted(conflicts.items())]
+        raise RuntimeError(f"refusing to upload with {what} conflicts:\n" + "\n".join(lines))
 
     def _write_metadata(self, storage_id: str, md: Dict[str, Any]) -> None:
         if isinstance(self._storage_manager, storage.SharedFSStorageManager):

@@ -166,9 +166,43 @@ Tensor conv_igemm_dgrad(const Tensor& dy_in, const Tensor& w, int64_t pad) {
   return dx;
 }
 
+// Weight gradient of y = conv2d(x, w, stride, pad) given dy; with `acc` (the parameter's
+// persistent .grad view, fp32 or bf16, [K, C, R, S] channels_last) it is added in place and
+// returned.
+Tensor conv_igemm_wgrad(const Tensor& dy_in, const Tensor& x, const Tensor& w, int64_t stride,
+                        int64_t pad, const OptT& acc) {
+  const Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const c10::DeviceGuard dg(dy.device());
+  check_nhwc(x, "conv_igemm_wgrad");
+  check_nhwc(dy, "conv_igemm_wgrad");
+  const dca::ConvGeom g = geom(x, w, stride, pad);
+  TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.K && dy.size(2) == g.P && dy.size(3) == g.Q,
+              "conv_igemm_wgrad: dy shape does not match the convolution output");
+  TORCH_CHECK(g.M < (1 << 24), "conv_igemm_wgrad: at most 2^24 output pixels");
+  Tensor ws = torch::empty({dca::conv_igemm_wgrad_ws_floats(g)}, dy.options().dtype(at::kFloat));
+  Tensor out;
+  bool accumulate = false;
+  if (acc.has_value() && acc->defined()) {
+    out = *acc;
+    TORCH_CHECK(out.device() == dy.device() && out.sizes() == w.sizes() &&
+                    (out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16) &&
+                    out.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_igemm_wgrad: accumulation target must be a channels_last fp32/bf16 tensor shaped like w");
+    accumulate = true;
+  } else {
+    out = torch::empty(w.sizes(), w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
+  dca::conv_igemm_wgrad(dy.data_ptr(), x.data_ptr(), ws.data_ptr<float>(), out.data_ptr(),
+                        out.scalar_type() == at::kFloat, accumulate, g, stream());
+  return out;
+}
+
 }  // namespace
 
 void register_conv_ops(pybind11::module& m) {
+  m.def("conv_igemm_wgrad", &conv_igemm_wgrad, pybind11::arg("dy"), pybind11::arg("x"),
+        pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"),
+        pybind11::arg("acc") = pybind11::none());
   m.def("conv_igemm_fwd", &conv_igemm_fwd, pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stats"));
   m.def("conv_igemm_dgrad", &conv_igemm_dgrad, pybind11::arg("dy"), pybind11::arg("w"),

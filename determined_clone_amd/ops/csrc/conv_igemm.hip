@@ -287,6 +287,237 @@ __global__ __launch_bounds__(kThreads) void flip_transpose_kernel(const uint16_t
   }
 }
 
+// ------------------------------------------------------------------ weight gradient
+// dW[k][r][s][c] = sum_m dy[m][k] * x[n][p*str + r - pad][q*str + s - pad][c]: a GEMM with the
+// 10^4..10^6 output pixels as its reduction. Grid = (k tile, tap, c tile) x pixel splits; each
+// workgroup streams 64-pixel stages of dy [64][BKO] and of the tap-shifted x [64][BC] (zero rows
+// for padding / past the split) into LDS by global_load_lds, and both MFMA operands come out of
+// those m-major images through ds_read_b64_tr_b16 (guide T10): lane (r, h) of a 32x32x16 fragment
+// takes column r of rows 16ks + 8h + 0..7 with two transposed reads, the same rows for dy and x
+// so the k sums match. 16-B chunks are XOR-swizzled by row (f = (row & 3) << 2 on 256-B rows,
+// ((row >> 1) & 1) << 2 on 128-B rows) so the 4 rows x 64 B of a 32-lane transposed read hit 64
+// distinct banks. fp32 split tiles go to a workspace; wgrad_reduce_kernel sums them in a fixed
+// order (deterministic) into dW, optionally accumulating into the parameter's .grad view.
+template <int ROWB>
+__device__ __forceinline__ int wswz(int row) {
+  if constexpr (ROWB == 256) return (row & 3) << 2;
+  return ((row >> 1) & 1) << 2;
+}
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ s16x4 tr_read(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+__device__ __forceinline__ bf16x8 cat8(s16x4 a, s16x4 b) {
+  const s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// floor(a / d) for 0 <= a < 2^24 via the float reciprocal, corrected to exact.
+__device__ __forceinline__ int fdiv(int a, int d, float inv) {
+  int q = static_cast<int>(static_cast<float>(a) * inv);
+  q += (q + 1) * d <= a;
+  q -= q * d > a;
+  return q;
+}
+
+constexpr int kWM = 64;  // pixels per stage
+
+template <int BKO, int BC>
+__global__ __launch_bounds__(kThreads, 2) void conv_wgrad_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, float* __restrict__ ws,
+    ConvGeom g, int rows_per_split, float inv_pq, float inv_q) {
+  constexpr int TA = BKO / 2, TB = BC / 2;  // wave tile (2 x 2 waves)
+  constexpr int FA = TA / 32, FB = TB / 32;
+  constexpr int RA = BKO * 2, RB = BC * 2;          // LDS row bytes
+  constexpr int LA = RA / 16, LB = RB / 16;          // lanes per row in a glds instruction
+  constexpr int IA = kWM * BKO * 2 / 1024 / 4;       // glds per wave per stage
+  constexpr int IB = kWM * BC * 2 / 1024 / 4;
+  constexpr int STAGE = kWM * (BKO + BC);            // elements
+  static_assert(IA >= 1 && IB >= 1, "tile too small");
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int CT = g.C / BC, RS = g.R * g.S;
+  int t = blockIdx.x;
+  const int ct = t % CT;
+  t /= CT;
+  const int tap = t % RS;
+  const int kt = t / RS;
+  const int k0 = kt * BKO, c0 = ct * BC;
+  const int r = tap / g.S, s = tap - r * g.S;
+  const int mb = blockIdx.y * rows_per_split;
+  const int me = min(g.M, mb + rows_per_split);
+  const int PQ = g.P * g.Q;
+
+  auto stage = [&](int m_base, int buf) {
+    uint16_t* As = lds + buf * STAGE;
+    uint16_t* Bs = As + kWM * BKO;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int j = wv + 4 * i;                  // instruction index within the tile
+      const int row = j * (64 / LA) + lane / LA;
+      const int chunk = (lane % LA) ^ wswz<RA>(row);
+      const int m = m_base + row;
+      const uint16_t* src = m < me ? dy + (static_cast<int64_t>(m) * g.K + k0 + chunk * 8) : g_zero_block;
+      glds16(src, As + j * 512);
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int j = wv + 4 * i;
+      const int row = j * (64 / LB) + lane / LB;
+      const int chunk = (lane % LB) ^ wswz<RB>(row);
+      const int m = m_base + row;
+      const uint16_t* src = g_zero_block;
+      if (m < me) {
+        const int n = fdiv(m, PQ, inv_pq), rem = m - n * PQ;
+        const int p = fdiv(rem, g.Q, inv_q), q = rem - p * g.Q;
+        const int ih = p * g.stride - g.pad + r, iw = q * g.stride - g.pad + s;
+        if (static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+            static_cast<unsigned>(iw) < static_cast<unsigned>(g.W))
+          src = x + ((static_cast<int64_t>(n * g.H + ih) * g.W + iw) * g.C + c0 + chunk * 8);
+      }
+      glds16(src, Bs + j * 512);
+    }
+  };
+
+  const int wa = wv & 1, wb = wv >> 1;
+  // transposed read: lane 4q + p of a 16-lane group addresses row q, columns 4p .. 4p+3
+  const int h = lane >> 5, gq = (lane >> 2) & 3, gp = lane & 3, half16 = (lane >> 4) & 1;
+
+  f32x16 acc[FA][FB];
+#pragma unroll
+  for (int i = 0; i < FA; ++i)
+#pragma unroll
+    for (int j = 0; j < FB; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nst = (me - mb + kWM - 1) / kWM;
+  if (nst > 0) stage(mb, 0);
+  wait_vmcnt<0>();
+  barrier_raw();
+  for (int it = 0; it < nst; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < nst) stage(mb + (it + 1) * kWM, buf ^ 1);
+    const uint16_t* As = lds + buf * STAGE;
+    const uint16_t* Bs = As + kWM * BKO;
+#pragma unroll
+    for (int ks = 0; ks < kWM / 16; ++ks) {
+      const int row0 = 16 * ks + 8 * h + gq;  // + 4 for the second read
+      bf16x8 a[FA], b[FB];
+#pragma unroll
+      for (int i = 0; i < FA; ++i) {
+        const int col = wa * TA + i * 32 + half16 * 16 + 4 * gp;
+        const int ch = col >> 3, off = col & 7;
+        const uint16_t* p0 = As + row0 * BKO + (((ch ^ wswz<RA>(row0)) << 3) | off);
+        const uint16_t* p1 = As + (row0 + 4) * BKO + (((ch ^ wswz<RA>(row0 + 4)) << 3) | off);
+        a[i] = cat8(tr_read(p0), tr_read(p1));
+      }
+#pragma unroll
+      for (int j = 0; j < FB; ++j) {
+        const int col = wb * TB + j * 32 + half16 * 16 + 4 * gp;
+        const int ch = col >> 3, off = col & 7;
+        const uint16_t* p0 = Bs + row0 * BC + (((ch ^ wswz<RB>(row0)) << 3) | off);
+        const uint16_t* p1 = Bs + (row0 + 4) * BC + (((ch ^ wswz<RB>(row0 + 4)) << 3) | off);
+        b[j] = cat8(tr_read(p0), tr_read(p1));
+      }
+#pragma unroll
+      for (int i = 0; i < FA; ++i)
+#pragma unroll
+        for (int j = 0; j < FB; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+    }
+    wait_vmcnt<0>();
+    barrier_raw();
+  }
+  // fp32 split tile -> ws[split][k][tap][c] (the weight's own [K][R][S][C] order)
+  float* out = ws + static_cast<int64_t>(blockIdx.y) * g.K * RS * g.C;
+  const int cl = lane & 31;
+#pragma unroll
+  for (int i = 0; i < FA; ++i)
+#pragma unroll
+    for (int j = 0; j < FB; ++j) {
+      const int c = c0 + wb * TB + j * 32 + cl;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int k = k0 + wa * TA + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        out[(static_cast<int64_t>(k) * RS + tap) * g.C + c] = acc[i][j][reg];
+      }
+    }
+}
+
+// dW (+)= sum over splits in a fixed order; 8 elements per thread.
+template <typename OUT>
+__global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(const float* __restrict__ ws,
+                                                                int splits, int64_t n,
+                                                                void* __restrict__ dw,
+                                                                bool accumulate) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (v * 8 >= n) return;
+  float a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = 0.f;
+  for (int sp = 0; sp < splits; ++sp) {
+    float p[8];
+    Vec8<F32>::load(ws + sp * n + v * 8, p);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += p[k];
+  }
+  char* dst = reinterpret_cast<char*>(dw) + v * 8 * Vec8<OUT>::bytes;
+  if (accumulate) {
+    float o[8];
+    Vec8<OUT>::load(dst, o);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += o[k];
+  }
+  Vec8<OUT>::store(dst, a);
+}
+
+struct WgCfg {
+  int bko, bc, splits, rows_per_split;
+};
+
+WgCfg wgrad_cfg(const ConvGeom& g) {
+  static const int target = [] {
+    const char* e = std::getenv("DCA_IGEMM_WG_BLOCKS");  // tuning sweeps only
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 1024;
+  }();
+  WgCfg c;
+  c.bko = g.K % 128 == 0 ? 128 : 64;
+  c.bc = g.C % 128 == 0 ? 128 : 64;
+  const int tiles = (g.K / c.bko) * g.R * g.S * (g.C / c.bc);
+  int64_t sp = (target + tiles - 1) / tiles;
+  const int64_t max_sp = (g.M + 8 * kWM - 1) / (8 * kWM);  // >= 8 stages per split
+  if (sp > max_sp) sp = max_sp;
+  if (sp < 1) sp = 1;
+  int64_t rps = (g.M + sp - 1) / sp;
+  rps = (rps + kWM - 1) / kWM * kWM;
+  c.rows_per_split = static_cast<int>(rps);
+  c.splits = static_cast<int>((g.M + rps - 1) / rps);
+  return c;
+}
+
+template <int BKO, int BC>
+void launch_wgrad(const void* dy, const void* x, float* ws, const ConvGeom& g, const WgCfg& c,
+                  hipStream_t st) {
+  constexpr size_t lds = static_cast<size_t>(kWM) * (BKO + BC) * 2 * 2;
+  const dim3 grid((g.K / BKO) * g.R * g.S * (g.C / BC), c.splits);
+  auto kern = conv_wgrad_kernel<BKO, BC>;
+  static const bool attr = [&] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, st, static_cast<const uint16_t*>(dy),
+                     static_cast<const uint16_t*>(x), ws, g, c.rows_per_split,
+                     1.0f / static_cast<float>(g.P * g.Q), 1.0f / static_cast<float>(g.Q));
+}
+
 struct Cfg {
   int bm, bn;
 };
@@ -373,6 +604,26 @@ void conv_igemm_fwd(const void* x, const void* w, void* y, float* partial, const
                     hipStream_t st) {
   if (partial) fwd_dispatch<true>(x, w, y, partial, g, st);
   else fwd_dispatch<false>(x, w, y, nullptr, g, st);
+}
+
+int64_t conv_igemm_wgrad_ws_floats(const ConvGeom& g) {
+  const WgCfg c = wgrad_cfg(g);
+  return static_cast<int64_t>(c.splits) * g.K * g.R * g.S * g.C;
+}
+
+void conv_igemm_wgrad(const void* dy, const void* x, float* ws, void* dw, bool dw_f32,
+                      bool accumulate, const ConvGeom& g, hipStream_t st) {
+  const WgCfg c = wgrad_cfg(g);
+  if (c.bko == 128 && c.bc == 128) launch_wgrad<128, 128>(dy, x, ws, g, c, st);
+  else if (c.bko == 128) launch_wgrad<128, 64>(dy, x, ws, g, c, st);
+  else if (c.bc == 128) launch_wgrad<64, 128>(dy, x, ws, g, c, st);
+  else launch_wgrad<64, 64>(dy, x, ws, g, c, st);
+  const int64_t n = static_cast<int64_t>(g.K) * g.R * g.S * g.C;
+  const int rg = static_cast<int>((n / 8 + kThreads - 1) / kThreads);
+  if (dw_f32)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<F32>, dim3(rg), dim3(kThreads), 0, st, ws, c.splits, n, dw, accumulate);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<BF16>, dim3(rg), dim3(kThreads), 0, st, ws, c.splits, n, dw, accumulate);
 }
 
 void conv_flip_transpose(const void* w, void* wt, int K, int C, int RS, hipStream_t st) {
