@@ -1,11 +1,17 @@
 """TensorBoard task (reference: `harness/determined/exec/tensorboard.py`, which fetches trial event
 files from checkpoint storage and starts the TensorBoard server).
 
-TensorBoard is not part of this image, so the task serves the scalars itself: it resolves each
-experiment's synced event-file directory (``<storage>/tensorboard/<cluster>/experiment/<id>``),
-parses the TF event files natively (:func:`determined_clone_amd.tensorboard.read_scalars`) and serves
-``/`` (HTML index), ``/data/runs`` and ``/data/scalars?run=...&tag=...`` (JSON, TensorBoard's scalar
-route shape: ``[[wall_time, step, value], ...]``). Its address is registered as the task's proxy.
+TensorBoard is not part of this image, so the task serves the event data itself. Each
+experiment's event files (``tensorboard/<cluster>/experiment/<id>`` in its checkpoint storage --
+shared_fs, directory, s3, gcs or azure) are synced into a local directory by the fetchers of
+:mod:`determined_clone_amd.tensorboard.fetchers` (once before serving, then every few seconds in
+a background thread, like the reference's fetch threads), parsed natively
+(:func:`~determined_clone_amd.tensorboard.read_scalars` / ``read_images``) and served as
+``/`` (HTML index with scalar tables and the latest image of each image tag), ``/data/runs``,
+``/data/scalars?run=...&tag=...`` (TensorBoard's scalar route shape:
+``[[wall_time, step, value], ...]``), ``/data/images?run=...&tag=...`` (``[{step, wall_time,
+height, width, index}]``) and ``/data/image?run=...&tag=...&index=N`` (the PNG). Its address is
+registered as the task's proxy.
 
 Usage: ``python -m determined_clone_amd.exec.tensorboard EXP_ID... [--logdir DIR] [--port N]``.
 """
@@ -16,18 +22,18 @@ import os
 import sys
 import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
-from typing import Dict, List, Optional
-from urllib.parse import parse_qs, urlparse
+from typing import Any, Dict, List, Optional
+from urllib.parse import parse_qs, quote, urlparse
 
 from determined_clone_amd import _info
-from determined_clone_amd.tensorboard import read_scalars
+from determined_clone_amd.tensorboard import fetchers, read_images, read_scalars
 from determined_clone_amd.util import proxy_secret_ok, routable_address
 
 
-def collect(logdirs: Dict[str, str]) -> Dict[str, Dict[str, list]]:
+def collect(logdirs: Dict[str, str], reader=read_scalars) -> Dict[str, Dict[str, list]]:
     runs: Dict[str, Dict[str, list]] = {}
     for name, d in logdirs.items():
-        for run, tags in read_scalars(d).items():
+        for run, tags in reader(d).items():
             runs[f"{name}/{run}" if run != "." else name] = tags
     return runs
 
@@ -58,21 +64,43 @@ def make_server(logdirs: Dict[str, str], host: Optional[str] = None, port: int =
                 if series is None:
                     return self._send(404, b'{"error": "no such run/tag"}', "application/json")
                 return self._send(200, json.dumps([[w, s, v] for s, w, v in series]).encode(), "application/json")
+            images = collect(logdirs, read_images)
+            if u.path.endswith("/data/images") or u.path.endswith("/data/image"):
+                series = images.get(q.get("run", ""), {}).get(q.get("tag", ""))
+                if series is None:
+                    return self._send(404, b'{"error": "no such run/tag"}', "application/json")
+                if u.path.endswith("/data/images"):
+                    meta = [{"step": st, "wall_time": w, "height": im["height"], "width": im["width"],
+                             "index": i} for i, (st, w, im) in enumerate(series)]
+                    return self._send(200, json.dumps(meta).encode(), "application/json")
+                try:
+                    return self._send(200, series[int(q.get("index", "-1"))][2]["png"], "image/png")
+                except (ValueError, IndexError):
+                    return self._send(404, b'{"error": "no such image"}', "application/json")
             rows = []
             for r, tags in sorted(runs.items()):
                 for t, series in sorted(tags.items()):
                     last = series[-1]
                     rows.append(f"<tr><td>{html.escape(r)}</td><td>{html.escape(t)}</td><td>{len(series)}</td>"
                                 f"<td>{last[0]}</td><td>{last[2]:.6g}</td></tr>")
+            imgs = []
+            for r, tags in sorted(images.items()):
+                for t, series in sorted(tags.items()):
+                    st = series[-1][0]
+                    src = f"data/image?run={quote(r)}&tag={quote(t)}&index={len(series) - 1}"
+                    imgs.append(f"<figure><img src=\"{html.escape(src)}\"><figcaption>{html.escape(r)} "
+                                f"{html.escape(t)} step {st}</figcaption></figure>")
             page = ("<html><head><title>determined_clone_amd tensorboard</title></head><body>"
                     "<h2>Scalars</h2><table border=1><tr><th>run</th><th>tag</th><th>points</th>"
-                    "<th>last step</th><th>last value</th></tr>" + "".join(rows) + "</table></body></html>")
+                    "<th>last step</th><th>last value</th></tr>" + "".join(rows) + "</table>"
+                    + ("<h2>Images</h2>" + "".join(imgs) if imgs else "") + "</body></html>")
             return self._send(200, page.encode(), "text/html")
 
     return ThreadingHTTPServer((routable_address() if host is None else host, port), H)
 
 
-def _experiment_logdirs(exp_ids: List[str]) -> Dict[str, str]:
+def _experiment_sources(exp_ids: List[str]) -> List[Dict[str, Any]]:
+    """Per experiment: its checkpoint storage config and the event-file path inside it."""
     from determined_clone_amd.common.api import Session
 
     info = _info.get_cluster_info()
@@ -81,15 +109,52 @@ def _experiment_logdirs(exp_ids: List[str]) -> Dict[str, str]:
     if info is not None:
         s.token = info.session_token
     cluster_id = s.get("/api/v1/master").get("cluster_id", "")
-    out = {}
+    out = []
     for eid in exp_ids:
         cfg = s.get(f"/api/v1/experiments/{eid}")["config"]
-        cs = cfg.get("checkpoint_storage") or {}
-        root = cs.get("host_path") or cs.get("container_path") or ""
-        if cs.get("storage_path"):
-            root = os.path.join(root, cs["storage_path"])
-        out[f"exp{eid}"] = os.path.join(root, "tensorboard", cluster_id, "experiment", str(eid))
+        out.append({"name": f"exp{eid}", "storage": cfg.get("checkpoint_storage") or {},
+                    "path": f"tensorboard/{cluster_id}/experiment/{eid}"})
     return out
+
+
+class SyncedLogdirs:
+    """Fetchers for every (storage, path) source into one local directory, refreshed by a
+    background thread every ``interval`` seconds (reference: TBFetchIterationThread)."""
+
+    def __init__(self, sources: List[Dict[str, Any]], local_dir: str, interval: float = 5.0) -> None:
+        self.local_dir = local_dir
+        self.interval = interval
+        self.logdirs: Dict[str, str] = {}
+        self._fetchers: List[fetchers.Fetcher] = []
+        by_storage: Dict[str, Dict[str, Any]] = {}
+        for src in sources:
+            key = json.dumps(src["storage"], sort_keys=True)
+            ent = by_storage.setdefault(key, {"storage": src["storage"], "paths": []})
+            ent["paths"].append(src["path"])
+            self.logdirs[src["name"]] = os.path.join(local_dir, src["path"])
+        for ent in by_storage.values():
+            self._fetchers.append(fetchers.build(ent["storage"], ent["paths"], local_dir))
+        self._stop = threading.Event()
+        self.fetched = 0
+
+    def fetch_once(self) -> int:
+        n = 0
+        for f in self._fetchers:
+            try:
+                n += f.fetch_new()
+            except Exception as e:  # noqa: BLE001 - a storage hiccup must not kill the task
+                print(f"tensorboard fetch failed: {e}", file=sys.stderr, flush=True)
+        self.fetched += n
+        return n
+
+    def start(self) -> None:
+        def loop() -> None:
+            while not self._stop.wait(self.interval):
+                self.fetch_once()
+        threading.Thread(target=loop, daemon=True, name="tb-fetch").start()
+
+    def stop(self) -> None:
+        self._stop.set()
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -100,7 +165,13 @@ def main(argv: Optional[List[str]] = None) -> int:
     a = p.parse_args(argv)
     logdirs = {f"dir{i}": d for i, d in enumerate(a.logdir)}
     if a.experiment_ids:
-        logdirs.update(_experiment_logdirs(a.experiment_ids))
+        import tempfile
+
+        synced = SyncedLogdirs(_experiment_sources(a.experiment_ids), tempfile.mkdtemp(prefix="det-tb-"))
+        n = synced.fetch_once()
+        print(f"fetched {n} tensorboard file(s)", flush=True)
+        synced.start()
+        logdirs.update(synced.logdirs)
     srv = make_server(logdirs, port=a.port)
     addr = f"http://{srv.server_address[0]}:{srv.server_address[1]}"
     print(f"serving tensorboard scalars at {addr}", flush=True)

@@ -310,3 +310,54 @@ def read_scalars(logdir: str) -> Dict[str, Dict[str, List[Tuple[int, float, floa
         for series in tags.values():
             series.sort()
     return runs
+
+
+def decode_image_event(record: bytes) -> List[Tuple[str, int, float, Dict[str, Any]]]:
+    """Event -> [(tag, step, wall_time, {"height", "width", "png"})] for its Summary.Value.image
+    entries (summary.proto: Value.image = 4; Image{height=1, width=2, colorspace=3,
+    encoded_image_string=4})."""
+    wall, step, summaries, out = 0.0, 0, [], []
+    for num, wire, v in _fields(record):
+        if num == 1 and wire == 1:
+            (wall,) = struct.unpack("<d", v)
+        elif num == 2 and wire == 0:
+            step = v
+        elif num == 5 and wire == 2:
+            summaries.append(v)
+    for s in summaries:
+        for num, wire, v in _fields(s):
+            if num != 1 or wire != 2:
+                continue
+            tag, img = None, None
+            for n2, w2, v2 in _fields(v):
+                if n2 == 1 and w2 == 2:
+                    tag = v2.decode("utf-8", "replace")
+                elif n2 == 4 and w2 == 2:
+                    img = {"height": 0, "width": 0, "png": b""}
+                    for n3, w3, v3 in _fields(v2):
+                        if n3 == 1 and w3 == 0:
+                            img["height"] = v3
+                        elif n3 == 2 and w3 == 0:
+                            img["width"] = v3
+                        elif n3 == 4 and w3 == 2:
+                            img["png"] = bytes(v3)
+            if tag is not None and img is not None:
+                out.append((tag, int(step), float(wall), img))
+    return out
+
+
+def read_images(logdir: str) -> Dict[str, Dict[str, List[Tuple[int, float, Dict[str, Any]]]]]:
+    """{run: {tag: [(step, wall_time, {"height", "width", "png"})]}} for every event file."""
+    runs: Dict[str, Dict[str, List[Tuple[int, float, Dict[str, Any]]]]] = {}
+    for root, _dirs, files in os.walk(logdir):
+        for fn in sorted(files):
+            if "tfevents" not in fn:
+                continue
+            run = os.path.relpath(root, logdir)
+            for rec in read_records(os.path.join(root, fn)):
+                for tag, step, wall, img in decode_image_event(rec):
+                    runs.setdefault(run, {}).setdefault(tag, []).append((step, wall, img))
+    for tags in runs.values():
+        for series in tags.values():
+            series.sort(key=lambda t: (t[0], t[1]))
+    return runs

@@ -178,3 +178,46 @@ def test_bad_credentials_are_rejected(tmp_path):
             sm.upload(str(tmp_path), "u")
     finally:
         srv.shutdown()
+
+
+def test_tensorboard_fetcher_syncs_event_files_from_object_storage(backend, tmp_path, monkeypatch):
+    """Trial side: TensorboardManager uploads event files to the object store; TB task side: the
+    fetcher pulls new / grown files and the task serves their scalars and images (reference
+    tensorboard/fetchers/{s3,gcs,azure}.py, exec/tensorboard.py)."""
+    import urllib.request
+
+    from determined_clone_amd import tensorboard
+    from determined_clone_amd.exec import tensorboard as tb_task
+    from determined_clone_amd.tensorboard import fetchers
+
+    sm, handler = backend
+    base = tmp_path / "trial-tb"
+    rel = "tensorboard/c1/experiment/7/trial/3"
+    mgr = tensorboard.TensorboardManager(base, None, sm, rel)
+    w = mgr.metric_writer()
+    w.on_metrics("training", 1, {"loss": 0.5})
+    png = b"\x89PNG\r\n\x1a\nfakepng"
+    w._w._write(tensorboard.encode_image_event("samples", png, 2, 3, step=1))
+    w._w.flush()
+    mgr.sync()
+    assert any("tensorboard/c1/experiment/7/trial/3/" in k for k in handler.objects)
+    local = tmp_path / "tb-local"
+    f = fetchers.build({"type": "s3"}, ["tensorboard/c1/experiment/7"], str(local), manager=sm)
+    assert f.fetch_new() == 1
+    assert f.fetch_new() == 0  # nothing changed
+    w.on_metrics("training", 2, {"loss": 0.25})
+    w._w.flush()
+    mgr.sync()
+    assert f.fetch_new() == 1  # the grown event file again
+    logdir = str(local / "tensorboard/c1/experiment/7")
+    runs = tensorboard.read_scalars(logdir)
+    (run, tags), = runs.items()
+    assert run == "trial/3" and [s for s, _, _ in next(iter(tags.values()))] == [1, 2]
+    srv = tb_task.make_server({"exp7": logdir}, host="127.0.0.1")
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    url = f"http://127.0.0.1:{srv.server_address[1]}"
+    meta = json.load(urllib.request.urlopen(f"{url}/data/images?run=exp7/trial/3&tag=samples"))
+    assert meta[0]["height"] == 2 and meta[0]["width"] == 3 and meta[0]["step"] == 1
+    assert urllib.request.urlopen(f"{url}/data/image?run=exp7/trial/3&tag=samples&index=0").read() == png
+    assert b"<img" in urllib.request.urlopen(url + "/").read()
+    srv.shutdown()
