@@ -94,6 +94,7 @@ class ExitedReason:
     USER_CANCELED = "USER_CANCELED"
     INVALID_HP = "INVALID_HP"
     INIT_INVALID_HP = "INIT_INVALID_HP"
+    USER_REQUESTED_STOP = "USER_REQUESTED_STOP"  # model.UserRequestedStop (early exit from code)
 
 
 # --------------------------------------------------------------------------- base

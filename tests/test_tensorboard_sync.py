@@ -42,3 +42,25 @@ def test_shared_fs_sync_and_per_cluster_dir(tmp_path, monkeypatch):
     got = list(pathlib.Path(a.sync_path).rglob("events.out.tfevents*"))
     assert len(got) == 1 and ca in str(got[0])
     assert not list(pathlib.Path(tmp_path, "tensorboard", cb).rglob("*"))
+
+
+def test_tensorboard_task_syncs_shared_fs_experiment_dirs(tmp_path):
+    """The TB task's SyncedLogdirs: one fetcher per storage, experiment dirs copied locally and
+    re-fetched when the trial writes more (reference exec/tensorboard.py fetch loop)."""
+    from determined_clone_amd.exec import tensorboard as tb_task
+
+    store = {"type": "shared_fs", "host_path": str(tmp_path / "store")}
+    mgr = tensorboard.build("cl", "5", "9", store)
+    w = mgr.metric_writer()
+    w.on_metrics("training", 1, {"loss": 1.0})
+    mgr.sync()
+    synced = tb_task.SyncedLogdirs([{"name": "exp5", "storage": store,
+                                     "path": "tensorboard/cl/experiment/5"}], str(tmp_path / "local"))
+    assert synced.fetch_once() == 1 and synced.fetch_once() == 0
+    runs = tensorboard.read_scalars(synced.logdirs["exp5"])
+    assert list(runs) == ["trial/9"]
+    w.on_metrics("training", 2, {"loss": 0.5})
+    mgr.sync()
+    assert synced.fetch_once() == 1
+    (series,) = tensorboard.read_scalars(synced.logdirs["exp5"])["trial/9"].values()
+    assert [s for s, _, _ in series] == [1, 2]
