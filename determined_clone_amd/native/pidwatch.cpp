@@ -240,15 +240,17 @@ int run_server(int on_fail, int on_exit, double grace, bool signal_children, con
         if (s.back() == 'q') graceful.insert(wpid);
         continue;  // 'k' keepalives (or 'q' followed by EOF later)
       }
-      // EOF / error: the worker is gone
-      const bool ok = wpid >= 0 && graceful.count(wpid);
+      // EOF / error: the worker is gone. Copy the pid out before erase(): wpid refers into the
+      // map node (use-after-free found by the ASan build, tests/test_native_sanitizers.py).
+      const int gone = wpid;
+      const bool ok = gone >= 0 && graceful.count(gone);
       close(p.fd);
       conn_pid.erase(p.fd);
       if (!ok && !failed) {
         failed = true;
         fail_time = now_s();
         fprintf(stderr, "dca-pidwatch: worker %d exited without a graceful shutdown; "
-                "stopping the job\n", wpid);
+                "stopping the job\n", gone);
         if (on_fail) signal_all(child, pids, on_fail, signal_children);
       }
     }
