@@ -261,18 +261,58 @@ def pointwise_dual(conv1: nn.Conv2d, proj: nn.Conv2d, x: torch.Tensor):
     return pointwise_conv(conv1, x), pointwise_conv(proj, x)
 
 
+# Weight gradients: MIOpen's backward-weight solvers or the split-pixel implicit-GEMM MFMA kernel
+# of csrc/conv_igemm.hip (numerics: tools/bench_igemm.py, tests/test_conv_gpu.py). "auto" times
+# both once per shape (like cudnn.benchmark) and keeps the faster; "1" / "0" force one.
+IGEMM_WGRAD = os.environ.get("DCA_IGEMM_WGRAD", "auto")
+
+
+def _igemm_wgrad_ok(args) -> bool:
+    dy, x, w = args[0], args[1], args[2]
+    stride, pad, dil, groups = args[4], args[5], args[6], args[9]
+    if IGEMM_WGRAD == "0" or not IGEMM or not x.is_cuda or args[7]:  # transposed conv
+        return False
+    if x.dtype != torch.bfloat16 or dy.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return False
+    if groups != 1 or list(dil) != [1, 1] or stride[0] != stride[1] or pad[0] != pad[1]:
+        return False
+    if w.shape[2] != w.shape[3] or pad[0] >= w.shape[2] or x.shape[1] % 64 or w.shape[0] % 64:
+        return False
+    if not (x.is_contiguous(memory_format=torch.channels_last)
+            and w.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    m = dy.shape[0] * dy.shape[2] * dy.shape[3]
+    return m < 2 ** 24 and x.numel() < 2 ** 31 and dy.numel() < 2 ** 31
+
+
 def _wgrad(args, weight: torch.Tensor) -> Optional[torch.Tensor]:
     """Weight gradient of ``convolution_backward(*args)``: on the side stream (accumulated into
     ``weight.grad``, returns None) when the parameter has a persistent ``.grad`` view
     (``ops/_grad.py``; ``DCA_WGRAD_STREAM=0`` disables), else computed inline and returned."""
     bwd = torch.ops.aten.convolution_backward
+    dy, x = args[0], args[1]
+    use_ours = False
+    if _igemm_wgrad_ok(args):
+        st, pad = args[4][0], args[5][0]
+        if IGEMM_WGRAD == "1":
+            use_ours = True
+        else:
+            cands = (lambda: bwd(*args, [False, True, False])[1],
+                     lambda: _ext.load().conv_igemm_wgrad(dy, x, args[2], st, pad))
+            use_ours = _choose(("wgrad", tuple(x.shape), tuple(args[2].shape), st, pad), cands) == 1
+
+    def compute(acc=None):
+        if use_ours:
+            return _ext.load().conv_igemm_wgrad(dy, x, args[2], args[4][0], args[5][0], acc)
+        dw = bwd(*args, [False, True, False])[1]
+        return acc.add_(dw) if acc is not None else dw
+
     s = _grad.side_stream_for(weight)
     if s is None:
-        return bwd(*args, [False, True, False])[1]
-    _grad.fork(s, (args[0], args[1]))
+        return compute()
+    _grad.fork(s, (dy, x))
     with torch.cuda.stream(s):
-        dw = bwd(*args, [False, True, False])[1]
-        _grad.target(weight).add_(dw)
+        compute(_grad.target(weight))
     return None
 
 

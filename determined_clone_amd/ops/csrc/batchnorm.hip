@@ -432,15 +432,17 @@ constexpr int kUReduceBwd = 4;  // 4 x (16 B dy + 16 B x [+ 16 B dy2] + 1 B mask
 constexpr int kUApply = 4;
 
 struct ReduceTuning {
-  int64_t elems_per_block, min_blocks, max_blocks;
+  int64_t elems_per_block, min_blocks, max_blocks, cap_floats;
 };
 inline const ReduceTuning& reduce_tuning() {
-  // DCA_BN_REDUCE="elems,min,max" overrides the workgroup-count heuristic (tuning sweeps only).
+  // DCA_BN_REDUCE="elems,min,max[,cap]" overrides the workgroup-count heuristic and the
+  // per-statistic partials cap (tuning sweeps only).
   static const ReduceTuning t = [] {
-    ReduceTuning r{32768, 256, 2048};
+    ReduceTuning r{32768, 256, 2048, int64_t(1) << 18};
     if (const char* e = std::getenv("DCA_BN_REDUCE")) {
-      long long a = 0, b = 0, c = 0;
-      if (std::sscanf(e, "%lld,%lld,%lld", &a, &b, &c) == 3 && a > 0 && b > 0 && c >= b) r = {a, b, c};
+      long long a = 0, b = 0, c = 0, d = 0;
+      const int n = std::sscanf(e, "%lld,%lld,%lld,%lld", &a, &b, &c, &d);
+      if (n >= 3 && a > 0 && b > 0 && c >= b) r = {a, b, c, n == 4 && d > 0 ? d : r.cap_floats};
     }
     return r;
   }();
@@ -456,7 +458,7 @@ inline int reduce_blocks(int64_t M, int C, const ReduceGeom& g) {
   int64_t b = (total + t.elems_per_block - 1) / t.elems_per_block;
   if (b < t.min_blocks) b = t.min_blocks;
   if (b > t.max_blocks) b = t.max_blocks;
-  const int64_t cap = std::max<int64_t>(64, (int64_t(1) << 18) / C);
+  const int64_t cap = std::max<int64_t>(64, t.cap_floats / C);
   if (b > cap) b = cap;
   int64_t rows_iter = (M + g.rpi - 1) / g.rpi;
   if (b > rows_iter) b = rows_iter;

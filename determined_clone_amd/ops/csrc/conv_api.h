@@ -28,11 +28,12 @@ struct ConvGeom {
 int conv_igemm_row_blocks(const ConvGeom& g);
 void conv_igemm_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
                     hipStream_t st);
-// Weight gradient dW [K][R][S][C] (bf16 or fp32; accumulate adds into it) from dy [M][K] and x;
-// ws: conv_igemm_wgrad_ws_floats(g) fp32 scratch.
+// Weight gradient dW (bf16 or fp32; accumulate adds into it) from dy [M][K] and x, stored
+// [K][R][S][C] (channels_last) or, with dw_kcrs, [K][C][R][S]; ws: conv_igemm_wgrad_ws_floats(g)
+// fp32 scratch.
 int64_t conv_igemm_wgrad_ws_floats(const ConvGeom& g);
 void conv_igemm_wgrad(const void* dy, const void* x, float* ws, void* dw, bool dw_f32,
-                      bool accumulate, const ConvGeom& g, hipStream_t st);
+                      bool accumulate, bool dw_kcrs, const ConvGeom& g, hipStream_t st);
 // w [K][RS][C] -> wt [C][RS][K] with the taps reversed (stride-1 data-gradient weight).
 void conv_flip_transpose(const void* w, void* wt, int K, int C, int RS, hipStream_t st);
 }  // namespace dca

@@ -181,19 +181,20 @@ Tensor conv_igemm_wgrad(const Tensor& dy_in, const Tensor& x, const Tensor& w, i
   TORCH_CHECK(g.M < (1 << 24), "conv_igemm_wgrad: at most 2^24 output pixels");
   Tensor ws = torch::empty({dca::conv_igemm_wgrad_ws_floats(g)}, dy.options().dtype(at::kFloat));
   Tensor out;
-  bool accumulate = false;
+  bool accumulate = false, kcrs = false;
   if (acc.has_value() && acc->defined()) {
     out = *acc;
+    kcrs = out.is_contiguous() && !out.is_contiguous(at::MemoryFormat::ChannelsLast);
     TORCH_CHECK(out.device() == dy.device() && out.sizes() == w.sizes() &&
                     (out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16) &&
-                    out.is_contiguous(at::MemoryFormat::ChannelsLast),
-                "conv_igemm_wgrad: accumulation target must be a channels_last fp32/bf16 tensor shaped like w");
+                    (kcrs || out.is_contiguous(at::MemoryFormat::ChannelsLast)),
+                "conv_igemm_wgrad: accumulation target must be a dense fp32/bf16 tensor shaped like w");
     accumulate = true;
   } else {
     out = torch::empty(w.sizes(), w.options().memory_format(at::MemoryFormat::ChannelsLast));
   }
   dca::conv_igemm_wgrad(dy.data_ptr(), x.data_ptr(), ws.data_ptr<float>(), out.data_ptr(),
-                        out.scalar_type() == at::kFloat, accumulate, g, stream());
+                        out.scalar_type() == at::kFloat, accumulate, kcrs, g, stream());
   return out;
 }
 

@@ -449,12 +449,15 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_kernel(
     }
 }
 
-// dW (+)= sum over splits in a fixed order; 8 elements per thread.
+// dW (+)= sum over splits in a fixed order; 8 elements per thread. The workspace is in the
+// weight's [K][R][S][C] order; `kcrs` writes dW in [K][C][R][S] order instead (a contiguous NCHW
+// .grad view of a channels_last parameter).
 template <typename OUT>
 __global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(const float* __restrict__ ws,
                                                                 int splits, int64_t n,
                                                                 void* __restrict__ dw,
-                                                                bool accumulate) {
+                                                                bool accumulate, bool kcrs, int RS,
+                                                                int C) {
   const int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   if (v * 8 >= n) return;
   float a[8];
@@ -466,14 +469,26 @@ __global__ __launch_bounds__(kThreads) void wgrad_reduce_kernel(const float* __r
 #pragma unroll
     for (int k = 0; k < 8; ++k) a[k] += p[k];
   }
-  char* dst = reinterpret_cast<char*>(dw) + v * 8 * Vec8<OUT>::bytes;
-  if (accumulate) {
-    float o[8];
-    Vec8<OUT>::load(dst, o);
+  if (!kcrs || RS == 1) {
+    char* dst = reinterpret_cast<char*>(dw) + v * 8 * Vec8<OUT>::bytes;
+    if (accumulate) {
+      float o[8];
+      Vec8<OUT>::load(dst, o);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] += o[k];
+      for (int k = 0; k < 8; ++k) a[k] += o[k];
+    }
+    Vec8<OUT>::store(dst, a);
+    return;
   }
-  Vec8<OUT>::store(dst, a);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t e = v * 8 + k;  // [K][RS][C]
+    const int64_t c = e % C, rest = e / C;
+    const int64_t tap = rest % RS, kk = rest / RS;
+    const int64_t d = (kk * C + c) * RS + tap;
+    float o = accumulate ? Elem<OUT>::get(dw, d) : 0.f;
+    Elem<OUT>::put(dw, d, a[k] + o);
+  }
 }
 
 struct WgCfg {
@@ -612,7 +627,7 @@ int64_t conv_igemm_wgrad_ws_floats(const ConvGeom& g) {
 }
 
 void conv_igemm_wgrad(const void* dy, const void* x, float* ws, void* dw, bool dw_f32,
-                      bool accumulate, const ConvGeom& g, hipStream_t st) {
+                      bool accumulate, bool dw_kcrs, const ConvGeom& g, hipStream_t st) {
   const WgCfg c = wgrad_cfg(g);
   if (c.bko == 128 && c.bc == 128) launch_wgrad<128, 128>(dy, x, ws, g, c, st);
   else if (c.bko == 128) launch_wgrad<128, 64>(dy, x, ws, g, c, st);
@@ -620,10 +635,13 @@ void conv_igemm_wgrad(const void* dy, const void* x, float* ws, void* dw, bool d
   else launch_wgrad<64, 64>(dy, x, ws, g, c, st);
   const int64_t n = static_cast<int64_t>(g.K) * g.R * g.S * g.C;
   const int rg = static_cast<int>((n / 8 + kThreads - 1) / kThreads);
+  const int RS = g.R * g.S;
   if (dw_f32)
-    hipLaunchKernelGGL(wgrad_reduce_kernel<F32>, dim3(rg), dim3(kThreads), 0, st, ws, c.splits, n, dw, accumulate);
+    hipLaunchKernelGGL(wgrad_reduce_kernel<F32>, dim3(rg), dim3(kThreads), 0, st, ws, c.splits, n, dw,
+                       accumulate, dw_kcrs, RS, g.C);
   else
-    hipLaunchKernelGGL(wgrad_reduce_kernel<BF16>, dim3(rg), dim3(kThreads), 0, st, ws, c.splits, n, dw, accumulate);
+    hipLaunchKernelGGL(wgrad_reduce_kernel<BF16>, dim3(rg), dim3(kThreads), 0, st, ws, c.splits, n, dw,
+                       accumulate, dw_kcrs, RS, g.C);
 }
 
 void conv_flip_transpose(const void* w, void* wt, int K, int C, int RS, hipStream_t st) {

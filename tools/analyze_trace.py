@@ -10,6 +10,12 @@ from collections import defaultdict
 
 def category(name: str) -> str:
     n = name
+    if "dca" in n and "conv_fwd_kernel" in n:
+        return "dca conv igemm (fwd + stride-1 dgrad)"
+    if "dca" in n and ("conv_wgrad_kernel" in n or "wgrad_reduce" in n):
+        return "dca conv wgrad"
+    if "dca" in n and "flip_transpose" in n:
+        return "dca conv weight flip"
     if "bn_" in n and "dca" in n:
         return "dca BatchNorm(+add+ReLU)"
     if "dca" in n and ("sgd_kernel" in n or "adam_kernel" in n or "lamb_" in n or "sumsq" in n
