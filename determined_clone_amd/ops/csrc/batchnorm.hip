@@ -89,7 +89,7 @@ __device__ __forceinline__ void st8(void* base, int64_t elem_off, const float (&
 // the tensors' producer (a convolution, or the previous pass) wrote/read them ascending, so the
 // rows it touched last are still in the 256 MB Infinity Cache when the first chunks run here;
 // the apply pass then walks ascending and starts on the rows this pass read last.
-template <typename T, bool BWD, int U>
+template <typename T, bool BWD, int U, bool NT = false>
 __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
     const void* __restrict__ x, const void* __restrict__ dy, const void* __restrict__ dy2,
     const uint8_t* __restrict__ mask, const float* __restrict__ mean, int64_t M, int C, int tpr,
@@ -117,10 +117,10 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t off = (r + u * rpi) * C + c;
-        rx[u] = ld8<T>(x, off);
+        rx[u] = NT ? ld8nt<T>(x, off) : ld8<T>(x, off);
         if (BWD) {
-          rg[u] = ld8<T>(dy, off);
-          if (dy2) rg2[u] = ld8<T>(dy2, off);
+          rg[u] = NT ? ld8nt<T>(dy, off) : ld8<T>(dy, off);
+          if (dy2) rg2[u] = NT ? ld8nt<T>(dy2, off) : ld8<T>(dy2, off);
           mk[u] = relu ? mask[off >> 3] : 0xffu;
         }
       }
@@ -498,6 +498,26 @@ inline int apply_blocks(int64_t M, const RowGeom& g, const ApplyTuning& t) {
   return static_cast<int>(b);
 }
 
+// Reduce-pass variant: the statistics passes stream with NONTEMPORAL loads by default (-3% on
+// the bs-1024 ResNet-50 BN shapes, fwd+bwd 32.3 -> 31.4 ms per step in tools/bench_bn.py,
+// profiles/round4_bn_reduce_nt_ab.txt). DCA_BN_REDUCE_VAR="U_bwd,nt" (A/B sweeps only): rows in
+// flight per lane in the backward pass (4 | 8) and nontemporal loads (0 | 1).
+struct ReduceVar {
+  int u_bwd;
+  bool nt;
+};
+inline const ReduceVar& reduce_var() {
+  static const ReduceVar v = [] {
+    ReduceVar r{kUReduceBwd, true};
+    if (const char* e = std::getenv("DCA_BN_REDUCE_VAR")) {
+      int u = 0, nt = 0;
+      if (std::sscanf(e, "%d,%d", &u, &nt) == 2 && (u == 4 || u == 8)) r = {u, nt != 0};
+    }
+    return r;
+  }();
+  return v;
+}
+
 template <typename T>
 void launch_reduce(bool bwd, const void* x, const void* dy, const void* dy2, const uint8_t* y,
                    const float* mean,
@@ -505,12 +525,20 @@ void launch_reduce(bool bwd, const void* x, const void* dy, const void* dy2, con
                    hipStream_t st) {
   dim3 grid(B, g.cgroups);
   size_t lds = static_cast<size_t>(g.rpi) * g.tpr * 16 * sizeof(float);
-  if (bwd)
-    hipLaunchKernelGGL((bn_reduce_kernel<T, true, kUReduceBwd>), grid, dim3(kBlock), lds, st, x,
-                       dy, dy2, y, mean, M, C, g.tpr, g.rpi, relu, partial);
-  else
-    hipLaunchKernelGGL((bn_reduce_kernel<T, false, kUReduceFwd>), grid, dim3(kBlock), lds, st, x,
-                       dy, dy2, y, mean, M, C, g.tpr, g.rpi, relu, partial);
+  const ReduceVar& v = reduce_var();
+#define DCA_RED(BW, UU, NTT)                                                                       \
+  hipLaunchKernelGGL((bn_reduce_kernel<T, BW, UU, NTT>), grid, dim3(kBlock), lds, st, x, dy, dy2, y, \
+                     mean, M, C, g.tpr, g.rpi, relu, partial)
+  if (bwd) {
+    if (v.u_bwd == 8) {
+      if (v.nt) DCA_RED(true, 8, true); else DCA_RED(true, 8, false);
+    } else {
+      if (v.nt) DCA_RED(true, kUReduceBwd, true); else DCA_RED(true, kUReduceBwd, false);
+    }
+  } else {
+    if (v.nt) DCA_RED(false, kUReduceFwd, true); else DCA_RED(false, kUReduceFwd, false);
+  }
+#undef DCA_RED
 }
 
 template <typename T>

@@ -107,7 +107,7 @@ def main() -> None:
             del x, y, dy
             torch.cuda.empty_cache()
         print(json.dumps(res), flush=True)
-    tw = {"mi_wgrad1": 0.0, "ig_wgrad1": 0.0}
+    tw = {"mi_wgrad1": 0.0, "ig_wgrad1": 0.0, "lib_fwd1": 0.0, "ig_fwd1": 0.0}
     for H, ci, co, st, cnt in SHAPES1:
         x = torch.randn(3, ci, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
         w = (torch.randn(co, ci, 1, 1, device="cuda") / ci ** 0.5).bfloat16().contiguous(memory_format=torch.channels_last)
@@ -116,19 +116,36 @@ def main() -> None:
         wref = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [st, st], [0, 0],
                                                    [1, 1], False, [0, 0], 1, [False, True, False])[1]
         res = {"k": 1, "H": H, "cin": ci, "cout": co, "stride": st,
-               "wgrad_rel_err": round(rel_err(C.conv_igemm_wgrad(dy, x, w, st, 0), wref), 5)}
+               "wgrad_rel_err": round(rel_err(C.conv_igemm_wgrad(dy, x, w, st, 0), wref), 5),
+               "fwd_rel_err": round(rel_err(C.conv_igemm_fwd(x, w, st, 0, True)[0], y), 5)}
         if not a.check_only:
             n = a.batch
             x = torch.randn(n, ci, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
             y = F.conv2d(x, w, stride=st)
             dy = torch.randn_like(y)
             flops = 2.0 * n * y.shape[2] * y.shape[3] * co * ci
+            W2 = w.view(co, ci)
+
+            def gemm_fwd():
+                v = x.permute(0, 2, 3, 1)
+                if st > 1:
+                    v = v[:, ::st, ::st, :]
+                return torch.mm(v.reshape(-1, ci), W2.t())
+
             for rnd in range(2):
                 miw = timed(lambda: torch.ops.aten.convolution_backward(
                     dy, x, w, None, [st, st], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False]))
                 igw = timed(lambda: C.conv_igemm_wgrad(dy, x, w, st, 0))
+                mif = timed(lambda: F.conv2d(x, w, stride=st))
+                gmf = timed(gemm_fwd)
+                igf = timed(lambda: C.conv_igemm_fwd(x, w, st, 0, True))
+            io = (x.numel() // (st * st) + y.numel()) * 2
             res.update({"mi_wgrad_us": round(miw, 1), "ig_wgrad_us": round(igw, 1),
-                        "ig_wgrad_tf": round(flops / igw / 1e6, 1)})
+                        "ig_wgrad_tf": round(flops / igw / 1e6, 1), "mi_fwd_us": round(mif, 1),
+                        "gemm_fwd_us": round(gmf, 1), "ig_fwd_us": round(igf, 1),
+                        "ig_fwd_TBps": round(io / igf / 1e6, 2)})
+            tw["lib_fwd1"] += min(mif, gmf) * cnt
+            tw["ig_fwd1"] += igf * cnt
             tw["mi_wgrad1"] += miw * cnt
             tw["ig_wgrad1"] += igw * cnt
             del x, y, dy
