@@ -282,7 +282,7 @@ def _igemm_wgrad_ok(args) -> bool:
             and w.is_contiguous(memory_format=torch.channels_last)):
         return False
     m = dy.shape[0] * dy.shape[2] * dy.shape[3]
-    return m < 2 ** 24 and x.numel() < 2 ** 31 and dy.numel() < 2 ** 31
+    return m < 2 ** 24 and x.numel() < 2 ** 30 and dy.numel() < 2 ** 30
 
 
 def _wgrad(args, weight: torch.Tensor) -> Optional[torch.Tensor]:
@@ -459,7 +459,7 @@ def igemm_supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     if not w.is_contiguous(memory_format=torch.channels_last) or torch.is_autocast_enabled():
         return False
     n, c, h, ww = x.shape
-    return n * c * h * ww < 2 ** 31 and n * conv.out_channels * h * ww < 2 ** 31
+    return n * c * h * ww < 2 ** 30 and n * conv.out_channels * h * ww < 2 ** 30
 
 
 class _IgemmConv(torch.autograd.Function):

@@ -103,7 +103,8 @@ void check_nhwc(const Tensor& t, const char* what) {
               ": bf16 4-D GPU tensor required");
   TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), what, ": channels_last layout required");
   TORCH_CHECK(t.size(1) % 64 == 0, what, ": channels must be a multiple of 64");
-  TORCH_CHECK(t.numel() < (int64_t{1} << 31), what, ": tensor too large for 32-bit offsets");
+  // byte offsets of the buffer loads are 32-bit with 2^31 as the out-of-range marker
+  TORCH_CHECK(t.numel() < (int64_t{1} << 30), what, ": tensor too large for 32-bit byte offsets");
 }
 
 dca::ConvGeom geom(const Tensor& x, const Tensor& w, int64_t stride, int64_t pad) {

@@ -72,6 +72,17 @@ __device__ __forceinline__ void barrier_raw() {
   asm volatile("" ::: "memory");
 }
 
+// buffer_load_dwordx4 ... lds: a 16-B piece per lane straight into LDS (wave-uniform LDS base +
+// lane * 16). The buffer descriptor's range check returns zeros for an offset past num_records:
+// padding taps and rows past M pass kOOB instead of branching to a zero block.
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff, uint32_t soff,
+                                       void* lds_dst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      rsrc, (__attribute__((address_space(3))) void*)(lds_dst), 16, voff, soff, 0, 0);
+}
+
 template <int BM, int BN, int WM, int WN, int NSTAGE, bool STATS>
 __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
@@ -80,7 +91,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
   constexpr int TM = BM / WM, TN = BN / WN;  // wave tile: pixels x channels
   constexpr int FM = TM / 32, FN = TN / 32;
   static_assert(FM >= 1 && FN >= 1, "wave tile below one 32x32 MFMA tile");
-  constexpr int A_INS = BM / 32;  // glds per wave per stage (8 rows x 128 B each, 4 waves)
+  constexpr int A_INS = BM / 32;  // buffer-lds loads per wave per stage (8 rows x 128 B each)
   constexpr int B_INS = BN / 32;
   constexpr int STAGE = (BM + BN) * kBK;  // elements per LDS stage
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
@@ -91,58 +102,71 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
   const int mt = t / NT, nt = t - mt * NT;
   const int m0 = mt * BM, n0 = nt * BN;
   const int PQ = g.P * g.Q;
-  const int KT = g.R * g.S * (g.C / kBK);
   const int CT = g.C / kBK;
+  const int KT = g.R * g.S * CT;
 
-  // ---- per-lane gather state: for each A instruction, the output pixel's input origin
-  int a_off[A_INS];    // element offset of x[n][ih0][iw0][0] (may be "negative" for pad rows)
+  // num_records in bytes (< 2^31 by the host checks, so kOOB is always out of range)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(x), 0, static_cast<int>(static_cast<uint32_t>(g.N * g.H * g.W) * g.C * 2u),
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(w), 0, static_cast<int>(static_cast<uint32_t>(g.K * g.R * g.S * g.C) * 2u),
+      0x00020000);
+
+  // ---- per-lane gather state: for each A load, the output pixel's input origin
+  uint32_t a_vo[A_INS];  // byte offset of x[n][ih0][iw0][chunk*8] (wraps for pad rows; never used then)
   int a_ih[A_INS], a_iw[A_INS];
-  int a_chunk[A_INS];  // source 16-B chunk (0..7) this lane fetches (swizzle inverse)
 #pragma unroll
   for (int i = 0; i < A_INS; ++i) {
     const int j = wv + 4 * i;
     const int row = 8 * j + (lane >> 3);
     const int m = m0 + row;
-    a_chunk[i] = (lane & 7) ^ swz(row);
+    const int chunk = (lane & 7) ^ swz(row);
     if (m < g.M) {
       const int n = m / PQ, rem = m - n * PQ, p = rem / g.Q, q = rem - p * g.Q;
       a_ih[i] = p * g.stride - g.pad;
       a_iw[i] = q * g.stride - g.pad;
-      a_off[i] = ((n * g.H + a_ih[i]) * g.W + a_iw[i]) * g.C;
+      a_vo[i] = static_cast<uint32_t>((((n * g.H + a_ih[i]) * g.W + a_iw[i]) * g.C + chunk * 8) * 2);
     } else {
       a_ih[i] = -(1 << 20);  // never valid
       a_iw[i] = 0;
-      a_off[i] = 0;
+      a_vo[i] = kOOB;
     }
   }
   const int RSC = g.R * g.S * g.C;
-  int b_off[B_INS];
+  uint32_t b_vo[B_INS];
 #pragma unroll
   for (int i = 0; i < B_INS; ++i) {
     const int j = wv + 4 * i;
     const int row = 8 * j + (lane >> 3);
-    b_off[i] = (n0 + row) * RSC + ((lane & 7) ^ swz(row)) * 8;
+    b_vo[i] = static_cast<uint32_t>(((n0 + row) * RSC + ((lane & 7) ^ swz(row)) * 8) * 2);
   }
 
-  auto stage = [&](int kt, int buf) {
-    const int tap = kt / CT, cc = kt - tap * CT;
-    const int r = tap / g.S, s = tap - r * g.S;
-    const int tap_off = (r * g.W + s) * g.C + cc * kBK;
+  // the stage to load next, as loop-carried (tap r, s; channel chunk cc) counters -- no divisions
+  int ld_r = 0, ld_s = 0, ld_cc = 0;
+  auto stage = [&](int buf) {
+    const uint32_t tap_b = static_cast<uint32_t>(((ld_r * g.W + ld_s) * g.C + ld_cc * kBK) * 2);
     uint16_t* As = lds + buf * STAGE;
     uint16_t* Bs = As + BM * kBK;
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
       const int j = wv + 4 * i;
-      const bool ok = static_cast<unsigned>(a_ih[i] + r) < static_cast<unsigned>(g.H) &&
-                      static_cast<unsigned>(a_iw[i] + s) < static_cast<unsigned>(g.W);
-      const uint16_t* src = ok ? x + (a_off[i] + tap_off + a_chunk[i] * 8) : g_zero_block;
-      glds16(src, As + j * 8 * kBK);
+      const bool ok = static_cast<unsigned>(a_ih[i] + ld_r) < static_cast<unsigned>(g.H) &&
+                      static_cast<unsigned>(a_iw[i] + ld_s) < static_cast<unsigned>(g.W);
+      blds16(xr, ok ? a_vo[i] + tap_b : kOOB, 0, As + j * 8 * kBK);
     }
-    const int wk = tap * g.C + cc * kBK;
+    const uint32_t wk = static_cast<uint32_t>(((ld_r * g.S + ld_s) * g.C + ld_cc * kBK) * 2);
 #pragma unroll
     for (int i = 0; i < B_INS; ++i) {
       const int j = wv + 4 * i;
-      glds16(w + b_off[i] + wk, Bs + j * 8 * kBK);
+      blds16(wr, b_vo[i], wk, Bs + j * 8 * kBK);
+    }
+    if (++ld_cc == CT) {
+      ld_cc = 0;
+      if (++ld_s == g.S) {
+        ld_s = 0;
+        ++ld_r;
+      }
     }
   };
 
@@ -157,13 +181,18 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
+  // fragment addresses (element offsets inside a stage) for k-substep ks
+  auto frag = [&](const uint16_t* base, int row, int ks) {
+    return *reinterpret_cast<const bf16x8*>(base + row * kBK + (((2 * ks + h) ^ swz(row)) << 3));
+  };
+
   // NSTAGE-deep LDS ring: stages kt+1 .. kt+NSTAGE-1 are in flight while stage kt is computed.
   // Every wave issues LPS loads per stage, so "stage kt+1 landed" is vmcnt(LPS * (stages issued
   // after it)); raw s_barrier (not __syncthreads, which would drain vmcnt to 0) publishes it.
   constexpr int LPS = A_INS + B_INS;
 #pragma unroll
   for (int p = 0; p < NSTAGE - 1; ++p)
-    if (p < KT) stage(p, p);
+    if (p < KT) stage(p);
   if constexpr (NSTAGE == 3) {
     if (KT > 1) wait_vmcnt<LPS>();
     else wait_vmcnt<0>();
@@ -173,32 +202,39 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
   barrier_raw();
   int buf = 0;
   for (int kt = 0; kt < KT; ++kt) {
-    const int ahead = kt + NSTAGE - 1;
-    if (ahead < KT) {
+    if (kt + NSTAGE - 1 < KT) {
       int nb = buf + NSTAGE - 1;
       if (nb >= NSTAGE) nb -= NSTAGE;
-      stage(ahead, nb);
+      stage(nb);
     }
     const uint16_t* As = lds + buf * STAGE;
     const uint16_t* Bs = As + BM * kBK;
+    // fragments of substep ks+1 are read while the MFMAs of ks run
+    bf16x8 a0[FN], b0[FM], a1[FN], b1[FM];
 #pragma unroll
-    for (int ks = 0; ks < kBK / 16; ++ks) {
-      const int cidx = 2 * ks + h;
-      bf16x8 a[FN], b[FM];
+    for (int i = 0; i < FN; ++i) a0[i] = frag(Bs, wn * TN + i * 32 + r32, 0);
 #pragma unroll
-      for (int i = 0; i < FN; ++i) {
-        const int row = wn * TN + i * 32 + r32;
-        a[i] = *reinterpret_cast<const bf16x8*>(Bs + row * kBK + ((cidx ^ swz(row)) << 3));
-      }
+    for (int j = 0; j < FM; ++j) b0[j] = frag(As, wm * TM + j * 32 + r32, 0);
 #pragma unroll
-      for (int j = 0; j < FM; ++j) {
-        const int row = wm * TM + j * 32 + r32;
-        b[j] = *reinterpret_cast<const bf16x8*>(As + row * kBK + ((cidx ^ swz(row)) << 3));
+    for (int ks = 0; ks < kBK / 16; ks += 2) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i) a1[i] = frag(Bs, wn * TN + i * 32 + r32, ks + 1);
+#pragma unroll
+      for (int j = 0; j < FM; ++j) b1[j] = frag(As, wm * TM + j * 32 + r32, ks + 1);
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma32(a0[i], b0[j], acc[i][j]);
+      if (ks + 2 < kBK / 16) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i) a0[i] = frag(Bs, wn * TN + i * 32 + r32, ks + 2);
+#pragma unroll
+        for (int j = 0; j < FM; ++j) b0[j] = frag(As, wm * TM + j * 32 + r32, ks + 2);
       }
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int j = 0; j < FM; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < FM; ++j) acc[i][j] = mfma32(a1[i], b1[j], acc[i][j]);
     }
     // stage kt+1 must have landed; later stages may stay in flight
     if constexpr (NSTAGE == 3) {
