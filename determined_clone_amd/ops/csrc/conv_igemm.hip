@@ -389,6 +389,28 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_kernel(
   const int me = min(g.M, mb + rows_per_split);
   const int PQ = g.P * g.Q;
 
+  // buffer loads into LDS with hardware out-of-range zeros (see conv_fwd_kernel); the x rows of
+  // each lane advance 64 pixels per stage, so their (n, p, q) are carried, not divided for
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(dy), 0, static_cast<int>(static_cast<uint32_t>(g.M) * g.K * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(x), 0, static_cast<int>(static_cast<uint32_t>(g.N * g.H * g.W) * g.C * 2u),
+      0x00020000);
+  int xb_n[IB], xb_p[IB], xb_q[IB];
+  uint32_t xb_c[IB];  // byte offset of this lane's channel chunk within a pixel row
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int j = wv + 4 * i;
+    const int row = j * (64 / LB) + lane / LB;
+    const int m = mb + row;
+    xb_n[i] = fdiv(m, PQ, inv_pq);
+    const int rem = m - xb_n[i] * PQ;
+    xb_p[i] = fdiv(rem, g.Q, inv_q);
+    xb_q[i] = rem - xb_p[i] * g.Q;
+    xb_c[i] = static_cast<uint32_t>((c0 + ((lane % LB) ^ wswz<RB>(row)) * 8) * 2);
+  }
+  const int dq = kWM % g.Q, dp = (kWM / g.Q) % g.P, dn = kWM / PQ;
+
   auto stage = [&](int m_base, int buf) {
     uint16_t* As = lds + buf * STAGE;
     uint16_t* Bs = As + kWM * BKO;
@@ -398,25 +420,27 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_kernel(
       const int row = j * (64 / LA) + lane / LA;
       const int chunk = (lane % LA) ^ wswz<RA>(row);
       const int m = m_base + row;
-      const uint16_t* src = m < me ? dy + (static_cast<int64_t>(m) * g.K + k0 + chunk * 8) : g_zero_block;
-      glds16(src, As + j * 512);
+      const uint32_t vo =
+          m < me ? (static_cast<uint32_t>(m) * g.K + static_cast<uint32_t>(k0 + chunk * 8)) * 2u : kOOB;
+      blds16(dyr, vo, 0, As + j * 512);
     }
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const int j = wv + 4 * i;
       const int row = j * (64 / LB) + lane / LB;
-      const int chunk = (lane % LB) ^ wswz<RB>(row);
       const int m = m_base + row;
-      const uint16_t* src = g_zero_block;
-      if (m < me) {
-        const int n = fdiv(m, PQ, inv_pq), rem = m - n * PQ;
-        const int p = fdiv(rem, g.Q, inv_q), q = rem - p * g.Q;
-        const int ih = p * g.stride - g.pad + r, iw = q * g.stride - g.pad + s;
-        if (static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
-            static_cast<unsigned>(iw) < static_cast<unsigned>(g.W))
-          src = x + ((static_cast<int64_t>(n * g.H + ih) * g.W + iw) * g.C + c0 + chunk * 8);
-      }
-      glds16(src, Bs + j * 512);
+      const int ih = xb_p[i] * g.stride - g.pad + r, iw = xb_q[i] * g.stride - g.pad + s;
+      const bool ok = m < me && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(g.W);
+      const uint32_t vo =
+          ok ? static_cast<uint32_t>((xb_n[i] * g.H + ih) * g.W + iw) * static_cast<uint32_t>(g.C) * 2u + xb_c[i]
+             : kOOB;
+      blds16(xr, vo, 0, Bs + j * 512);
+      // advance this row by kWM pixels
+      int q = xb_q[i] + dq, p = xb_p[i] + dp, n = xb_n[i] + dn;
+      if (q >= g.Q) { q -= g.Q; ++p; }
+      while (p >= g.P) { p -= g.P; ++n; }
+      xb_q[i] = q; xb_p[i] = p; xb_n[i] = n;
     }
   };
 
