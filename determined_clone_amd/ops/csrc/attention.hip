@@ -214,7 +214,7 @@ template <int D, bool CAUSAL, int KT, bool PIPE>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
-    Strides ks, Strides vs, Strides os, float scale_log2, int order) {
+    Strides ks, Strides vs, Strides os, float scale_log2, int order, const int* __restrict__ kvlen) {
   // KT = keys per LDS tile (one barrier pair per tile), consumed in 32-key MFMA sub-tiles
   constexpr int QB = 128;      // queries per workgroup
   constexpr int RS = D + kPad; // LDS row stride (elements)
@@ -231,6 +231,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   const int r = lane & 31, hf = lane >> 5;
   const Blk blk = xcd_block(order);
   const int b = blk.z, h = blk.y;
+  // key padding: keys at or past kvlen[b] are masked like keys past Sk (>= 1 key kept)
+  if (kvlen) Sk = min(Sk, max(kvlen[b], 1));
   // heaviest (largest causal extent) query blocks first
   const int q_blk = (CAUSAL ? (gridDim.x - 1 - blk.x) : blk.x) * QB;
   const int q0 = q_blk + w * 32;
@@ -431,7 +433,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const uint16_t* __restrict__ o, const uint16_t* __restrict__ dO, const float* __restrict__ lse,
     float* __restrict__ delta, uint16_t* __restrict__ dq, int Sq, int Sk, int H, Strides qs,
     Strides ks, Strides vs, Strides os, Strides dos, Strides dqs, float scale_log2, float scale,
-    int order) {
+    int order, const int* __restrict__ kvlen) {
   // KT = keys per LDS tile (one barrier pair per tile), consumed in 32-key MFMA sub-tiles
   constexpr int QB = 128;
   constexpr int RS = D + kPad;
@@ -445,6 +447,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   const int r = lane & 31, hf = lane >> 5;
   const Blk blk = xcd_block(order);
   const int b = blk.z, h = blk.y;
+  // key padding: keys at or past kvlen[b] are masked like keys past Sk (>= 1 key kept)
+  if (kvlen) Sk = min(Sk, max(kvlen[b], 1));
   const int q_blk = (CAUSAL ? (gridDim.x - 1 - blk.x) : blk.x) * QB;
   const int q0 = q_blk + w * 32;
   const int my_q = q0 + r;
@@ -570,7 +574,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     const uint16_t* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
     uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int Sq, int Sk, int H, Strides qs,
     Strides ks, Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale,
-    int order) {
+    int order, const int* __restrict__ kvlen) {
   constexpr int KB = 128;
   static_assert(QT == 32 || QT == 64, "query tile");
   constexpr int RS = D + kPad;
@@ -588,6 +592,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   const int r = lane & 31, hf = lane >> 5;
   const Blk blk = xcd_block(order);
   const int b = blk.z, h = blk.y;
+  const int SkT = Sk;  // rows of dK/dV to write (padded keys get zeros)
+  // key padding: keys at or past kvlen[b] are masked like keys past Sk (>= 1 key kept)
+  if (kvlen) Sk = min(Sk, max(kvlen[b], 1));
   const int k_blk = blk.x * KB;
   const int kw0 = k_blk + 32 * w;
   const int my_key = kw0 + r;
@@ -735,8 +742,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
         tile(std::false_type{}, half);
     }
   }
-  store_rows<D>(dk + b * dks.b + h * dks.h + static_cast<int64_t>(my_key) * dks.s, dkacc, scale, hf, my_key < Sk);
-  store_rows<D>(dv + b * dvs.b + h * dvs.h + static_cast<int64_t>(my_key) * dvs.s, dvacc, 1.f, hf, my_key < Sk);
+  store_rows<D>(dk + b * dks.b + h * dks.h + static_cast<int64_t>(my_key) * dks.s, dkacc, scale, hf, my_key < SkT);
+  store_rows<D>(dv + b * dvs.b + h * dvs.h + static_cast<int64_t>(my_key) * dvs.s, dvacc, 1.f, hf, my_key < SkT);
 }
 
 size_t fwd_lds(int D, int KT = 64) {  // K tile + V tile (see attn_fwd_kernel's VPAD)
@@ -810,7 +817,7 @@ int dkdv_qt() {
 template <int D, bool C>
 void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse,
                 int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs, Strides os,
-                float scale_log2, hipStream_t st) {
+                float scale_log2, const int* kvlen, hipStream_t st) {
   dim3 grid((Sq + 127) / 128, H, B);
   auto go = [&](auto ktag) {
     constexpr int KT = decltype(ktag)::value;
@@ -819,7 +826,7 @@ void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
       hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
-                         scale_log2, attn_order(C));
+                         scale_log2, attn_order(C), kvlen);
     };
     if constexpr (D == 64) {  // D = 128 with two live score tiles spills
       if (fwd_pipe()) {
@@ -843,12 +850,12 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
                 const uint16_t* dO, const float* lse, float* delta, uint16_t* dq, uint16_t* dk,
                 uint16_t* dv, int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs,
                 Strides os, Strides dos, Strides dqs, Strides dks, Strides dvs, float scale_log2,
-                float scale, hipStream_t st) {
+                float scale, const int* kvlen, hipStream_t st) {
   auto dq_go = [&](auto kern, size_t l1) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l1));
     hipLaunchKernelGGL(kern, dim3((Sq + 127) / 128, H, B), dim3(256), l1, st, q, k, v, o, dO, lse,
-                       delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2, scale, attn_order(C));
+                       delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2, scale, attn_order(C), kvlen);
   };
   bool dq_done = false;
   if constexpr (D == 64) {
@@ -864,11 +871,11 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
   if (dkdv_qt() == 64) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H, B), dim3(256),
                        bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
-                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C));
+                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen);
   } else {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 32>), dim3((Sk + 127) / 128, H, B), dim3(256),
                        bwd_dkdv_lds(D, 32), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
-                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C));
+                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen);
   }
 }
 
@@ -876,7 +883,7 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
 
 void attention_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H,
                    int Sq, int Sk, int D, const int64_t* qs, const int64_t* ks, const int64_t* vs,
-                   const int64_t* os, float scale, bool causal, hipStream_t st) {
+                   const int64_t* os, float scale, bool causal, const int* kvlen, hipStream_t st) {
   const float sl2 = scale * 1.4426950408889634f;
   Strides a{qs[0], qs[1], qs[2]}, bb{ks[0], ks[1], ks[2]}, c{vs[0], vs[1], vs[2]}, d{os[0], os[1], os[2]};
   auto Q = static_cast<const uint16_t*>(q);
@@ -884,11 +891,11 @@ void attention_fwd(const void* q, const void* k, const void* v, void* o, float* 
   auto V = static_cast<const uint16_t*>(v);
   auto O = static_cast<uint16_t*>(o);
   if (D == 64) {
-    if (causal) launch_fwd<64, true>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, st);
-    else launch_fwd<64, false>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, st);
+    if (causal) launch_fwd<64, true>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, st);
+    else launch_fwd<64, false>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, st);
   } else {
-    if (causal) launch_fwd<128, true>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, st);
-    else launch_fwd<128, false>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, st);
+    if (causal) launch_fwd<128, true>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, st);
+    else launch_fwd<128, false>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, st);
   }
 }
 
@@ -897,17 +904,17 @@ void attention_bwd(const void* q, const void* k, const void* v, const void* o, c
                    int B, int H, int Sq, int Sk, int D, const int64_t* st_q, const int64_t* st_k,
                    const int64_t* st_v, const int64_t* st_o, const int64_t* st_do,
                    const int64_t* st_dq, const int64_t* st_dk, const int64_t* st_dv, float scale,
-                   bool causal, hipStream_t stream) {
+                   bool causal, const int* kvlen, hipStream_t stream) {
   const float sl2 = scale * 1.4426950408889634f;
   auto S = [](const int64_t* p) { return Strides{p[0], p[1], p[2]}; };
   auto c16 = [](const void* p) { return static_cast<const uint16_t*>(p); };
   auto m16 = [](void* p) { return static_cast<uint16_t*>(p); };
   if (D == 64) {
-    if (causal) launch_bwd<64, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
-    else launch_bwd<64, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
+    if (causal) launch_bwd<64, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, stream);
+    else launch_bwd<64, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, stream);
   } else {
-    if (causal) launch_bwd<128, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
-    else launch_bwd<128, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, stream);
+    if (causal) launch_bwd<128, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, stream);
+    else launch_bwd<128, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, stream);
   }
 }
 

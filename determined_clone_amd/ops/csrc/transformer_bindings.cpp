@@ -204,8 +204,18 @@ AttnStrides bshd_strides(const Tensor& t, const char* name) {
   return {{t.stride(0), t.stride(2), t.stride(1)}};
 }
 
+// kv_len: optional int32 [B] valid key count per batch row (right padding, e.g. an HF
+// attention_mask); keys at or past it get zero weight and zero dK/dV
+const int* kvlen_ptr(const OptT& kv_len, int B) {
+  if (!kv_len.has_value()) return nullptr;
+  const Tensor& t = *kv_len;
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kInt && t.is_contiguous() && t.numel() == B,
+              "attention: kv_len must be a contiguous int32 GPU tensor [B]");
+  return t.data_ptr<int>();
+}
+
 std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, double scale,
-                             bool causal) {
+                             bool causal, const OptT& kv_len) {
   TORCH_CHECK(q.is_cuda(), "attention: GPU tensors required");
   const c10::DeviceGuard g(q.device());
   const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
@@ -220,13 +230,14 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   auto os = bshd_strides(o, "o");
   dca::attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                      B, H, Sq, Sk, D, qs.v, ks.v, vs.v, os.v, static_cast<float>(scale), causal,
-                     stream());
+                     kvlen_ptr(kv_len, B), stream());
   return {o, lse};
 }
 
 std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v,
                              const Tensor& o, const Tensor& lse, double scale, bool causal,
-                             const OptT& dq_out, const OptT& dk_out, const OptT& dv_out) {
+                             const OptT& dq_out, const OptT& dk_out, const OptT& dv_out,
+                             const OptT& kv_len) {
   const c10::DeviceGuard g(q.device());
   const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
   const int Sk = k.size(1);
@@ -246,7 +257,8 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   dca::attention_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dO.data_ptr(),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), nullptr,
                      dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, H, Sq, Sk, D, qs.v, ks.v, vs.v,
-                     os.v, dos.v, dqs.v, dks.v, dvs.v, static_cast<float>(scale), causal, stream());
+                     os.v, dos.v, dqs.v, dks.v, dvs.v, static_cast<float>(scale), causal,
+                     kvlen_ptr(kv_len, B), stream());
   return {dq, dk, dv};
 }
 // logits [N, V] contiguous, target [N] int64 -> (lse [N], per-row loss [N])
@@ -292,11 +304,13 @@ void register_transformer_ops(pybind11::module& m) {
         pybind11::arg("bias"), pybind11::arg("need_db") = true,
         pybind11::arg("dbias_acc") = pybind11::none());
   m.def("rope", &rope_apply);
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", &attn_fwd, pybind11::arg("q"), pybind11::arg("k"), pybind11::arg("v"),
+        pybind11::arg("scale"), pybind11::arg("causal"), pybind11::arg("kv_len") = pybind11::none());
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("attn_bwd", &attn_bwd, pybind11::arg("dout"), pybind11::arg("q"), pybind11::arg("k"),
         pybind11::arg("v"), pybind11::arg("o"), pybind11::arg("lse"), pybind11::arg("scale"),
         pybind11::arg("causal"), pybind11::arg("dq_out") = pybind11::none(),
-        pybind11::arg("dk_out") = pybind11::none(), pybind11::arg("dv_out") = pybind11::none());
+        pybind11::arg("dk_out") = pybind11::none(), pybind11::arg("dv_out") = pybind11::none(),
+        pybind11::arg("kv_len") = pybind11::none());
 }

@@ -56,8 +56,9 @@ def reference_rope(x, cos, sin, rot_dim: Optional[int] = None):
     return out.to(x.dtype)
 
 
-def reference_attention(q, k, v, causal=True, scale=None):
-    """q/k/v [B, S, H, D] -> [B, S, H, D] (fp32 math)."""
+def reference_attention(q, k, v, causal=True, scale=None, key_lengths=None):
+    """q/k/v [B, S, H, D] -> [B, S, H, D] (fp32 math). ``key_lengths`` [B]: keys at or past it
+    are masked (right padding), clamped to at least one key like the kernels."""
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
     s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
@@ -65,6 +66,10 @@ def reference_attention(q, k, v, causal=True, scale=None):
         S = s.shape[-1]
         mask = torch.ones(s.shape[-2], S, dtype=torch.bool, device=s.device).triu(1)
         s = s.masked_fill(mask, float("-inf"))
+    if key_lengths is not None:
+        kl = key_lengths.to(s.device).long().clamp_min(1)
+        pad = torch.arange(s.shape[-1], device=s.device)[None, :] >= kl[:, None]
+        s = s.masked_fill(pad[:, None, None, :], float("-inf"))
     p = torch.softmax(s, dim=-1)
     return torch.matmul(p, vf).transpose(1, 2).to(q.dtype)
 
@@ -280,17 +285,17 @@ def rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
 
 class _FlashAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, causal, scale):
-        o, lse = _ext.load().attn_fwd(q, k, v, scale, causal)
-        ctx.save_for_backward(q, k, v, o, lse)
+    def forward(ctx, q, k, v, causal, scale, kv_len):
+        o, lse = _ext.load().attn_fwd(q, k, v, scale, causal, kv_len)
+        ctx.save_for_backward(q, k, v, o, lse, kv_len)
         ctx.causal, ctx.scale = causal, scale
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse = ctx.saved_tensors
-        dq, dk, dv = _ext.load().attn_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal)
-        return dq, dk, dv, None, None
+        q, k, v, o, lse, kv_len = ctx.saved_tensors
+        dq, dk, dv = _ext.load().attn_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal, kv_len=kv_len)
+        return dq, dk, dv, None, None, None
 
 
 class _CrossEntropy(torch.autograd.Function):
@@ -327,35 +332,44 @@ class _FlashAttentionQKVPacked(torch.autograd.Function):
     backward writes dQ/dK/dV straight into one packed gradient (no stack/cat)."""
 
     @staticmethod
-    def forward(ctx, qkv, causal, scale):
+    def forward(ctx, qkv, causal, scale, kv_len):
         q, k, v = qkv.unbind(2)
-        o, lse = _ext.load().attn_fwd(q, k, v, scale, causal)
-        ctx.save_for_backward(qkv, o, lse)
+        o, lse = _ext.load().attn_fwd(q, k, v, scale, causal, kv_len)
+        ctx.save_for_backward(qkv, o, lse, kv_len)
         ctx.causal, ctx.scale = causal, scale
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, lse = ctx.saved_tensors
+        qkv, o, lse, kv_len = ctx.saved_tensors
         q, k, v = qkv.unbind(2)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.unbind(2)
-        _ext.load().attn_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal, dq, dk, dv)
-        return dqkv, None, None
+        _ext.load().attn_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal, dq, dk, dv, kv_len)
+        return dqkv, None, None, None
+
+
+def _kv_len(key_lengths: Optional[torch.Tensor], B: int, device) -> Optional[torch.Tensor]:
+    if key_lengths is None:
+        return None
+    if key_lengths.numel() != B:
+        raise ValueError(f"key_lengths must have one entry per batch row ({B})")
+    return key_lengths.to(device=device, dtype=torch.int32).contiguous()
 
 
 def flash_attention_qkvpacked(qkv: torch.Tensor, causal: bool = True,
-                              scale: Optional[float] = None) -> torch.Tensor:
+                              scale: Optional[float] = None,
+                              key_lengths: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``flash_attention`` for a packed [B, S, 3, H, D] QKV tensor -> [B, S, H, D]."""
     scale = scale if scale is not None else 1.0 / math.sqrt(qkv.shape[-1])
-    if not qkv.is_cuda:
-        q, k, v = qkv.unbind(2)
-        return reference_attention(q, k, v, causal, scale)
     q, k, v = qkv.unbind(2)
+    if not qkv.is_cuda:
+        return reference_attention(q, k, v, causal, scale, key_lengths)
     if not _attn_gpu_ok(q, k, v):
         raise ValueError("flash_attention_qkvpacked: GPU path needs bf16 [B,S,3,H,D] with D in "
                          "{64,128} and 16-byte aligned rows")
-    return _FlashAttentionQKVPacked.apply(qkv, causal, float(scale))
+    return _FlashAttentionQKVPacked.apply(qkv, causal, float(scale),
+                                          _kv_len(key_lengths, qkv.shape[0], qkv.device))
 
 
 def _attn_gpu_ok(q, k, v) -> bool:
@@ -368,16 +382,20 @@ def _attn_gpu_ok(q, k, v) -> bool:
 
 
 def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = True,
-                    scale: Optional[float] = None) -> torch.Tensor:
-    """softmax(q k^T * scale [+ causal mask]) v for [B, S, H, Dh] operands (Dh in {64, 128},
-    bf16 on GPU). Never materialises the S x S score matrix."""
+                    scale: Optional[float] = None,
+                    key_lengths: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """softmax(q k^T * scale [+ causal mask] [+ key padding]) v for [B, S, H, Dh] operands (Dh in
+    {64, 128}, bf16 on GPU). Never materialises the S x S score matrix. ``key_lengths`` [B]
+    (any integer dtype) is the number of valid keys per batch row -- right-padded batches such as
+    an HF ``attention_mask``; padded keys get zero weight and zero dK/dV, and every query row
+    (padded ones too) attends to the valid keys, as with an additive padding mask."""
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if not q.is_cuda:
-        return reference_attention(q, k, v, causal, scale)
+        return reference_attention(q, k, v, causal, scale, key_lengths)
     if not _attn_gpu_ok(q, k, v):
         raise ValueError("flash_attention: GPU path needs bf16 [B,S,H,D] with D in {64,128} and "
                          "16-byte aligned rows")
-    return _FlashAttention.apply(q, k, v, causal, float(scale))
+    return _FlashAttention.apply(q, k, v, causal, float(scale), _kv_len(key_lengths, q.shape[0], q.device))
 
 
 __all__ = ["layer_norm", "bias_gelu", "rope", "rope_tables", "flash_attention",

@@ -45,7 +45,10 @@ class EmbeddingProcessor(experimental.TorchBatchProcessor):
         self.context = context
         model = build_encoder()
         if torch.cuda.is_available():
-            model = model.to(torch.bfloat16)
+            # bf16 + the MFMA attention kernels; padded documents go through key-length masking
+            from determined_clone_amd.transformers import use_flash_attention
+
+            model = use_flash_attention(model.to(torch.bfloat16))
         self.model = context.prepare_model_for_inference(model)
         self.indices, self.embeddings = [], []
         self.last_index = 0

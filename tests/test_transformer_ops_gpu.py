@@ -117,6 +117,92 @@ def test_flash_attention(D, causal, S):
         assert _rel(a.grad, b.grad) < 2e-2, _rel(a.grad, b.grad)
 
 
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("Sq,Sk", [(300, 300), (77, 300), (512, 129)])
+def test_flash_attention_key_padding(D, causal, Sq, Sk):
+    """Per-row key lengths (right padding): lengths of 1, inside a tile, on a tile boundary and
+    the full length; padded keys must get exactly zero dK / dV."""
+    if causal and Sq != Sk:
+        pytest.skip("causal needs Sq == Sk")
+    _C()
+    torch.manual_seed(6)
+    B, H = 4, 2
+    lens = torch.tensor([1, Sk // 2 + 3, min(128, Sk), Sk], device="cuda")
+    q = torch.randn(B, Sq, H, D, device="cuda").bfloat16()
+    k, v = (torch.randn(B, Sk, H, D, device="cuda").bfloat16() for _ in range(2))
+    qs = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    qr = [t.float().clone().requires_grad_(True) for t in (q, k, v)]
+    o = T.flash_attention(*qs, causal=causal, key_lengths=lens)
+    o2 = T.reference_attention(*qr, causal=causal, key_lengths=lens)
+    assert _rel(o, o2) < 1e-2, _rel(o, o2)
+    g = torch.randn_like(o2)
+    o.backward(g.bfloat16())
+    o2.backward(g)
+    for a, b in zip(qs, qr):
+        assert _rel(a.grad, b.grad) < 2e-2, _rel(a.grad, b.grad)
+    for b_, L in enumerate(lens.tolist()):
+        if L < Sk:
+            assert qs[1].grad[b_, L:].abs().max().item() == 0
+            assert qs[2].grad[b_, L:].abs().max().item() == 0
+
+
+def test_flash_attention_key_padding_qkvpacked():
+    _C()
+    torch.manual_seed(7)
+    B, S, H, D = 3, 200, 4, 64
+    lens = torch.tensor([200, 64, 130], dtype=torch.int64, device="cuda")
+    qkv = torch.randn(B, S, 3, H, D, device="cuda").bfloat16().requires_grad_(True)
+    o = T.flash_attention_qkvpacked(qkv, causal=False, key_lengths=lens)
+    qkv2 = qkv.detach().float().requires_grad_(True)
+    o2 = T.reference_attention(*qkv2.unbind(2), causal=False, key_lengths=lens)
+    assert _rel(o, o2) < 1e-2
+    g = torch.randn_like(o2)
+    o.backward(g.bfloat16())
+    o2.backward(g)
+    assert _rel(qkv.grad, qkv2.grad) < 2e-2
+
+
+@pytest.mark.parametrize("family", ["bert", "vit"])
+def test_hf_models_on_flash_attention_match_sdpa(family):
+    """HF BERT with a right-padded attention_mask and ViT (S = 197, no mask) on the
+    ``dca_mfma`` attention backend agree with HF's own SDPA path, forward and backward."""
+    transformers = pytest.importorskip("transformers")
+    from determined_clone_amd.transformers import use_flash_attention
+
+    _C()
+    torch.manual_seed(8)
+    if family == "bert":
+        cfg = transformers.BertConfig(vocab_size=1000, hidden_size=256, num_hidden_layers=2,
+                                      num_attention_heads=4, intermediate_size=512,
+                                      attention_probs_dropout_prob=0.0, hidden_dropout_prob=0.0)
+        make = transformers.BertModel
+        ids = torch.randint(1, 1000, (3, 96), device="cuda")
+        mask = (torch.arange(96, device="cuda")[None] < torch.tensor([96, 40, 7], device="cuda")[:, None]).long()
+        inputs = {"input_ids": ids, "attention_mask": mask}
+    else:
+        cfg = transformers.ViTConfig(image_size=224, patch_size=16, hidden_size=256, num_hidden_layers=2,
+                                     num_attention_heads=4, intermediate_size=512,
+                                     attention_probs_dropout_prob=0.0, hidden_dropout_prob=0.0)
+        make = transformers.ViTModel
+        inputs = {"pixel_values": torch.randn(2, 3, 224, 224, device="cuda").bfloat16()}
+        mask = None
+    ref = make(cfg).cuda().bfloat16()
+    ours = make(cfg).cuda().bfloat16()
+    ours.load_state_dict(ref.state_dict())
+    ref.set_attn_implementation("sdpa")
+    use_flash_attention(ours)
+    outs = []
+    for m in (ref, ours):
+        h = m(**inputs).last_hidden_state
+        keep = mask[..., None].to(h.dtype) if mask is not None else torch.ones_like(h[..., :1])
+        (h.float() * keep).square().mean().backward()
+        wq = next(p for n, p in m.named_parameters() if n.endswith(("query.weight", "q_proj.weight")))
+        outs.append((h.float() * keep, wq.grad.float()))
+    assert _rel(outs[1][0], outs[0][0]) < 2e-2
+    assert _rel(outs[1][1], outs[0][1]) < 5e-2
+
+
 def test_flash_attention_strided_qkv_slices():
     """Operands sliced from a fused QKV projection output [B, S, 3, H, D] need no copies."""
     _C()
