@@ -49,8 +49,12 @@ def share_devices(devs: List[Dict[str, Any]], slots_per_gpu: int) -> List[Dict[s
     return out
 
 
-def detect_devices(artificial_slots: int = 0, slots_per_gpu: int = 1) -> List[Dict[str, Any]]:
+def detect_devices(artificial_slots: int = 0, slots_per_gpu: int = 1,
+                   max_gpus: int = 0) -> List[Dict[str, Any]]:
     devs = _detect_physical(artificial_slots)
+    if max_gpus > 0:  # the first N ROCm devices (e.g. a 1/2/4/8-GPU run on one node)
+        gpus = [d for d in devs if d["type"] == "rocm"][:max_gpus]
+        devs = gpus or devs
     return share_devices(devs, slots_per_gpu) if slots_per_gpu > 1 else devs
 
 
@@ -98,7 +102,8 @@ class _Task:
 class Agent:
     def __init__(self, master_url: str, agent_id: Optional[str] = None, pool: str = "default",
                  artificial_slots: int = 0, label: str = "", username: str = "admin",
-                 password: str = "", workdir: Optional[str] = None, slots_per_gpu: int = 1) -> None:
+                 password: str = "", workdir: Optional[str] = None, slots_per_gpu: int = 1,
+                 max_gpus: int = 0) -> None:
         self.session = Session(master_url)
         tok = self.session.post("/api/v1/auth/login", {"username": username, "password": password})["token"]
         self.session.token = tok
@@ -106,7 +111,7 @@ class Agent:
         self.id = agent_id or socket.gethostname()
         self.pool = pool
         self.label = label
-        self.devices = detect_devices(artificial_slots, slots_per_gpu)
+        self.devices = detect_devices(artificial_slots, slots_per_gpu, max_gpus)
         self.tasks: Dict[str, _Task] = {}
         self.workdir = workdir or tempfile.mkdtemp(prefix="det-clone-agent-")
         os.makedirs(self.workdir, exist_ok=True)  # the zygote binds its socket here right away
@@ -255,6 +260,7 @@ def main() -> None:
     ap.add_argument("--label", default="")
     ap.add_argument("--slots-per-gpu", type=int, default=1,
                     help="expose each MI355X as this many slots (HP-search trials sharing a GPU)")
+    ap.add_argument("--max-gpus", type=int, default=0, help="use only the first N GPUs (0 = all)")
     ap.add_argument("--master-cert-file", default=None,
                     help="CA / self-signed cert of an HTTPS master, or 'noverify'")
     ap.add_argument("--master-cert-name", default=None,
@@ -269,7 +275,7 @@ def main() -> None:
     if args.master_cert_name:
         os.environ["DET_MASTER_CERT_NAME"] = args.master_cert_name
     Agent(args.master_url, args.agent_id, args.resource_pool, args.artificial_slots, args.label,
-          slots_per_gpu=args.slots_per_gpu).run()
+          slots_per_gpu=args.slots_per_gpu, max_gpus=args.max_gpus).run()
 
 
 if __name__ == "__main__":

@@ -50,5 +50,5 @@ class CIFARTrial(pytorch.PyTorchTrial):
 
     def build_validation_data_loader(self):
         n = int(self.context.get_hparams().get("val_records", 10000))
-        return pytorch.DataLoader(cifar.SyntheticCIFAR10(n, seed=1),
+        return pytorch.DataLoader(cifar.SyntheticCIFAR10(n, seed=1, label_noise=0.0),
                                   batch_size=self.context.get_per_slot_batch_size())

@@ -31,3 +31,29 @@ def test_bench_asha_cpu_plumbing(tmp_path):
     assert res["experiment_state"] == "COMPLETED"
     assert res["trials_completed"] == 4
     assert res["value"] > 0
+    assert 0 < res["startup_share"] < 1 and res["startup_mean_s"] > 0
+    assert res["allocations"] >= 4 and len(res["validation_error_quartiles"]) == 5
+
+
+def test_detect_devices_max_gpus(monkeypatch):
+    from determined_clone_amd.agent import agent as A
+
+    phys = [{"id": i, "uuid": f"g{i}", "type": "rocm"} for i in range(8)]
+    monkeypatch.setattr(A, "_detect_physical", lambda artificial_slots=0: [dict(d) for d in phys])
+    devs = A.detect_devices(0, slots_per_gpu=4, max_gpus=2)
+    assert len(devs) == 8 and {d["device_index"] for d in devs} == {0, 1}
+    assert len(A.detect_devices(0, 1, 0)) == 8
+
+
+def test_synthetic_cifar_is_learnable_but_noisy():
+    import numpy as np
+
+    from determined_clone_amd.models.cifar import SyntheticCIFAR10
+
+    tr, va = SyntheticCIFAR10(2000, seed=0), SyntheticCIFAR10(500, seed=1, label_noise=0.0)
+    assert tr.x.dtype == np.float16 and tr[0][0].shape == (3, 32, 32)
+    # nearest-class-mean on raw pixels is far from perfect (position jitter + low signal) ...
+    means = np.stack([tr.x[tr.y == c].astype(np.float32).mean(0) for c in range(10)])
+    pred = ((va.x.astype(np.float32)[:, None] - means[None]) ** 2).sum((2, 3, 4)).argmin(1)
+    acc = (pred == va.y).mean()
+    assert 0.15 < acc < 0.95, acc

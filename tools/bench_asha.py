@@ -9,11 +9,15 @@ fused BN+ReLU HIP kernel, fused SGD) as separate trial processes; adaptive ASHA 
 them. The value is COMPLETED trials / wall-clock hours from experiment creation to the searcher's
 shutdown (trial process start-up, validation and checkpointing included).
 
-Search length is scaled down from the example's 8 x 50k-image epochs (``--records-per-epoch``,
-``--epochs``) so a run fits a short GPU slot; the searcher config (adaptive_asha, standard mode,
-max_concurrent_trials) is the example's. Data: synthetic CIFAR-shaped tensors (no network).
+Defaults are the example's search (examples/cifar10_asha/adaptive.yaml): 50,000 records x 8
+epochs, 64 trials, 16 concurrent, batch 128, on ``--gpus N`` GPUs of this node (each GPU exposed as
+ceil(16 / N) slots so the 16 concurrent trials are gang-scheduled onto them). Data: synthetic
+CIFAR-shaped, class-conditional with position jitter and 10 % label noise (models/cifar.py), so the
+validation errors spread and ASHA really prunes. The JSON also reports the share of allocation
+time spent in trial start-up (process spawn to the first training batch, from the trials'
+DET_STARTUP_TRACE marks) and the spread of final validation errors.
 
-Usage: ``python tools/bench_asha.py [--slots-per-gpu 8 --max-trials 32 --max-concurrent 8]``;
+Usage: ``python tools/bench_asha.py [--gpus N] [--max-trials 64 --max-concurrent 16]``;
 prints one JSON line.
 """
 import argparse
@@ -70,36 +74,59 @@ def _print_trace(s: Session, trials: list) -> None:
               file=sys.stderr, flush=True)
 
 
+def _startup_share(m, s: Session, trials: list) -> dict:
+    """Start-up seconds (spawn -> first training batch, one mark per trial process) summed over
+    every allocation, over the summed allocation wall time."""
+    import re
+
+    marks = []
+    for t in trials:
+        for line in s.get(f"/api/v1/trials/{t['id']}/logs")["logs"]:
+            mm = re.search(r"startup: first train batch at \+([0-9.]+)s", line["log"])
+            if mm:
+                marks.append(float(mm.group(1)))
+    rows = m.db.all("SELECT start_time, end_time FROM allocations")
+    alloc_s = sum(max(0.0, (r["end_time"] or time.time()) - (r["start_time"] or 0.0)) for r in rows)
+    return {"share": round(sum(marks) / alloc_s, 4) if alloc_s else None,
+            "mean_s": round(sum(marks) / len(marks), 3) if marks else None, "allocations": len(rows)}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--slots-per-gpu", type=int, default=8)
-    ap.add_argument("--max-trials", type=int, default=32)
-    ap.add_argument("--max-concurrent", type=int, default=8)
-    ap.add_argument("--epochs", type=int, default=4)
-    ap.add_argument("--records-per-epoch", type=int, default=6400)
+    ap.add_argument("--gpus", type=int, default=0, help="GPUs of this node to use (0 = all)")
+    ap.add_argument("--slots-per-gpu", type=int, default=0,
+                    help="slots per GPU (0 = ceil(max_concurrent / gpus))")
+    ap.add_argument("--max-trials", type=int, default=64)
+    ap.add_argument("--max-concurrent", type=int, default=16)
+    ap.add_argument("--epochs", type=int, default=8)
+    ap.add_argument("--records-per-epoch", type=int, default=50000)
     ap.add_argument("--batch", type=int, default=128)
-    ap.add_argument("--timeout", type=float, default=1500.0)
+    ap.add_argument("--timeout", type=float, default=3000.0)
     ap.add_argument("--cpu", action="store_true", help="artificial CPU slots (plumbing check)")
     ap.add_argument("--trace", action="store_true",
-                    help="DET_STARTUP_TRACE=1 in the trials; print mean start-up phase times to stderr")
+                    help="also print mean start-up phase times to stderr")
     args = ap.parse_args()
 
     tmp = tempfile.mkdtemp(prefix="det-asha-bench-")
     m = Master(os.path.join(tmp, "m.db"),
                checkpoint_storage={"type": "shared_fs", "host_path": os.path.join(tmp, "ckpt")})
     srv = MasterServer(m, "127.0.0.1", 0).start()
+    from determined_clone_amd.agent.agent import _detect_physical
+
+    phys = [d for d in _detect_physical() if d["type"] == "rocm"]
+    n_gpus = min(args.gpus, len(phys)) if args.gpus and phys else len(phys)
+    spg = args.slots_per_gpu or max(1, -(-args.max_concurrent // max(1, n_gpus)))
     agent = Agent(m.master_url, "agent-0", artificial_slots=args.max_concurrent if args.cpu else 0,
-                  workdir=os.path.join(tmp, "agent"), slots_per_gpu=args.slots_per_gpu).start_background()
-    n_gpus = len({d.get("device_index", d["id"]) for d in agent.devices if d["type"] == "rocm"})
+                  workdir=os.path.join(tmp, "agent"), slots_per_gpu=spg,
+                  max_gpus=n_gpus if not args.cpu else 0).start_background()
     s = Session(m.master_url)
     s.token = s.post("/api/v1/auth/login", {"username": "admin", "password": ""})["token"]
     try:
         cfg = search_config(args)
-        if args.trace:
-            env = cfg.setdefault("environment", {}).setdefault("environment_variables", [])
-            env.append("DET_STARTUP_TRACE=1")
-            if os.environ.get("DET_STARTUP_PROFILE"):
-                env.append("DET_STARTUP_PROFILE=1")
+        env = cfg.setdefault("environment", {}).setdefault("environment_variables", [])
+        env.append("DET_STARTUP_TRACE=1")  # per-trial start-up marks (start-up share below)
+        if os.environ.get("DET_STARTUP_PROFILE"):
+            env.append("DET_STARTUP_PROFILE=1")
         body = {"config": cfg, "model_definition": base64.b64encode(
             tar_directory(os.path.join(ROOT, "examples", "cifar10_asha"))).decode()}
         t0 = time.time()
@@ -120,11 +147,9 @@ def main() -> None:
         trials = s.get(f"/api/v1/experiments/{eid}/trials")["trials"]
         done = [t for t in trials if t["state"] == "COMPLETED"]
         steps = sum(int(t.get("steps_completed") or 0) for t in done)
-        best = None
-        for t in done:
-            v = t.get("best_validation")
-            if v is not None and (best is None or v < best):
-                best = v
+        vals = sorted(t["best_validation"] for t in done if t.get("best_validation") is not None)
+        best = vals[0] if vals else None
+        startup = _startup_share(m, s, trials)
         if args.trace:
             _print_trace(s, trials)
         if state != "COMPLETED":
@@ -138,9 +163,13 @@ def main() -> None:
             "unit": "trials/hr", "n_gpus": n_gpus, "higher_is_better": True,
             "experiment_state": state, "trials_completed": len(done), "trials_created": len(trials),
             "batches_trained": steps, "wall_s": round(wall, 1), "best_validation_error": best,
+            "validation_error_quartiles": [round(vals[int(q * (len(vals) - 1))], 4) for q in (0, .25, .5, .75, 1)]
+            if vals else None,
+            "startup_share": startup["share"], "startup_mean_s": startup["mean_s"],
+            "allocations": startup["allocations"],
             "dtype": "bf16" if not args.cpu else "fp32", "data": "synthetic CIFAR-10-shaped",
             "config": {"model": "cifar10_cnn", "searcher": "adaptive_asha", "max_trials": args.max_trials,
-                       "max_concurrent_trials": args.max_concurrent, "slots_per_gpu": args.slots_per_gpu,
+                       "max_concurrent_trials": args.max_concurrent, "slots_per_gpu": spg,
                        "max_length_epochs": args.epochs, "records_per_epoch": args.records_per_epoch,
                        "global_batch": args.batch}}), flush=True)
     finally:
