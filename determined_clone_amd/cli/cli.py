@@ -167,8 +167,8 @@ def experiment_create(args):
         for p in parts[:-1]:
             d = d.setdefault(p, {})
         d[parts[-1]] = yaml.safe_load(v)
-    if args.test:
-        return _local_test(cfg, args.model_def)
+    if args.local:
+        return _local_test(cfg, args.model_def) if args.test else _local_train(cfg, args.model_def)
     body: Dict[str, Any] = {"config": cfg, "activate": not args.paused}
     if args.model_def:
         body["model_definition"] = base64.b64encode(tar_directory(args.model_def)).decode()
@@ -177,6 +177,8 @@ def experiment_create(args):
     if args.project_id:
         body["project_id"] = args.project_id
     s = session(args)
+    if args.test:
+        return _cluster_test(s, body, cfg)
     exp = s.post("/api/v1/experiments", body)["experiment"]
     print(f"Created experiment {exp['id']}")
     if getattr(args, "publish", None):
@@ -216,24 +218,107 @@ def _publish_first_trial(args, s: Session, eid: int) -> None:
         _wait_terminal(s, eid)
 
 
-def _local_test(cfg: Dict[str, Any], context: Optional[str]) -> None:
-    """``--test``: validate the config and run one batch of train + validate locally."""
-    from determined_clone_amd import pytorch
+def _test_experiment_config(cfg: Dict[str, Any]) -> Dict[str, Any]:
+    """The cluster test experiment (reference `_execution.py:77-120` _make_test_experiment_config):
+    one batch, validation after it, no restarts, no kept checkpoints."""
+    import uuid
+
+    t = dict(cfg)
+    t.update({
+        "description": f"[test-mode] {t.get('description', str(uuid.uuid4()))}",
+        "scheduling_unit": 1, "min_validation_period": {"batches": 1}, "max_restarts": 0,
+        "checkpoint_storage": {**(t.get("checkpoint_storage") or {}), "save_experiment_best": 0,
+                               "save_trial_best": 0, "save_trial_latest": 0},
+        "searcher": {"name": "single", "metric": (t.get("searcher") or {}).get("metric", "validation_loss"),
+                     "max_length": {"batches": 1}},
+    })
+    return t
+
+
+def _cluster_test(s: Session, body: Dict[str, Any], cfg: Dict[str, Any]) -> None:
+    """``det e create --test``: validate the config on the master, then run a one-batch test
+    experiment on the cluster and follow it (reference `cli/experiment.py:269-281`)."""
+    s.post("/api/v1/experiments", dict(body, validate_only=True))
+    print("Experiment configuration validation succeeded")
+    exp = s.post("/api/v1/experiments", dict(body, config=_test_experiment_config(cfg), activate=True))["experiment"]
+    print(f"Created test experiment {exp['id']}")
+    state = _wait_terminal(s, exp["id"])
+    trials = s.get(f"/api/v1/experiments/{exp['id']}/trials")["trials"]
+    if state != "COMPLETED":
+        for t in trials[:1]:
+            for line in s.get(f"/api/v1/trials/{t['id']}/logs")["logs"][-30:]:
+                print(line["log"], end="" if line["log"].endswith("\n") else "\n")
+        raise SystemExit(f"Test experiment {exp['id']} ended {state}")
+    s.post(f"/api/v1/experiments/{exp['id']}/archive")
+    print(f"Test experiment {exp['id']} completed successfully")
+
+
+def _local_setup(cfg: Dict[str, Any], context: Optional[str]):
     from determined_clone_amd.config import expconf
     from determined_clone_amd.exec.harness import load_trial_class
 
     full = expconf.complete(cfg)
     if context:
         os.environ["DET_CONTEXT_DIR"] = os.path.abspath(context)
+        if os.path.abspath(context) not in sys.path:
+            sys.path.insert(0, os.path.abspath(context))
     hp = {k: (v.get("val") if isinstance(v, dict) and v.get("type") == "const" else
               v.get("minval") if isinstance(v, dict) and "minval" in v else
               (v.get("vals") or [None])[0] if isinstance(v, dict) and "vals" in v else v)
           for k, v in full["hyperparameters"].items()}
-    cls = load_trial_class(full["entrypoint"])
+    return full, hp, load_trial_class(full["entrypoint"])
+
+
+def _local_test(cfg: Dict[str, Any], context: Optional[str]) -> None:
+    """``--local --test``: validate the config and run one batch of train + validate locally
+    (reference `cli/experiment.py:327-354` local_experiment / test_one_batch)."""
+    from determined_clone_amd import pytorch
+
+    full, hp, cls = _local_setup(cfg, context)
     with pytorch.init(hparams=hp, exp_conf=full) as ctx:
         pytorch.Trainer(cls(ctx), ctx).fit(max_length=pytorch.Batch(1), test_mode=True,
                                            checkpoint_policy="none")
     print("Model definition test succeeded")
+
+
+def _train_unit(spec: Any, gbs: Optional[int]):
+    """An expconf length ({batches: N} / {epochs: N} / {records: N} / bare int = batches)."""
+    from determined_clone_amd import pytorch
+
+    if spec is None:
+        return None
+    if not isinstance(spec, dict):
+        return pytorch.Batch(int(spec))
+    unit, n = next(iter(spec.items()))
+    if int(n) <= 0:  # expconf's "no period" default
+        return None
+    if unit == "epochs":
+        return pytorch.Epoch(int(n))
+    if unit == "records":
+        return pytorch.Batch(max(1, -(-int(n) // int(gbs or 1))))
+    return pytorch.Batch(int(n))
+
+
+def _local_train(cfg: Dict[str, Any], context: Optional[str]) -> None:
+    """``--local`` (without ``--test``): train one trial here, on this machine's GPUs, for the
+    searcher's ``max_length`` with the config's validation / checkpoint periods -- no master.
+    Hyperparameters take their const / first / lower-bound values. (The reference stops at
+    ``--local --test``; full local training is this framework's addition.)"""
+    from determined_clone_amd import pytorch
+
+    full, hp, cls = _local_setup(cfg, context)
+    gbs = hp.get("global_batch_size")
+    max_length = _train_unit((full.get("searcher") or {}).get("max_length"), gbs)
+    if max_length is None:
+        raise SystemExit("--local training needs searcher.max_length")
+    with pytorch.init(hparams=hp, exp_conf=full) as ctx:
+        pytorch.Trainer(cls(ctx), ctx).fit(
+            max_length=max_length,
+            validation_period=_train_unit(full.get("min_validation_period"), gbs),
+            checkpoint_period=_train_unit(full.get("min_checkpoint_period"), gbs),
+            checkpoint_policy="all")
+    unit = "epochs" if isinstance(max_length, pytorch.Epoch) else "batches"
+    print(f"Local training finished ({max_length.value} {unit})")
 
 
 def _follow_first_trial(s: Session, eid: int) -> None:
@@ -898,6 +983,8 @@ def build_parser() -> argparse.ArgumentParser:
     sp = cmd(e, "create", experiment_create)
     sp.add_argument("config_file"); sp.add_argument("model_def", nargs="?")
     sp.add_argument("--paused", action="store_true"); sp.add_argument("--test", "--test-mode", dest="test", action="store_true")
+    sp.add_argument("--local", action="store_true",
+                    help="run here instead of on the cluster (with --test: one batch; without: the whole trial)")
     sp.add_argument("--template"); sp.add_argument("--project-id", type=int)
     sp.add_argument("--config", action="append", help="override: key.path=value")
     sp.add_argument("-f", "--follow-first-trial", action="store_true")

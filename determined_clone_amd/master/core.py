@@ -197,7 +197,8 @@ class Master:
     def create_experiment(self, config_text: Any, model_def: Optional[bytes] = None,
                           parent_id: Optional[int] = None, activate: bool = True,
                           project_id: Optional[int] = None, owner_id: int = 1,
-                          template: Optional[str] = None, unmanaged: bool = False) -> Experiment:
+                          template: Optional[str] = None, unmanaged: bool = False,
+                          validate_only: bool = False) -> Optional[Experiment]:
         raw = expconf.parse(config_text)
         if template:
             t = self.db.one("SELECT config FROM templates WHERE name=?", [template])
@@ -213,6 +214,8 @@ class Master:
             # Experiment-level GC policy (save_*) over the cluster's storage backend.
             raw["checkpoint_storage"] = {**self.checkpoint_storage, **cs}
         cfg = expconf.complete(raw)
+        if validate_only:  # CreateExperimentRequest.validateOnly: check the config, create nothing
+            return None
         seed = cfg["reproducibility"].get("experiment_seed")
         if seed is None:
             seed = int(time.time() * 1000) % (2 ** 31)

@@ -334,11 +334,14 @@ def create_experiment(r: Req) -> Any:
         e = r.m.create_experiment(r.body["config"], blob, r.body.get("parent_id"),
                                   activate=r.body.get("activate", True),
                                   project_id=r.body.get("project_id"), owner_id=r.user["id"],
-                                  template=r.body.get("template"), unmanaged=bool(r.body.get("unmanaged")))
+                                  template=r.body.get("template"), unmanaged=bool(r.body.get("unmanaged")),
+                                  validate_only=bool(r.body.get("validate_only")))
     except InvalidConfigurationException as ex:
         raise HTTPError(400, str(ex))
     except KeyError as ex:
         raise HTTPError(404, str(ex))
+    if e is None:
+        return {"experiment": None, "config": None}
     return {"experiment": r.m.experiment_api(e.id), "config": e.config}
 
 

@@ -159,6 +159,75 @@ function metricCharts(rowsBySeries) {
   })), "batches")));
 }
 
+// Parallel coordinates (reference ExperimentVisualization HpParallelCoordinates): one vertical
+// axis per hyperparameter plus the searcher metric, one polyline per trial, coloured from best
+// (red) to worst (blue) on the metric. Categorical / string hparams get evenly spaced categories.
+function hpAxes(trials, keys) {
+  return keys.map((k) => {
+    const vals = trials.map((t) => (t.hparams || {})[k]);
+    const numeric = vals.every((v) => typeof v === "number");
+    if (numeric) {
+      const lo = Math.min(...vals), hi = Math.max(...vals);
+      const log = lo > 0 && hi / lo > 50;
+      const f = (v) => (log ? Math.log10(v) : v);
+      const a = f(lo), b = f(hi);
+      return { key: k, pos: (v) => (b === a ? 0.5 : (f(v) - a) / (b - a)), ticks: [lo, hi].map(fmtNum), log };
+    }
+    const cats = [...new Set(vals.map((v) => JSON.stringify(v)))].sort();
+    return { key: k, pos: (v) => (cats.length < 2 ? 0.5 : cats.indexOf(JSON.stringify(v)) / (cats.length - 1)), ticks: cats, cats: true };
+  });
+}
+function parallelCoords(title, trials, keys, metric, smallerIsBetter) {
+  const NS = "http://www.w3.org/2000/svg";
+  const scored = trials.filter((t) => typeof t.best_validation === "number");
+  const W = Math.max(460, 130 * (keys.length + 1)), H = 280, T = 24, B = 30, L = 40, R = 40;
+  const svg = document.createElementNS(NS, "svg");
+  svg.setAttribute("viewBox", `0 0 ${W} ${H}`);
+  svg.setAttribute("class", "pcoords");
+  const mk = (tag, attrs, text) => {
+    const e = document.createElementNS(NS, tag);
+    for (const [k, v] of Object.entries(attrs)) e.setAttribute(k, v);
+    if (text !== undefined) e.textContent = text;
+    svg.appendChild(e);
+    return e;
+  };
+  if (!scored.length || !keys.length) {
+    mk("text", { x: W / 2, y: H / 2, "text-anchor": "middle", fill: "#6b7685", "font-size": 12 }, "no scored trials");
+    return h("div", { class: "card chart wide" }, h("div", { class: "title" }, title), svg);
+  }
+  const axes = hpAxes(scored, keys);
+  const ms = scored.map((t) => t.best_validation);
+  const m0 = Math.min(...ms), m1 = Math.max(...ms);
+  axes.push({ key: metric, pos: (v) => (m1 === m0 ? 0.5 : (v - m0) / (m1 - m0)), ticks: [m0, m1].map(fmtNum), metric: true });
+  const xs = axes.map((_, i) => L + (i * (W - L - R)) / Math.max(1, axes.length - 1));
+  const y = (p) => H - B - p * (H - T - B);
+  // colour: 0 = best, 1 = worst
+  const rank = (v) => (m1 === m0 ? 0 : smallerIsBetter === false ? (m1 - v) / (m1 - m0) : (v - m0) / (m1 - m0));
+  const colour = (q) => `rgb(${Math.round(200 - 170 * q)},${Math.round(40 + 60 * q)},${Math.round(46 + 150 * q)})`;
+  // worst first so the best trials are drawn on top
+  for (const t of scored.slice().sort((a, b) => rank(b.best_validation) - rank(a.best_validation))) {
+    const pts = axes.map((a, i) => xs[i] + "," + y(a.pos(a.metric ? t.best_validation : t.hparams[a.key])));
+    const line = mk("polyline", { points: pts.join(" "), fill: "none", stroke: colour(rank(t.best_validation)),
+      "stroke-width": 1.4, "stroke-opacity": 0.8, "data-trial": t.id });
+    const tip = document.createElementNS(NS, "title");
+    tip.textContent = `trial ${t.id}: ${metric}=${fmtNum(t.best_validation)}`;
+    line.appendChild(tip);
+  }
+  axes.forEach((a, i) => {
+    mk("line", { x1: xs[i], x2: xs[i], y1: T, y2: H - B, stroke: "#6b7685" });
+    mk("text", { x: xs[i], y: 14, "text-anchor": "middle", "font-size": 11, "font-weight": a.metric ? "bold" : "normal" },
+      a.key + (a.log ? " (log)" : ""));
+    const ticks = a.cats ? a.ticks : [a.ticks[0], a.ticks[1]];
+    ticks.forEach((tk, j) => {
+      const p = a.cats ? (ticks.length < 2 ? 0.5 : j / (ticks.length - 1)) : j;
+      mk("text", { x: xs[i] + 4, y: y(p) + (j === 0 && !a.cats ? -2 : 10), "font-size": 9, fill: "#6b7685" }, String(tk).replace(/^"|"$/g, ""));
+    });
+  });
+  return h("div", { class: "card chart wide" }, h("div", { class: "title" }, title), svg,
+    h("div", { class: "legend" }, h("span", {}, h("i", { style: `background:${colour(0)}` }), "best"),
+      h("span", {}, h("i", { style: `background:${colour(1)}` }), "worst")));
+}
+
 // ------------------------------------------------------------------------------------ pages
 async function pageLogin(params) {
   const user = h("input", { placeholder: "username", value: "determined", autocomplete: "username" });
@@ -261,7 +330,14 @@ async function pageExperiment(params, id) {
         [{ name: metric, points: vh.validation_history.map((v) => [v.end_time - e.start_time, v.searcher_metric]) }], "seconds since start"),
       lineChart("Trials by best validation", [{ name: metric, points: trials.filter((t) => typeof t.best_validation === "number").map((t) => [t.id, t.best_validation]) }], "trial id")));
     }
-    parts.push(h("h2", {}, "Trials"), table(cols, trials, { sortKey: "id", desc: false }));
+    const picked = new Set();
+    cols.unshift({ key: "pick", label: "", render: (t) => h("input", { type: "checkbox", class: "pick",
+      onchange: (ev) => { if (ev.target.checked) picked.add(t.id); else picked.delete(t.id); } }) });
+    const compare = h("button", { onclick: () => {
+      if (picked.size < 1) { alert("select trials to compare"); return; }
+      nav("#/compare", { trials: [...picked].sort((a, b) => a - b).join(",") });
+    } }, "Compare selected");
+    parts.push(h("h2", {}, "Trials"), h("div", { class: "toolbar" }, compare), table(cols, trials, { sortKey: "id", desc: false }));
     body = parts;
   } else if (tab === "visualization") {
     // hyperparameter search view: learning curves of up to 20 trials + metric vs each numeric hparam
@@ -274,7 +350,12 @@ async function pageExperiment(params, id) {
     const numeric = [...new Set(trials.flatMap((t) => Object.keys(t.hparams || {})))]
       .filter((k) => trials.some((t) => typeof (t.hparams || {})[k] === "number"));
     const scored = trials.filter((t) => typeof t.best_validation === "number");
-    body = [h("div", { class: "charts" }, lineChart(`Validation ${metric} by trial`, curves, "batches")),
+    const hpKeys = [...new Set(trials.flatMap((t) => Object.keys(t.hparams || {})))]
+      .filter((k) => trials.every((t) => (t.hparams || {})[k] !== undefined && typeof t.hparams[k] !== "object"))
+      .filter((k) => new Set(trials.map((t) => JSON.stringify(t.hparams[k]))).size > 1);
+    body = [h("div", { class: "charts" }, parallelCoords(`Hyperparameters → best ${metric}`, trials, hpKeys, metric,
+      (e.config.searcher || {}).smaller_is_better)),
+      h("div", { class: "charts" }, lineChart(`Validation ${metric} by trial`, curves, "batches")),
       h("h2", {}, `Best ${metric} vs hyperparameters`),
       numeric.length ? h("div", { class: "charts" }, numeric.map((k) => lineChart(k,
         [{ name: k, points: scored.filter((t) => typeof t.hparams[k] === "number").map((t) => [t.hparams[k], t.best_validation]) }],
@@ -325,7 +406,7 @@ async function pageTrial(params, id) {
     h("div", { class: "toolbar" }, link("#/experiments/" + t.experiment_id, `experiment ${t.experiment_id}`),
       h("span", { class: "muted" }, `batches ${t.steps_completed || 0} · restarts ${t.restarts || 0} · started ${fmtTime(t.start_time)}`),
       !["COMPLETED", "CANCELED", "ERROR"].includes(t.state) ? h("button", { onclick: () => act(() => api.post(`/api/v1/trials/${id}/kill`)) }, "Kill") : null),
-    tabs(`#/trials/${id}`, tab, ["metrics", "hyperparameters", "checkpoints", "logs", "profiler"]));
+    tabs(`#/trials/${id}`, tab, ["metrics", "workloads", "hyperparameters", "checkpoints", "logs", "profiler"]));
   let body;
   if (tab === "metrics") {
     const { metrics } = await api.get(`/api/v1/trials/${id}/metrics`);
@@ -336,12 +417,71 @@ async function pageTrial(params, id) {
       Object.entries(t.hparams || {}).map(([k, v]) => ({ k, v })), { sortKey: "k", desc: false });
   } else if (tab === "checkpoints") {
     body = checkpointTable((await api.get(`/api/v1/trials/${id}/checkpoints`)).checkpoints);
+  } else if (tab === "workloads") {
+    body = await workloadsView(id, params.get("filter") || "");
   } else if (tab === "profiler") {
     body = await profilerView(id);
   } else {
     body = logView(`/api/v1/trials/${id}/logs`);
   }
   return h("div", {}, head, body);
+}
+
+// Workloads tab (reference TrialDetailsWorkloads): training / validation / checkpoint rows in
+// batch order with their metrics; filter to validations or checkpoints.
+async function workloadsView(id, filter) {
+  const q = filter ? "?filter=FILTER_OPTION_" + filter : "";
+  const { workloads } = await api.get(`/api/v1/trials/${id}/workloads${q}`);
+  const rows = workloads.map((w, i) => {
+    const kind = Object.keys(w)[0], x = w[kind];
+    const m = ((x.metrics || {}).avg_metrics) || {};
+    return { i, kind, batches: x.total_batches, end_time: x.end_time,
+      detail: kind === "checkpoint" ? `${x.uuid} (${(x.state || "").replace(/^STATE_/, "")})`
+        : Object.entries(m).filter(([, v]) => typeof v === "number").map(([k, v]) => `${k}=${fmtNum(v)}`).join("  ") };
+  });
+  const sel = h("select", { onchange: (ev) => nav(`#/trials/${id}`, { tab: "workloads", filter: ev.target.value }) },
+    [["", "all workloads"], ["VALIDATION", "validations"], ["CHECKPOINT", "checkpoints"]].map(([v, l]) =>
+      h("option", { value: v, selected: v === filter }, l)));
+  return h("div", {}, h("div", { class: "toolbar" }, sel, h("span", { class: "muted" }, `${rows.length} workloads`)),
+    table([
+      { key: "kind", label: "Type", render: (r) => badge(r.kind.toUpperCase()) },
+      { key: "batches", label: "Batches" },
+      { key: "detail", label: "Metrics / checkpoint", render: (r) => h("span", { class: "mono" }, r.detail) },
+      { key: "end_time", label: "Finished", render: (r) => fmtTime(r.end_time) },
+    ], rows, { sortKey: "i", desc: false }));
+}
+
+// Trial comparison (reference TrialsComparisonModal): hyperparameters side by side, the latest
+// summary of each metric, and every metric's curves overlaid, one series per trial.
+async function pageCompare(params) {
+  const ids = (params.get("trials") || "").split(",").filter((x) => /^\d+$/.test(x));
+  if (!ids.length) return h("div", { class: "muted" }, "no trials selected");
+  const q = ids.map((i) => "trial_ids=" + i).join("&");
+  const { trials } = await api.get(`/api/v1/trials/time-series?${q}`);
+  const hpKeys = [...new Set(trials.flatMap((x) => Object.keys(x.trial.hparams || {})))].sort();
+  const hpRows = hpKeys.map((k) => {
+    const vals = trials.map((x) => (x.trial.hparams || {})[k]);
+    const differs = new Set(vals.map((v) => JSON.stringify(v))).size > 1;
+    return h("tr", { class: differs ? "differs" : "" }, h("td", {}, k),
+      vals.map((v) => h("td", {}, typeof v === "object" ? JSON.stringify(v) : fmtNum(v))));
+  });
+  const series = [...new Set(trials.flatMap((x) => Object.keys(x.metrics)))].sort();
+  const last = (pts) => (pts && pts.length ? pts[pts.length - 1].value : undefined);
+  const sumRows = [
+    h("tr", {}, h("td", {}, "state"), trials.map((x) => h("td", {}, badge(x.trial.state)))),
+    h("tr", {}, h("td", {}, "batches"), trials.map((x) => h("td", {}, fmtNum(x.trial.steps_completed)))),
+    h("tr", {}, h("td", {}, "best validation"), trials.map((x) => h("td", {}, fmtNum(x.trial.best_validation)))),
+    ...series.map((sname) => h("tr", {}, h("td", {}, sname), trials.map((x) => h("td", {}, fmtNum(last(x.metrics[sname])))))),
+  ];
+  const headRow = h("tr", {}, h("th", {}, ""), trials.map((x) => h("th", {}, link("#/trials/" + x.trial.id, "trial " + x.trial.id))));
+  const charts = series.map((sname) => lineChart(sname, trials.map((x) => ({
+    name: "trial " + x.trial.id,
+    points: (x.metrics[sname] || []).filter((p) => typeof p.value === "number").map((p) => [p.steps_completed, p.value]),
+  })), "batches"));
+  return h("div", {}, h("h1", {}, `Compare trials ${ids.join(", ")}`),
+    h("h2", {}, "Hyperparameters"), h("table", { class: "compare" }, h("thead", {}, headRow.cloneNode(true)), h("tbody", {}, hpRows)),
+    h("h2", {}, "Latest metrics"), h("table", { class: "compare" }, h("thead", {}, headRow), h("tbody", {}, sumRows)),
+    h("h2", {}, "Curves"), h("div", { class: "charts" }, charts));
 }
 
 // Profiler tab (reference TrialDetailsProfiles): system metrics vs seconds since the first
@@ -574,6 +714,7 @@ const ROUTES = [
   [/^\/experiments$/, pageExperiments, true],
   [/^\/experiments\/(\d+)$/, pageExperiment, true],
   [/^\/trials\/(\d+)$/, pageTrial, false],
+  [/^\/compare$/, pageCompare, false],
   [/^\/cluster$/, pageCluster, true],
   [/^\/jobs$/, pageJobs, true],
   [/^\/tasks$/, pageTasks, true],

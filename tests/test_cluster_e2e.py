@@ -256,3 +256,77 @@ def test_profiler_ships_timings_and_system_metrics(cluster):
     assert tb[0]["batches"] == list(range(48)) and all(v >= 0 for v in tb[0]["values"])
     sysb = s.get(f"/api/v1/trials/{tid}/profiler/metrics", params={"labels.name": "cpu_util_simple"})["batches"]
     assert sysb and len(sysb[0]["values"]) == len(sysb[0]["timestamps"]) >= 1
+
+
+def test_webui_visualization_compare_and_workloads_render(cluster):
+    """The HP parallel-coordinates view, the trial comparison page and the workloads tab render
+    against a finished random search (node + a minimal DOM shim, tests/webui_render.js)."""
+    import json
+    import subprocess
+
+    from determined_clone_amd import webui
+
+    if shutil.which("node") is None:
+        pytest.skip("node not installed")
+    m, s, ctx, _ = cluster
+    cfg = BASE.replace("lr: 0.01", "lr: {type: log, minval: -3, maxval: -1}\n  width: {type: categorical, vals: [8, 16]}") + \
+        "searcher: {name: random, metric: val_loss, max_length: {batches: 8}, max_trials: 3, max_concurrent_trials: 3}\n"
+    eid = _create(s, ctx, cfg)
+    assert _wait(s, eid, timeout=400) == "COMPLETED"
+    tids = sorted(t["id"] for t in s.get(f"/api/v1/experiments/{eid}/trials")["trials"])
+    routes = [f"/experiments/{eid}?tab=visualization", f"/compare?trials={tids[0]},{tids[1]}",
+              f"/trials/{tids[0]}?tab=workloads", f"/trials/{tids[0]}?tab=workloads&filter=CHECKPOINT",
+              f"/experiments/{eid}?tab=trials"]
+    out = subprocess.run(["node", os.path.join(HERE, "webui_render.js"), os.path.join(webui.STATIC_DIR, "app.js"),
+                          m.master_url, s.token] + routes, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-3000:]
+    viz, cmp_, wl, wl_ck, tr = json.loads(out.stdout.strip().splitlines()[-1])
+    for r in (viz, cmp_, wl, wl_ck, tr):
+        assert "error" not in r, r.get("error")
+    # one polyline per scored trial across the lr / width / val_loss axes
+    assert sorted(viz["trial_lines"]) == tids
+    assert "lr (log)" in viz["text"] or "lr" in viz["text"]
+    assert "width" in viz["text"] and "Hyperparameters" in viz["text"]
+    assert f"trial {tids[0]}" in cmp_["text"] and f"trial {tids[1]}" in cmp_["text"]
+    assert "validation.val_loss" in cmp_["text"] and "training.loss" in cmp_["text"]
+    assert cmp_["tags"].get("svg", 0) >= 2
+    # 8 batches with validation every 4: training + validation rows + the final checkpoint
+    assert "VALIDATION" in wl["text"] and "TRAINING" in wl["text"] and "CHECKPOINT" in wl["text"]
+    assert "VALIDATION" not in wl_ck["text"] and "CHECKPOINT" in wl_ck["text"]
+    assert "Compare selected" in tr["text"]
+
+
+def test_cli_create_test_mode_and_local(cluster, tmp_path, capsys, monkeypatch):
+    """``det e create --test`` validates on the master and runs a one-batch test experiment on the
+    cluster; ``--local --test`` runs one batch here; ``--local`` trains the whole trial here
+    (reference cli/experiment.py:253-354)."""
+    from determined_clone_amd.cli import cli
+
+    m, s, ctx, tmp = cluster
+    monkeypatch.setattr(cli, "AUTH_FILE", tmp_path / "auth.json")
+    monkeypatch.chdir(tmp_path)
+    base = ["-m", m.master_url, "-u", "admin"]
+    cfgf = tmp_path / "c.yaml"
+    cfgf.write_text(BASE + "searcher: {name: adaptive_asha, metric: val_loss, max_length: {batches: 8}, "
+                    "max_trials: 4}\n")
+    n_before = len(s.get("/api/v1/experiments")["experiments"])
+    assert cli.main(base + ["experiment", "create", "--test", str(cfgf), ctx]) == 0
+    out = capsys.readouterr().out
+    assert "validation succeeded" in out and "completed successfully" in out
+    exps = s.get("/api/v1/experiments")["experiments"]
+    assert len(exps) == n_before + 1
+    test_exp = max(exps, key=lambda e: e["id"])
+    assert test_exp["searcher_type"] == "single" and test_exp["archived"]
+    (t,) = s.get(f"/api/v1/experiments/{test_exp['id']}/trials")["trials"]
+    assert t["steps_completed"] == 1
+    # an invalid config is refused at validation, before any experiment exists
+    bad = tmp_path / "bad.yaml"
+    bad.write_text("entrypoint: x:y\nsearcher: {name: single}\n")
+    assert cli.main(base + ["experiment", "create", "--test", str(bad), ctx]) != 0
+    assert len(s.get("/api/v1/experiments")["experiments"]) == n_before + 1
+    capsys.readouterr()
+    monkeypatch.syspath_prepend(ctx)
+    assert cli.main(["experiment", "create", "--local", "--test", str(cfgf), ctx]) == 0
+    assert "Model definition test succeeded" in capsys.readouterr().out
+    assert cli.main(["experiment", "create", "--local", str(cfgf), ctx]) == 0
+    assert "Local training finished (8 batches)" in capsys.readouterr().out
