@@ -1,7 +1,10 @@
 """CIFAR-10 CNN used for the adaptive_asha search config (reference: the CIFAR-10 PyTorch example
 of the e2e fixtures / docs: 4 conv layers + dropout + 2 FC). NHWC bf16-friendly: the conv stack runs
 channels_last, BatchNorm+ReLU uses the fused HIP kernel on the GPU. Offline synthetic data."""
-from typing import Any, Dict
+import fcntl
+import os
+import tempfile
+from typing import Any, Dict, Optional
 
 import numpy as np
 import torch
@@ -39,10 +42,34 @@ class SyntheticCIFAR10(torch.utils.data.Dataset):
     training labels are replaced by random classes. A small CNN needs several epochs and a sane
     learning rate to get the validation error down (too high a rate diverges), so an HP search
     sees a real spread of validation errors -- what ASHA's promotions act on. Stored as fp16
-    (50,000 records: 307 MB per trial process)."""
+    (50,000 records: 307 MB, one shared copy per node -- see ``cache_dir``)."""
 
     def __init__(self, n: int, seed: int, signal: float = 0.12, label_noise: float = 0.1,
-                 max_shift: int = 4) -> None:
+                 max_shift: int = 4, cache_dir: Optional[str] = None) -> None:
+        """``cache_dir`` (default ``$DET_DATA_CACHE`` or the temp dir): the arrays are generated
+        once per parameter set into ``<cache_dir>/dca_synthetic_cifar/`` (under a file lock) and
+        memory-mapped by every later instance -- the 16 trial processes of an HP search share one
+        page-cache copy instead of each spending seconds generating 307 MB at start-up."""
+        cache_dir = cache_dir or os.environ.get("DET_DATA_CACHE") or tempfile.gettempdir()
+        key = f"n{n}_s{seed}_sig{signal}_ln{label_noise}_sh{max_shift}_v1"
+        d = os.path.join(cache_dir, "dca_synthetic_cifar")
+        try:
+            os.makedirs(d, exist_ok=True)
+            xp, yp = os.path.join(d, key + ".x.npy"), os.path.join(d, key + ".y.npy")
+            with open(os.path.join(d, key + ".lock"), "w") as lk:
+                fcntl.flock(lk, fcntl.LOCK_EX)
+                if not (os.path.exists(xp) and os.path.exists(yp)):
+                    self._generate(n, seed, signal, label_noise, max_shift)
+                    for path, arr in ((xp, self.x), (yp, self.y)):
+                        tmp = f"{path}.{os.getpid()}.tmp.npy"
+                        np.save(tmp, arr)
+                        os.replace(tmp, path)
+            self.x = np.load(xp, mmap_mode="r")
+            self.y = np.load(yp)
+        except OSError:  # read-only / full cache dir: generate in memory
+            self._generate(n, seed, signal, label_noise, max_shift)
+
+    def _generate(self, n: int, seed: int, signal: float, label_noise: float, max_shift: int) -> None:
         g = np.random.RandomState(seed)
         side = 32 + 2 * max_shift
         proto = torch.from_numpy(np.random.RandomState(99).randn(10, 3, side, side).astype(np.float32))
