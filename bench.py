@@ -184,8 +184,8 @@ def _run_rank(args: argparse.Namespace) -> None:
         # (profiles/round2_miopen_immediate_mode_ab.txt); DCA_CONV_BENCHMARK=1 runs the find
         torch.backends.cudnn.benchmark = os.environ.get("DCA_CONV_BENCHMARK", "0") == "1"
     hparams = {"global_batch_size": args.batch * world, "warmup": args.warmup, "steps": args.steps}
-    # the timed step runs eagerly: optimizations.hip_graph is refused for MIOpen convolutions
-    # (pytorch/_graph.py), and train_batch's timestamps must run on every step
+    # the timed step runs eagerly: train_batch's per-step timestamps must run on every step (a
+    # HIP-graph replay skips the Python body); the step is GPU-bound at bs 1024 anyway
     exp_conf = {"optimizations": {"aggregation_frequency": 1, "average_training_metrics": True}}
     with pytorch.init(hparams=hparams, exp_conf=exp_conf) as ctx:
         trial = ResNet50BenchTrial(ctx)

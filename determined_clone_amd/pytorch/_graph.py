@@ -16,13 +16,20 @@ on ROCm) and replays it for every later batch:
 
 Requirements (checked by :func:`unsupported_reason`): one GPU per trial (RCCL collectives are not
 captured), ``aggregation_frequency == 1``, every wrapped optimizer a graph-capturable fused
-optimizer, no MIOpen convolutions (their replays diverge from eager: measured), and a
-``train_batch`` without host synchronisation or data-dependent Python control flow. Transformer
-trials (fused LayerNorm / attention / bias-GELU / cross-entropy, hipBLASLt GEMMs, fused AdamW with
-device-side clipping) replay bit-exactly. The reference has no equivalent (its step is eager).
+optimizer, and a ``train_batch`` without host synchronisation or data-dependent Python control
+flow. Transformer trials (fused LayerNorm / attention / bias-GELU / cross-entropy, hipBLASLt
+GEMMs, fused AdamW with device-side clipping) and ResNets replay bit-exactly.
+
+MIOpen convolutions: models with convolutions switch MIOpen to its deterministic solvers
+(``torch.backends.cudnn.deterministic = True``) before the warm-up steps. Root cause of the
+eager-vs-replay divergence measured in earlier rounds (profiles/round4_hip_graph_miopen_root_cause.txt):
+nothing was missing from the graph -- MIOpen's default solver for small strided 1x1 NHWC
+convolutions (ConvAsmImplicitGemmGTCDynamicFwdXdlopsNHWC, a split-K kernel accumulating with
+atomics) is nondeterministic run to run (relative 4e-5 between two EAGER calls), and the replay
+merely ran it with a different atomic order; a few SGD steps amplified that. With deterministic
+solvers eager and replay agree bit for bit. The reference has no equivalent (its step is eager).
 """
 import logging
-import os
 from typing import Any, Callable, List, Optional
 
 import torch
@@ -45,16 +52,12 @@ def unsupported_reason(context: Any) -> Optional[str]:
     for opt in context.optimizers:
         if not isinstance(opt, fused_optim.FusedOptimizerBase) or not opt.graph_capturable:
             return f"optimizer {type(opt).__name__} is not graph-capturable"
-    if torch.backends.cudnn.enabled and os.environ.get("DCA_HIP_GRAPH_FORCE") != "1":
-        convs = (torch.nn.Conv1d, torch.nn.Conv2d, torch.nn.Conv3d, torch.nn.ConvTranspose2d)
-        if any(isinstance(mod, convs) for m in context.models for mod in m.modules()):
-            # Measured (tools/probe_graph_gpu.py): replays of a step with MIOpen convolutions
-            # diverge from the eager step, while the same model on PyTorch's native convolutions
-            # and every non-MIOpen path here (fused BN / optimizers / attention / LayerNorm /
-            # hipBLASLt GEMMs) replay bit-exactly. MIOpen issues work that stream capture does
-            # not record, so such models stay eager.
-            return "MIOpen convolutions are not HIP-graph capture safe"
     return None
+
+
+def _has_convs(context: Any) -> bool:
+    convs = (torch.nn.Conv1d, torch.nn.Conv2d, torch.nn.Conv3d, torch.nn.ConvTranspose2d)
+    return any(isinstance(mod, convs) for m in context.models for mod in m.modules())
 
 
 class GraphedTrainStep:
@@ -70,6 +73,10 @@ class GraphedTrainStep:
         self.replays = 0
         for opt in context.optimizers:
             opt.enable_device_hparams()
+        if torch.backends.cudnn.enabled and not torch.backends.cudnn.deterministic and _has_convs(context):
+            # before the eager warm-up steps, so warm-up, capture and replay run the same solvers
+            logger.info("hip_graph: MIOpen switched to deterministic convolution solvers")
+            torch.backends.cudnn.deterministic = True
 
     # ------------------------------------------------------------------ helpers
     def _matches(self, leaves: List[Any], spec: Any) -> bool:

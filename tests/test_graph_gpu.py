@@ -93,10 +93,10 @@ def _run(trial_cls, graph, tmp_path):
 
 @pytest.mark.parametrize("trial_cls", [_ResNetTrial, _GPTTrial])
 def test_graph_step_matches_eager(trial_cls, tmp_path, monkeypatch):
-    """Replays are bit-exact with the eager step. The ResNet runs its convolutions on PyTorch's
-    native kernels here: MIOpen convolutions are refused (see the next test)."""
-    if trial_cls is _ResNetTrial:
-        monkeypatch.setattr(torch.backends.cudnn, "enabled", False)
+    """Replays are bit-exact with the eager step. The ResNet's MIOpen convolutions run their
+    deterministic solvers in both runs (the graph runner switches them on; the eager reference
+    needs the same solvers to be comparable bit for bit)."""
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
     eager, _, lr_e, step_e = _run(trial_cls, False, tmp_path)
     graph, runner, lr_g, step_g = _run(trial_cls, True, tmp_path)
     assert runner is not None and runner.replays == STEPS - 3  # warm-up 3, capture+replay at 4
@@ -105,6 +105,8 @@ def test_graph_step_matches_eager(trial_cls, tmp_path, monkeypatch):
         torch.testing.assert_close(graph[n], e, atol=0, rtol=0, msg=lambda m: f"{n}: {m}")
 
 
-def test_graph_refused_with_miopen_convolutions(tmp_path):
+def test_graph_with_miopen_convolutions_switches_to_deterministic_solvers(tmp_path, monkeypatch):
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", False)
     _, runner, _, step = _run(_ResNetTrial, True, tmp_path)
-    assert runner is None and step == STEPS  # trained eagerly
+    assert runner is not None and runner.replays == STEPS - 3 and step == STEPS
+    assert torch.backends.cudnn.deterministic
