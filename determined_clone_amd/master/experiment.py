@@ -106,6 +106,7 @@ class Experiment:
         self.weight = float(res.get("weight") or 1.0)
         self.pool = res.get("resource_pool") or "default"
         self.max_slots = res.get("max_slots")
+        self.created_at = time.time()  # job submission time (fair-share group age)
         self.smaller_is_better = bool(config["searcher"].get("smaller_is_better", True))
 
     # ------------------------------------------------------------------ searcher plumbing
@@ -201,6 +202,8 @@ class Experiment:
         req = AllocationRequest(alloc_id, t.task_id, self.job_id, self.slots_per_trial,
                                 self.priority, self.weight, self.pool, True,
                                 name=f"Trial {t.id} (Experiment {self.id})")
+        req.max_slots = int(self.max_slots) if self.max_slots is not None else -1
+        req.job_submit_time = self.created_at
         # HPC launcher options (expconf `slurm` / `pbs`: slots_per_node, gpu_type, sbatch_args)
         req.hpc = {"slurm": self.config.get("slurm") or {}, "pbs": self.config.get("pbs") or {}}
         self.master.db.upsert("allocations", {"allocation_id": alloc_id, "task_id": t.task_id,

@@ -71,6 +71,8 @@ class AllocationRequest:
         self.label = label
         self.name = name
         self.submit_time = time.time()
+        self.job_submit_time = self.submit_time  # the job's; experiments set their creation time
+        self.max_slots = -1  # the job's resources.max_slots (fair share), -1 = unlimited
         self.job_position = 0
         self.blocked_agents: List[str] = []
         self.placements: List[Dict[str, Any]] = []
@@ -190,6 +192,7 @@ class ResourceManager:
             nr.priority, nr.weight, nr.submit_time = r.priority, r.weight, r.submit_time
             nr.job_position, nr.preemptible, nr.pool = r.job_position, r.preemptible, r.pool
             nr.label, nr.blocked_agents = r.label, list(r.blocked_agents)
+            nr.max_slots, nr.job_submit_time = r.max_slots, r.job_submit_time
             pend.append(nr)
         run = []
         for r in self.running.values():
@@ -198,6 +201,7 @@ class ResourceManager:
             nr.priority, nr.weight = r.priority, r.weight
             nr.start_time = r.start_time or 0.0
             nr.preemptible = r.preemptible and not r.preempt_requested
+            nr.max_slots, nr.submit_time, nr.job_submit_time = r.max_slots, r.submit_time, r.job_submit_time
             run.append(nr)
         return agents, pend, run
 

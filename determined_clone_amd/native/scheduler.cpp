@@ -67,6 +67,8 @@ struct Request {
   std::string pool;
   std::string label;
   std::vector<std::string> blocked_agents;
+  int max_slots = -1;            // the job's resources.max_slots (fair share), -1 = unlimited
+  double job_submit_time = 0.0;  // when the job (experiment / command) was submitted
 };
 
 struct Running {
@@ -77,6 +79,9 @@ struct Running {
   double weight = 1.0;
   double start_time = 0.0;
   bool preemptible = true;
+  int max_slots = -1;
+  double submit_time = 0.0;      // request submission (task-list order with the pending ones)
+  double job_submit_time = 0.0;
 };
 
 struct Placement {
@@ -295,101 +300,190 @@ class Scheduler {
     return d;
   }
 
+  // Max-min fair share over jobs ("groups"), following the reference's fair_share.go:
+  //  1. every request (pending and running, in submission order) joins its job's group; pending
+  //     ones that could not be placed even after preemption, and ones larger than the whole pool,
+  //     are left out (they would waste offered slots); a group's demand is capped at max_slots;
+  //  2. slots already held by non-preemptible allocations are offered first (pre-offers);
+  //  3. progressive filling: groups in order of increasing demand (then age) each get
+  //     max(1, capacity * weight / total_weight) per round until demands are met or the pool is
+  //     empty; when it is empty and some group cannot start even its smallest task with what it
+  //     was offered, the newest such group is disabled and its offer returned (multi-slot
+  //     deadlock breaking);
+  //  4. groups holding more than their offer release preemptible allocations (oldest request
+  //     first) -- unless preemption is off; groups under it start pending tasks that fit.
+  // Placements are applied as they are made, so one call never hands the same slots to two
+  // tasks (the reference lists both and lets a later allocation step reject the second).
   Decision fair_share(std::vector<Agent>& agents, std::vector<Request>& pending,
                       std::vector<Running>& running) {
     Decision d;
+    for (auto& r : pending) {  // zero-slot tasks need no offer, only room on an agent
+      if (r.slots != 0) continue;
+      auto ps = find_fit(r, agents, fit_);
+      if (ps.empty()) continue;
+      apply(agents, r.alloc_id, ps);
+      d.start.emplace_back(r.alloc_id, ps);
+    }
     int capacity = 0;
-    for (auto& a : agents)
-      if (a.enabled) capacity += a.usable_slots();
-    struct Group {
-      double weight = 1.0;
-      int running = 0;
-      int demand = 0;
-      double share = 0;
-      std::vector<Request*> pend;
-      std::vector<Running*> run;
+    for (auto& a : agents) capacity += a.usable_slots();
+
+    struct Task {
+      double t;
+      size_t idx;
+      Request* req;   // pending
+      Running* run;   // allocated
+      int slots() const { return req ? req->slots : run->slots; }
+      bool preemptible() const { return req ? req->preemptible : run->preemptible; }
     };
-    std::map<std::string, Group> groups;
-    for (auto& r : running) {
-      auto& g = groups[r.job_id];
-      g.weight = r.weight;
-      g.running += r.slots;
-      g.demand += r.slots;
-      g.run.push_back(&r);
-    }
-    for (auto& r : pending) {
-      auto& g = groups[r.job_id];
-      g.weight = r.weight;
-      g.demand += r.slots;
-      g.pend.push_back(&r);
-    }
-    // Water-filling: groups demanding less than their weighted share keep their demand; the
-    // remaining capacity is re-split among the rest by weight.
-    std::vector<std::string> open;
-    for (auto& kv : groups) open.push_back(kv.first);
-    double left = capacity;
-    while (!open.empty()) {
-      double wsum = 0;
-      for (auto& id : open) wsum += groups[id].weight;
-      bool changed = false;
-      std::vector<std::string> still;
-      for (auto& id : open) {
-        auto& g = groups[id];
-        const double fair = wsum > 0 ? left * g.weight / wsum : 0;
-        if (g.demand <= fair) {
-          g.share = g.demand;
-          changed = true;
-        } else {
-          still.push_back(id);
-        }
+    std::vector<Task> tasks;
+    for (size_t i = 0; i < running.size(); ++i)
+      tasks.push_back({running[i].submit_time, i, nullptr, &running[i]});
+    for (size_t i = 0; i < pending.size(); ++i)
+      tasks.push_back({pending[i].submit_time, running.size() + i, &pending[i], nullptr});
+    std::stable_sort(tasks.begin(), tasks.end(), [](const Task& x, const Task& y) {
+      return x.t != y.t ? x.t < y.t : x.idx < y.idx;
+    });
+
+    struct Group {
+      std::string job;
+      double weight = 1.0, registered = 0.0;
+      int max_slots = -1, order = 0;
+      bool disabled = false;
+      int demand = 0, active = 0, presubscribed = 0, offered = 0;
+      std::vector<Task> pend, alloc;
+    };
+    // A pending task counts toward its group's demand if it could be placed once the preemptible
+    // allocations were released. (The reference checks the slots free right now, so on a full
+    // pool a newly submitted job never receives a share and nothing is ever preempted for it;
+    // its vectors, whose allocated tasks hold no device slots, behave the same under both rules.)
+    std::vector<Agent> reclaimable = agents;
+    if (preemption_)
+      for (auto& run : running)
+        if (run.preemptible) release(reclaimable, run.alloc_id, 0);
+    std::vector<Group> groups;
+    std::map<std::string, size_t> index;
+    for (auto& t : tasks) {
+      const int n = t.slots();
+      if (n == 0 || n > capacity) continue;
+      if (t.req && find_fit(*t.req, reclaimable, fit_).empty()) continue;
+      const std::string& job = t.req ? t.req->job_id : t.run->job_id;
+      auto it = index.find(job);
+      if (it == index.end()) {
+        Group g;
+        g.job = job;
+        g.weight = t.req ? t.req->weight : t.run->weight;
+        g.max_slots = t.req ? t.req->max_slots : t.run->max_slots;
+        g.registered = t.req ? t.req->job_submit_time : t.run->job_submit_time;
+        g.order = static_cast<int>(groups.size());
+        it = index.emplace(job, groups.size()).first;
+        groups.push_back(std::move(g));
       }
-      if (!changed) {
-        for (auto& id : still) groups[id].share = wsum > 0 ? left * groups[id].weight / wsum : 0;
+      Group& g = groups[it->second];
+      g.demand += n;
+      if (t.req) {
+        g.pend.push_back(t);
+      } else {
+        if (!t.preemptible()) g.presubscribed += n;
+        g.active += n;
+        g.alloc.push_back(t);
+      }
+    }
+    for (auto& g : groups)
+      if (g.max_slots >= 0) g.demand = std::min(g.demand, g.max_slots);
+
+    // ---- slot offers
+    std::map<int, int> preoffers;  // group order -> slots still pre-offered
+    for (auto& g : groups) {
+      if (g.presubscribed == 0) continue;
+      g.offered = g.presubscribed;
+      preoffers[g.order] = g.presubscribed;
+      capacity -= g.presubscribed;
+    }
+    std::stable_sort(groups.begin(), groups.end(), [](const Group& x, const Group& y) {
+      if (x.demand != y.demand) return x.demand < y.demand;
+      return x.registered < y.registered;
+    });
+    std::vector<size_t> newest_first(groups.size());
+    for (size_t i = 0; i < groups.size(); ++i) newest_first[i] = i;
+    std::stable_sort(newest_first.begin(), newest_first.end(), [&](size_t x, size_t y) {
+      if (groups[x].registered != groups[y].registered) return groups[x].registered > groups[y].registered;
+      return groups[x].order > groups[y].order;
+    });
+    auto total_weight = [&]() {
+      double w = 0;
+      for (auto& g : groups)
+        if (!g.disabled && g.offered < g.demand) w += g.weight;
+      return w;
+    };
+    double tw = total_weight();
+    // Rounds until every group is satisfied or disabled, or a round changes nothing. Offers are
+    // clamped at zero: a group can hold more non-preemptible slots than its (max_slots-capped)
+    // demand and the pool can be oversubscribed, and a negative offer would never terminate.
+    for (;;) {
+      bool open = false, progress = false;
+      const int start_capacity = capacity;
+      for (auto& g : groups) {
+        if (g.disabled || g.offered >= g.demand) continue;
+        open = true;
+        // max(1, floor(share)); a pool of zero-weight groups fills one slot per group per round
+        const int fair = tw > 0 ? std::max(1, static_cast<int>(start_capacity * g.weight / tw)) : 1;
+        int offer = std::max(0, std::min({fair, capacity, g.demand - g.offered}));
+        int& pre = preoffers[g.order];
+        const int pre_before = pre;
+        // the reference's accountForPreoffers, arithmetic kept as is
+        if (pre > 0) {
+          if (pre == offer) pre = offer = 0;
+          if (pre > offer) { pre -= offer; offer = 0; }
+          if (pre < offer) pre = 0;
+        }
+        progress = progress || offer > 0 || pre != pre_before;
+        g.offered += offer;
+        capacity -= offer;
+        if (g.offered >= g.demand) tw = total_weight();
+      }
+      if (!open) break;
+      if (capacity <= 0) {
+        // multi-slot deadlock: the newest group whose offer cannot start even its smallest
+        // pending task gives its offer back
+        bool adjusted = false;
+        for (size_t i : newest_first) {
+          Group& g = groups[i];
+          int smallest = -1;
+          for (auto& t : g.pend) smallest = smallest < 0 ? t.slots() : std::min(smallest, t.slots());
+          if (!g.disabled && g.offered < g.demand && smallest > g.offered) {
+            capacity += g.offered;
+            g.offered = 0;
+            g.disabled = true;
+            adjusted = true;
+            tw = total_weight();
+            break;
+          }
+        }
+        if (!adjusted) break;
+      } else if (!progress) {
         break;
       }
-      left = capacity;
-      for (auto& kv : groups)
-        if (std::find(still.begin(), still.end(), kv.first) == still.end()) left -= kv.second.share;
-      open = still;
     }
-    // Start tasks of under-share groups, most-starved first.
-    std::vector<std::string> order;
-    for (auto& kv : groups) order.push_back(kv.first);
-    std::sort(order.begin(), order.end(), [&](const std::string& a, const std::string& b) {
-      const double ra = groups[a].share > 0 ? groups[a].running / groups[a].share : 1e9;
-      const double rb = groups[b].share > 0 ? groups[b].running / groups[b].share : 1e9;
-      return ra != rb ? ra < rb : a < b;
-    });
-    bool starved = false;
-    for (auto& id : order) {
-      auto& g = groups[id];
-      std::sort(g.pend.begin(), g.pend.end(), [](Request* a, Request* b) { return req_order(*a, *b); });
-      for (Request* r : g.pend) {
-        if (g.running + r->slots > std::ceil(g.share - 1e-9) && g.running > 0) {
-          starved = true;
-          break;
+
+    // ---- decisions
+    for (auto& g : groups) {
+      if (g.active > g.offered) {
+        if (!preemption_) continue;
+        for (auto& t : g.alloc) {
+          if (!t.preemptible()) continue;
+          d.preempt.push_back(t.run->alloc_id);
+          g.active -= t.slots();
+          if (g.active <= g.offered) break;
         }
-        auto ps = find_fit(*r, agents, fit_);
-        if (ps.empty()) {
-          starved = true;
-          break;
-        }
-        apply(agents, r->alloc_id, ps);
-        d.start.emplace_back(r->alloc_id, ps);
-        g.running += r->slots;
-      }
-    }
-    // Preempt newest allocations of groups above their share while someone is starved.
-    if (starved && preemption_) {
-      for (auto& kv : groups) {
-        auto& g = kv.second;
-        std::sort(g.run.begin(), g.run.end(), [](Running* a, Running* b) { return a->start_time > b->start_time; });
-        int over = g.running - static_cast<int>(std::floor(g.share + 1e-9));
-        for (Running* r : g.run) {
-          if (over <= 0) break;
-          if (!r->preemptible) continue;
-          d.preempt.push_back(r->alloc_id);
-          over -= r->slots;
+      } else if (g.active < g.offered) {
+        int room = g.offered - g.active;
+        for (auto& t : g.pend) {
+          if (t.slots() > room) continue;
+          auto ps = find_fit(*t.req, agents, fit_);
+          if (ps.empty()) continue;
+          apply(agents, t.req->alloc_id, ps);
+          d.start.emplace_back(t.req->alloc_id, ps);
+          room -= t.slots();
         }
       }
     }
@@ -488,7 +582,9 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("preemptible", &Request::preemptible)
       .def_readwrite("pool", &Request::pool)
       .def_readwrite("label", &Request::label)
-      .def_readwrite("blocked_agents", &Request::blocked_agents);
+      .def_readwrite("blocked_agents", &Request::blocked_agents)
+      .def_readwrite("max_slots", &Request::max_slots)
+      .def_readwrite("job_submit_time", &Request::job_submit_time);
   py::class_<Running>(m, "Running")
       .def(py::init<>())
       .def_readwrite("alloc_id", &Running::alloc_id)
@@ -497,7 +593,10 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("priority", &Running::priority)
       .def_readwrite("weight", &Running::weight)
       .def_readwrite("start_time", &Running::start_time)
-      .def_readwrite("preemptible", &Running::preemptible);
+      .def_readwrite("preemptible", &Running::preemptible)
+      .def_readwrite("max_slots", &Running::max_slots)
+      .def_readwrite("submit_time", &Running::submit_time)
+      .def_readwrite("job_submit_time", &Running::job_submit_time);
   py::class_<Placement>(m, "Placement")
       .def(py::init<>())
       .def_readwrite("agent_id", &Placement::agent_id)

@@ -123,7 +123,9 @@ def test_fair_share_preempts_over_share_group():
     running = [run(f"j1-{i}", 1, job="j1", t=i) for i in range(8)]
     d = N.Scheduler("fair_share", "best", True).schedule(agents, [req("j2-0", 4, job="j2")], running)
     assert len(d.preempt) == 4
-    assert set(d.preempt) == {f"j1-{i}" for i in range(4, 8)}  # newest first
+    # oldest request first, as the reference's assignTasks (fair_share_test.go
+    # TestFairShareMaxSlotsReleaseAllocatedTasks releases task1 and task2)
+    assert set(d.preempt) == {f"j1-{i}" for i in range(4)}
 
 
 def test_detect_kfd_on_fake_sysfs(tmp_path):
