@@ -104,6 +104,7 @@ def _run_rank(args: argparse.Namespace) -> None:
             self.opt = context.wrap_optimizer(opt)
             self.t0 = self.t1 = None
             self.events = []
+            self.mid_state = {}
 
         def _mark(self) -> float:
             if torch.cuda.is_available():
@@ -129,6 +130,8 @@ def _run_rank(args: argparse.Namespace) -> None:
             loss = F.cross_entropy(logits.float(), labels)
             self.context.backward(loss)
             self.context.step_optimizer(self.opt)
+            if batch_idx == self.warmup + self.steps // 2 and torch.cuda.is_available():
+                self.mid_state = _gpu_state()  # clocks / power WHILE the timed steps run (sysfs)
             if batch_idx == self.warmup + self.steps - 1:
                 if torch.cuda.is_available():
                     ev = torch.cuda.Event(enable_timing=True)
@@ -172,7 +175,8 @@ def _run_rank(args: argparse.Namespace) -> None:
         # step (alloc retries). Wait (bounded) for the device's memory to come back first.
         free0, total = torch.cuda.mem_get_info()
         t_wait = time.time()
-        while free0 < 0.8 * total and time.time() - t_wait < 60:
+        wait_s = float(os.environ.get("DCA_BENCH_MEM_WAIT_S", "60"))
+        while free0 < 0.8 * total and time.time() - t_wait < wait_s:
             time.sleep(2)
             free0, total = torch.cuda.mem_get_info()
         print(json.dumps({"device_free_gb_at_start": round(free0 / 2**30, 1),
@@ -207,7 +211,8 @@ def _run_rank(args: argparse.Namespace) -> None:
             ev = trial.events
             step_ms = [round(a.elapsed_time(b), 2) for a, b in zip(ev[:-1], ev[1:])]
             ms_stats = torch.cuda.memory_stats()
-            print(json.dumps({"rank": ctx.distributed.rank, "gpu_state_end": _gpu_state()}), file=sys.stderr)
+            print(json.dumps({"rank": ctx.distributed.rank, "gpu_state_mid": trial.mid_state,
+                              "gpu_state_end": _gpu_state()}), file=sys.stderr)
             print(json.dumps({"rank": ctx.distributed.rank, "step_ms": step_ms,
                               "max_reserved_gb": round(torch.cuda.max_memory_reserved() / 2**30, 1),
                               "alloc_retries": ms_stats.get("num_alloc_retries", 0),
@@ -228,6 +233,12 @@ def _run_rank(args: argparse.Namespace) -> None:
                 "data": f"synthetic (random 224x224x3 images + labels {where}, random-init weights)",
                 "device": torch.cuda.get_device_name() if on_gpu else "cpu",
                 "world_size": pg_size, "backend": backend,
+                # slow-mode evidence (profiles/round4_bench_slow_mode.txt): allocator retries mean the
+                # step ran short of device memory (another process's HBM not yet returned)
+                "diagnostics": {"alloc_retries": int(ms_stats.get("num_alloc_retries", 0)) if on_gpu else 0,
+                                "device_free_gb_at_start": round(free0 / 2**30, 1) if on_gpu else None,
+                                "max_reserved_gb": round(torch.cuda.max_memory_reserved() / 2**30, 1) if on_gpu else None,
+                                "max_allocated_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else None},
                 "config": {"model": "resnet50", "global_batch": args.batch * world, "seq_len": None,
                            "image_size": 224, "parallelism": f"dp{world}",
                            "trial": "PyTorchTrial", "optimizer": f"SGD momentum ({opt_name})",

@@ -53,6 +53,16 @@ def target(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 SIDE_STREAM = os.environ.get("DCA_WGRAD_STREAM", "1") != "0"
 _streams = {}
 _pending = set()
+# Tensors the side stream reads are kept alive by reference until join() instead of
+# ``record_stream``: with record_stream every activation / gradient block freed during backward
+# stays unusable until the lagging side stream passes it, the next forward cannot reuse it, and
+# the caching allocator grew a ResNet-50 bs-1024 process to 222 GB reserved for 42.5 GB of live
+# tensors -- past the HBM left on a box where another process still held memory, where every
+# allocation miss became a 1-25 s free-all-and-retry (profiles/round4_bench_slow_mode.txt).
+# Released after the current stream has waited for the side stream, the blocks return to the
+# current stream's pool immediately reusable. DCA_WGRAD_KEEPALIVE=0 restores record_stream.
+KEEPALIVE = os.environ.get("DCA_WGRAD_KEEPALIVE", "1") != "0"
+_keep = []
 
 
 def side_stream_for(p: Optional[torch.Tensor]) -> Optional["torch.cuda.Stream"]:
@@ -77,7 +87,10 @@ def fork(stream: "torch.cuda.Stream", tensors=()) -> None:
     stream.wait_event(ev)
     for t in tensors:
         if t is not None:
-            t.record_stream(stream)
+            if KEEPALIVE:
+                _keep.append(t)
+            else:
+                t.record_stream(stream)
     _pending.add(stream)
 
 
@@ -93,6 +106,7 @@ def join() -> None:
     for s in list(_pending):
         cur.wait_stream(s)
     _pending.clear()
+    _keep.clear()  # the current stream is now ordered after every side-stream read
 
 
 def comm_stream() -> Optional["torch.cuda.Stream"]:

@@ -468,6 +468,24 @@ class _PyTorchTrialController:
                                                     self.context._hip_graph_warmup)
         return self._graphed
 
+    _scratch_released = False
+
+    def _release_first_step_scratch(self) -> None:
+        """After the first training step, return the caching allocator's free blocks to the
+        device once (``DCA_RELEASE_FIRST_STEP_SCRATCH``, default on). The first step carries
+        one-off allocations -- the convolution chooser timing every candidate, MIOpen / GEMM
+        workspaces, optimizer state creation -- that otherwise stay reserved and fragment the
+        pool: a ResNet-50 bs-1024 process kept 219 GB reserved for a ~90 GB steady state, and with
+        less free HBM than that (another process's memory not yet returned) every later
+        allocation miss turned into a free-all-and-retry costing 1-25 s
+        (profiles/round4_bench_slow_mode.txt)."""
+        if self._scratch_released or self.context.device.type != "cuda":
+            return
+        self._scratch_released = True
+        if os.environ.get("DCA_RELEASE_FIRST_STEP_SCRATCH", "1") != "0":
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+
     def _train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, Any]:
         self.context._loss_ids = {}
         t0 = time.time()
@@ -487,6 +505,7 @@ class _PyTorchTrialController:
                 and self.context._should_communicate_and_update():
             self.context._scaler.update()
         util.startup_mark("first train batch")
+        self._release_first_step_scratch()
         if isinstance(out, torch.Tensor):
             out = {"loss": out}
         if not isinstance(out, dict):
