@@ -472,13 +472,12 @@ class _PyTorchTrialController:
 
     def _release_first_step_scratch(self) -> None:
         """After the first training step, return the caching allocator's free blocks to the
-        device once (``DCA_RELEASE_FIRST_STEP_SCRATCH``, default on). The first step carries
+        device once (``DCA_RELEASE_FIRST_STEP_SCRATCH``, default on): the first step carries
         one-off allocations -- the convolution chooser timing every candidate, MIOpen / GEMM
-        workspaces, optimizer state creation -- that otherwise stay reserved and fragment the
-        pool: a ResNet-50 bs-1024 process kept 219 GB reserved for a ~90 GB steady state, and with
-        less free HBM than that (another process's memory not yet returned) every later
-        allocation miss turned into a free-all-and-retry costing 1-25 s
-        (profiles/round4_bench_slow_mode.txt)."""
+        workspaces, optimizer state creation -- that need not stay reserved for the rest of the
+        trial. (The large reserved-vs-live gap of the round-3 bench came from elsewhere -- the
+        side-stream gradients' record_stream, fixed in ops/_grad.py; see
+        profiles/round4_bench_slow_mode.txt.)"""
         if self._scratch_released or self.context.device.type != "cuda":
             return
         self._scratch_released = True
