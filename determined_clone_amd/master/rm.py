@@ -202,6 +202,8 @@ class ResourceManager:
             nr.start_time = r.start_time or 0.0
             nr.preemptible = r.preemptible and not r.preempt_requested
             nr.max_slots, nr.submit_time, nr.job_submit_time = r.max_slots, r.submit_time, r.job_submit_time
+            nr.job_position = r.job_position
+            nr.agents = [p["agent_id"] for p in r.placements]
             run.append(nr)
         return agents, pend, run
 

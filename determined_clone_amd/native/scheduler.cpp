@@ -62,7 +62,7 @@ struct Request {
   int priority = 42;  // smaller = more important (Determined convention)
   double weight = 1.0;
   double submit_time = 0.0;
-  int job_position = 0;  // user re-ordering within the queue (UpdateJobQueue)
+  double job_position = 0;  // the job's queue position (UpdateJobQueue); smaller runs first
   bool preemptible = true;
   std::string pool;
   std::string label;
@@ -82,6 +82,8 @@ struct Running {
   int max_slots = -1;
   double submit_time = 0.0;      // request submission (task-list order with the pending ones)
   double job_submit_time = 0.0;
+  double job_position = 0;
+  std::vector<std::string> agents;  // where it runs (zero-slot allocations hold no slot ids)
 };
 
 struct Placement {
@@ -204,6 +206,17 @@ static void release(std::vector<Agent>& agents, const std::string& alloc, int ze
   (void)zero_slots;
 }
 
+// Frees what running allocation ``r`` holds: its slots, or its zero-slot container count.
+static void release_running(std::vector<Agent>& agents, const Running& r) {
+  if (r.slots == 0) {
+    for (auto& id : r.agents)
+      for (auto& a : agents)
+        if (a.id == id && a.zero_slot_used > 0) a.zero_slot_used--;
+    return;
+  }
+  release(agents, r.alloc_id, 0);
+}
+
 // ------------------------------------------------------------------ policies
 class Scheduler {
  public:
@@ -224,6 +237,7 @@ class Scheduler {
   static bool req_order(const Request& a, const Request& b) {
     if (a.priority != b.priority) return a.priority < b.priority;
     if (a.job_position != b.job_position) return a.job_position < b.job_position;
+    if (a.job_submit_time != b.job_submit_time) return a.job_submit_time < b.job_submit_time;
     if (a.submit_time != b.submit_time) return a.submit_time < b.submit_time;
     return a.alloc_id < b.alloc_id;
   }
@@ -242,60 +256,102 @@ class Scheduler {
     return d;
   }
 
+  // Priority scheduling with preemption and backfilling, after the reference's priority.go
+  // (prioritySchedulerWithFilter / trySchedulingTaskViaPreemption). Zero-slot and slot tasks are
+  // scheduled independently. Per priority level (smallest number first), pending tasks are fitted
+  // in queue order (position, job submission, request submission) onto a working copy of the
+  // agents -- a fitted task holds its slots in that copy whether or not it is started -- and:
+  //  * started only while nothing has been chosen for preemption; once some higher-priority task
+  //    failed to fit, lower levels are "backfilling" and start only preemptible tasks (and only
+  //    with preemption on);
+  //  * a task that does not fit first checks whether the preemptions already chosen make room,
+  //    else preempts running allocations from the lowest priority (99) up to its own level, newest
+  //    in queue order first -- at its own level only jobs queued behind it -- until it fits; the
+  //    victims are released only if it then fits.
   Decision priority(std::vector<Agent>& agents, std::vector<Request>& pending,
                     std::vector<Running>& running) {
     Decision d;
     std::sort(pending.begin(), pending.end(), req_order);
-    // Zero-slot and slot tasks are scheduled independently.
+    std::vector<Running*> runs;
+    for (auto& r : running) runs.push_back(&r);
+    std::sort(runs.begin(), runs.end(), [](const Running* a, const Running* b) {
+      if (a->priority != b->priority) return a->priority < b->priority;
+      if (a->job_position != b->job_position) return a->job_position < b->job_position;
+      if (a->job_submit_time != b->job_submit_time) return a->job_submit_time < b->job_submit_time;
+      if (a->submit_time != b->submit_time) return a->submit_time < b->submit_time;
+      return a->alloc_id < b->alloc_id;
+    });
+    constexpr int kMaxPriority = 99;
     for (int zero = 0; zero < 2; ++zero) {
-      std::map<int, std::vector<Request*>> by_prio;
+      const bool want_zero = zero == 1;
+      std::map<int, std::vector<Request*>> pend_by_prio;
+      std::map<int, std::vector<Running*>> run_by_prio;
       for (auto& r : pending)
-        if ((r.slots == 0) == (zero == 1)) by_prio[r.priority].push_back(&r);
+        if ((r.slots == 0) == want_zero) pend_by_prio[r.priority].push_back(&r);
+      for (auto* r : runs)
+        if ((r->slots == 0) == want_zero) run_by_prio[r->priority].push_back(r);
+      std::vector<Agent> local = agents;
       bool backfilling = false;
-      std::set<std::string> to_release;
-      for (auto& kv : by_prio) {
+      std::vector<std::string> to_release;
+      auto released = [&](const std::string& id) {
+        return std::find(to_release.begin(), to_release.end(), id) != to_release.end();
+      };
+      for (auto& kv : pend_by_prio) {
+        const int prio = kv.first;
+        std::vector<std::pair<Request*, std::vector<Placement>>> ok;
         std::vector<Request*> failed;
         for (Request* r : kv.second) {
-          auto ps = find_fit(*r, agents, fit_);
+          auto ps = find_fit(*r, local, fit_);
           if (ps.empty()) {
             failed.push_back(r);
             continue;
           }
-          const bool allowed = to_release.empty() && (!backfilling || (preemption_ && r->preemptible));
-          if (allowed) {
-            apply(agents, r->alloc_id, ps);
-            d.start.emplace_back(r->alloc_id, ps);
+          apply(local, r->alloc_id, ps);
+          ok.emplace_back(r, ps);
+        }
+        if (to_release.empty()) {
+          for (auto& rp : ok) {
+            if (backfilling && !(preemption_ && rp.first->preemptible)) continue;
+            apply(agents, rp.first->alloc_id, rp.second);
+            d.start.emplace_back(rp.first->alloc_id, rp.second);
           }
         }
         if (!failed.empty()) backfilling = true;
         if (!preemption_) continue;
         for (Request* r : failed) {
-          // Victims: lower-priority (larger number), preemptible, newest first.
-          std::vector<Running*> victims;
-          for (auto& run : running)
-            if (run.priority > r->priority && run.preemptible && !to_release.count(run.alloc_id) &&
-                (run.slots == 0) == (r->slots == 0))
-              victims.push_back(&run);
-          std::sort(victims.begin(), victims.end(), [](Running* a, Running* b) {
-            if (a->priority != b->priority) return a->priority > b->priority;
-            return a->start_time > b->start_time;
-          });
-          std::vector<Agent> trial = agents;
-          std::vector<std::string> chosen;
+          auto ps = find_fit(*r, local, fit_);
+          if (!ps.empty()) {  // room once the already chosen preemptions complete
+            apply(local, r->alloc_id, ps);
+            continue;
+          }
+          std::vector<Agent> trial = local;
+          std::vector<std::string> victims;
           bool placed = false;
-          for (Running* v : victims) {
-            release(trial, v->alloc_id, 0);
-            chosen.push_back(v->alloc_id);
-            if (!find_fit(*r, trial, fit_).empty()) {
-              placed = true;
-              break;
+          for (int p = kMaxPriority; p >= prio && !placed; --p) {
+            auto it = run_by_prio.find(p);
+            if (it == run_by_prio.end()) continue;
+            auto& cands = it->second;
+            for (int i = static_cast<int>(cands.size()) - 1; i >= 0; --i) {
+              Running* c = cands[i];
+              if (p == prio && r->job_position >= c->job_position) break;
+              if (!c->preemptible || released(c->alloc_id)) continue;
+              release_running(trial, *c);
+              victims.push_back(c->alloc_id);
+              auto fit = find_fit(*r, trial, fit_);
+              if (!fit.empty()) {
+                apply(trial, r->alloc_id, fit);
+                placed = true;
+                break;
+              }
             }
           }
-          if (placed)
-            for (auto& c : chosen) to_release.insert(c);
+          if (placed) {
+            local = std::move(trial);
+            for (auto& v : victims) to_release.push_back(v);
+          }
         }
       }
-      for (auto& a : to_release) d.preempt.push_back(a);
+      for (auto& v : to_release) d.preempt.push_back(v);
     }
     return d;
   }
@@ -596,7 +652,9 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("preemptible", &Running::preemptible)
       .def_readwrite("max_slots", &Running::max_slots)
       .def_readwrite("submit_time", &Running::submit_time)
-      .def_readwrite("job_submit_time", &Running::job_submit_time);
+      .def_readwrite("job_submit_time", &Running::job_submit_time)
+      .def_readwrite("job_position", &Running::job_position)
+      .def_readwrite("agents", &Running::agents);
   py::class_<Placement>(m, "Placement")
       .def(py::init<>())
       .def_readwrite("agent_id", &Placement::agent_id)

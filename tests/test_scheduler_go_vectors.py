@@ -1,5 +1,7 @@
-"""The reference's fair-share scheduler test vectors (master/internal/rm/agentrm/fair_share_test.go),
-ported case by case onto the native scheduler (native/scheduler.cpp ``Scheduler("fair_share")``).
+"""The reference's fair-share and priority scheduler test vectors
+(master/internal/rm/agentrm/{fair_share,priority}_test.go), ported case by case onto the native
+scheduler (native/scheduler.cpp). priority_test.go's TestSortTasksByPriorityAndTimestamps checks an
+internal sort helper and is covered through the queue-order cases instead.
 
 Harness semantics follow the reference's setupSchedulerStates (scheduler_test.go:451-544):
 * tasks are submitted in list order (each gets a later submission time); a task without a group
@@ -218,3 +220,268 @@ def test_fair_share_terminates_when_non_preemptible_exceed_max_slots():
     t = [MTask("task1", 1, g1, allocated=a, non_preemptible=True),
          MTask("task2", 1, g1, allocated=a, non_preemptible=True), MTask("task3", 1, g1)]
     assert run_fair_share([a], t) == (set(), set())
+
+
+# ------------------------------------------------------------------------------ priority.go
+# master/internal/rm/agentrm/priority_test.go, on Scheduler("priority"). Multi-round cases follow
+# its AllocateTasks / AddUnallocatedTasks / RemoveTask helpers: a started task takes the slots of
+# the placement the scheduler returned and becomes a running allocation; removing it frees them.
+# Tasks marked ``started`` begin on their agent with their slots (or zero-slot container) held.
+
+
+@dataclass
+class PAgent:
+    id: str
+    slots: int = 0
+    max_zero: int = 0
+
+
+@dataclass
+class PTask:
+    id: str
+    slots: int
+    priority: int
+    job: Optional[str] = None
+    started_on: Optional[PAgent] = None
+    non_preemptible: bool = False
+
+
+class PrioritySim:
+    def __init__(self, agents, tasks, preemption):
+        self.sched = N.Scheduler("priority", "best", preemption)
+        self.agents = {}
+        for a in agents:
+            x = N.Agent()
+            x.id, x.num_slots, x.max_zero_slot = a.id, a.slots, a.max_zero
+            x.slot_owner, x.slot_enabled = [""] * a.slots, [True] * a.slots
+            self.agents[a.id] = x
+        self.pending, self.running, self.clock, self.positions = {}, {}, 0.0, {}
+        for t in tasks:
+            self.add(t)
+
+    def _job(self, t):
+        return t.job or t.id
+
+    def add(self, t):
+        self.clock += 1.0
+        if t.started_on is not None:
+            r = N.Running()
+            r.alloc_id, r.job_id, r.slots, r.priority = t.id, self._job(t), t.slots, t.priority
+            r.preemptible = not t.non_preemptible
+            r.submit_time = r.job_submit_time = self.clock
+            a = self.agents[t.started_on.id]
+            if t.slots == 0:
+                a.zero_slot_used += 1
+            else:
+                owners = list(a.slot_owner)
+                free = [i for i, o in enumerate(owners) if not o][: t.slots]
+                for i in free:
+                    owners[i] = t.id
+                a.slot_owner = owners
+            r.agents = [a.id]
+            self.running[t.id] = r
+        else:
+            r = N.Request()
+            r.alloc_id, r.job_id, r.slots, r.priority = t.id, self._job(t), t.slots, t.priority
+            r.preemptible = not t.non_preemptible
+            r.submit_time = r.job_submit_time = self.clock
+            self.pending[t.id] = r
+
+    def schedule(self, positions=None):
+        pend = list(self.pending.values())
+        run = list(self.running.values())
+        for x in pend + run:
+            x.job_position = float((positions or {}).get(x.job_id, 0.0))
+        d = self.sched.schedule(list(self.agents.values()), pend, run)
+        return d
+
+    def allocate(self, d):
+        for alloc, places in d.start:
+            req = self.pending.pop(alloc)
+            r = N.Running()
+            r.alloc_id, r.job_id, r.slots, r.priority = req.alloc_id, req.job_id, req.slots, req.priority
+            r.preemptible, r.submit_time, r.job_submit_time = req.preemptible, req.submit_time, req.job_submit_time
+            r.agents = [p.agent_id for p in places]
+            for p in places:
+                a = self.agents[p.agent_id]
+                if not p.slots:
+                    a.zero_slot_used += 1
+                owners = list(a.slot_owner)
+                for i in p.slots:
+                    assert not owners[i], "slot handed out twice"
+                    owners[i] = alloc
+                a.slot_owner = owners
+            self.running[alloc] = r
+
+    def remove(self, alloc):
+        r = self.running.pop(alloc)
+        for aid in r.agents:
+            a = self.agents[aid]
+            if r.slots == 0:
+                a.zero_slot_used -= 1
+            a.slot_owner = ["" if o == alloc else o for o in a.slot_owner]
+
+
+def started(d):
+    return {alloc for alloc, _ in d.start}
+
+
+LOW, MED, HIGH = 50, 45, 40
+
+
+def _std_tasks(zero_slot_4_and_6=True):
+    # task1..6 of PreemptionDisabled / AddTasks / AllSlotsAllocated / AllTasksFinished
+    s4, s6 = (0, 0) if zero_slot_4_and_6 else (1, 1)
+    return [PTask("task1", 4, LOW, "g1"), PTask("task2", 1, LOW, "g1"), PTask("task3", 1, HIGH, "g2"),
+            PTask("task4", s4, HIGH, "g2"), PTask("task5", 4, HIGH, "g2"), PTask("task6", s6, LOW, "g1")]
+
+
+def test_priority_max_zero_slot_container():
+    sim = PrioritySim([PAgent("agent1", 4, 0)], [PTask("task1", 4, HIGH, "g2"), PTask("task6", 0, LOW, "g1")], True)
+    assert started(sim.schedule()) == {"task1"}
+
+
+def test_priority_preemption_disabled():
+    sim = PrioritySim([PAgent("agent1", 4, 100), PAgent("agent2", 4, 100)], _std_tasks(), False)
+    assert started(sim.schedule()) == {"task2", "task3", "task4", "task5", "task6"}
+    # the scheduler works on copies: the caller's agent state is untouched
+    assert all(not any(a.slot_owner) for a in sim.agents.values())
+
+
+def test_priority_preemption_disabled_higher_priority_blocks_lower_priority():
+    sim = PrioritySim([PAgent("agent1", 4), PAgent("agent2", 4)],
+                      [PTask("task1", 4, LOW, "g1"), PTask("task2", 1, LOW, "g1"), PTask("task3", 12, HIGH, "g2")], False)
+    assert started(sim.schedule()) == set()
+
+
+def test_priority_preemption_disabled_add_tasks():
+    sim = PrioritySim([PAgent("agent1", 4, 100), PAgent("agent2", 4, 100)], _std_tasks(), False)
+    d = sim.schedule()
+    assert started(d) == {"task2", "task3", "task4", "task5", "task6"}
+    sim.allocate(d)
+    for i in (7, 8, 9):
+        sim.add(PTask(f"task{i}", 1, LOW, "g1"))
+    assert started(sim.schedule()) == {"task7", "task8"}
+
+
+def test_priority_preemption_disabled_all_slots_allocated():
+    sim = PrioritySim([PAgent("agent1", 4), PAgent("agent2", 4)], _std_tasks(False), False)
+    d = sim.schedule()
+    assert started(d) == {"task2", "task3", "task4", "task5", "task6"}
+    sim.allocate(d)
+    sim.add(PTask("task7", 1, HIGH, "g2"))
+    sim.add(PTask("task8", 1, HIGH, "g2"))
+    assert started(sim.schedule()) == set()
+
+
+def test_priority_preemption_disabled_lower_priority_must_wait():
+    sim = PrioritySim([PAgent("agent1", 4)],
+                      [PTask("task1", 1, LOW, "g1"), PTask("task2", 1, HIGH, "g2"), PTask("task3", 1, HIGH, "g2"),
+                       PTask("task4", 1, HIGH, "g2"), PTask("task5", 2, HIGH, "g2")], False)
+    d1 = sim.schedule()
+    assert started(d1) == {"task2", "task3", "task4"}
+    sim.allocate(d1)
+    assert started(sim.schedule()) == set()
+    for alloc in started(d1):
+        sim.remove(alloc)
+    assert started(sim.schedule()) == {"task1", "task5"}
+
+
+def test_priority_preemption_disabled_task_finished():
+    sim = PrioritySim([PAgent("agent1", 4, 100)], [PTask("task1", 4, HIGH, "g1")], False)
+    d = sim.schedule()
+    sim.allocate(d)
+    sim.remove("task1")
+    for t in (PTask("task7", 1, HIGH, "g1"), PTask("task8", 1, HIGH, "g1"), PTask("task9", 0, HIGH, "g1")):
+        sim.add(t)
+    assert started(sim.schedule()) == {"task7", "task8", "task9"}
+
+
+def test_priority_preemption_disabled_all_tasks_finished():
+    sim = PrioritySim([PAgent("agent1", 4), PAgent("agent2", 4)], _std_tasks(False), False)
+    d = sim.schedule()
+    assert started(d) == {"task2", "task3", "task4", "task5", "task6"}
+    sim.allocate(d)
+    sim.add(PTask("task7", 4, HIGH, "g2"))
+    for alloc in started(d):
+        sim.remove(alloc)
+    assert started(sim.schedule()) == {"task1", "task7"}
+
+
+def test_priority_preemption_disabled_zero_slot_task():
+    sim = PrioritySim([PAgent("agent1", 4, 1)], [PTask("task1", 0, LOW, "g1"), PTask("task2", 0, LOW, "g1")], False)
+    d = sim.schedule()
+    assert started(d) == {"task1"}
+    sim.allocate(d)
+    sim.add(PTask("task3", 0, HIGH, "g2"))
+    d = sim.schedule()
+    assert started(d) == set() and set(d.preempt) == set()
+
+
+def test_priority_preemption():
+    a1, a2 = PAgent("agent1", 4), PAgent("agent2", 4)
+    sim = PrioritySim([a1, a2], [
+        PTask("low-priority task cannot be backfilled because preemption exists", 1, LOW, "g1"),
+        PTask("medium-priority task should be preempted", 4, MED, "g2", started_on=a1),
+        PTask("high-priority task should not be preempted", 4, HIGH, "g3", started_on=a2),
+        PTask("high-priority task causes preemption but should not be scheduled", 4, HIGH, "g3"),
+        PTask("high-priority oversized task triggers backfilling", 8, HIGH, "g3")], True)
+    d = sim.schedule()
+    assert started(d) == set()
+    assert set(d.preempt) == {"medium-priority task should be preempted"}
+
+
+def test_priority_backfilling():
+    a1, a2 = PAgent("agent1", 4), PAgent("agent2", 4)
+    sim = PrioritySim([a1, a2], [
+        PTask("low-priority task should be preempted", 1, 55, "g1", started_on=a1),
+        PTask("lower-priority task causes preemption but should not be scheduled", 1, 50, "g2"),
+        PTask("medium-priority task should be backfilled", 1, 45, "g3"),
+        PTask("high-priority task should not be preempted", 4, 40, "g4", started_on=a2),
+        PTask("high-priority task should be scheduled", 2, 40, "g4"),
+        PTask("high-priority oversized task triggers backfilling", 8, 40, "g4")], True)
+    d = sim.schedule()
+    assert started(d) == {"medium-priority task should be backfilled", "high-priority task should be scheduled"}
+    assert set(d.preempt) == {"low-priority task should be preempted"}
+
+
+def test_priority_preemption_zero_slot_task():
+    a1, a2 = PAgent("agent1", 0, 1), PAgent("agent2", 0, 1)
+    sim = PrioritySim([a1, a2], [
+        PTask("low-priority task cannot be scheduled", 0, LOW, "g1"),
+        PTask("medium-priority task should be preempted", 0, MED, "g2", started_on=a1),
+        PTask("high-priority task should not be preempted", 0, HIGH, "g3", started_on=a2),
+        PTask("high-priority task causes preemption but should not be scheduled", 0, HIGH, "g3")], True)
+    d = sim.schedule()
+    assert started(d) == set()
+    assert set(d.preempt) == {"medium-priority task should be preempted"}
+
+
+def test_priority_backfilling_zero_slot_task():
+    a1, a2 = PAgent("agent1", 0, 4), PAgent("agent2", 0, 1)
+    sim = PrioritySim([a1, a2], [
+        PTask("low-priority task should be scheduled", 0, 55, "g1"),
+        PTask("medium-priority task should not be preempted", 0, 50, "g2", started_on=a1),
+        PTask("high-priority task should not be preempted", 0, 45, "g3", started_on=a2),
+        PTask("high-priority task should be scheduled", 0, 45, "g3")], True)
+    d = sim.schedule()
+    assert started(d) == {"low-priority task should be scheduled", "high-priority task should be scheduled"}
+    assert set(d.preempt) == set()
+
+
+@pytest.mark.parametrize("positions", [{"1": 1, "2": 2, "3": 1.5}, {"1": 1, "2": 1, "3": 0.999}])
+def test_priority_preempt_one_by_position(positions):
+    a1, a2 = PAgent("agent1", 4), PAgent("agent2", 4)
+    sim = PrioritySim([a1, a2], [PTask("1", 1, 42, "1", started_on=a1), PTask("2", 4, 42, "2", started_on=a2),
+                                 PTask("3", 4, 42, "3")], True)
+    d = sim.schedule(positions)
+    assert started(d) == set() and set(d.preempt) == {"2"}
+
+
+def test_priority_no_preemption_by_position():
+    a1, a2 = PAgent("agent1", 4), PAgent("agent2", 4)
+    sim = PrioritySim([a1, a2], [PTask("1", 1, 42, "1", started_on=a1), PTask("2", 4, 42, "2", started_on=a2),
+                                 PTask("3", 8, 42, "3")], True)
+    # job 3 sits between jobs 1 and 2: only job 2 is behind it, and freeing job 2 is not enough
+    d = sim.schedule({"1": 1, "2": 2, "3": 1.5})
+    assert started(d) == set() and set(d.preempt) == set()
