@@ -90,6 +90,20 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int base) {
   return __builtin_bit_cast(bf16x8, u);
 }
 
+// O *= alpha for the deferred-max rescale, one v_mul_f32 per register. Written as plain f32x16
+// arithmetic the compiler emits 8 v_pk_mul_f32 per accumulator (packed f32 VALU costs ~22-26
+// extra cycles each beside MFMAs on gfx950 -- an anti-lever) AND if-converts the wave-uniform
+// `if (__any(upd))` around it, so every sub-tile paid 16 packed multiplies (ISA census of this
+// file, round 4). volatile asm keeps the multiplies single-issue and inside the branch.
+__device__ __forceinline__ void rescale16(f32x16& a, float s) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float t = a[i];
+    asm volatile("v_mul_f32 %0, %1, %2" : "=v"(t) : "v"(t), "v"(s));
+    a[i] = t;
+  }
+}
+
 // v_exp_f32 directly (inputs are finite or -inf; no denormal range fix-up needed)
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -298,7 +312,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         m = mnew;
         if (__any(upd)) {
   #pragma unroll
-          for (int n = 0; n < D / 32; ++n) oacc[n] *= alpha;
+          for (int n = 0; n < D / 32; ++n) rescale16(oacc[n], alpha);
         }
         const bf16x8 p0 = pack8(sc, 0), p1 = pack8(sc, 8);
   #pragma unroll
@@ -384,7 +398,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       m = mnew;
       if (__any(upd)) {
 #pragma unroll
-        for (int n = 0; n < D / 32; ++n) oacc[n] *= alpha;
+        for (int n = 0; n < D / 32; ++n) rescale16(oacc[n], alpha);
       }
       const bf16x8 p0 = pack8(sc, 0), p1 = pack8(sc, 8);
 #pragma unroll
