@@ -44,10 +44,13 @@ def test_shared_fs_sync_and_per_cluster_dir(tmp_path, monkeypatch):
     assert not list(pathlib.Path(tmp_path, "tensorboard", cb).rglob("*"))
 
 
-def test_tensorboard_task_syncs_shared_fs_experiment_dirs(tmp_path):
+def test_tensorboard_task_syncs_shared_fs_experiment_dirs(tmp_path, monkeypatch):
     """The TB task's SyncedLogdirs: one fetcher per storage, experiment dirs copied locally and
     re-fetched when the trial writes more (reference exec/tensorboard.py fetch loop)."""
     from determined_clone_amd.exec import tensorboard as tb_task
+
+    # a private local event-file directory: the default one persists across processes
+    monkeypatch.setenv("DET_TENSORBOARD_DIR", str(tmp_path / "tb-local"))
 
     store = {"type": "shared_fs", "host_path": str(tmp_path / "store")}
     mgr = tensorboard.build("cl", "5", "9", store)

@@ -68,8 +68,20 @@ def main(path: str, steps: int = 3, step_marker: str = "sgd_kernel", per_step: i
     print("\nby category (ms/step):")
     for c, v in sorted(by_cat.items(), key=lambda x: -x[1]):
         print(f"  {c:32s} {v / steps:8.3f}  {100 * v / (busy / 1e6):5.1f}%")
+    skey = "Stream_Id" if seg and "Stream_Id" in seg[0] else ("Queue_Id" if seg and "Queue_Id" in seg[0] else None)
+    if skey:
+        # per stream / queue: the training step's critical path is the main stream's busy time
+        by_stream = defaultdict(lambda: defaultdict(float))
+        for r in seg:
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            by_stream[r[skey]][category(r["Kernel_Name"])] += d
+        print(f"\nby {skey} (ms/step busy; categories):")
+        for sid, cats in sorted(by_stream.items(), key=lambda x: -sum(x[1].values())):
+            tot = sum(cats.values()) / steps
+            parts = ", ".join(f"{c} {v / steps:.1f}" for c, v in sorted(cats.items(), key=lambda x: -x[1])[:6])
+            print(f"  {skey}={sid}: {tot:8.3f}  [{parts}]")
     print("\ntop kernels (ms/step, calls/step):")
-    for n, (v, c) in sorted(by_name.items(), key=lambda x: -x[1][0])[:25]:
+    for n, (v, c) in sorted(by_name.items(), key=lambda x: -x[1][0])[:40]:
         print(f"  {v / steps:8.3f} {c / steps:5.0f}  {n}")
     if by_grid:
         # per-launch-shape times of the kernels matching `by_grid` (grid size identifies the layer)
