@@ -431,7 +431,7 @@ async function pageTrial(params, id) {
 // batch order with their metrics; filter to validations or checkpoints.
 async function workloadsView(id, filter) {
   const q = filter ? "?filter=FILTER_OPTION_" + filter : "";
-  const { workloads } = await api.get(`/api/v1/trials/${id}/workloads${q}`);
+  const { workloads } = await api.get(`/api/v1/trials/${id}/workloads` + q);
   const rows = workloads.map((w, i) => {
     const kind = Object.keys(w)[0], x = w[kind];
     const m = ((x.metrics || {}).avg_metrics) || {};
