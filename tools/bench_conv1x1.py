@@ -5,8 +5,9 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "determined_clone_amd", "ops", "tuned", "miopen", "db"))
-os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "miopen", "cache"))
+from determined_clone_amd.ops import miopen_db  # noqa: E402
+
+miopen_db.use_private_copy("tools")  # never write the shipped DB from a bench
 
 import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
