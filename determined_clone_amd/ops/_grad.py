@@ -60,9 +60,12 @@ _pending = set()
 # tensors -- past the HBM left on a box where another process still held memory, where every
 # allocation miss became a 1-25 s free-all-and-retry (profiles/round4_bench_slow_mode.txt).
 # Released after the current stream has waited for the side stream, the blocks return to the
-# current stream's pool immediately reusable. DCA_WGRAD_KEEPALIVE=0 restores record_stream.
+# current stream's pool immediately reusable. Entries whose side-stream reads have demonstrably
+# finished (an event recorded after them has completed) are dropped earlier, at the next fork, so
+# code that runs several backward passes before an optimizer step (and so before join()) holds
+# only what the side stream has not reached yet. DCA_WGRAD_KEEPALIVE=0 restores record_stream.
 KEEPALIVE = os.environ.get("DCA_WGRAD_KEEPALIVE", "1") != "0"
-_keep = []
+_keep = []  # [tensors, event recorded on the side stream after their readers (or None yet)]
 
 
 def side_stream_for(p: Optional[torch.Tensor]) -> Optional["torch.cuda.Stream"]:
@@ -82,15 +85,23 @@ def side_stream_for(p: Optional[torch.Tensor]) -> Optional["torch.cuda.Stream"]:
 def fork(stream: "torch.cuda.Stream", tensors=()) -> None:
     """Order ``stream`` after the work queued so far on the current stream; keep ``tensors``
     (allocated on the current stream) alive until ``stream`` has used them."""
+    if KEEPALIVE and _keep and _keep[-1][1] is None:
+        # everything the previous fork's caller queued on the side stream precedes this event
+        done = torch.cuda.Event()
+        done.record(stream)
+        _keep[-1][1] = done
+    while KEEPALIVE and _keep and _keep[0][1] is not None and _keep[0][1].query():
+        _keep.pop(0)  # those reads have executed: the blocks may be reused by the current stream
     ev = torch.cuda.Event()
     ev.record()
     stream.wait_event(ev)
-    for t in tensors:
-        if t is not None:
-            if KEEPALIVE:
-                _keep.append(t)
-            else:
-                t.record_stream(stream)
+    live = [t for t in tensors if t is not None]
+    if KEEPALIVE:
+        if live:
+            _keep.append([live, None])
+    else:
+        for t in live:
+            t.record_stream(stream)
     _pending.add(stream)
 
 

@@ -240,6 +240,35 @@ def test_side_stream_weight_gradients_match_inline(monkeypatch, model_fn):
     assert not _grad.pending()
 
 
+def test_side_stream_inputs_released_without_optimizer_step(monkeypatch):
+    """Side-stream weight-gradient inputs are held by reference (not record_stream) until join();
+    with several backward passes before any optimizer step (gradient accumulation in user code),
+    the inputs whose side-stream reads have executed are dropped at the next fork, so the held set
+    does not grow with the number of backward passes."""
+    from determined_clone_amd.models import resnet
+    from determined_clone_amd.ops import _grad
+    from determined_clone_amd.ops import optim as fopt
+
+    monkeypatch.setattr(_grad, "SIDE_STREAM", True)
+    monkeypatch.setattr(_grad, "KEEPALIVE", True)
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    model = resnet.to_mi355x_layout(resnet.resnet18_bottleneck_tiny(num_classes=10)).to(dev)
+    opt = fopt.FusedSGD(model.parameters(), lr=0.1, momentum=0.9)
+    x = torch.randn(16, 3, 64, 64, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device=dev)
+    opt.zero_grad()
+    F.cross_entropy(model(x).float(), y).backward()
+    per_pass = len(_grad._keep)
+    assert per_pass > 0 and _grad.pending()
+    for _ in range(3):
+        torch.cuda.synchronize()  # the side stream has executed everything queued so far
+        F.cross_entropy(model(x).float(), y).backward()
+        assert len(_grad._keep) <= per_pass + 1, (len(_grad._keep), per_pass)
+    opt.step()  # joins
+    assert not _grad.pending() and not _grad._keep
+
+
 @pytest.mark.parametrize("side", [True, False])
 @pytest.mark.parametrize("hw", [(224, 224), (64, 48)])
 def test_stem_space_to_depth_matches_fp32(monkeypatch, side, hw):
