@@ -140,21 +140,66 @@ def _pw_forward(x: torch.Tensor, weight: torch.Tensor, stride: int) -> torch.Ten
     return (lib, gemm)[_choose(("fwd", tuple(x.shape), cout, stride, x.dtype), (lib, gemm))]()
 
 
+# 1x1 forward on the implicit-GEMM MFMA kernel (csrc/conv_igemm.hip, R = S = 1) when its output
+# feeds a training BatchNorm: the epilogue emits the BN's per-block statistics, so the BN skips its
+# reduce pass over the output. Per shape, "auto" times {best library conv + BN forward} against
+# {implicit GEMM with statistics + BN forward on them} once (like the other choosers) and keeps
+# the faster; the backward stays on the library / GEMM paths below. DCA_IG1X1=1 forces, 0 disables.
+IG1X1 = os.environ.get("DCA_IG1X1", "auto")
+
+
+def _ig1x1_ok(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    if IG1X1 == "0" or not IGEMM or not x.is_cuda or torch.is_autocast_enabled():
+        return False
+    if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
+        return False
+    n, cin, h, w = x.shape
+    cout = weight.shape[0]
+    if cin % 64 or cout % 64 or not weight.is_contiguous(memory_format=torch.channels_last):
+        return False
+    return x.numel() < 2 ** 30 and n * cout * h * w < 2 ** 30
+
+
+def _ig1x1_wins(x: torch.Tensor, weight: torch.Tensor, stride: int) -> bool:
+    if IG1X1 == "1":
+        return True
+    C = _ext.load()
+    cout = weight.shape[0]
+    f = dict(device=x.device, dtype=torch.float32)
+    g, b, rm, rv = torch.ones(cout, **f), torch.zeros(cout, **f), torch.zeros(cout, **f), torch.ones(cout, **f)
+
+    def lib_then_bn():
+        C.bn_fwd_train(_pw_forward(x, weight, stride), None, g, b, rm, rv, None, 0.1, 1e-5, True, None)
+
+    def igemm_stats_then_bn():
+        y, part = C.conv_igemm_fwd(x, weight, stride, 0, True)
+        C.bn_fwd_train(y, None, g, b, rm, rv, None, 0.1, 1e-5, True, part)
+
+    key = ("fwd1x1+bn", tuple(x.shape), cout, stride, x.dtype)
+    return _choose(key, (lib_then_bn, igemm_stats_then_bn)) == 1
+
+
 class _PointwiseLib(torch.autograd.Function):
-    """1x1 / no-padding convolution with per-direction library choice (MIOpen or hipBLASLt)."""
+    """1x1 / no-padding convolution with per-direction library choice (MIOpen or hipBLASLt);
+    with ``stats`` the forward runs on the implicit-GEMM kernel and also returns the following
+    BatchNorm's partial statistics (an empty tensor otherwise)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride):
-        y = _pw_forward(x, weight, stride)
+    def forward(ctx, x, weight, stride, stats=False):
+        if stats:
+            y, partial = _ext.load().conv_igemm_fwd(x, weight, stride, 0, True)
+        else:
+            y, partial = _pw_forward(x, weight, stride), x.new_empty(0, dtype=torch.float32)
+        ctx.mark_non_differentiable(partial)
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
         # x is a fused BN output whose identity-shortcut gradient arrives through a sink
         # (ops/batchnorm.py ResidualGradSink): the backward-data GEMM can accumulate into it
         ctx.sink = getattr(x, "_dca_grad_sink", None) if ACC_RESIDUAL else None
-        return y
+        return y, partial
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dpartial=None):
         x, weight = ctx.saved_tensors
         st = ctx.stride
         dy = dy.contiguous(memory_format=torch.channels_last)
@@ -198,7 +243,7 @@ class _PointwiseLib(torch.autograd.Function):
                     dx = cands[pick]()
             else:
                 dx = lib()
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class _PointwiseDual(torch.autograd.Function):
@@ -532,7 +577,11 @@ def pointwise_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> 
         return y
     if _lib_supported(conv, x):
         x = x.contiguous(memory_format=torch.channels_last)
-        return _PointwiseLib.apply(x, conv.weight, conv.stride[0])
+        stats = bool(bn_stats) and _ig1x1_ok(x, conv.weight) and _ig1x1_wins(x, conv.weight, conv.stride[0])
+        y, partial = _PointwiseLib.apply(x, conv.weight, conv.stride[0], stats)
+        if stats:
+            y._dca_bn_partials = partial
+        return y
     return conv(x)
 
 

@@ -240,6 +240,41 @@ def test_side_stream_weight_gradients_match_inline(monkeypatch, model_fn):
     assert not _grad.pending()
 
 
+def test_pointwise_igemm_with_bn_stats_matches_library_path(monkeypatch):
+    """1x1 convolutions forced onto the implicit-GEMM kernel with the BatchNorm statistics in its
+    epilogue (DCA_IG1X1=1) train the tiny bottleneck ResNet like the library path (IG1X1=0):
+    same loss and gradients within bf16 noise, and the BNs really consumed fused statistics."""
+    from determined_clone_amd.models import resnet
+    from determined_clone_amd.ops import conv as conv_ops
+
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    base = resnet.to_mi355x_layout(resnet.resnet18_bottleneck_tiny(num_classes=10)).to(dev)
+    x = torch.randn(16, 3, 64, 64, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device=dev)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setattr(conv_ops, "IG1X1", mode)
+        model = copy.deepcopy(base)
+        hits = []
+        orig = conv_ops._PointwiseLib.apply
+
+        def spy(*a):
+            r = orig(*a)
+            hits.append(bool(a[3]) if len(a) > 3 else False)
+            return r
+
+        monkeypatch.setattr(conv_ops._PointwiseLib, "apply", spy)
+        loss = F.cross_entropy(model(x).float(), y)
+        loss.backward()
+        out[mode] = (loss.item(), [p.grad.float().clone() for p in model.parameters()])
+        if mode == "1":
+            assert sum(hits) >= 4, hits  # conv1 / conv3 of the blocks took the fused-stats path
+    assert abs(out["0"][0] - out["1"][0]) < 2e-2 * max(1.0, abs(out["0"][0]))
+    for a, b in zip(out["0"][1], out["1"][1]):
+        assert (a - b).norm().item() <= 5e-2 * a.norm().item() + 1e-4
+
+
 def test_side_stream_inputs_released_without_optimizer_step(monkeypatch):
     """Side-stream weight-gradient inputs are held by reference (not record_stream) until join();
     with several backward passes before any optimizer step (gradient accumulation in user code),
