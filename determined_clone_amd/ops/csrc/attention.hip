@@ -224,7 +224,12 @@ struct KVPrefetch {
 // + one exchange with lane^32), and P^T -- still in registers -- is directly the B operand of
 // O^T += V^T P^T (no LDS round trip for P). V^T fragments come from the row-major V tile through
 // ds_read_b64_tr_b16 (hardware transpose), so K and V are staged exactly as they arrive from HBM.
-template <int D, bool CAUSAL, int KT, bool PIPE>
+//
+// MSUM: the softmax row sums come out of the matrix core instead of 16 dependent v_add_f32 per
+// sub-tile: one more O^T-shaped MFMA pair per sub-tile with an all-ones A operand, whose every
+// row is sum_k P^T[k][q] (the same bf16 P the O product uses), rescaled with O by the deferred max.
+// The MFMA pipe runs at ~30% here while VALU issue and its dependency chains bound the loop.
+template <int D, bool CAUSAL, int KT, bool PIPE, bool MSUM = false>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
@@ -262,6 +267,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   f32x16 oacc[D / 32];
 #pragma unroll
   for (int n = 0; n < D / 32; ++n) oacc[n] = zero16();
+  f32x16 lacc = zero16();  // MSUM: every register = this lane's query row sum
+  const bf16x8 ones8 = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
   float m = -INFINITY, l = 0.f;
   const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
   // tr-read lane address pieces (see T10: lane 4q+p of a 16-lane group -> row q, cols 4p..4p+3)
@@ -305,16 +312,23 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         for (int i = 0; i < 16; ++i) {
           const float p = fast_exp2(fmaf(sc[i], scale_log2, -mref));
           sc[i] = p;
-          rs += p;
+          if constexpr (!MSUM) rs += p;
         }
-        rs = half_sum(rs);
-        l = l * alpha + rs;
+        if constexpr (!MSUM) {
+          rs = half_sum(rs);
+          l = l * alpha + rs;
+        }
         m = mnew;
         if (__any(upd)) {
   #pragma unroll
           for (int n = 0; n < D / 32; ++n) rescale16(oacc[n], alpha);
+          if constexpr (MSUM) rescale16(lacc, alpha);
         }
         const bf16x8 p0 = pack8(sc, 0), p1 = pack8(sc, 8);
+        if constexpr (MSUM) {
+          lacc = mfma32(ones8, p0, lacc);
+          lacc = mfma32(ones8, p1, lacc);
+        }
   #pragma unroll
         for (int n = 0; n < D / 32; ++n) {
   #pragma unroll
@@ -391,16 +405,23 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       for (int i = 0; i < 16; ++i) {
         const float p = fast_exp2(fmaf(sc[i], scale_log2, -mref));
         sc[i] = p;
-        rs += p;
+        if constexpr (!MSUM) rs += p;
       }
-      rs = half_sum(rs);
-      l = l * alpha + rs;
+      if constexpr (!MSUM) {
+        rs = half_sum(rs);
+        l = l * alpha + rs;
+      }
       m = mnew;
       if (__any(upd)) {
 #pragma unroll
         for (int n = 0; n < D / 32; ++n) rescale16(oacc[n], alpha);
+        if constexpr (MSUM) rescale16(lacc, alpha);
       }
       const bf16x8 p0 = pack8(sc, 0), p1 = pack8(sc, 8);
+      if constexpr (MSUM) {
+        lacc = mfma32(ones8, p0, lacc);
+        lacc = mfma32(ones8, p1, lacc);
+      }
 #pragma unroll
       for (int n = 0; n < D / 32; ++n) {
 #pragma unroll
@@ -413,6 +434,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   }
   // 8-byte stores here: the widened form (store_rows) measured -2..-3% on this kernel at S >= 2048
   // (+1.5% at S 1024), +2.5-4% on the backward kernels (profiles/round3_attention_epilogue_ab.txt)
+  if constexpr (MSUM) l = lacc[0];
   if (my_q < Sq) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     uint16_t* orow = o + b * os.b + h * os.h + static_cast<int64_t>(my_q) * os.s;
@@ -807,6 +829,15 @@ bool dq_pipe() {
   return on;
 }
 
+// forward row sums on the matrix core (attn_fwd_kernel MSUM; DCA_ATTN_FWD_MSUM=1)
+bool fwd_msum() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCA_ATTN_FWD_MSUM");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
 // keys per LDS tile of the forward kernel (DCA_ATTN_FWD_KT=128: half the barriers per MFMA)
 int fwd_kt() {
   static const int kt = [] {
@@ -842,13 +873,16 @@ void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
       hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
                          scale_log2, attn_order(C), kvlen);
     };
+    const bool ms = fwd_msum();
     if constexpr (D == 64) {  // D = 128 with two live score tiles spills
       if (fwd_pipe()) {
-        launch(attn_fwd_kernel<D, C, KT, true>);
+        if (ms) launch(attn_fwd_kernel<D, C, KT, true, true>);
+        else launch(attn_fwd_kernel<D, C, KT, true>);
         return;
       }
     }
-    launch(attn_fwd_kernel<D, C, KT, false>);
+    if (ms) launch(attn_fwd_kernel<D, C, KT, false, true>);
+    else launch(attn_fwd_kernel<D, C, KT, false>);
   };
   if constexpr (D == 64) {  // D = 128 at KT = 128 exceeds the register file (spills)
     if (fwd_kt() == 128) {
