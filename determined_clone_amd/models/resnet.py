@@ -95,7 +95,7 @@ class Bottleneck(nn.Module):
                 y1 = pointwise_conv(self.conv1, x, self.bn1.training)
                 yd = pointwise_conv(ds_conv, x, ds_bn.training)
             else:
-                y1, yd = pointwise_dual(self.conv1, ds_conv, x)
+                y1, yd = pointwise_dual(self.conv1, ds_conv, x, self.bn1.training)
             identity = ds_bn(yd)
             out = self.bn1(y1)
         # 3x3: implicit-GEMM MFMA kernel whose epilogue also reduces bn2's statistics

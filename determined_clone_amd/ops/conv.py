@@ -254,15 +254,20 @@ class _PointwiseDual(torch.autograd.Function):
     gradient (after zero-filling it) that autograd then sums with a full-size add."""
 
     @staticmethod
-    def forward(ctx, x, w1, w2, stride):
-        y1 = _pw_forward(x, w1, 1)
-        y2 = _pw_forward(x, w2, stride)
+    def forward(ctx, x, w1, w2, stride, stats1=False, stats2=False):
+        # statsN: that output runs on the implicit-GEMM kernel with its BN's partial statistics
+        # (see _ig1x1_wins); an empty tensor stands in for partials not produced
+        C = _ext.load()
+        empty = x.new_empty(0, dtype=torch.float32)
+        y1, p1 = C.conv_igemm_fwd(x, w1, 1, 0, True) if stats1 else (_pw_forward(x, w1, 1), empty)
+        y2, p2 = C.conv_igemm_fwd(x, w2, stride, 0, True) if stats2 else (_pw_forward(x, w2, stride), empty)
+        ctx.mark_non_differentiable(p1, p2)
         ctx.save_for_backward(x, w1, w2)
         ctx.stride = stride
-        return y1, y2
+        return y1, y2, p1, p2
 
     @staticmethod
-    def backward(ctx, dy1, dy2):
+    def backward(ctx, dy1, dy2, _dp1=None, _dp2=None):
         x, w1, w2 = ctx.saved_tensors
         st = ctx.stride
         n, cin, h, w = x.shape
@@ -294,16 +299,24 @@ class _PointwiseDual(torch.autograd.Function):
                 ho, wo = dy2.shape[2], dy2.shape[3]
                 small = torch.mm(_rows(dy2, 1), W2).view(n, ho, wo, cin)
                 dx.permute(0, 2, 3, 1)[:, ::st, ::st, :].add_(small)
-        return dx, dw1, dw2, None
+        return dx, dw1, dw2, None, None, None
 
 
-def pointwise_dual(conv1: nn.Conv2d, proj: nn.Conv2d, x: torch.Tensor):
-    """``(conv1(x), proj(x))`` for a downsampling bottleneck (see :class:`_PointwiseDual`)."""
+def pointwise_dual(conv1: nn.Conv2d, proj: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False):
+    """``(conv1(x), proj(x))`` for a downsampling bottleneck (see :class:`_PointwiseDual`); with
+    ``bn_stats`` each output may carry its BatchNorm's partial statistics (``_ig1x1_wins``)."""
     if (not supported(conv1, x) and _lib_supported(conv1, x) and _lib_supported(proj, x)
             and conv1.stride == (1, 1)):
         x = x.contiguous(memory_format=torch.channels_last)
-        return _PointwiseDual.apply(x, conv1.weight, proj.weight, proj.stride[0])
-    return pointwise_conv(conv1, x), pointwise_conv(proj, x)
+        s1 = bool(bn_stats) and _ig1x1_ok(x, conv1.weight) and _ig1x1_wins(x, conv1.weight, 1)
+        s2 = bool(bn_stats) and _ig1x1_ok(x, proj.weight) and _ig1x1_wins(x, proj.weight, proj.stride[0])
+        y1, y2, p1, p2 = _PointwiseDual.apply(x, conv1.weight, proj.weight, proj.stride[0], s1, s2)
+        if s1:
+            y1._dca_bn_partials = p1
+        if s2:
+            y2._dca_bn_partials = p2
+        return y1, y2
+    return pointwise_conv(conv1, x, bn_stats), pointwise_conv(proj, x, bn_stats)
 
 
 # Weight gradients: MIOpen's backward-weight solvers or the split-pixel implicit-GEMM MFMA kernel
