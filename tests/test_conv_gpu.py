@@ -253,13 +253,13 @@ def test_pointwise_igemm_with_bn_stats_matches_library_path(monkeypatch):
     x = torch.randn(16, 3, 64, 64, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 10, (16,), device=dev)
     out = {}
+    orig = conv_ops._PointwiseLib.apply
     for mode in ("0", "1"):
         monkeypatch.setattr(conv_ops, "IG1X1", mode)
         model = copy.deepcopy(base)
         hits = []
-        orig = conv_ops._PointwiseLib.apply
 
-        def spy(*a):
+        def spy(*a, hits=hits):
             r = orig(*a)
             hits.append(bool(a[3]) if len(a) > 3 else False)
             return r
