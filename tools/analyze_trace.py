@@ -80,6 +80,19 @@ def main(path: str, steps: int = 3, step_marker: str = "sgd_kernel", per_step: i
             tot = sum(cats.values()) / steps
             parts = ", ".join(f"{c} {v / steps:.1f}" for c, v in sorted(cats.items(), key=lambda x: -x[1])[:6])
             print(f"  {skey}={sid}: {tot:8.3f}  [{parts}]")
+        # which weight-gradient kernels run on which stream, and what precedes them there
+        wg = defaultdict(lambda: [0.0, 0])
+        prev_on = {}
+        for r in seg:
+            sid = r[skey]
+            if category(r["Kernel_Name"]).startswith("conv bwd-weight"):
+                key = (sid, r["Kernel_Name"][:70], prev_on.get(sid, "-")[:50])
+                wg[key][0] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+                wg[key][1] += 1
+            prev_on[sid] = r["Kernel_Name"]
+        print(f"\nweight-gradient kernels by {skey} (ms/step, calls/step, preceded on that stream by):")
+        for (sid, n, pv), (v, c) in sorted(wg.items(), key=lambda x: (x[0][0], -x[1][0]))[:30]:
+            print(f"  {skey}={sid} {v / steps:7.3f} {c / steps:4.1f}  {n} | after: {pv}")
     print("\ntop kernels (ms/step, calls/step):")
     for n, (v, c) in sorted(by_name.items(), key=lambda x: -x[1][0])[:40]:
         print(f"  {v / steps:8.3f} {c / steps:5.0f}  {n}")
