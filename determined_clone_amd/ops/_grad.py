@@ -32,7 +32,16 @@ def target(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     if not ENABLED or p is None or not getattr(p, "_dca_direct_grad", False):
         return None
     g = p.grad
-    if g is None or g.dtype != p.dtype or not g.is_contiguous() or g.shape != p.shape:
+    if g is None or g.dtype != p.dtype or g.shape != p.shape:
+        return None
+    # dense in the parameter's own layout: contiguous, or a channels_last convolution weight
+    # (FlatParamSpace gives .grad the parameter's strides; the k x k weight-gradient paths --
+    # MIOpen + add_, the implicit-GEMM kernel's KRSC store, the stem's add_ -- all take either.
+    # Requiring plain contiguity kept every 3x3 / 7x7 weight gradient of a channels_last ResNet
+    # off the side stream: 17 MIOpen backward-weight calls, ~6.5 ms of a 80 ms step, on the
+    # critical path -- profiles/round4_resnet50_step_breakdown_default.txt)
+    if not (g.is_contiguous() or (g.dim() == 4 and g.stride() == p.stride()
+                                  and g.is_contiguous(memory_format=torch.channels_last))):
         return None
     if g.dtype not in (torch.float32, torch.bfloat16):
         return None
