@@ -33,6 +33,7 @@ class _Conv1x1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stats):
         y, partial = _ext.load().conv1x1_fwd(x, weight, stats)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         ctx.save_for_backward(x, weight)
         if partial is not None:
             ctx.mark_non_differentiable(partial)
@@ -191,6 +192,7 @@ class _PointwiseLib(torch.autograd.Function):
         else:
             y, partial = _pw_forward(x, weight, stride), x.new_empty(0, dtype=torch.float32)
         ctx.mark_non_differentiable(partial)
+        ctx.set_materialize_grads(False)  # autograd would zero-fill a gradient for `partial`
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
         # x is a fused BN output whose identity-shortcut gradient arrives through a sink
@@ -262,8 +264,10 @@ class _PointwiseDual(torch.autograd.Function):
         y1, p1 = C.conv_igemm_fwd(x, w1, 1, 0, True) if stats1 else (_pw_forward(x, w1, 1), empty)
         y2, p2 = C.conv_igemm_fwd(x, w2, stride, 0, True) if stats2 else (_pw_forward(x, w2, stride), empty)
         ctx.mark_non_differentiable(p1, p2)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for p1 / p2
         ctx.save_for_backward(x, w1, w2)
         ctx.stride = stride
+        ctx.shapes = (y1.shape, y2.shape)
         return y1, y2, p1, p2
 
     @staticmethod
@@ -272,6 +276,10 @@ class _PointwiseDual(torch.autograd.Function):
         st = ctx.stride
         n, cin, h, w = x.shape
         bwd = torch.ops.aten.convolution_backward
+        if dy1 is None or dy2 is None:  # one output unused (grads are not materialised)
+            z = lambda s: x.new_zeros(s).contiguous(memory_format=torch.channels_last)  # noqa: E731
+            dy1 = z(ctx.shapes[0]) if dy1 is None else dy1
+            dy2 = z(ctx.shapes[1]) if dy2 is None else dy2
         dy1 = dy1.contiguous(memory_format=torch.channels_last)
         dy2 = dy2.contiguous(memory_format=torch.channels_last)
         a1 = (dy1, x, w1, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
@@ -526,6 +534,7 @@ class _IgemmConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride, pad, stats):
         y, partial = _ext.load().conv_igemm_fwd(x, weight, stride, pad, stats)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         ctx.save_for_backward(x, weight)
         ctx.stride, ctx.pad = stride, pad
         if partial is not None:
