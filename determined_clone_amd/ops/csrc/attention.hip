@@ -181,38 +181,51 @@ __device__ __forceinline__ Blk xcd_block(int order) {
   return {v % nx, (v / nx) % ny, v / (nx * ny)};
 }
 
-// Register double buffer for a pair of [64 rows][D] tiles (K and V): fetch() issues the HBM loads of
+// Register double buffer for a pair of [ROWS][D] tiles (K and V): fetch() issues the HBM loads of
 // the NEXT tile before the current tile's MFMAs, store() writes them to LDS after the barrier.
+// Loads go through buffer descriptors whose range ends after row n_rows - 1: rows past it (the
+// tail tile, padded keys) come back as zeros from the hardware range check -- no per-chunk
+// branches, and 32-bit lane offsets computed once instead of 64-bit addresses per tile (the
+// host checks that (Sk + ROWS) * row stride stays below 2^31 bytes).
 template <int D, int ROWS = 64, int VPAD = kPad>
 struct KVPrefetch {
   static constexpr int CPR = D / 8;
-  static constexpr int N = 2 * ROWS * CPR / 256;
+  static constexpr int PER = ROWS * CPR / 256;  // 16-B chunks per thread per tensor
+  static constexpr int N = 2 * PER;
   uint4 reg[N];
-  __device__ __forceinline__ void fetch(const uint16_t* __restrict__ kb, Strides ks,
-                                        const uint16_t* __restrict__ vb, Strides vs, int r0,
-                                        int n_rows) {
+  uint32_t voff[N];  // byte offset of this lane's chunk j in a tile starting at row 0
+  __amdgpu_buffer_rsrc_t kr, vr;
+  uint32_t kstep, vstep;  // bytes per row
+  __device__ __forceinline__ void init(const uint16_t* __restrict__ kb, Strides ks,
+                                       const uint16_t* __restrict__ vb, Strides vs, int n_rows) {
+    kstep = static_cast<uint32_t>(ks.s) * 2u;
+    vstep = static_cast<uint32_t>(vs.s) * 2u;
+    kr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(kb), 0,
+                                           static_cast<int>((n_rows - 1) * kstep + 2u * D), 0x00020000);
+    vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(vb), 0,
+                                           static_cast<int>((n_rows - 1) * vstep + 2u * D), 0x00020000);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      const int c = threadIdx.x + 256 * j;
-      const int which = c / (ROWS * CPR);
-      const int cc = c % (ROWS * CPR);
+      const int cc = threadIdx.x + 256 * (j % PER);
       const int rr = cc / CPR, d0 = (cc % CPR) * 8;
-      reg[j] = make_uint4(0, 0, 0, 0);
-      if (r0 + rr < n_rows) {
-        const uint16_t* src = which ? vb + static_cast<int64_t>(r0 + rr) * vs.s
-                                    : kb + static_cast<int64_t>(r0 + rr) * ks.s;
-        reg[j] = *reinterpret_cast<const uint4*>(src + d0);
-      }
+      voff[j] = static_cast<uint32_t>(rr) * (j < PER ? kstep : vstep) + 2u * d0;
+    }
+  }
+  __device__ __forceinline__ void fetch(int r0) {
+    const uint32_t ko = static_cast<uint32_t>(r0) * kstep, vo = static_cast<uint32_t>(r0) * vstep;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const auto t = __builtin_amdgcn_raw_buffer_load_b128(j < PER ? kr : vr,
+                                                           voff[j] + (j < PER ? ko : vo), 0, 0);
+      reg[j] = __builtin_bit_cast(uint4, t);
     }
   }
   __device__ __forceinline__ void store(uint16_t* Ks, uint16_t* Vs) const {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      const int c = threadIdx.x + 256 * j;
-      const int which = c / (ROWS * CPR);
-      const int cc = c % (ROWS * CPR);
+      const int cc = threadIdx.x + 256 * (j % PER);
       const int rr = cc / CPR, d0 = (cc % CPR) * 8;
-      *reinterpret_cast<uint4*>(which ? Vs + rr * (D + VPAD) + d0 : Ks + rr * (D + kPad) + d0) = reg[j];
+      *reinterpret_cast<uint4*>(j >= PER ? Vs + rr * (D + VPAD) + d0 : Ks + rr * (D + kPad) + d0) = reg[j];
     }
   }
 };
@@ -275,27 +288,29 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   const int tr_row = (r & 15) >> 2;
   const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
   KVPrefetch<D, KT, VPAD> pf;
-  pf.fetch(kb, ks, vb, vs, 0, Sk);
+  pf.init(kb, ks, vb, vs, Sk);
+  pf.fetch(0);
   for (int kt = 0; kt < k_end; kt += KT) {
     __syncthreads();
     pf.store(Ks, Vs);
     __syncthreads();
-    if (kt + KT < k_end) pf.fetch(kb, ks, vb, vs, kt + KT, Sk);
+    if (kt + KT < k_end) pf.fetch(kt + KT);
     if constexpr (PIPE) {
       // online softmax of one sub-tile's scores and O^T += V^T P^T
       auto softmax_pv = [&](f32x16 sc, const int sub, const int kb0, const bool need_mask) {
         // sc[i]: key = kb0 + (i&3) + 8(i>>2) + 4hf, query = my_q
         // row max on the RAW scores (scale > 0 commutes with max); the scale is folded into the
         // exponent's FMA below -- one VALU op per score instead of a multiply and a subtract
+        if (need_mask) {
+  #pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+            sc[i] = (key >= Sk || (CAUSAL && key > my_q)) ? -INFINITY : sc[i];
+          }
+        }
         float mx = -INFINITY;
   #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if (need_mask) {
-            const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-            if (key >= Sk || (CAUSAL && key > my_q)) sc[i] = -INFINITY;
-          }
-          mx = fmaxf(mx, sc[i]);
-        }
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[i]);
         mx = half_max(mx);
         // deferred max (T13): the running max m moves only when a score exceeds it by more than
         // kRescaleLog2 (p <= 2^kRescaleLog2 meanwhile: exact in the fp32 accumulators, 8 bits of
@@ -372,23 +387,31 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       const int kb0 = kt + 32 * sub;
       if (kb0 >= k_end) break;
       if (CAUSAL && kb0 > q0 + 31) break;  // wave-uniform: the rest of this tile is masked
+      // every K fragment read issued before the first MFMA: one LDS wait instead of one per MFMA
+      bf16x8 kf[D / 16];
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) kf[s] = load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf);
       f32x16 sc = zero16();
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s)
-        sc = mfma32(load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf), qf[s], sc);
+      for (int s = 0; s < D / 16; ++s) sc = mfma32(kf[s], qf[s], sc);
+      __builtin_amdgcn_sched_group_barrier(0x100, D / 16, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, D / 16, 0);
       // sc[i]: key = kb0 + (i&3) + 8(i>>2) + 4hf, query = my_q
       const bool need_mask = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0);
+      // one wave-uniform branch around the whole mask (selects, no per-score branches: written
+      // inside the max loop, the compiler emitted a scalar test + branch per score on every tile)
+      if (need_mask) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          sc[i] = (key >= Sk || (CAUSAL && key > my_q)) ? -INFINITY : sc[i];
+        }
+      }
       // row max on the RAW scores (scale > 0 commutes with max); the scale is folded into the
       // exponent's FMA below -- one VALU op per score instead of a multiply and a subtract
       float mx = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (need_mask) {
-          const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-          if (key >= Sk || (CAUSAL && key > my_q)) sc[i] = -INFINITY;
-        }
-        mx = fmaxf(mx, sc[i]);
-      }
+      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[i]);
       mx = half_max(mx);
       // deferred max (T13): the running max m moves only when a score exceeds it by more than
       // kRescaleLog2 (p <= 2^kRescaleLog2 meanwhile: exact in the fp32 accumulators, 8 bits of
@@ -516,12 +539,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
   const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
   KVPrefetch<D, KT> pf;
-  pf.fetch(kb, ks, vb, vs, 0, Sk);
+  pf.init(kb, ks, vb, vs, Sk);
+  pf.fetch(0);
   for (int kt = 0; kt < k_end; kt += KT) {
     __syncthreads();
     pf.store(Ks, Vs);
     __syncthreads();
-    if (kt + KT < k_end) pf.fetch(kb, ks, vb, vs, kt + KT, Sk);
+    if (kt + KT < k_end) pf.fetch(kt + KT);
     // S^T = K Q^T and dP^T = V dO^T for the 32-key sub-tile `sub` of the staged tile
     auto sdp = [&](const int sub, f32x16& sc, f32x16& dp) {
       sc = zero16();
@@ -656,20 +680,26 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   float pl = 0.f, pd = 0.f;
   constexpr bool ROWC = D == 128;
   const float inv_sl2 = 1.f / scale_log2;
-  auto fetch = [&](int qt) {
+  // Q / dO tiles through buffer descriptors ending after row Sq - 1: rows past it load as zeros
+  // (hardware range check; see KVPrefetch), 32-bit lane offsets computed once
+  constexpr int PER = NPF / 2;  // chunks per thread per tensor (j < PER: Q, else dO)
+  const uint32_t qstep = static_cast<uint32_t>(qs.s) * 2u, dstep = static_cast<uint32_t>(dos.s) * 2u;
+  const __amdgpu_buffer_rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(qb), 0, static_cast<int>((Sq - 1) * qstep + 2u * D), 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(dob), 0, static_cast<int>((Sq - 1) * dstep + 2u * D), 0x00020000);
+  uint32_t pvo[NPF];
 #pragma unroll
-    for (int j = 0; j < NPF; ++j) {
-      const int c = threadIdx.x + 256 * j;
-      const int which = c / (QT * CPR);  // 0: Q, 1: dO
-      const int cc = c % (QT * CPR);
-      const int rr = cc / CPR, d0 = (cc % CPR) * 8;
-      pf[j] = make_uint4(0, 0, 0, 0);
-      if (qt + rr < Sq) {
-        const uint16_t* src = which ? dob + static_cast<int64_t>(qt + rr) * dos.s
-                                    : qb + static_cast<int64_t>(qt + rr) * qs.s;
-        pf[j] = *reinterpret_cast<const uint4*>(src + d0);
-      }
-    }
+  for (int j = 0; j < NPF; ++j) {
+    const int cc = threadIdx.x + 256 * (j % PER);
+    pvo[j] = static_cast<uint32_t>(cc / CPR) * (j < PER ? qstep : dstep) + 2u * ((cc % CPR) * 8);
+  }
+  auto fetch = [&](int qt) {
+    const uint32_t qo = static_cast<uint32_t>(qt) * qstep, dof = static_cast<uint32_t>(qt) * dstep;
+#pragma unroll
+    for (int j = 0; j < NPF; ++j)
+      pf[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            j < PER ? qr : dr, pvo[j] + (j < PER ? qo : dof), 0, 0));
     if (threadIdx.x < QT) {
       const int qi = qt + threadIdx.x;
       if constexpr (ROWC) {
@@ -690,10 +720,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {
-      const int c = threadIdx.x + 256 * j;
-      const int which = c / (QT * CPR);
-      const int cc = c % (QT * CPR);
-      *reinterpret_cast<uint4*>((which ? dOs : Qs) + (cc / CPR) * RS + (cc % CPR) * 8) = pf[j];
+      const int cc = threadIdx.x + 256 * (j % PER);
+      *reinterpret_cast<uint4*>((j >= PER ? dOs : Qs) + (cc / CPR) * RS + (cc % CPR) * 8) = pf[j];
     }
     if (threadIdx.x < QT) {
       lse_s[threadIdx.x] = pl;
@@ -819,6 +847,15 @@ bool fwd_pipe() {
   return on;
 }
 
+// forward pipelining at D = 128 (DCA_ATTN_FWD_PIPE128=1, opt-in until measured)
+bool fwd_pipe128() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCA_ATTN_FWD_PIPE128");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
 // dQ kernel (D = 64): issue a sub-tile pair's S / dP products before their softmax gradients
 // (DCA_ATTN_DQ_PIPE=1)
 bool dq_pipe() {
@@ -874,12 +911,15 @@ void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
                          scale_log2, attn_order(C), kvlen);
     };
     const bool ms = fwd_msum();
-    if constexpr (D == 64) {  // D = 128 with two live score tiles spills
-      if (fwd_pipe()) {
+    // D = 128: the pipelined form fits without spills only without MSUM (246 VGPRs)
+    if (fwd_pipe() && (D == 64 || (!ms && fwd_pipe128()))) {
+      if constexpr (D == 64) {
         if (ms) launch(attn_fwd_kernel<D, C, KT, true, true>);
         else launch(attn_fwd_kernel<D, C, KT, true>);
-        return;
+      } else {
+        launch(attn_fwd_kernel<D, C, KT, true>);
       }
+      return;
     }
     if (ms) launch(attn_fwd_kernel<D, C, KT, false, true>);
     else launch(attn_fwd_kernel<D, C, KT, false>);

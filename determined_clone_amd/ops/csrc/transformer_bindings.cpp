@@ -204,6 +204,13 @@ AttnStrides bshd_strides(const Tensor& t, const char* name) {
   return {{t.stride(0), t.stride(2), t.stride(1)}};
 }
 
+// K / V (and, in the backward, Q / dO) tiles load through buffer descriptors with 32-bit byte
+// offsets (attention.hip KVPrefetch): one (batch, head) slice must span < 2 GiB
+void check_range(const Tensor& t, const char* name) {
+  TORCH_CHECK((t.size(1) + 256) * t.stride(1) * 2 < (int64_t(1) << 31),
+              "attention: a (batch, head) slice of ", name, " must span < 2 GiB (sequence x row stride)");
+}
+
 // kv_len: optional int32 [B] valid key count per batch row (right padding, e.g. an HF
 // attention_mask); keys at or past it get zero weight and zero dK/dV
 const int* kvlen_ptr(const OptT& kv_len, int B) {
@@ -225,6 +232,8 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
               "attention: k/v shape mismatch");
   TORCH_CHECK(!causal || Sq == Sk, "attention: causal requires Sq == Sk");
   auto qs = bshd_strides(q, "q"), ks = bshd_strides(k, "k"), vs = bshd_strides(v, "v");
+  check_range(k, "k");
+  check_range(v, "v");
   Tensor o = torch::empty({B, Sq, H, D}, q.options());
   Tensor lse = torch::empty({B, H, Sq}, q.options().dtype(at::kFloat));
   auto os = bshd_strides(o, "o");
@@ -244,6 +253,7 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   Tensor dO = dout.stride(3) == 1 ? dout : dout.contiguous();
   auto qs = bshd_strides(q, "q"), ks = bshd_strides(k, "k"), vs = bshd_strides(v, "v");
   auto os = bshd_strides(o, "o"), dos = bshd_strides(dO, "dout");
+  for (const Tensor* t : {&q, &k, &v, &dO}) check_range(*t, "q/k/v/dout");
   TORCH_CHECK(lse.is_contiguous() && lse.numel() == static_cast<int64_t>(B) * H * Sq, "attention: lse");
   // optional preallocated outputs (e.g. views into one packed dQKV buffer)
   Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({B, Sq, H, D}, q.options());
