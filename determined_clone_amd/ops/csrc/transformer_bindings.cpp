@@ -253,7 +253,7 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   Tensor dO = dout.stride(3) == 1 ? dout : dout.contiguous();
   auto qs = bshd_strides(q, "q"), ks = bshd_strides(k, "k"), vs = bshd_strides(v, "v");
   auto os = bshd_strides(o, "o"), dos = bshd_strides(dO, "dout");
-  for (const Tensor* t : {&q, &k, &v, &dO}) check_range(*t, "q/k/v/dout");
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&q, &k, &v, &dO}) check_range(*t, "q/k/v/dout");
   TORCH_CHECK(lse.is_contiguous() && lse.numel() == static_cast<int64_t>(B) * H * Sq, "attention: lse");
   // optional preallocated outputs (e.g. views into one packed dQKV buffer)
   Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({B, Sq, H, D}, q.options());
