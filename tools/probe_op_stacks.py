@@ -39,7 +39,7 @@ def main() -> None:
         def train_batch(self, batch, epoch_idx, batch_idx):
             if batch_idx == 3:
                 torch.cuda.synchronize()
-                self.prof = profile(activities=[ProfilerActivity.CPU], with_stack=True)
+                self.prof = profile(activities=[ProfilerActivity.CPU], with_stack=True, record_shapes=True)
                 self.prof.__enter__()
             x, y = batch
             loss = F.cross_entropy(self.model(x).float(), y)
@@ -53,8 +53,15 @@ def main() -> None:
                     if ev.name == a.op:
                         st = [s for s in (ev.stack or []) if "determined_clone_amd" in s or "bench" in s
                               or "torch/autograd" in s or "torch/nn" in s][:6]
-                        stacks[" <- ".join(st) or "(no python frame)"] += 1
-                for st, c in stacks.most_common(20):
+                        # enclosing ops (e.g. autograd::engine::evaluate_function: XBackward) and
+                        # the filled tensor's shape: identifies callers without a Python frame
+                        par, chain = ev.cpu_parent, []
+                        while par is not None and len(chain) < 4:
+                            chain.append(par.name)
+                            par = par.cpu_parent
+                        shp = str(ev.input_shapes[0]) if ev.input_shapes else "?"
+                        stacks[" <- ".join(st or chain) + f"  shape={shp}"] += 1
+                for st, c in stacks.most_common(30):
                     print(f"{c / a.steps:6.1f}/step  {st}", flush=True)
             return {"loss": loss}
 
