@@ -246,7 +246,7 @@ template <int D, bool CAUSAL, int KT, bool PIPE, bool MSUM = false>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
-    Strides ks, Strides vs, Strides os, float scale_log2, int order, const int* __restrict__ kvlen) {
+    Strides ks, Strides vs, Strides os, float scale_log2, int order, const int* __restrict__ kvlen, int G) {
   // KT = keys per LDS tile (one barrier pair per tile), consumed in 32-key MFMA sub-tiles
   constexpr int QB = 128;      // queries per workgroup
   constexpr int RS = D + kPad; // LDS row stride (elements)
@@ -270,8 +270,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   const int q0 = q_blk + w * 32;
   const int my_q = q0 + r;
   const uint16_t* qb = q + b * qs.b + h * qs.h;
-  const uint16_t* kb = k + b * ks.b + h * ks.h;
-  const uint16_t* vb = v + b * vs.b + h * vs.h;
+  // grouped-query attention: G consecutive query heads share K/V head h / G
+  const uint16_t* kb = k + b * ks.b + (h / G) * ks.h;
+  const uint16_t* vb = v + b * vs.b + (h / G) * vs.h;
 
   bf16x8 qf[D / 16];
 #pragma unroll
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const uint16_t* __restrict__ o, const uint16_t* __restrict__ dO, const float* __restrict__ lse,
     float* __restrict__ delta, uint16_t* __restrict__ dq, int Sq, int Sk, int H, Strides qs,
     Strides ks, Strides vs, Strides os, Strides dos, Strides dqs, float scale_log2, float scale,
-    int order, const int* __restrict__ kvlen) {
+    int order, const int* __restrict__ kvlen, int G) {
   // KT = keys per LDS tile (one barrier pair per tile), consumed in 32-key MFMA sub-tiles
   constexpr int QB = 128;
   constexpr int RS = D + kPad;
@@ -512,8 +513,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   const int q0 = q_blk + w * 32;
   const int my_q = q0 + r;
   const bool q_ok = my_q < Sq;
-  const uint16_t* kb = k + b * ks.b + h * ks.h;
-  const uint16_t* vb = v + b * vs.b + h * vs.h;
+  const uint16_t* kb = k + b * ks.b + (h / G) * ks.h;  // grouped-query: K/V head h / G
+  const uint16_t* vb = v + b * vs.b + (h / G) * vs.h;
   const int64_t bh = static_cast<int64_t>(b) * H + h;
 
   bf16x8 qf[D / 16], dof[D / 16];
@@ -634,7 +635,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     const uint16_t* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
     uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int Sq, int Sk, int H, Strides qs,
     Strides ks, Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale,
-    int order, const int* __restrict__ kvlen) {
+    int order, const int* __restrict__ kvlen, int G) {
   constexpr int KB = 128;
   static_assert(QT == 32 || QT == 64, "query tile");
   constexpr int RS = D + kPad;
@@ -658,9 +659,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   const int k_blk = blk.x * KB;
   const int kw0 = k_blk + 32 * w;
   const int my_key = kw0 + r;
-  const uint16_t* qb = q + b * qs.b + h * qs.h;
-  const uint16_t* dob = dO + b * dos.b + h * dos.h;
-  const int64_t bh = static_cast<int64_t>(b) * H + h;
+  // h is the K/V head (grid y runs over H / G of them); its G query heads h*G .. h*G+G-1 are swept
+  // one after another below, dK / dV summing over all of them in the same registers
+  const uint16_t* qb = q;
+  const uint16_t* dob = dO;
+  int64_t bh = 0;
 
   bf16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
@@ -684,10 +687,18 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   // (hardware range check; see KVPrefetch), 32-bit lane offsets computed once
   constexpr int PER = NPF / 2;  // chunks per thread per tensor (j < PER: Q, else dO)
   const uint32_t qstep = static_cast<uint32_t>(qs.s) * 2u, dstep = static_cast<uint32_t>(dos.s) * 2u;
-  const __amdgpu_buffer_rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc(
+  __amdgpu_buffer_rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(qb), 0, static_cast<int>((Sq - 1) * qstep + 2u * D), 0x00020000);
-  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(dob), 0, static_cast<int>((Sq - 1) * dstep + 2u * D), 0x00020000);
+  __amdgpu_buffer_rsrc_t dr = qr;
+  auto set_head = [&](int hq) {
+    qb = q + b * qs.b + hq * qs.h;
+    dob = dO + b * dos.b + hq * dos.h;
+    bh = static_cast<int64_t>(b) * H + hq;
+    qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(qb), 0,
+                                           static_cast<int>((Sq - 1) * qstep + 2u * D), 0x00020000);
+    dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(dob), 0,
+                                           static_cast<int>((Sq - 1) * dstep + 2u * D), 0x00020000);
+  };
   uint32_t pvo[NPF];
 #pragma unroll
   for (int j = 0; j < NPF; ++j) {
@@ -715,6 +726,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   const int tr_row = (r & 15) >> 2;
   const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
   const int q_start = CAUSAL ? (k_blk / QT) * QT : 0;
+  for (int g = 0; g < G; ++g) {
+  set_head(h * G + g);
   if (q_start < Sq) fetch(q_start);
   for (int qt = q_start; qt < Sq; qt += QT) {
     __syncthreads();
@@ -806,6 +819,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
         tile(std::false_type{}, half);
     }
   }
+  }  // query heads of this K/V head
   store_rows<D>(dk + b * dks.b + h * dks.h + static_cast<int64_t>(my_key) * dks.s, dkacc, scale, hf, my_key < SkT);
   store_rows<D>(dv + b * dvs.b + h * dvs.h + static_cast<int64_t>(my_key) * dvs.s, dvacc, 1.f, hf, my_key < SkT);
 }
@@ -899,7 +913,7 @@ int dkdv_qt() {
 template <int D, bool C>
 void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse,
                 int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs, Strides os,
-                float scale_log2, const int* kvlen, hipStream_t st) {
+                float scale_log2, const int* kvlen, int G, hipStream_t st) {
   dim3 grid((Sq + 127) / 128, H, B);
   auto go = [&](auto ktag) {
     constexpr int KT = decltype(ktag)::value;
@@ -908,7 +922,7 @@ void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
       hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
-                         scale_log2, attn_order(C), kvlen);
+                         scale_log2, attn_order(C), kvlen, G);
     };
     const bool ms = fwd_msum();
     // D = 128: the pipelined form fits without spills only without MSUM (246 VGPRs)
@@ -938,12 +952,12 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
                 const uint16_t* dO, const float* lse, float* delta, uint16_t* dq, uint16_t* dk,
                 uint16_t* dv, int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs,
                 Strides os, Strides dos, Strides dqs, Strides dks, Strides dvs, float scale_log2,
-                float scale, const int* kvlen, hipStream_t st) {
+                float scale, const int* kvlen, int G, hipStream_t st) {
   auto dq_go = [&](auto kern, size_t l1) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l1));
     hipLaunchKernelGGL(kern, dim3((Sq + 127) / 128, H, B), dim3(256), l1, st, q, k, v, o, dO, lse,
-                       delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2, scale, attn_order(C), kvlen);
+                       delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2, scale, attn_order(C), kvlen, G);
   };
   bool dq_done = false;
   if constexpr (D == 64) {
@@ -957,13 +971,13 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
   }
   if (!dq_done) dq_go(attn_bwd_dq_kernel<D, C, 64, false>, bwd_dq_lds(D, 64));
   if (dkdv_qt() == 64) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H, B), dim3(256),
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H / G, B), dim3(256),
                        bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
-                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen);
+                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen, G);
   } else {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 32>), dim3((Sk + 127) / 128, H, B), dim3(256),
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 32>), dim3((Sk + 127) / 128, H / G, B), dim3(256),
                        bwd_dkdv_lds(D, 32), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
-                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen);
+                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen, G);
   }
 }
 
@@ -971,7 +985,8 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
 
 void attention_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H,
                    int Sq, int Sk, int D, const int64_t* qs, const int64_t* ks, const int64_t* vs,
-                   const int64_t* os, float scale, bool causal, const int* kvlen, hipStream_t st) {
+                   const int64_t* os, float scale, bool causal, const int* kvlen, int G,
+                   hipStream_t st) {
   const float sl2 = scale * 1.4426950408889634f;
   Strides a{qs[0], qs[1], qs[2]}, bb{ks[0], ks[1], ks[2]}, c{vs[0], vs[1], vs[2]}, d{os[0], os[1], os[2]};
   auto Q = static_cast<const uint16_t*>(q);
@@ -979,11 +994,11 @@ void attention_fwd(const void* q, const void* k, const void* v, void* o, float* 
   auto V = static_cast<const uint16_t*>(v);
   auto O = static_cast<uint16_t*>(o);
   if (D == 64) {
-    if (causal) launch_fwd<64, true>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, st);
-    else launch_fwd<64, false>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, st);
+    if (causal) launch_fwd<64, true>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, G, st);
+    else launch_fwd<64, false>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, G, st);
   } else {
-    if (causal) launch_fwd<128, true>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, st);
-    else launch_fwd<128, false>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, st);
+    if (causal) launch_fwd<128, true>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, G, st);
+    else launch_fwd<128, false>(Q, K, V, O, lse, B, H, Sq, Sk, a, bb, c, d, sl2, kvlen, G, st);
   }
 }
 
@@ -992,17 +1007,17 @@ void attention_bwd(const void* q, const void* k, const void* v, const void* o, c
                    int B, int H, int Sq, int Sk, int D, const int64_t* st_q, const int64_t* st_k,
                    const int64_t* st_v, const int64_t* st_o, const int64_t* st_do,
                    const int64_t* st_dq, const int64_t* st_dk, const int64_t* st_dv, float scale,
-                   bool causal, const int* kvlen, hipStream_t stream) {
+                   bool causal, const int* kvlen, int G, hipStream_t stream) {
   const float sl2 = scale * 1.4426950408889634f;
   auto S = [](const int64_t* p) { return Strides{p[0], p[1], p[2]}; };
   auto c16 = [](const void* p) { return static_cast<const uint16_t*>(p); };
   auto m16 = [](void* p) { return static_cast<uint16_t*>(p); };
   if (D == 64) {
-    if (causal) launch_bwd<64, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, stream);
-    else launch_bwd<64, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, stream);
+    if (causal) launch_bwd<64, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, G, stream);
+    else launch_bwd<64, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, G, stream);
   } else {
-    if (causal) launch_bwd<128, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, stream);
-    else launch_bwd<128, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, stream);
+    if (causal) launch_bwd<128, true>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, G, stream);
+    else launch_bwd<128, false>(c16(q), c16(k), c16(v), c16(o), c16(dO), lse, delta, m16(dq), m16(dk), m16(dv), B, H, Sq, Sk, S(st_q), S(st_k), S(st_v), S(st_o), S(st_do), S(st_dq), S(st_dk), S(st_dv), sl2, scale, kvlen, G, stream);
   }
 }
 

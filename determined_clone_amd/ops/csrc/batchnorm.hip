@@ -65,6 +65,21 @@ inline RowGeom row_geom(int C) {
 using ReduceGeom = RowGeom;
 inline ReduceGeom reduce_geom(int C) { return row_geom(C); }
 
+// Apply-pass block -> (channel group, row chunk). With more channel groups than one (C > 8 * tpr)
+// the launcher may use a flat grid (gridDim.y == 1) whose FASTEST index is the channel group, so
+// the blocks that share a row range -- together covering whole rows -- run together and each row's
+// bytes are streamed at once, instead of one channel slice of every row per pass over the tensor
+// (blockIdx.y slowest). DCA_BN_APPLY_FLAT=0 keeps the 2-D grid.
+struct BlkMap {
+  int cg, bx, nb;
+};
+__device__ __forceinline__ BlkMap apply_block_map(int C, int tpr) {
+  if (gridDim.y > 1) return {static_cast<int>(blockIdx.y), static_cast<int>(blockIdx.x), static_cast<int>(gridDim.x)};
+  const int ncg = (C / 8 + tpr - 1) / tpr;
+  return {static_cast<int>(blockIdx.x) % ncg, static_cast<int>(blockIdx.x) / ncg,
+          static_cast<int>(gridDim.x) / ncg};
+}
+
 struct RowRange {
   int64_t begin, end;
 };
@@ -294,9 +309,10 @@ __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
     int rpi, bool relu, uint8_t* __restrict__ mask) {
   const int tid = threadIdx.x;
   const int lc = tid % tpr, r0 = tid / tpr;
-  const int c = (blockIdx.y * tpr + lc) * 8;
+  const BlkMap bm = apply_block_map(C, tpr);
+  const int c = (bm.cg * tpr + lc) * 8;
   if (c >= C) return;
-  const RowRange rr = chunk_rows(M, rpi, blockIdx.x, gridDim.x);
+  const RowRange rr = chunk_rows(M, rpi, bm.bx, bm.nb);
   float a[8], b[8];
   {
     const float4 a0 = *reinterpret_cast<const float4*>(scale + c);
@@ -368,9 +384,10 @@ __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
     void* __restrict__ dres, int64_t M, int C, int tpr, int rpi, bool relu) {
   const int tid = threadIdx.x;
   const int lc = tid % tpr, r0 = tid / tpr;
-  const int c = (blockIdx.y * tpr + lc) * 8;
+  const BlkMap bm = apply_block_map(C, tpr);
+  const int c = (bm.cg * tpr + lc) * 8;
   if (c >= C) return;
-  const RowRange rr = chunk_rows(M, rpi, blockIdx.x, gridDim.x);
+  const RowRange rr = chunk_rows(M, rpi, bm.bx, bm.nb);
   float k1[8], k2[8], k3[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { k1[k] = coef[c + k]; k2[k] = coef[C + c + k]; k3[k] = coef[2 * C + c + k]; }
@@ -498,6 +515,17 @@ inline int apply_blocks(int64_t M, const RowGeom& g, const ApplyTuning& t) {
   return static_cast<int>(b);
 }
 
+inline dim3 apply_grid(int64_t M, const RowGeom& g, const ApplyTuning& t) {
+  static const bool flat = [] {
+    const char* e = std::getenv("DCA_BN_APPLY_FLAT");
+    return !(e && std::atoi(e) == 0);
+  }();
+  const int bx = apply_blocks(M, g, t);
+  if (flat && g.cgroups > 1 && static_cast<int64_t>(bx) * g.cgroups < (int64_t{1} << 31))
+    return dim3(bx * g.cgroups, 1);  // see apply_block_map
+  return dim3(bx, g.cgroups);
+}
+
 // Reduce-pass variant: the statistics passes stream with NONTEMPORAL loads by default (-3% on
 // the bs-1024 ResNet-50 BN shapes, fwd+bwd 32.3 -> 31.4 ms per step in tools/bench_bn.py,
 // profiles/round4_bn_reduce_nt_ab.txt). DCA_BN_REDUCE_VAR="U_bwd,nt" (A/B sweeps only): rows in
@@ -547,7 +575,7 @@ void launch_apply_fwd(const void* x, const void* res, void* y, const float* scal
                       hipStream_t st) {
   const RowGeom g = row_geom(C);
   const ApplyTuning t = apply_tuning(M * C);
-  dim3 grid(apply_blocks(M, g, t), g.cgroups);
+  const dim3 grid = apply_grid(M, g, t);
   switch (t.u) {
     case 2: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, 2>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
     case 8: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, 8>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
@@ -561,7 +589,7 @@ void launch_apply_bwd(const void* dy, const void* dy2, const uint8_t* mask, cons
                       hipStream_t st) {
   const RowGeom g = row_geom(C);
   const ApplyTuning t = apply_tuning(M * C);
-  dim3 grid(apply_blocks(M, g, t), g.cgroups);
+  const dim3 grid = apply_grid(M, g, t);
   switch (t.u) {
     case 2: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 2>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
     case 8: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 8>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
@@ -730,9 +758,10 @@ __global__ __launch_bounds__(kBlock) void bn_pool_apply_bwd_kernel(
     PoolGeom g) {
   const int tid = threadIdx.x;
   const int lc = tid % tpr, r0 = tid / tpr;
-  const int c = (blockIdx.y * tpr + lc) * 8;
+  const BlkMap bm = apply_block_map(C, tpr);
+  const int c = (bm.cg * tpr + lc) * 8;
   if (c >= C) return;
-  const RowRange rr = chunk_rows(M, rpi, blockIdx.x, gridDim.x);
+  const RowRange rr = chunk_rows(M, rpi, bm.bx, bm.nb);
   float k1[8], k2[8], k3[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { k1[k] = coef[c + k]; k2[k] = coef[C + c + k]; k3[k] = coef[2 * C + c + k]; }

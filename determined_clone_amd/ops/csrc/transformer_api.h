@@ -42,14 +42,14 @@ void rope(TDtype dt, const void* x, void* y, const float* cosT, const float* sin
           int H, int S, int D, int rot, bool backward, hipStream_t st);
 void attention_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int H,
                    int Sq, int Sk, int D, const int64_t* qs, const int64_t* ks, const int64_t* vs,
-                   const int64_t* os, float scale, bool causal, const int* kvlen,
+                   const int64_t* os, float scale, bool causal, const int* kvlen, int G,
                    hipStream_t st);
 void attention_bwd(const void* q, const void* k, const void* v, const void* o, const void* dO,
                    const float* lse, float* delta, float* dq_acc, void* dq, void* dk, void* dv,
                    int B, int H, int Sq, int Sk, int D, const int64_t* st_q, const int64_t* st_k,
                    const int64_t* st_v, const int64_t* st_o, const int64_t* st_do,
                    const int64_t* st_dq, const int64_t* st_dk, const int64_t* st_dv, float scale,
-                   bool causal, const int* kvlen, hipStream_t stream);
+                   bool causal, const int* kvlen, int G, hipStream_t stream);
 void cross_entropy_fwd(TDtype dt, const void* logits, const int64_t* target, float* lse,
                        float* loss, int64_t rows, int V, int64_t ignore_index, hipStream_t st);
 void cross_entropy_bwd(TDtype dt, const void* logits, const int64_t* target, const float* lse,

@@ -228,8 +228,9 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
   const int Sk = k.size(1);
   TORCH_CHECK(D == 64 || D == 128, "attention: head dim must be 64 or 128");
-  TORCH_CHECK(k.size(0) == B && k.size(2) == H && k.size(3) == D && v.sizes() == k.sizes(),
-              "attention: k/v shape mismatch");
+  const int Hkv = k.size(2);  // grouped-query attention: H % Hkv == 0 query heads per K/V head
+  TORCH_CHECK(k.size(0) == B && Hkv > 0 && H % Hkv == 0 && k.size(3) == D && v.sizes() == k.sizes(),
+              "attention: k/v shape mismatch (K/V heads must divide the query heads)");
   TORCH_CHECK(!causal || Sq == Sk, "attention: causal requires Sq == Sk");
   auto qs = bshd_strides(q, "q"), ks = bshd_strides(k, "k"), vs = bshd_strides(v, "v");
   check_range(k, "k");
@@ -239,7 +240,7 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   auto os = bshd_strides(o, "o");
   dca::attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
                      B, H, Sq, Sk, D, qs.v, ks.v, vs.v, os.v, static_cast<float>(scale), causal,
-                     kvlen_ptr(kv_len, B), stream());
+                     kvlen_ptr(kv_len, B), H / Hkv, stream());
   return {o, lse};
 }
 
@@ -250,6 +251,8 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   const c10::DeviceGuard g(q.device());
   const int B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3);
   const int Sk = k.size(1);
+  const int Hkv = k.size(2);
+  TORCH_CHECK(Hkv > 0 && H % Hkv == 0 && v.sizes() == k.sizes(), "attention: k/v heads must divide q heads");
   Tensor dO = dout.stride(3) == 1 ? dout : dout.contiguous();
   auto qs = bshd_strides(q, "q"), ks = bshd_strides(k, "k"), vs = bshd_strides(v, "v");
   auto os = bshd_strides(o, "o"), dos = bshd_strides(dO, "dout");
@@ -257,8 +260,8 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   TORCH_CHECK(lse.is_contiguous() && lse.numel() == static_cast<int64_t>(B) * H * Sq, "attention: lse");
   // optional preallocated outputs (e.g. views into one packed dQKV buffer)
   Tensor dq = dq_out.has_value() ? *dq_out : torch::empty({B, Sq, H, D}, q.options());
-  Tensor dk = dk_out.has_value() ? *dk_out : torch::empty({B, Sk, H, D}, q.options());
-  Tensor dv = dv_out.has_value() ? *dv_out : torch::empty({B, Sk, H, D}, q.options());
+  Tensor dk = dk_out.has_value() ? *dk_out : torch::empty({B, Sk, Hkv, D}, q.options());
+  Tensor dv = dv_out.has_value() ? *dv_out : torch::empty({B, Sk, Hkv, D}, q.options());
   TORCH_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(),
               "attention: gradient output shape mismatch");
   auto fo = q.options().dtype(at::kFloat);
@@ -268,7 +271,7 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
                      lse.data_ptr<float>(), delta.data_ptr<float>(), nullptr,
                      dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B, H, Sq, Sk, D, qs.v, ks.v, vs.v,
                      os.v, dos.v, dqs.v, dks.v, dvs.v, static_cast<float>(scale), causal,
-                     kvlen_ptr(kv_len, B), stream());
+                     kvlen_ptr(kv_len, B), H / Hkv, stream());
   return {dq, dk, dv};
 }
 // logits [N, V] contiguous, target [N] int64 -> (lse [N], per-row loss [N])

@@ -57,9 +57,13 @@ def reference_rope(x, cos, sin, rot_dim: Optional[int] = None):
 
 
 def reference_attention(q, k, v, causal=True, scale=None, key_lengths=None):
-    """q/k/v [B, S, H, D] -> [B, S, H, D] (fp32 math). ``key_lengths`` [B]: keys at or past it
-    are masked (right padding), clamped to at least one key like the kernels."""
+    """q [B, S, H, D], k/v [B, Sk, Hkv, D] with Hkv dividing H (grouped-query attention: query
+    head h reads K/V head h // (H / Hkv)) -> [B, S, H, D] (fp32 math). ``key_lengths`` [B]: keys
+    at or past it are masked (right padding), clamped to at least one key like the kernels."""
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if k.shape[2] != q.shape[2]:
+        g = q.shape[2] // k.shape[2]
+        k, v = k.repeat_interleave(g, dim=2), v.repeat_interleave(g, dim=2)
     qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
     s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
     if causal:
@@ -375,6 +379,8 @@ def flash_attention_qkvpacked(qkv: torch.Tensor, causal: bool = True,
 def _attn_gpu_ok(q, k, v) -> bool:
     if not (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128)):
         return False
+    if k.shape != v.shape or k.shape[2] == 0 or q.shape[2] % k.shape[2]:
+        return False
     for t in (q, k, v):
         if t.stride(-1) != 1 or any(s % 8 for s in t.stride()[:3]) or t.data_ptr() % 16:
             return False
@@ -385,7 +391,9 @@ def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: b
                     scale: Optional[float] = None,
                     key_lengths: Optional[torch.Tensor] = None) -> torch.Tensor:
     """softmax(q k^T * scale [+ causal mask] [+ key padding]) v for [B, S, H, Dh] operands (Dh in
-    {64, 128}, bf16 on GPU). Never materialises the S x S score matrix. ``key_lengths`` [B]
+    {64, 128}, bf16 on GPU). k / v may have fewer heads Hkv dividing H (grouped-query / multi-query
+    attention: H / Hkv consecutive query heads share a K/V head; dK / dV sum over the group inside
+    the kernel). Never materialises the S x S score matrix. ``key_lengths`` [B]
     (any integer dtype) is the number of valid keys per batch row -- right-padded batches such as
     an HF ``attention_mask``; padded keys get zero weight and zero dK/dV, and every query row
     (padded ones too) attends to the valid keys, as with an additive padding mask."""
@@ -393,8 +401,8 @@ def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: b
     if not q.is_cuda:
         return reference_attention(q, k, v, causal, scale, key_lengths)
     if not _attn_gpu_ok(q, k, v):
-        raise ValueError("flash_attention: GPU path needs bf16 [B,S,H,D] with D in {64,128} and "
-                         "16-byte aligned rows")
+        raise ValueError("flash_attention: GPU path needs bf16 [B,S,H,D] with D in {64,128}, "
+                         "K/V heads dividing the query heads and 16-byte aligned rows")
     return _FlashAttention.apply(q, k, v, causal, float(scale), _kv_len(key_lengths, q.shape[0], q.device))
 
 

@@ -61,7 +61,7 @@ def flash_attention_forward(module: torch.nn.Module, query: torch.Tensor, key: t
     causal = bool(kwargs.get("is_causal", getattr(module, "is_causal", False)))
     Sq, Sk = query.shape[2], key.shape[2]
     usable = (query.is_cuda and query.dtype == torch.bfloat16 and query.shape[-1] in (64, 128)
-              and key.shape[1] == query.shape[1] and not (dropout > 0 and module.training)
+              and query.shape[1] % key.shape[1] == 0 and not (dropout > 0 and module.training)
               and (not causal or Sq == Sk))
     kv_len = None
     if usable and attention_mask is not None:

@@ -92,3 +92,17 @@ def test_hf_bert_on_cpu_falls_back_to_sdpa():
     with torch.no_grad():
         torch.testing.assert_close(b(input_ids=ids, attention_mask=mask).last_hidden_state,
                                    a(input_ids=ids, attention_mask=mask).last_hidden_state)
+
+
+def test_reference_attention_grouped_query_matches_sdpa_gqa():
+    """K/V with fewer heads (GQA / MQA): query head h reads K/V head h // (H / Hkv)."""
+    torch.manual_seed(12)
+    B, S, H, Hkv, D = 2, 9, 6, 2, 8
+    q = torch.randn(B, S, H, D)
+    k, v = (torch.randn(B, S, Hkv, D) for _ in range(2))
+    for causal in (True, False):
+        o = T.flash_attention(q, k, v, causal=causal)
+        ref = F.scaled_dot_product_attention(
+            q.transpose(1, 2), k.repeat_interleave(H // Hkv, 2).transpose(1, 2),
+            v.repeat_interleave(H // Hkv, 2).transpose(1, 2), is_causal=causal).transpose(1, 2)
+        torch.testing.assert_close(o, ref, atol=1e-5, rtol=1e-5)

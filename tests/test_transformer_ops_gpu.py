@@ -147,6 +147,33 @@ def test_flash_attention_key_padding(D, causal, Sq, Sk):
             assert qs[2].grad[b_, L:].abs().max().item() == 0
 
 
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("H,Hkv", [(8, 2), (6, 1), (4, 4)])
+def test_flash_attention_grouped_query(D, causal, H, Hkv):
+    """Grouped-query / multi-query attention: K/V with Hkv heads shared by H / Hkv query heads
+    each; dK / dV are the sums over each group (fp32 reference through repeat_interleave)."""
+    _C()
+    torch.manual_seed(8)
+    B, S = 2, 300
+    lens = torch.tensor([S, 131], device="cuda")
+    q = torch.randn(B, S, H, D, device="cuda").bfloat16()
+    k, v = (torch.randn(B, S, Hkv, D, device="cuda").bfloat16() for _ in range(2))
+    qs = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    qr = [t.float().clone().requires_grad_(True) for t in (q, k, v)]
+    o = T.flash_attention(*qs, causal=causal, key_lengths=lens)
+    o2 = T.reference_attention(*qr, causal=causal, key_lengths=lens)
+    assert o.shape == (B, S, H, D)
+    assert _rel(o, o2) < 1e-2, _rel(o, o2)
+    g = torch.randn_like(o2)
+    o.backward(g.bfloat16())
+    o2.backward(g)
+    for a, b in zip(qs, qr):
+        assert a.grad.shape == b.grad.shape
+        assert _rel(a.grad, b.grad) < 2e-2, _rel(a.grad, b.grad)
+    assert qs[1].grad[1, 131:].abs().max().item() == 0
+
+
 def test_flash_attention_key_padding_qkvpacked():
     _C()
     torch.manual_seed(7)
@@ -163,8 +190,8 @@ def test_flash_attention_key_padding_qkvpacked():
     assert _rel(qkv.grad, qkv2.grad) < 2e-2
 
 
-@pytest.mark.parametrize("family", ["bert", "vit"])
-def test_hf_models_on_flash_attention_match_sdpa(family):
+@pytest.mark.parametrize("family", ["bert", "vit", "llama_gqa"])
+def test_hf_models_on_flash_attention_match_sdpa(family, monkeypatch):
     """HF BERT with a right-padded attention_mask and ViT (S = 197, no mask) on the
     ``dca_mfma`` attention backend agree with HF's own SDPA path, forward and backward."""
     transformers = pytest.importorskip("transformers")
@@ -180,6 +207,14 @@ def test_hf_models_on_flash_attention_match_sdpa(family):
         ids = torch.randint(1, 1000, (3, 96), device="cuda")
         mask = (torch.arange(96, device="cuda")[None] < torch.tensor([96, 40, 7], device="cuda")[:, None]).long()
         inputs = {"input_ids": ids, "attention_mask": mask}
+    elif family == "llama_gqa":  # causal, grouped-query K/V (2 K/V heads for 4 query heads)
+        cfg = transformers.LlamaConfig(vocab_size=1000, hidden_size=256, num_hidden_layers=2,
+                                       num_attention_heads=4, num_key_value_heads=2,
+                                       intermediate_size=512, max_position_embeddings=256)
+        make = transformers.LlamaModel
+        ids = torch.randint(1, 1000, (3, 96), device="cuda")
+        mask = (torch.arange(96, device="cuda")[None] < torch.tensor([96, 40, 7], device="cuda")[:, None]).long()
+        inputs = {"input_ids": ids, "attention_mask": mask}
     else:
         cfg = transformers.ViTConfig(image_size=224, patch_size=16, hidden_size=256, num_hidden_layers=2,
                                      num_attention_heads=4, intermediate_size=512,
@@ -192,6 +227,9 @@ def test_hf_models_on_flash_attention_match_sdpa(family):
     ours.load_state_dict(ref.state_dict())
     ref.set_attn_implementation("sdpa")
     use_flash_attention(ours)
+    calls = []
+    orig = T.flash_attention
+    monkeypatch.setattr(T, "flash_attention", lambda *a, **k: calls.append(a[1].shape) or orig(*a, **k))
     outs = []
     for m in (ref, ours):
         h = m(**inputs).last_hidden_state
@@ -201,6 +239,9 @@ def test_hf_models_on_flash_attention_match_sdpa(family):
         outs.append((h.float() * keep, wq.grad.float()))
     assert _rel(outs[1][0], outs[0][0]) < 2e-2
     assert _rel(outs[1][1], outs[0][1]) < 5e-2
+    assert len(calls) == cfg.num_hidden_layers  # every layer ran on the MFMA kernels (no SDPA fallback)
+    if family == "llama_gqa":
+        assert calls[0][2] == 2  # K/V passed with their own 2 heads (no repeat)
 
 
 def test_flash_attention_strided_qkv_slices():
