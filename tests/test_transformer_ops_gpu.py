@@ -1,5 +1,6 @@
 """Numerics of the transformer HIP kernels (LayerNorm, bias+GELU, RoPE, MFMA flash attention)
 against plain PyTorch fp32 references (run on an MI355X)."""
+import copy
 import math
 
 import pytest
@@ -222,8 +223,10 @@ def test_hf_models_on_flash_attention_match_sdpa(family, monkeypatch):
         make = transformers.ViTModel
         inputs = {"pixel_values": torch.randn(2, 3, 224, 224, device="cuda").bfloat16()}
         mask = None
-    ref = make(cfg).cuda().bfloat16()
-    ours = make(cfg).cuda().bfloat16()
+    # separate config objects: set_attn_implementation writes the model's config, and a shared
+    # one would switch the SDPA reference model to the backend under test as well
+    ref = make(copy.deepcopy(cfg)).cuda().bfloat16()
+    ours = make(copy.deepcopy(cfg)).cuda().bfloat16()
     ours.load_state_dict(ref.state_dict())
     ref.set_attn_implementation("sdpa")
     use_flash_attention(ours)
