@@ -224,24 +224,33 @@ def test_hf_models_on_flash_attention_match_sdpa(family, monkeypatch):
         inputs = {"pixel_values": torch.randn(2, 3, 224, 224, device="cuda").bfloat16()}
         mask = None
     # separate config objects: set_attn_implementation writes the model's config, and a shared
-    # one would switch the SDPA reference model to the backend under test as well
-    ref = make(copy.deepcopy(cfg)).cuda().bfloat16()
+    # one would switch the SDPA reference models to the backend under test as well.
+    # Judged against an fp32 SDPA model: ours (bf16) must be no worse than HF's own bf16 SDPA path
+    # (the query-weight gradient is small and cancellation-heavy, so bf16 alone moves it by several percent).
+    ref32 = make(copy.deepcopy(cfg)).cuda().float()
+    refb = make(copy.deepcopy(cfg)).cuda().bfloat16()
     ours = make(copy.deepcopy(cfg)).cuda().bfloat16()
-    ours.load_state_dict(ref.state_dict())
-    ref.set_attn_implementation("sdpa")
+    refb.load_state_dict(ref32.state_dict())
+    ours.load_state_dict(ref32.state_dict())
+    for m in (ref32, refb):
+        m.set_attn_implementation("sdpa")
     use_flash_attention(ours)
+    outs = []
     calls = []
     orig = T.flash_attention
     monkeypatch.setattr(T, "flash_attention", lambda *a, **k: calls.append(a[1].shape) or orig(*a, **k))
-    outs = []
-    for m in (ref, ours):
-        h = m(**inputs).last_hidden_state
+    for m in (ref32, refb, ours):
+        kw = dict(inputs)
+        if "pixel_values" in kw:
+            kw["pixel_values"] = kw["pixel_values"].to(next(m.parameters()).dtype)
+        h = m(**kw).last_hidden_state
         keep = mask[..., None].to(h.dtype) if mask is not None else torch.ones_like(h[..., :1])
         (h.float() * keep).square().mean().backward()
         wq = next(p for n, p in m.named_parameters() if n.endswith(("query.weight", "q_proj.weight")))
         outs.append((h.float() * keep, wq.grad.float()))
-    assert _rel(outs[1][0], outs[0][0]) < 2e-2
-    assert _rel(outs[1][1], outs[0][1]) < 5e-2
+    for k_ in range(2):
+        err_sdpa, err_ours = _rel(outs[1][k_], outs[0][k_]), _rel(outs[2][k_], outs[0][k_])
+        assert err_ours < max(2 * err_sdpa, 2e-2), (k_, err_ours, err_sdpa)
     assert len(calls) == cfg.num_hidden_layers  # every layer ran on the MFMA kernels (no SDPA fallback)
     if family == "llama_gqa":
         assert calls[0][2] == 2  # K/V passed with their own 2 heads (no repeat)
