@@ -32,6 +32,7 @@ def main():
     p.add_argument("--gpt2", action="store_true", help="only the GPT-2-medium shape (16x1024x16x64)")
     p.add_argument("--shapes", default="", help="B,S,H,D[;B,S,H,D...] instead of the defaults")
     p.add_argument("--noncausal", action="store_true")
+    p.add_argument("--kv-heads", type=int, default=0, help="grouped-query K/V heads (0: = H)")
     a = p.parse_args()
     shapes = ((16, 1024, 16, 64), (8, 2048, 16, 64), (4, 4096, 8, 128))
     if a.shapes:
@@ -42,18 +43,20 @@ def main():
     wo = T.flash_attention(*w, causal=causal)
     timeit(lambda: torch.autograd.grad(wo, w, wo, retain_graph=True), 100)
     for B, S, H, D in shapes[:1] if a.gpt2 else shapes:
-        q, k, v = (torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-                   for _ in range(3))
+        hk = a.kv_heads or H
+        q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+        k, v = (torch.randn(B, S, hk, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+                for _ in range(2))
         g = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16)
         flops = 4 * B * H * S * S * D / (2 if causal else 1)
         if a.only in ("", "fwd"):
             ms = timeit(lambda: T.flash_attention(q, k, v, causal=causal), a.iters)
-            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "causal": causal, "pass": "fwd", "ms": round(ms, 4),
+            print(json.dumps({"B": B, "S": S, "H": H, "Hkv": hk, "D": D, "causal": causal, "pass": "fwd", "ms": round(ms, 4),
                               "tflops": round(flops / ms / 1e9, 1)}), flush=True)
         if a.only in ("", "bwd"):
             o = T.flash_attention(q, k, v, causal=causal)
             ms = timeit(lambda: torch.autograd.grad(o, (q, k, v), g, retain_graph=True), a.iters)
-            print(json.dumps({"B": B, "S": S, "H": H, "D": D, "causal": causal, "pass": "bwd", "ms": round(ms, 4),
+            print(json.dumps({"B": B, "S": S, "H": H, "Hkv": hk, "D": D, "causal": causal, "pass": "bwd", "ms": round(ms, 4),
                               "tflops": round(2.5 * flops / ms / 1e9, 1)}), flush=True)
 
 

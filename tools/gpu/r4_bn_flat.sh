@@ -22,3 +22,7 @@ done
 # attention backward per-kernel times at the GPT-2 shape (what else runs inside the timed bwd)
 cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/attn -o run --output-format csv -- python3 $ROOT/tools/bench_attn.py --gpt2 --only bwd > $O/attn_run.log 2>&1 || exit 1
 cd $ROOT && f=$(find $O/attn -name 'run_kernel_stats.csv' | head -1) && cut -d, -f1-8 $f | head -14
+# grouped-query attention throughput (Llama-style 32 query / 8 K/V heads at D 128) vs MHA
+cd $ROOT && timeout -k 10 200 python3 tools/bench_attn.py --shapes "2,4096,32,128" > $O/gqa.log 2>&1 && \
+timeout -k 10 200 python3 tools/bench_attn.py --shapes "2,4096,32,128" --kv-heads 8 >> $O/gqa.log 2>&1 || exit 1
+grep '"pass"' $O/gqa.log
