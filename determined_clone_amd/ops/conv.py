@@ -124,6 +124,9 @@ def _from_rows(m: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
 # gradient (see _PointwiseLib); DCA_PW_ACC_RESIDUAL=0 keeps the two gradients separate
 ACC_RESIDUAL = os.environ.get("DCA_PW_ACC_RESIDUAL", "1") != "0"
 ACC_HITS = 0  # backward passes that took the accumulate path (tests)
+# projection-shortcut data gradient added at the strided positions by a HIP kernel
+# (csrc/conv_igemm.hip strided_accumulate); DCA_STRIDED_ACC=0 uses ATen's strided add_
+STRIDED_ACC = os.environ.get("DCA_STRIDED_ACC", "1") != "0"
 
 
 def _pw_forward(x: torch.Tensor, weight: torch.Tensor, stride: int) -> torch.Tensor:
@@ -309,7 +312,12 @@ class _PointwiseDual(torch.autograd.Function):
             else:
                 ho, wo = dy2.shape[2], dy2.shape[3]
                 small = torch.mm(_rows(dy2, 1), W2).view(n, ho, wo, cin)
-                dx.permute(0, 2, 3, 1)[:, ::st, ::st, :].add_(small)
+                if STRIDED_ACC and dx.dtype == torch.bfloat16 and cin % 8 == 0 and \
+                        dx.is_contiguous(memory_format=torch.channels_last):
+                    # HIP kernel: 16-B lanes at HBM rate (ATen's strided add ran at 1.1-2.5 TB/s)
+                    _ext.load().strided_accumulate(dx, small.permute(0, 3, 1, 2), st)
+                else:
+                    dx.permute(0, 2, 3, 1)[:, ::st, ::st, :].add_(small)
         return dx, dw1, dw2, None, None, None
 
 

@@ -201,7 +201,27 @@ Tensor conv_igemm_wgrad(const Tensor& dy_in, const Tensor& x, const Tensor& w, i
 
 }  // namespace
 
+// dx (channels_last [N, C, H, W]) += small (channels_last [N, C, Ho, Wo]) at the stride-s
+// positions, in place.
+void strided_accumulate(Tensor& dx, const Tensor& small, int64_t s) {
+  const c10::DeviceGuard dg(dx.device());
+  TORCH_CHECK(dx.is_cuda() && dx.scalar_type() == at::kBFloat16 && small.scalar_type() == at::kBFloat16 &&
+                  dx.dim() == 4 && small.dim() == 4, "strided_accumulate: bf16 4-D GPU tensors");
+  TORCH_CHECK(dx.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  small.is_contiguous(at::MemoryFormat::ChannelsLast), "strided_accumulate: channels_last");
+  const int64_t N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
+  const int64_t Ho = small.size(2), Wo = small.size(3);
+  TORCH_CHECK(s >= 1 && small.size(0) == N && small.size(1) == C && C % 8 == 0 &&
+                  (Ho - 1) * s < H && (Wo - 1) * s < W, "strided_accumulate: shape mismatch");
+  TORCH_CHECK(N * H * W * C < (int64_t{1} << 40), "strided_accumulate: too large");
+  dca::strided_accumulate(dx.data_ptr(), small.data_ptr(), static_cast<int>(N), static_cast<int>(H),
+                          static_cast<int>(W), static_cast<int>(C), static_cast<int>(Ho),
+                          static_cast<int>(Wo), static_cast<int>(s), stream());
+}
+
 void register_conv_ops(pybind11::module& m) {
+  m.def("strided_accumulate", &strided_accumulate, pybind11::arg("dx"), pybind11::arg("small"),
+        pybind11::arg("stride"));
   m.def("conv_igemm_wgrad", &conv_igemm_wgrad, pybind11::arg("dy"), pybind11::arg("x"),
         pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"),
         pybind11::arg("acc") = pybind11::none());

@@ -26,6 +26,7 @@
 //  * one barrier per stage: issue the NEXT stage's loads, compute the current one, then
 //    vmcnt(0) + barrier (the "minimum 2-phase" loop of guide T3/T4);
 //  * tiles are dealt XCD-contiguously (neighbouring pixel tiles share input rows in an XCD's L2).
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -702,6 +703,45 @@ void conv_igemm_wgrad(const void* dy, const void* x, float* ws, void* dw, bool d
   else
     hipLaunchKernelGGL(wgrad_reduce_kernel<BF16>, dim3(rg), dim3(kThreads), 0, st, ws, c.splits, n, dw,
                        accumulate, dw_kcrs, RS, g.C);
+}
+
+// dx[n][s*i][s*j][:] += small[n][i][j][:] (NHWC bf16): the projection shortcut's data gradient of
+// a stride-s downsampling block added in place at the strided positions of conv1's data gradient.
+// One lane per 16 B (8 channels), fp32 add, grid-stride; ATen's generic strided add ran this at
+// 1.1-2.5 TB/s (64-bit index arithmetic per element, 2-byte accesses; round-4 step breakdown).
+__global__ __launch_bounds__(256) void strided_accumulate_kernel(uint16_t* __restrict__ dx,
+                                                                 const uint16_t* __restrict__ small,
+                                                                 int64_t n_vec, int c8, int Wo, int Ho,
+                                                                 int W, int H, int s) {
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n_vec;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int cv = static_cast<int>(t % c8);
+    const int64_t pix = t / c8;  // (n, i, j) of the small tensor
+    const int j = static_cast<int>(pix % Wo);
+    const int64_t ni = pix / Wo;
+    const int i = static_cast<int>(ni % Ho);
+    const int64_t n = ni / Ho;
+    const int64_t dpix = (n * H + static_cast<int64_t>(s) * i) * W + static_cast<int64_t>(s) * j;
+    uint4* dp = reinterpret_cast<uint4*>(dx + (dpix * c8 + cv) * 8);
+    const uint4 a = *dp;
+    const uint4 b = *reinterpret_cast<const uint4*>(small + t * 8);
+    auto add2 = [](uint32_t x, uint32_t y) {
+      const float lo = __uint_as_float(x << 16) + __uint_as_float(y << 16);
+      const float hi = __uint_as_float(x & 0xffff0000u) + __uint_as_float(y & 0xffff0000u);
+      return pack_bf16x2(lo, hi);
+    };
+    *dp = make_uint4(add2(a.x, b.x), add2(a.y, b.y), add2(a.z, b.z), add2(a.w, b.w));
+  }
+}
+
+void strided_accumulate(void* dx, const void* small, int N, int H, int W, int C, int Ho, int Wo,
+                        int s, hipStream_t st) {
+  const int c8 = C / 8;
+  const int64_t n_vec = static_cast<int64_t>(N) * Ho * Wo * c8;
+  const int64_t blocks = std::min<int64_t>((n_vec + 255) / 256, 256 * 64);
+  hipLaunchKernelGGL(strided_accumulate_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st,
+                     static_cast<uint16_t*>(dx), static_cast<const uint16_t*>(small), n_vec, c8, Wo,
+                     Ho, W, H, s);
 }
 
 void conv_flip_transpose(const void* w, void* wt, int K, int C, int RS, hipStream_t st) {

@@ -479,3 +479,21 @@ def test_conv_igemm_wgrad_accumulates_into_grad_views(k, stride):
         out = C.conv_igemm_wgrad(dy, x, w, stride, pad, acc)
         assert out.data_ptr() == acc.data_ptr()
         _close(acc - base, ref, 1e-2, f"dw ({fmt})")
+
+
+@pytest.mark.parametrize("shape", [(4, 256, 56, 56, 2), (3, 64, 57, 29, 2), (2, 1024, 14, 14, 2), (2, 128, 9, 9, 3)])
+def test_strided_accumulate_matches_strided_add(shape):
+    """dx[:, :, s*i, s*j] += small[:, :, i, j] (the projection shortcut's data gradient of a
+    downsampling block) on the HIP kernel equals ATen's strided add bit for bit (fp32 add of two
+    bf16 values, one rounding)."""
+    from determined_clone_amd.ops import _ext
+
+    n, c, h, w, s = shape
+    ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
+    torch.manual_seed(0)
+    dx = torch.randn(n, c, h, w, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    small = torch.randn(n, c, ho, wo, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    want = dx.clone()
+    want[:, :, ::s, ::s] += small
+    _ext.load().strided_accumulate(dx, small, s)
+    torch.testing.assert_close(dx, want, atol=0, rtol=0)
