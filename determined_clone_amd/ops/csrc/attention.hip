@@ -861,11 +861,12 @@ bool fwd_pipe() {
   return on;
 }
 
-// forward pipelining at D = 128 (DCA_ATTN_FWD_PIPE128=1, opt-in until measured)
+// forward pipelining at D = 128: +1-3.5% D128 S4096 causal fwd in two same-box A/Bs
+// (profiles/round4_attention_branchfree_ab.txt, round4_attention_knobs.txt); DCA_ATTN_FWD_PIPE128=0 off
 bool fwd_pipe128() {
   static const bool on = [] {
     const char* e = std::getenv("DCA_ATTN_FWD_PIPE128");
-    return e && std::atoi(e) == 1;
+    return !(e && std::atoi(e) == 0);
   }();
   return on;
 }
