@@ -476,153 +476,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   }
 }
 
-// Forward variant with TWO 32-row query groups per wave (64 rows per wave, 256 per workgroup): each
-// K fragment (ds_read_b128) and V^T fragment (ds_read_b64_tr_b16) read from LDS feeds both groups'
-// MFMAs -- half the LDS reads per FLOP of attn_fwd_kernel -- and the two groups' softmax chains are
-// independent, so one group's exp / max / sum work can issue under the other's MFMAs (twice the
-// instruction-level parallelism per wave). D = 64 only (D = 128 would exceed the 512-register file).
-// DCA_ATTN_FWD_RG=2 selects it.
-template <int D, bool CAUSAL, int KT>
-__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_fwd_rg2_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
-    uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
-    Strides ks, Strides vs, Strides os, float scale_log2, int order, const int* __restrict__ kvlen, int G) {
-  constexpr int RG = 2;         // 32-row query groups per wave
-  constexpr int QB = 4 * 32 * RG;
-  constexpr int RS = D + kPad;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Ks = smem;
-  constexpr int VPAD = D == 128 ? kTrPad : kPad;
-  constexpr int RSV = D + VPAD;
-  uint16_t* Vs = Ks + KT * RS;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, hf = lane >> 5;
-  const Blk blk = xcd_block(order);
-  const int b = blk.z, h = blk.y;
-  if (kvlen) Sk = min(Sk, max(kvlen[b], 1));
-  const int q_blk = (CAUSAL ? (gridDim.x - 1 - blk.x) : blk.x) * QB;
-  const int q0 = q_blk + w * 32 * RG;  // group g: rows q0 + 32 g + r
-  const uint16_t* qb = q + b * qs.b + h * qs.h;
-  const uint16_t* kb = k + b * ks.b + (h / G) * ks.h;
-  const uint16_t* vb = v + b * vs.b + (h / G) * vs.h;
-
-  bf16x8 qf[RG][D / 16];
-  f32x16 oacc[RG][D / 32];
-  float m[RG], l[RG];
-#pragma unroll
-  for (int g = 0; g < RG; ++g) {
-    const int my_q = q0 + 32 * g + r;
-#pragma unroll
-    for (int s = 0; s < D / 16; ++s)
-      qf[g][s] = my_q < Sq ? load8(qb + static_cast<int64_t>(my_q) * qs.s + 16 * s + 8 * hf) : zero8();
-#pragma unroll
-    for (int n = 0; n < D / 32; ++n) oacc[g][n] = zero16();
-    m[g] = -INFINITY;
-    l[g] = 0.f;
-  }
-  const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
-  const int tr_row = (r & 15) >> 2;
-  const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
-  KVPrefetch<D, KT, VPAD> pf;
-  pf.init(kb, ks, vb, vs, Sk);
-  pf.fetch(0);
-  for (int kt = 0; kt < k_end; kt += KT) {
-    __syncthreads();
-    pf.store(Ks, Vs);
-    __syncthreads();
-    if (kt + KT < k_end) pf.fetch(kt + KT);
-#pragma unroll
-    for (int sub = 0; sub < KT / 32; ++sub) {
-      const int kb0 = kt + 32 * sub;
-      if (kb0 >= k_end) break;
-      if (CAUSAL && kb0 > q0 + 32 * RG - 1) break;  // wave-uniform: every row of the wave precedes
-      bf16x8 kf[D / 16];
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s) kf[s] = load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf);
-      f32x16 sc[RG];
-#pragma unroll
-      for (int g = 0; g < RG; ++g) sc[g] = zero16();
-#pragma unroll
-      for (int s = 0; s < D / 16; ++s)
-#pragma unroll
-        for (int g = 0; g < RG; ++g) sc[g] = mfma32(kf[s], qf[g][s], sc[g]);
-      __builtin_amdgcn_sched_group_barrier(0x100, D / 16, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, RG * D / 16, 0);
-      // this sub-tile's V^T fragments, shared by both groups
-      bf16x8 vfr[D / 32][2];
-#pragma unroll
-      for (int n = 0; n < D / 32; ++n)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RSV + 32 * n + tr_col;
-          vfr[n][s2] = cat8(tr_read(base), tr_read(base + 8 * RSV));
-        }
-#pragma unroll
-      for (int g = 0; g < RG; ++g) {
-        const int qg = q0 + 32 * g;
-        if (CAUSAL && kb0 > qg + 31) continue;  // wave-uniform: this group is fully masked
-        const int my_q = qg + r;
-        f32x16 sg = sc[g];
-        if ((kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > qg)) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-            sg[i] = (key >= Sk || (CAUSAL && key > my_q)) ? -INFINITY : sg[i];
-          }
-        }
-        float mx = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sg[i]);
-        mx = half_max(mx);
-        const float mcand = mx * scale_log2;
-        const bool upd = mcand > m[g] + kRescaleLog2;
-        const float mnew = upd ? mcand : m[g];
-        const float mref = mnew == -INFINITY ? 0.f : mnew;
-        const float alpha = upd ? fast_exp2(m[g] - mref) : 1.f;
-        float rs = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = fast_exp2(fmaf(sg[i], scale_log2, -mref));
-          sg[i] = p;
-          rs += p;
-        }
-        rs = half_sum(rs);
-        l[g] = l[g] * alpha + rs;
-        m[g] = mnew;
-        if (__any(upd)) {
-#pragma unroll
-          for (int n = 0; n < D / 32; ++n) rescale16(oacc[g][n], alpha);
-        }
-        const bf16x8 p0 = pack8(sg, 0), p1 = pack8(sg, 8);
-#pragma unroll
-        for (int n = 0; n < D / 32; ++n) {
-          oacc[g][n] = mfma32(vfr[n][0], p0, oacc[g][n]);
-          oacc[g][n] = mfma32(vfr[n][1], p1, oacc[g][n]);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < RG; ++g) {
-    const int my_q = q0 + 32 * g + r;
-    if (my_q < Sq) {
-      const float inv = l[g] > 0.f ? 1.f / l[g] : 0.f;
-      uint16_t* orow = o + b * os.b + h * os.h + static_cast<int64_t>(my_q) * os.s;
-#pragma unroll
-      for (int n = 0; n < D / 32; ++n)
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          uint2 pk;
-          pk.x = pack_bf16x2(oacc[g][n][4 * q4] * inv, oacc[g][n][4 * q4 + 1] * inv);
-          pk.y = pack_bf16x2(oacc[g][n][4 * q4 + 2] * inv, oacc[g][n][4 * q4 + 3] * inv);
-          *reinterpret_cast<uint2*>(orow + 32 * n + 8 * q4 + 4 * hf) = pk;
-        }
-      if (hf == 0) lse[(static_cast<int64_t>(b) * H + h) * Sq + my_q] = l[g] > 0.f ? m[g] + log2f(l[g]) : INFINITY;
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------ backward
 // Two kernels, no atomics (FlashAttention-2 style split, MI355X layouts):
 //  * attn_bwd_dq_kernel: one workgroup = 128 queries (4 waves x 32). Computes delta = rowsum(dO*O)
@@ -1058,31 +911,10 @@ int dkdv_qt() {
   return qt;
 }
 
-// forward with two 32-row query groups per wave (attn_fwd_rg2_kernel): DCA_ATTN_FWD_RG=2
-int fwd_rg() {
-  static const int rg = [] {
-    const char* e = std::getenv("DCA_ATTN_FWD_RG");
-    return (e && std::atoi(e) == 2) ? 2 : 1;
-  }();
-  return rg;
-}
-
 template <int D, bool C>
 void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse,
                 int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs, Strides os,
                 float scale_log2, const int* kvlen, int G, hipStream_t st) {
-  if constexpr (D == 64) {  // D = 128 with two groups exceeds 512 registers (spills)
-  if (fwd_rg() == 2) {
-    constexpr int KT = 64;
-    const size_t lds = fwd_lds(D, KT);
-    auto kern = attn_fwd_rg2_kernel<D, C, KT>;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    hipLaunchKernelGGL(kern, dim3((Sq + 255) / 256, H, B), dim3(256), lds, st, q, k, v, o, lse, Sq, Sk, H,
-                       qs, ks, vs, os, scale_log2, attn_order(C), kvlen, G);
-    return;
-  }
-  }
   dim3 grid((Sq + 127) / 128, H, B);
   auto go = [&](auto ktag) {
     constexpr int KT = decltype(ktag)::value;
