@@ -385,6 +385,9 @@ def test_linear_direct_grad_accumulation(bias, seq):
     for _ in range(2):
         (T.linear(xs[0], w1, b1) * g).float().sum().backward()
         (torch.nn.functional.linear(xs[1], w2, b2) * g).float().sum().backward()
+    from determined_clone_amd.ops import _grad
+
+    _grad.join()  # weight and bias gradients accumulate on the side stream
     assert [p.grad.data_ptr() for p in params] == ptrs
     assert len(calls) == 2 * len(params)
     assert _rel(w1.grad, w2.grad) < 1e-2
