@@ -167,8 +167,6 @@ class _BiasGelu(torch.autograd.Function):
 _WGRAD_SPLITK = os.environ.get("DCA_WGRAD_SPLITK", "1") != "0"
 # linear-layer weight gradients on the side stream (ops/_grad.py); A/B switch
 LINEAR_SIDE_STREAM = os.environ.get("DCA_LINEAR_WGRAD_STREAM", "1") != "0"
-# linear-layer bias gradients follow the weight gradient on the side stream; A/B switch
-BIAS_GRAD_SIDE = os.environ.get("DCA_BIAS_GRAD_SIDE", "1") != "0"
 
 
 def _wgrad_splits(tokens: int, m: int, n: int) -> int:
@@ -215,7 +213,6 @@ class _Linear(torch.autograd.Function):
         w_param, b_param = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = dw = db = None
-        side = None
         if ctx.needs_input_grad[1]:  # first: on the side stream it overlaps the data gradient
             x2 = x.reshape(-1, x.shape[-1])
             acc = _grad.target(w_param)
@@ -236,13 +233,7 @@ class _Linear(torch.autograd.Function):
         if b_param is not None and ctx.needs_input_grad[2]:
             acc = _grad.target(b_param)
             if dy2.shape[-1] % 8 == 0 and dy2.is_cuda:
-                # with a direct target, the bias reduction (a full read of dy) follows the weight
-                # gradient on the side stream (dy2 is kept alive by the fork above): the data
-                # gradient's stream goes on to the next layer instead of competing with the
-                # side-stream GEMM for 1-2 TB/s (round-4 GPT-2 kernel stats)
-                on_side = side is not None and acc is not None and BIAS_GRAD_SIDE
-                with torch.cuda.stream(side) if on_side else contextlib.nullcontext():
-                    out = _ext.load().bias_grad(dy2, acc)
+                out = _ext.load().bias_grad(dy2, acc)
                 db = None if acc is not None else out.to(b_param.dtype)
             else:
                 db = dy2.sum(0).to(b_param.dtype)
