@@ -78,25 +78,12 @@ KEEPALIVE = os.environ.get("DCA_WGRAD_KEEPALIVE", "1") != "0"
 _keep = []  # [tensors, event recorded on the side stream after their readers (or None yet)]
 
 
-# The last MAIN_TAIL weight gradients of a backward pass (by call order in the previous pass) run
-# on the current stream: at the end of backward the data-gradient stream would otherwise idle at
-# the join while the side stream drains its backlog. 0 (default) keeps every one on the side.
-MAIN_TAIL = int(os.environ.get("DCA_WGRAD_MAIN_TAIL", "0"))
-_calls = 0       # side-stream candidates seen since the last join
-_last_total = 0  # ... in the previous backward pass
-
-
 def side_stream_for(p: Optional[torch.Tensor]) -> Optional["torch.cuda.Stream"]:
     """The side stream to run ``p``'s weight gradient on, or None (feature off, CPU, graph
-    capture, no persistent ``.grad`` to accumulate into, or one of the backward pass's last
-    ``DCA_WGRAD_MAIN_TAIL`` weight gradients)."""
-    global _calls
+    capture, or no persistent ``.grad`` to accumulate into)."""
     if not SIDE_STREAM or p is None or not p.is_cuda or target(p) is None:
         return None
     if torch.cuda.is_current_stream_capturing():
-        return None
-    _calls += 1
-    if MAIN_TAIL and _last_total and _calls > _last_total - MAIN_TAIL:
         return None
     dev = p.device.index
     s = _streams.get(dev)
@@ -134,9 +121,6 @@ def pending() -> bool:
 
 def join() -> None:
     """Make the current stream wait for all side-stream gradient work."""
-    global _calls, _last_total
-    if _calls:
-        _last_total, _calls = _calls, 0
     if not _pending:
         return
     cur = torch.cuda.current_stream()
