@@ -112,11 +112,10 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][tpr*16]
   const int tid = threadIdx.x;
   const int lc = tid % tpr, r0 = tid / tpr;
-  const BlkMap bm = apply_block_map(C, tpr);  // channel-group-fastest on a flat grid
-  const int c = (bm.cg * tpr + lc) * 8;
+  const int c = (blockIdx.y * tpr + lc) * 8;
   const bool active = c < C;
-  const int bx = bm.nb - 1 - bm.bx;
-  const RowRange rr = chunk_rows(M, rpi, bx, bm.nb);
+  const int bx = static_cast<int>(gridDim.x) - 1 - static_cast<int>(blockIdx.x);
+  const RowRange rr = chunk_rows(M, rpi, bx, gridDim.x);
   float s[8], q[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
@@ -201,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
     float acc = 0.f;
     for (int r = 0; r < rpi; ++r) acc += lds[r * width + o];
     const int lco = o / 16, k = o % 16;
-    const int ch = (bm.cg * tpr + lco) * 8 + (k & 7);
+    const int ch = (blockIdx.y * tpr + lco) * 8 + (k & 7);
     if (ch < C) partial[(static_cast<int64_t>(bx) * 2 + (k >> 3)) * C + ch] = acc;
   }
 }
@@ -552,12 +551,7 @@ void launch_reduce(bool bwd, const void* x, const void* dy, const void* dy2, con
                    const float* mean,
                    int64_t M, int C, bool relu, float* partial, int B, const ReduceGeom& g,
                    hipStream_t st) {
-  // flat channel-group-fastest grid as in the apply passes (DCA_BN_REDUCE_FLAT=0: 2-D grid)
-  static const bool flat = [] {
-    const char* e = std::getenv("DCA_BN_REDUCE_FLAT");
-    return !(e && std::atoi(e) == 0);
-  }();
-  const dim3 grid = (flat && g.cgroups > 1) ? dim3(B * g.cgroups, 1) : dim3(B, g.cgroups);
+  dim3 grid(B, g.cgroups);
   size_t lds = static_cast<size_t>(g.rpi) * g.tpr * 16 * sizeof(float);
   const ReduceVar& v = reduce_var();
 #define DCA_RED(BW, UU, NTT)                                                                       \

@@ -1,5 +1,5 @@
 #!/bin/bash
-# BN apply passes: channel-group-fastest flat grid (default) vs the 2-D grid (DCA_BN_REDUCE_FLAT=0):
+# BN statistics (reduce) passes: channel-group-fastest flat grid (default) vs the 2-D grid (DCA_BN_REDUCE_FLAT=0):
 # numerics, per-kernel bandwidth at every ResNet-50 BN shape, and the ResNet-50 step, same box
 set -o pipefail
 ROOT=$(pwd)
