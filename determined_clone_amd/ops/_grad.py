@@ -88,40 +88,8 @@ def side_stream_for(p: Optional[torch.Tensor]) -> Optional["torch.cuda.Stream"]:
     dev = p.device.index
     s = _streams.get(dev)
     if s is None:
-        s = _streams[dev] = _make_side_stream(p.device)
+        s = _streams[dev] = torch.cuda.Stream(device=p.device)
     return s
-
-
-# Side stream on a subset of the compute units (DCA_WGRAD_CU_MASK, A/B experiments): "even" /
-# "odd" = every other CU, "lo" / "hi" = the lower / upper half of the CU mask, an integer = that
-# many CUs from the bottom. The weight-gradient kernels then cannot take CUs from the rest of the
-# chip, where the data-gradient / BatchNorm kernels of the critical path run. Unset: a plain stream.
-CU_MASK = os.environ.get("DCA_WGRAD_CU_MASK", "")
-
-
-def _make_side_stream(device: torch.device) -> "torch.cuda.Stream":
-    if not CU_MASK:
-        return torch.cuda.Stream(device=device)
-    import ctypes
-
-    n = torch.cuda.get_device_properties(device).multi_processor_count
-    if CU_MASK in ("even", "odd"):
-        sel = [i for i in range(n) if i % 2 == (0 if CU_MASK == "even" else 1)]
-    elif CU_MASK in ("lo", "hi"):
-        sel = list(range(n // 2)) if CU_MASK == "lo" else list(range(n // 2, n))
-    else:
-        sel = list(range(min(n, max(1, int(CU_MASK)))))
-    words = (n + 31) // 32
-    mask = (ctypes.c_uint32 * words)()
-    for i in sel:
-        mask[i // 32] |= 1 << (i % 32)
-    lib = ctypes.CDLL("libamdhip64.so")
-    handle = ctypes.c_void_p()
-    with torch.cuda.device(device):
-        err = lib.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(words), mask)
-    if err != 0:
-        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({err})")
-    return torch.cuda.ExternalStream(handle.value, device=device)
 
 
 def fork(stream: "torch.cuda.Stream", tensors=()) -> None:
