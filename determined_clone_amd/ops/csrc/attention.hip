@@ -242,7 +242,7 @@ struct KVPrefetch {
 // sub-tile: one more O^T-shaped MFMA pair per sub-tile with an all-ones A operand, whose every
 // row is sum_k P^T[k][q] (the same bf16 P the O product uses), rescaled with O by the deferred max.
 // The MFMA pipe runs at ~30% here while VALU issue and its dependency chains bound the loop.
-template <int D, bool CAUSAL, int KT, bool PIPE, bool MSUM = false, bool PRIO = false>
+template <int D, bool CAUSAL, int KT, bool PIPE, bool MSUM = false>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
@@ -345,9 +345,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
           lacc = mfma32(ones8, p0, lacc);
           lacc = mfma32(ones8, p1, lacc);
         }
-        // PRIO: this wave's MFMA bursts at raised issue priority, so the co-resident wave's
-        // softmax VALU does not delay them (DCA_ATTN_FWD_PRIO=1, A/B)
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
   #pragma unroll
         for (int n = 0; n < D / 32; ++n) {
   #pragma unroll
@@ -356,7 +353,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
             oacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RSV)), s2 ? p1 : p0, oacc[n]);
           }
         }
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       };
       // wave-uniform: every key of the tile exists and precedes every query of this wave
       if (kt + KT <= Sk && (!CAUSAL || kt + KT - 1 <= q0)) {
@@ -373,7 +369,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
             kb2[s] = load8(Ks + (32 * sub + 32 + r) * RS + 16 * s + 8 * hf);
           }
           f32x16 sa = zero16(), sb = zero16();
-          if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
   #pragma unroll
           for (int s = 0; s < D / 16; ++s) {
             sa = mfma32(ka[s], qf[s], sa);
@@ -382,7 +377,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
           // schedule: every fragment read issued before the first MFMA (one LDS wait)
           __builtin_amdgcn_sched_group_barrier(0x100, D / 8, 0);
           __builtin_amdgcn_sched_group_barrier(0x8, D / 8, 0);
-          if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
           softmax_pv(sa, sub, kt + 32 * sub, false);
           softmax_pv(sb, sub + 1, kt + 32 * sub + 32, false);
         }
@@ -867,15 +861,6 @@ bool fwd_pipe() {
   return on;
 }
 
-// forward MFMA bursts at raised wave priority (attn_fwd_kernel PRIO; DCA_ATTN_FWD_PRIO=1, D = 64)
-bool fwd_prio() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCA_ATTN_FWD_PRIO");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-
 // forward pipelining at D = 128: +1-3.5% D128 S4096 causal fwd in two same-box A/Bs
 // (profiles/round4_attention_branchfree_ab.txt, round4_attention_knobs.txt); DCA_ATTN_FWD_PIPE128=0 off
 bool fwd_pipe128() {
@@ -945,7 +930,6 @@ void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
     if (fwd_pipe() && (D == 64 || (!ms && fwd_pipe128()))) {
       if constexpr (D == 64) {
         if (ms) launch(attn_fwd_kernel<D, C, KT, true, true>);
-        else if (fwd_prio()) launch(attn_fwd_kernel<D, C, KT, true, false, true>);
         else launch(attn_fwd_kernel<D, C, KT, true>);
       } else {
         launch(attn_fwd_kernel<D, C, KT, true>);
