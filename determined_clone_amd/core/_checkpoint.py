@@ -107,14 +107,21 @@ class CheckpointContext:
             self._report_checkpoint(storage_id, resources, md)
             return storage_id
         storage_id = _storage_id or self._dist.broadcast(str(uuid.uuid4()) if self._dist.rank == 0 else None)
-        # a directory several local ranks share is uploaded once, by the lowest of them
-        want_upload = ckpt_dir is not None
+        if selector is not None and ckpt_dir is None:
+            raise RuntimeError("ckpt_dir has to be provided if selector is not None")
+        # A rank uploads when it has a selector (each rank contributes ITS selected files, even
+        # from a directory shared with other ranks; byte-identical duplicates are deduplicated by
+        # _resolve_conflicts), or when it is the lowest rank naming a shared directory without a
+        # selector (reference core/_checkpoint.py:305-318).
+        uid = None
         if ckpt_dir is not None:
             st = os.stat(ckpt_dir)
-            uids = self._dist.allgather((os.uname().nodename, st.st_dev, st.st_ino))
-            want_upload = uids.index(uids[self._dist.rank]) == self._dist.rank
-        else:
-            self._dist.allgather(None)
+            uid = (os.uname().nodename, st.st_dev, st.st_ino)
+        uids = self._dist.allgather(uid)
+        if not any(u is not None for u in uids):
+            raise RuntimeError("cannot call .upload(ckpt_dir=None, shard=True) from all ranks; "
+                               "at least one rank must have a valid ckpt_dir")
+        want_upload = selector is not None or (uid is not None and uids.index(uid) == self._dist.rank)
         res = {}
         if want_upload:
             res = _local_resources(ckpt_dir)
@@ -186,12 +193,24 @@ class CheckpointContext:
         return sel
 
     def _serve_local_chief(self, selector: Optional[Callable[[str], bool]]) -> None:
-        """Non-chief local ranks: answer the chief's per-file questions until it says done."""
+        """Non-chief local ranks: answer the chief's per-file questions until it says done. A
+        :class:`_ChiefFailed` sentinel (the chief's download raised) is re-raised here, so the
+        local ranks fail with the chief instead of waiting for a terminator that never comes."""
         while True:
             name = self._dist.broadcast_local(None)
             if name is None:
                 return
+            if isinstance(name, dict) and name.get("__chief_failed__"):
+                raise RuntimeError(f"checkpoint download failed on the local chief: {name['error']}")
             self._dist.gather_local(selector(name) if selector is not None else True)
+
+    def _chief_failed(self, exc: BaseException) -> None:
+        """Tell the waiting local ranks that the chief's download raised (see
+        :meth:`_serve_local_chief`)."""
+        try:
+            self._dist.broadcast_local({"__chief_failed__": True, "error": f"{type(exc).__name__}: {exc}"})
+        except Exception:  # the group itself is broken: nothing more to tell
+            logger.exception("could not tell the local ranks that the download failed")
 
     def download(self, storage_id: str, ckpt_dir: os.PathLike,
                  download_mode: DownloadMode = DownloadMode.LocalWorkersShareDownload,
@@ -205,8 +224,12 @@ class CheckpointContext:
             return
         want_filter = any(self._dist.allgather(selector is not None))
         if self._dist.local_rank == 0:
-            self._storage_manager.download(storage_id, ckpt_dir,
-                                           self._coordinated_selector(selector) if want_filter else None)
+            try:
+                self._storage_manager.download(storage_id, ckpt_dir,
+                                               self._coordinated_selector(selector) if want_filter else None)
+            except BaseException as e:
+                self._chief_failed(e)
+                raise
             self._dist.broadcast_local(None)
         else:
             self._serve_local_chief(selector)
@@ -227,7 +250,12 @@ class CheckpointContext:
         want_filter = any(self._dist.allgather(selector is not None))
         if self._dist.local_rank == 0:
             sel = self._coordinated_selector(selector) if want_filter else None
-            with self._storage_manager.restore_path(storage_id, sel) as p:
+            with contextlib.ExitStack() as stack:
+                try:
+                    p = stack.enter_context(self._storage_manager.restore_path(storage_id, sel))
+                except BaseException as e:
+                    self._chief_failed(e)
+                    raise
                 self._dist.broadcast_local(None)  # download finished
                 self._dist.broadcast_local(str(p))
                 try:

@@ -101,10 +101,14 @@ class DistributedContext:
         return self.cross_size
 
     def close(self) -> None:
-        """Release the process groups this context created (its gloo object groups, and the
-        default group when ``from_torch_distributed`` initialised it): a worker that exits with a
-        live gloo group can abort in the group's destructor ("terminate called without an active
-        exception") while a peer is still tearing down."""
+        """Release the gloo object-collective groups this context created (a worker that exits
+        with a live gloo SUBGROUP can abort in the group's destructor -- "terminate called without
+        an active exception" -- while a peer is still tearing down). The default process group is
+        left up, also when ``from_torch_distributed`` initialised it (the reference's close()
+        never tears torch.distributed down either): user code may still run collectives after the
+        Core API context exits, and the process's exit releases it
+        (``tests/test_distributed.py::test_default_group_survives_core_context_close`` exits
+        straight after close() on 2 gloo ranks)."""
         if self._closed:
             return
         self._closed = True

@@ -20,8 +20,10 @@ optimizer, and a ``train_batch`` without host synchronisation or data-dependent 
 flow. Transformer trials (fused LayerNorm / attention / bias-GELU / cross-entropy, hipBLASLt
 GEMMs, fused AdamW with device-side clipping) and ResNets replay bit-exactly.
 
-MIOpen convolutions: models with convolutions switch MIOpen to its deterministic solvers
-(``torch.backends.cudnn.deterministic = True``) before the warm-up steps. Root cause of the
+MIOpen convolutions: for models with convolutions, every call of the step function made by the
+graph runner (warm-up, capture, eager fallbacks) runs with MIOpen's deterministic solvers
+(``torch.backends.cudnn.deterministic = True`` for the duration of the call only, restored after
+it, so evaluation and other models keep the default solvers). Root cause of the
 eager-vs-replay divergence measured in earlier rounds (profiles/round4_hip_graph_miopen_root_cause.txt):
 nothing was missing from the graph -- MIOpen's default solver for small strided 1x1 NHWC
 convolutions (ConvAsmImplicitGemmGTCDynamicFwdXdlopsNHWC, a split-K kernel accumulating with
@@ -29,8 +31,9 @@ atomics) is nondeterministic run to run (relative 4e-5 between two EAGER calls),
 merely ran it with a different atomic order; a few SGD steps amplified that. With deterministic
 solvers eager and replay agree bit for bit. The reference has no equivalent (its step is eager).
 """
+import contextlib
 import logging
-from typing import Any, Callable, List, Optional
+from typing import Any, Callable, Iterator, List, Optional
 
 import torch
 from torch.utils import _pytree as pytree
@@ -73,10 +76,31 @@ class GraphedTrainStep:
         self.replays = 0
         for opt in context.optimizers:
             opt.enable_device_hparams()
-        if torch.backends.cudnn.enabled and not torch.backends.cudnn.deterministic and _has_convs(context):
-            # before the eager warm-up steps, so warm-up, capture and replay run the same solvers
-            logger.info("hip_graph: MIOpen switched to deterministic convolution solvers")
-            torch.backends.cudnn.deterministic = True
+        # MIOpen runs its deterministic solvers for every call of the step function this object
+        # makes (warm-up, capture, eager fallbacks), so warm-up, capture and replay run the same
+        # solvers; the process-wide flag is restored after each call, so evaluation, other
+        # models and later trials in the process keep the fastest (split-K atomic) solvers.
+        self._deterministic = (torch.backends.cudnn.enabled and not torch.backends.cudnn.deterministic
+                               and _has_convs(context))
+        if self._deterministic:
+            logger.info("hip_graph: MIOpen runs deterministic convolution solvers inside the "
+                        "graphed training step")
+
+    @contextlib.contextmanager
+    def _solvers(self) -> Iterator[None]:
+        if not self._deterministic:
+            yield
+            return
+        prev = torch.backends.cudnn.deterministic
+        torch.backends.cudnn.deterministic = True
+        try:
+            yield
+        finally:
+            torch.backends.cudnn.deterministic = prev
+
+    def _eager(self, batch: Any, epoch_idx: int, batch_idx: int) -> Any:
+        with self._solvers():
+            return self.fn(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
 
     # ------------------------------------------------------------------ helpers
     def _matches(self, leaves: List[Any], spec: Any) -> bool:
@@ -105,12 +129,12 @@ class GraphedTrainStep:
         self.calls += 1
         leaves, spec = pytree.tree_flatten(batch)
         if self.graph is None and self.calls <= self.warmup_steps:
-            return self.fn(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
+            return self._eager(batch, epoch_idx, batch_idx)
         if self.graph is None:
             return self._capture(leaves, spec, epoch_idx, batch_idx)
         if not self._matches(leaves, spec):
             logger.debug("batch structure/shape differs from the captured one: running eagerly")
-            return self.fn(batch=batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
+            return self._eager(batch, epoch_idx, batch_idx)
         self._load_inputs(leaves)
         for opt in self.context.optimizers:
             opt._step += 1  # the Python side of step() does not run on replay
@@ -127,7 +151,7 @@ class GraphedTrainStep:
             opt.refresh_device_hparams(opt._step + 1)  # the step about to be captured
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g), self._solvers():
             self.static_out = self.fn(batch=static_batch, epoch_idx=epoch_idx, batch_idx=batch_idx)
         self.graph = g
         logger.info("captured the training step as a HIP graph")

@@ -5,9 +5,13 @@ anything that dispatches through ``ALL_ATTENTION_FUNCTIONS``) to ``"dca_mfma"``:
 [B, H, S, D] views and go to ``ops.transformer.flash_attention`` as [B, S, H, D] strided views
 (no copies). A padding ``attention_mask`` -- the boolean [B, 1, Sq, Sk] mask HF builds from a
 right-padded ``attention_mask`` -- becomes per-row key lengths for the kernels' key-padding path,
-so padded BERT batches never materialise scores either. Anything else falls back to HF's SDPA
-path: masks that are not right padding (left padding, packed sequences, custom masks), attention
-dropout in training, grouped KV heads, head dims other than 64/128, non-bf16 or CPU tensors.
+so padded BERT batches never materialise scores either. The lengths are derived from the 2-D
+``attention_mask`` HF passes to the mask interface (one small [B, Sk] check per distinct mask
+object, cached by object and version, so a reused mask costs no host sync) and ride on the 4-D
+mask to the layers. Grouped KV heads (GQA / MQA, ``H % Hkv == 0``) run natively in the kernels.
+Anything else falls back to HF's SDPA path: masks that are not right padding (left padding,
+packed sequences, sliding windows, custom masks), attention dropout in training, head dims other
+than 64/128, non-bf16 or CPU tensors.
 
 The reference trains HF models through its Trainer callback (harness/determined/transformers/
 _hf_callback.py) on the stock CUDA attention; this module is the MI355X-side kernel hookup.
@@ -27,7 +31,12 @@ _cache: Tuple[Any, ...] = (None, -1, None, None)
 
 def mask_to_key_lengths(mask: torch.Tensor, causal: bool) -> Optional[torch.Tensor]:
     """Boolean [B, 1|H, Sq, Sk] mask (True = attend) -> int32 key lengths [B], or None when the
-    mask is not pure right padding (optionally combined with the causal triangle)."""
+    mask is not pure right padding (optionally combined with the causal triangle). A mask built by
+    this backend's mask function carries its lengths (no device check here); other masks are
+    compared against the padding pattern once per mask object."""
+    got = getattr(mask, "_dca_key_lengths", None)
+    if got is not None and getattr(mask, "_dca_causal", None) == causal:
+        return got if isinstance(got, torch.Tensor) else None
     global _cache
     ref, ver, cz, out = _cache
     if ref is not None and ref() is mask and ver == mask._version and cz == causal:
@@ -74,13 +83,54 @@ def flash_attention_forward(module: torch.nn.Module, query: torch.Tensor, key: t
     return T.flash_attention(q, k, v, causal=causal, scale=scaling, key_lengths=kv_len), None
 
 
+# 2-D padding mask -> lengths (or False: not right padding), keyed by object and version
+_lengths_cache: Tuple[Any, ...] = (None, -1, None)
+
+
+def padding_lengths(mask2d: torch.Tensor) -> Optional[torch.Tensor]:
+    """int32 key lengths [B] of a 2-D right-padding ``attention_mask`` [B, Sk] (1 = token), or
+    None when it is not right padding / a row is empty. One host sync on the small 2-D mask per
+    distinct mask (object, version)."""
+    global _lengths_cache
+    ref, ver, out = _lengths_cache
+    if ref is not None and ref() is mask2d and ver == mask2d._version:
+        return out if isinstance(out, torch.Tensor) else None
+    m = mask2d.bool()
+    lengths = m.sum(-1)
+    keys = torch.arange(m.shape[-1], device=m.device)
+    ok = torch.logical_and((m == (keys[None, :] < lengths[:, None])).all(), (lengths > 0).all())
+    res = lengths.to(torch.int32) if bool(ok) else False
+    _lengths_cache = (weakref.ref(mask2d), mask2d._version, res)
+    return res if isinstance(res, torch.Tensor) else None
+
+
+def _mask(*args: Any, **kwargs: Any) -> Optional[torch.Tensor]:
+    """HF mask-interface function: ``sdpa_mask`` (boolean 4-D masks, None when nothing is masked)
+    that also attaches the key lengths of a right-padding ``attention_mask`` to the mask it
+    returns, when the rest of the mask is the plain causal or bidirectional pattern."""
+    from transformers import masking_utils as mu
+
+    out = mu.sdpa_mask(*args, **kwargs)
+    mask2d = kwargs.get("attention_mask")
+    fn = kwargs.get("mask_function", mu.causal_mask_function)
+    causal = {mu.causal_mask_function: True,
+              getattr(mu, "bidirectional_mask_function", None): False}.get(fn)
+    if (isinstance(out, torch.Tensor) and isinstance(mask2d, torch.Tensor) and mask2d.dim() == 2
+            and causal is not None and kwargs.get("local_size") is None
+            and not kwargs.get("q_offset") and not kwargs.get("kv_offset")
+            and mask2d.shape[-1] == out.shape[-1]):
+        lengths = padding_lengths(mask2d)
+        out._dca_key_lengths = lengths if lengths is not None else False
+        out._dca_causal = causal
+    return out
+
+
 def register() -> str:
     """Register ``"dca_mfma"`` with HF's attention and mask interfaces (idempotent)."""
     from transformers import AttentionInterface, AttentionMaskInterface
-    from transformers.masking_utils import sdpa_mask
 
     AttentionInterface.register(NAME, flash_attention_forward)
-    AttentionMaskInterface.register(NAME, sdpa_mask)  # boolean masks, None when nothing is masked
+    AttentionMaskInterface.register(NAME, _mask)
     return NAME
 
 

@@ -107,6 +107,32 @@ def _worker(rank, world, port, root, log_dir, case, out):
             d = os.path.join(log_dir, f"dl{rank}")
             cc.download(sid, d)
             result["downloaded"] = sorted(os.listdir(d)) if os.path.isdir(d) else []
+        elif case.startswith("selectors"):
+            # both ranks share ONE directory and each selects its own files (reference
+            # core/_checkpoint.py:305-318: every rank with a selector uploads its selection)
+            shared = os.path.join(log_dir, "shared_ckpt")
+            os.makedirs(shared, exist_ok=True)
+            pathlib.Path(shared, f"part{rank}.bin").write_text(str(rank))
+            pathlib.Path(shared, "common.txt").write_text("same")
+            dist.allgather(None)  # every rank's files exist before anyone lists the directory
+            sel = (lambda p, r=rank: p in (f"part{r}.bin", "common.txt"))
+            result["sid"] = cc.upload(shared, {"steps_completed": 2}, shard=True, selector=sel)
+        elif case.startswith("chieffail"):
+            # the local chief's download raises: the other local rank must fail too, not hang
+            if rank == 0:
+                def boom(*a, **k):
+                    raise FileNotFoundError("no such checkpoint")
+                cc._storage_manager.download = boom
+            for mode in ("restore", "download"):
+                try:
+                    if mode == "restore":
+                        with cc.restore_path("missing-id") as _:
+                            pass
+                    else:
+                        cc.download("missing-id", os.path.join(log_dir, f"dl{rank}"))
+                    result[mode] = "no error"
+                except (RuntimeError, FileNotFoundError) as e:
+                    result[mode] = type(e).__name__ + ": " + str(e)
         with open(os.path.join(out, f"r{rank}.json"), "w") as f:
             json.dump(result, f)
     except Exception:  # noqa: BLE001
@@ -167,3 +193,18 @@ def test_merge_helpers_match_reference_semantics():
     assert conf == {} and merged == {"d/": 0, "d/f": 1, "g": 2}
     _, conf = ckpt_mod.merge_resources([{"d/": 0}, {"d": 5}])  # dir vs file
     assert conf == {"d": [0, 1]}
+
+
+def test_upload_sharded_each_rank_uploads_its_selection_from_a_shared_dir():
+    res, root, _ = _run("selectors")
+    sid = res[0]["sid"]
+    assert res[1]["sid"] == sid
+    files = sorted(os.listdir(os.path.join(root, sid)))
+    assert files == ["common.txt", "metadata.json", "part0.bin", "part1.bin"]
+
+
+def test_local_chief_download_failure_reaches_the_other_local_ranks():
+    res, _, _ = _run("chieffail")
+    for mode in ("restore", "download"):
+        assert res[0][mode].startswith("FileNotFoundError"), res[0]
+        assert res[1][mode].startswith("RuntimeError") and "local chief" in res[1][mode], res[1]

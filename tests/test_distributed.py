@@ -174,3 +174,27 @@ def test_default_group_survives_core_context_close():
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker_dist_after_close, args=(2, port, d), nprocs=2, join=True)
         assert sorted(os.listdir(d)) == ["ok0", "ok1"]
+
+
+def _worker_exit_after_close(rank: int, world: int, port: int, out_dir: str) -> None:
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "LOCAL_WORLD_SIZE": str(world)})
+    from determined_clone_amd import core
+
+    with core.init(distributed=core.DistributedContext.from_torch_distributed()) as ctx:
+        assert ctx.distributed.allgather(rank) == list(range(world))
+        assert ctx.distributed.allgather_local(rank) == list(range(world))
+    open(os.path.join(out_dir, f"ok{rank}"), "w").close()
+    # no destroy_process_group(): the process exits straight after close() with the default
+    # group still up, and must not abort in a group destructor
+
+
+def test_exit_straight_after_core_context_close_is_clean():
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.start_processes(_worker_exit_after_close, args=(2, _free_port(), d), nprocs=2,
+                                 start_method="spawn", join=False)
+        while not ctx.join():
+            pass
+        assert [p.exitcode for p in ctx.processes] == [0, 0]
+        assert sorted(os.listdir(d)) == ["ok0", "ok1"]

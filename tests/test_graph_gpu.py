@@ -106,7 +106,14 @@ def test_graph_step_matches_eager(trial_cls, tmp_path, monkeypatch):
 
 
 def test_graph_with_miopen_convolutions_switches_to_deterministic_solvers(tmp_path, monkeypatch):
+    """The runner's own step calls use the deterministic solvers; the process-wide flag is back
+    to its previous value afterwards (evaluation and other models keep the default solvers)."""
     monkeypatch.setattr(torch.backends.cudnn, "deterministic", False)
     _, runner, _, step = _run(_ResNetTrial, True, tmp_path)
     assert runner is not None and runner.replays == STEPS - 3 and step == STEPS
-    assert torch.backends.cudnn.deterministic
+    assert runner._deterministic
+    assert not torch.backends.cudnn.deterministic
+    seen = []
+    runner.fn = lambda **kw: seen.append(torch.backends.cudnn.deterministic)
+    runner._eager(None, 0, 0)
+    assert seen == [True] and not torch.backends.cudnn.deterministic
