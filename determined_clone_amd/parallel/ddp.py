@@ -24,6 +24,7 @@ import torch
 import torch.distributed as dist
 
 from determined_clone_amd.ops import _grad
+from determined_clone_amd.parallel import _caps
 from determined_clone_amd.parallel.flat import FlatBuffer, FlatParamSpace
 
 logger = logging.getLogger("determined_clone_amd.parallel")
@@ -32,7 +33,7 @@ MiB = 1 << 20
 
 
 class _Bucket:
-    __slots__ = ("buf", "start", "end", "nparams", "pending", "work", "comm", "launched")
+    __slots__ = ("buf", "start", "end", "nparams", "pending", "work", "comm", "launched", "averaged")
 
     def __init__(self, buf: FlatBuffer, start: int, end: int, nparams: int) -> None:
         self.buf = buf
@@ -43,6 +44,7 @@ class _Bucket:
         self.work: Any = None
         self.comm: Optional[torch.Tensor] = None
         self.launched = False
+        self.averaged = False
 
 
 class GradientSync:
@@ -115,8 +117,8 @@ class GradientSync:
             self._launch(self.buckets[self._next])
             self._next += 1
 
-    def _op(self) -> Any:
-        if self.average and not self.fold_average and dist.get_backend(self.group) == "nccl":
+    def _op(self, t: torch.Tensor) -> Any:
+        if self.average and not self.fold_average and _caps.tensor_collectives(self.group, t.device):
             return dist.ReduceOp.AVG
         return dist.ReduceOp.SUM
 
@@ -129,7 +131,9 @@ class GradientSync:
             if self.comm_dtype is not None and t.dtype != self.comm_dtype:
                 b.comm = t.to(self.comm_dtype)
                 t = b.comm
-            b.work = dist.all_reduce(t, op=self._op(), group=self.group, async_op=True)
+            op = self._op(t)
+            b.averaged = op == dist.ReduceOp.AVG  # else finish() divides by the world size
+            b.work = dist.all_reduce(t, op=op, group=self.group, async_op=True)
         b.launched = True
 
     def finish(self) -> None:
@@ -143,8 +147,8 @@ class GradientSync:
         self._next = len(self.buckets)
         if self.space.buffers and next(iter(self.space.buffers.values())).grad.is_cuda:
             _grad.join()
-        manual_div = self.average and not self.fold_average and self._op() == dist.ReduceOp.SUM
         for b in self.buckets:
+            manual_div = self.average and not self.fold_average and not b.averaged
             if b.work is not None:
                 b.work.wait()
             if b.comm is not None:

@@ -38,6 +38,7 @@ import torch.distributed as dist
 
 from determined_clone_amd.ops import _ext, _grad
 from determined_clone_amd.ops import optim as fopt
+from determined_clone_amd.parallel import _caps
 from determined_clone_amd.parallel.flat import ALIGN, FlatBuffer
 
 logger = logging.getLogger("determined_clone_amd.parallel")
@@ -147,7 +148,15 @@ class ZeroShardMixin:
         if self.world > 1 and overlap_comm:
             for p in self.space.params():
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
-        self._nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
+        dev = next(iter(self.space.buffers.values())).data.device if self.space.buffers else torch.device("cpu")
+        # in-place reduce-scatter / all-gather-into-tensor: RCCL, and gloo on host tensors
+        # (parallel/_caps.py), so the CPU multi-rank tests run the production branch
+        self._inplace = self.world > 1 and _caps.tensor_collectives(self.pg, dev)
+        self._gather_pending: Dict[Tuple[int, int], Any] = {}  # (state id, bucket) -> work
+        self._gather_hook: Any = None
+        # deferred (overlapped) parameter all-gather: only once attach_module() has hooked the
+        # module's state_dict (a standalone optimizer waits at the end of step())
+        self.defer_param_gather = False
 
     # ------------------------------------------------------------------ layout
     def _pad_multiple(self) -> int:
@@ -191,7 +200,7 @@ class ZeroShardMixin:
         # from there (after the main stream's work so far) instead of stalling the main stream
         side = _grad.comm_stream() if g.is_cuda else None
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-            if self.zero_stage >= 2 and self._nccl:
+            if self.zero_stage >= 2 and self._inplace:
                 out = g[b.start + self.rank * b.chunk: b.start + (self.rank + 1) * b.chunk]
                 b.work = dist.reduce_scatter_tensor(out, full, op=dist.ReduceOp.SUM, group=self.pg,
                                                     async_op=True)
@@ -226,6 +235,7 @@ class ZeroShardMixin:
 
     # ------------------------------------------------------------------ clip / overflow
     def prepare_grads(self, max_norm: float = 0.0, loss_scale: Optional[torch.Tensor] = None) -> None:
+        self.wait_params()
         _grad.join()
         self.space.ensure_views()
         slices = [st.buf.grad[a:b] for st in self._order for a0, a1, _ in st.owned
@@ -240,6 +250,7 @@ class ZeroShardMixin:
     @torch.no_grad()
     def step(self, closure: Any = None) -> Any:  # type: ignore[override]
         loss = closure() if closure is not None else None
+        self.wait_params()
         _grad.join()
         self.space.ensure_views()
         self._step += 1
@@ -255,23 +266,79 @@ class ZeroShardMixin:
         return loss
 
     def _allgather_params(self) -> None:
+        """All-gather every bucket's updated chunks into the flat parameter buffer.
+
+        With the in-place collective (RCCL; gloo on host tensors) the gathers are ASYNC and overlap
+        the next forward: buckets are issued last-bucket-first (buckets follow gradient-ready
+        order, i.e. roughly reverse layer order, so the first layers' parameters land first), and a
+        global module forward pre-hook makes the compute stream wait for exactly the buckets
+        holding a module's own parameters right before that module runs (a stream dependency,
+        no host sync). Anything else that reads the parameters -- the next optimizer step,
+        checkpoints, ``state_dict`` -- calls :meth:`wait_params` first."""
         if self.world == 1:
             return
-        works = []
-        for st in self._order:
-            d = st.buf.data
-            for b in st.buckets:
-                mine = d[b.start + self.rank * b.chunk: b.start + (self.rank + 1) * b.chunk]
-                if self._nccl:
-                    works.append(dist.all_gather_into_tensor(d[b.start:b.end], mine, group=self.pg,
-                                                             async_op=True))
-                else:
+        self.wait_params()
+        if not self._inplace:  # gloo on device tensors: list form, blocking
+            for st in self._order:
+                d = st.buf.data
+                for b in st.buckets:
+                    mine = d[b.start + self.rank * b.chunk: b.start + (self.rank + 1) * b.chunk]
                     outs = [d[b.start + r * b.chunk: b.start + (r + 1) * b.chunk] for r in range(self.world)]
                     dist.all_gather(outs, mine.clone(), group=self.pg)
-        for w in works:
+            return
+        pending: Dict[Tuple[int, int], Any] = {}
+        for st in self._order:
+            d = st.buf.data
+            for bi in range(len(st.buckets) - 1, -1, -1):
+                b = st.buckets[bi]
+                mine = d[b.start + self.rank * b.chunk: b.start + (self.rank + 1) * b.chunk]
+                pending[(id(st), bi)] = dist.all_gather_into_tensor(d[b.start:b.end], mine,
+                                                                    group=self.pg, async_op=True)
+        self._gather_pending = pending
+        if self.defer_param_gather and self.overlap_comm:
+            if self._gather_hook is None:
+                self._gather_hook = torch.nn.modules.module.register_module_forward_pre_hook(self._before_forward)
+        else:
+            self.wait_params()  # a stream dependency on RCCL; blocking on gloo
+
+    def attach_module(self, module: torch.nn.Module) -> "ZeroShardMixin":
+        """Let the parameter all-gather after ``step()`` overlap the next forward of ``module``
+        (see :meth:`_allgather_params`); every submodule's ``state_dict`` waits for the gathers
+        first. The engines (``pytorch/deepspeed``) attach their module."""
+        for m in module.modules():
+            m.register_state_dict_pre_hook(lambda *_a, **_k: self.wait_params())
+        self.defer_param_gather = True
+        return self
+
+    def _before_forward(self, module: torch.nn.Module, _inputs: Any) -> None:
+        pending = self._gather_pending
+        if not pending:
+            return
+        for p in module.parameters(recurse=False):
+            st = self._param_state.get(id(p))
+            if st is None:
+                continue
+            for bi in st.param_buckets[id(p)]:
+                w = pending.pop((id(st), bi), None)
+                if w is not None:
+                    w.wait()  # the current stream waits for this bucket's gather
+        if not pending:
+            self._drop_gather_hook()
+
+    def _drop_gather_hook(self) -> None:
+        if self._gather_hook is not None:
+            self._gather_hook.remove()
+            self._gather_hook = None
+
+    def wait_params(self) -> None:
+        """Make the current stream wait for every outstanding parameter all-gather."""
+        pending, self._gather_pending = self._gather_pending, {}
+        for w in pending.values():
             w.wait()
+        self._drop_gather_hook()
 
     def sync_master_from_model(self) -> None:
+        self.wait_params()
         with torch.no_grad():
             for st in self._order:
                 for a0, a1, o in st.owned:
@@ -279,6 +346,7 @@ class ZeroShardMixin:
 
     # ------------------------------------------------------------------ checkpoint (per-rank shard)
     def state_dict(self) -> Dict[str, Any]:  # type: ignore[override]
+        self.wait_params()
         groups = []
         for g in self.param_groups:
             pg = {k: v for k, v in g.items() if k != "params"}
@@ -296,6 +364,7 @@ class ZeroShardMixin:
                 "step": self._step, "param_groups": groups, "shards": shards}
 
     def load_state_dict(self, state_dict: Dict[str, Any]) -> None:  # type: ignore[override]
+        self.wait_params()
         self.load_shard_state_dicts([state_dict])
 
     def load_shard_state_dicts(self, shard_dicts: List[Dict[str, Any]]) -> None:

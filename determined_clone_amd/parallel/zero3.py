@@ -38,6 +38,7 @@ import torch.distributed as dist
 from torch import nn
 
 from determined_clone_amd.ops import _grad
+from determined_clone_amd.parallel import _caps
 from determined_clone_amd.parallel.flat import ALIGN
 
 logger = logging.getLogger("determined_clone_amd.parallel.zero3")
@@ -83,9 +84,9 @@ class _Unit:
             return
         self.full.untyped_storage().resize_(self.padded * self.esz)
         if self.world > 1:
-            if _nccl(self.pg):
+            if _caps.tensor_collectives(self.pg, self.full.device):
                 dist.all_gather_into_tensor(self.full, self.shard.data, group=self.pg)
-            else:  # gloo (CPU tests): list form
+            else:  # gloo on device tensors: list form
                 n = self.shard_numel
                 outs = [self.full[r * n:(r + 1) * n] for r in range(self.world)]
                 dist.all_gather(outs, self.shard.data.clone(), group=self.pg)
@@ -246,11 +247,11 @@ class Zero3Partitioner:
         u.release()
         if self.world > 1:
             n = u.shard_numel
-            if _nccl(self.pg):
+            if _caps.tensor_collectives(self.pg, full_grad.device):
                 out = torch.empty(n, dtype=full_grad.dtype, device=full_grad.device)
                 work = dist.reduce_scatter_tensor(out, full_grad, op=dist.ReduceOp.SUM,
                                                   group=self.pg, async_op=True)
-            else:  # gloo has no reduce-scatter: all-reduce and keep the own slice
+            else:  # gloo on device tensors: all-reduce and keep the own slice
                 work = dist.all_reduce(full_grad, op=dist.ReduceOp.SUM, group=self.pg,
                                        async_op=True)
                 out = full_grad[u.rank * n:(u.rank + 1) * n]
@@ -338,10 +339,6 @@ class Zero3Partitioner:
         for h in self._handles:
             h.remove()
         self._handles = []
-
-
-def _nccl(pg: Any) -> bool:
-    return dist.get_backend(pg) == "nccl"
 
 
 def _tensors(x: Any) -> List[torch.Tensor]:

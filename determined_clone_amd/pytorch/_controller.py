@@ -678,6 +678,10 @@ class _PyTorchTrialController:
     def _save(self, path: pathlib.Path) -> None:
         path.mkdir(parents=True, exist_ok=True)
         util.write_user_code(path, not self.local_training)
+        for o in self.context.optimizers:  # ZeRO: parameter all-gathers may still be in flight
+            wait = getattr(o, "wait_params", None)
+            if wait is not None:
+                wait()
         ckpt: Dict[str, Any] = {
             "models_state_dict": [m.state_dict() for m in self.context.models],
             "optimizers_state_dict": [o.state_dict() for o in self.context.optimizers],

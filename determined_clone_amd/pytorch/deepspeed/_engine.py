@@ -20,7 +20,11 @@ Supported config keys: train_batch_size, train_micro_batch_size_per_gpu,
 gradient_accumulation_steps, optimizer {type: Adam|AdamW|SGD|Lamb, params}, scheduler
 {type: WarmupLR|WarmupDecayLR|WarmupCosineLR, params}, gradient_clipping, bf16.enabled,
 fp16 {enabled, loss_scale, initial_scale_power, loss_scale_window, min_loss_scale},
-zero_optimization {stage (0-3), reduce_bucket_size, allgather_bucket_size, overlap_comm}
+zero_optimization {stage (0-3), reduce_bucket_size, allgather_bucket_size, overlap_comm,
+overlap_param_gather (stages 1-2: the post-step parameter all-gather overlaps the next forward,
+module by module; parameters are then valid inside module forwards, ``state_dict`` and engine
+checkpoints, and any other direct read must call ``engine.wait_params()`` first -- off by
+default)}
 (stage 3: :mod:`determined_clone_amd.parallel.zero3`, per-module parameter gather /
 gradient reduce-scatter; the stage3_* tuning keys are accepted),
 steps_per_print. Unknown keys are accepted and ignored (with a debug log), like DeepSpeed's
@@ -100,6 +104,7 @@ class DeepSpeedConfig:
         self.reduce_bucket_size = int(z.get("reduce_bucket_size", 32 * 2 ** 20))  # elements
         self.allgather_bucket_size = int(z.get("allgather_bucket_size", 32 * 2 ** 20))
         self.overlap_comm = bool(z.get("overlap_comm", True))
+        self.overlap_param_gather = bool(z.get("overlap_param_gather", False))
         self.steps_per_print = int(c.get("steps_per_print", 10))
 
 
@@ -344,6 +349,9 @@ class DeepSpeedEngine(torch.nn.Module):
             esz = 2 if (cfg.bf16 or cfg.fp16) else 4
             opt = cls(groups, stage=stage, group=self.group, overlap_comm=cfg.overlap_comm,
                       bucket_mb=max(1.0, cfg.reduce_bucket_size * esz / 2 ** 20), **defaults)
+            if cfg.overlap_param_gather:
+                # the post-step parameter all-gather overlaps the next forward of this module
+                opt.attach_module(self.module)
             return opt
         cls = {"adam": fopt.FusedAdam, "adamw": fopt.FusedAdamW, "sgd": fopt.FusedSGD,
                "lamb": fopt.FusedLAMB}[kind]
@@ -468,10 +476,20 @@ class DeepSpeedEngine(torch.nn.Module):
     def zero_grad(self) -> None:
         self.optimizer.zero_grad()
 
+    def wait_params(self) -> None:
+        """Wait for parameter all-gathers still in flight (``overlap_param_gather``) before
+        reading parameters outside a module forward."""
+        wait = getattr(self.optimizer, "wait_params", None)
+        if wait is not None:
+            wait()
+
     def module_state_dict(self) -> Dict[str, torch.Tensor]:
         """The module's full state dict (under ZeRO-3 every rank must call it: it gathers)."""
         if self._z3 is not None:
             return self._z3.full_state_dict()
+        wait = getattr(self.optimizer, "wait_params", None)
+        if wait is not None:  # ZeRO-1/2: parameter all-gathers may still be in flight
+            wait()
         return self.module.state_dict()
 
     # ------------------------------------------------------------------ checkpoint

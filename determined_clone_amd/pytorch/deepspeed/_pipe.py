@@ -369,6 +369,9 @@ class PipelineEngine(DeepSpeedEngine):
         d = pathlib.Path(save_dir) / str(tag)
         d.mkdir(parents=True, exist_ok=True)
         dp = self.grid.data_parallel_id
+        wait = getattr(self.optimizer, "wait_params", None)
+        if wait is not None:  # ZeRO-1/2: parameter all-gathers may still be in flight
+            wait()
         if dp == 0:
             for idx, sd in self.module.layer_state_dicts().items():
                 torch.save(sd, d / f"layer_{idx:02d}{self._mp_tag('-model_')}-model_states.pt")

@@ -141,12 +141,13 @@ def test_warmup_schedulers():
 
 
 # ------------------------------------------------------------------ multi-process engine equivalence
-def _engine_worker(rank, world, port, stage, out):
+def _engine_worker(rank, world, port, stage, out, overlap=False):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
     model = gpt2.gpt2("tiny", n_layer=1)
-    cfg = dict(DS_CONFIG, zero_optimization={"stage": stage}, train_micro_batch_size_per_gpu=2)
+    cfg = dict(DS_CONFIG, zero_optimization={"stage": stage, "overlap_param_gather": overlap},
+               train_micro_batch_size_per_gpu=2)
     eng, _, _, _ = det_ds.initialize(model=model, config=cfg)
     ds = TokenDataset(32)
     for step in range(3):
@@ -181,10 +182,12 @@ def _single_reference(out):
     return eng
 
 
-@pytest.mark.parametrize("stage", [1, 2])
-def test_engine_zero_two_ranks_matches_single_process(stage):
+@pytest.mark.parametrize("stage,overlap", [(1, False), (2, False), (2, True)])
+def test_engine_zero_two_ranks_matches_single_process(stage, overlap):
+    """overlap=True: the post-step parameter all-gathers stay in flight into the next forward
+    (zero_optimization.overlap_param_gather) and are waited for module by module."""
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_engine_worker, args=(2, _free_port(), stage, d), nprocs=2, join=True)
+        mp.spawn(_engine_worker, args=(2, _free_port(), stage, d, overlap), nprocs=2, join=True)
         final = torch.load(os.path.join(d, "final.pt"), weights_only=True)
         ref = _single_reference(d + "/ref")
         for k, v in ref.module.state_dict().items():

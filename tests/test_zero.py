@@ -40,12 +40,30 @@ def _data():
 STEPS = 4
 
 
-def _worker(rank, world, port, stage, kind, max_norm, bucket_mb, out_dir):
+def _count_collectives():
+    """Wrap the tensor collectives so the test can assert which ones ran (the production RCCL
+    branch: in-place reduce_scatter_tensor / all_gather_into_tensor, not the list fallbacks)."""
+    dist = torch.distributed
+    calls = {"reduce_scatter_tensor": 0, "all_gather_into_tensor": 0, "all_gather": 0}
+    for name in calls:
+        fn = getattr(dist, name)
+
+        def wrapped(*a, __fn=fn, __name=name, **k):
+            calls[__name] += 1
+            return __fn(*a, **k)
+        setattr(dist, name, wrapped)
+    return calls
+
+
+def _worker(rank, world, port, stage, kind, max_norm, bucket_mb, out_dir, defer=False):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    calls = _count_collectives()
     m = _model()
     cls = zero.zero_optimizer_for(kind)
     opt = cls(_groups(m), lr=0.05, stage=stage, bucket_mb=bucket_mb, first_bucket_mb=bucket_mb / 4)
+    if defer:
+        opt.attach_module(m)  # the engines' mode: gathers overlap the next forward
     x, y = _data()
     per = x.shape[0] // world
     for _ in range(STEPS):
@@ -56,8 +74,11 @@ def _worker(rank, world, port, stage, kind, max_norm, bucket_mb, out_dir):
         if max_norm:
             opt.prepare_grads(max_norm=max_norm)
         opt.step()
+    if defer:
+        assert opt._gather_pending and opt._gather_hook is not None  # still in flight after step()
     torch.save({"params": {k: v.detach().clone() for k, v in m.state_dict().items()},
-                "opt": opt.state_dict()}, os.path.join(out_dir, f"r{rank}.pt"))
+                "opt": opt.state_dict(), "calls": calls,
+                "pending_after_save": len(opt._gather_pending)}, os.path.join(out_dir, f"r{rank}.pt"))
     torch.distributed.destroy_process_group()
 
 
@@ -77,22 +98,27 @@ def _reference(kind, max_norm):
     return m, opt
 
 
-@pytest.mark.parametrize("stage,kind,max_norm,bucket_mb", [
-    (1, "adam", 0.0, 64.0),
-    (2, "adam", 0.0, 0.002),   # many small buckets: hooks fire bucket by bucket
-    (2, "adamw", 0.05, 0.002),  # global-norm clipping across shards
-    (2, "sgd", 0.0, 0.001),
+@pytest.mark.parametrize("stage,kind,max_norm,bucket_mb,defer", [
+    (1, "adam", 0.0, 64.0, False),
+    (2, "adam", 0.0, 0.002, True),   # many small buckets: hooks fire bucket by bucket
+    (2, "adamw", 0.05, 0.002, False),  # global-norm clipping across shards
+    (2, "sgd", 0.0, 0.001, True),
 ])
-def test_zero_matches_full_batch(stage, kind, max_norm, bucket_mb):
+def test_zero_matches_full_batch(stage, kind, max_norm, bucket_mb, defer):
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), stage, kind, max_norm, bucket_mb, d),
+        mp.spawn(_worker, args=(world, _free_port(), stage, kind, max_norm, bucket_mb, d, defer),
                  nprocs=world, join=True)
         ref, ref_opt = _reference(kind, max_norm)
         outs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
     for k, v in ref.state_dict().items():
         for o in outs:
             torch.testing.assert_close(o["params"][k], v, atol=1e-5, rtol=1e-5)
+    for o in outs:
+        # gloo on host tensors runs the same in-place collectives as RCCL (parallel/_caps.py)
+        assert o["calls"]["all_gather_into_tensor"] > 0 and o["calls"]["all_gather"] == 0, o["calls"]
+        assert (o["calls"]["reduce_scatter_tensor"] > 0) == (stage >= 2), o["calls"]
+        assert o["pending_after_save"] == 0
     # re-partition: both shards loaded into a single-rank ZeRO optimizer reproduce the
     # full optimizer state of the reference
     if kind != "sgd":
@@ -130,3 +156,51 @@ def test_single_rank_zero_equals_fused():
 def test_lamb_rejected():
     with pytest.raises(ValueError):
         zero.zero_optimizer_for("lamb")
+
+
+def _rs_worker(rank, world, port, out_dir):
+    """In-place bucket reduce-scatter exactly as ZeroShardMixin._launch issues it: the output is
+    the rank's own chunk of the bucket, a view into the reduced input."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    from determined_clone_amd.parallel import _caps
+
+    assert _caps.tensor_collectives(None, torch.device("cpu"))
+    chunk = 5
+    res = {}
+    for start in (0, 3):  # a bucket at offset 0 and one further into the flat buffer
+        flat = torch.arange(40, dtype=torch.float32) + 1000 * rank
+        full = flat[start:start + world * chunk]
+        out = full[rank * chunk:(rank + 1) * chunk]
+        before = flat.clone()
+        torch.distributed.reduce_scatter_tensor(out, full, op=torch.distributed.ReduceOp.SUM,
+                                                async_op=True).wait()
+        res[start] = (flat.clone(), before)
+    t = torch.tensor([float(rank + 1)])
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.AVG)
+    res["avg"] = t
+    torch.save(res, os.path.join(out_dir, f"rs{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_inplace_reduce_scatter_offsets_per_bucket(world):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rs_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        outs = [torch.load(os.path.join(d, f"rs{r}.pt"), weights_only=True) for r in range(world)]
+    chunk = 5
+    for r, o in enumerate(outs):
+        for start in (0, 3):
+            after, before = o[start]
+            lo, hi = start + r * chunk, start + (r + 1) * chunk
+            # own chunk == sum over ranks of that chunk; everything else untouched
+            want = sum(outs[q][start][1][lo:hi] for q in range(world))
+            torch.testing.assert_close(after[lo:hi], want)
+            mask = torch.ones(40, dtype=torch.bool)
+            mask[lo:hi] = False
+            torch.testing.assert_close(after[mask], before[mask])
+            # output = input + rank * chunk: the value at chunk offset i is the sum of element
+            # (start + r*chunk + i) over ranks
+            base = torch.arange(40, dtype=torch.float32)[lo:hi]
+            torch.testing.assert_close(after[lo:hi], world * base + 1000 * sum(range(world)))
+        torch.testing.assert_close(o["avg"], torch.tensor([(world + 1) / 2]))

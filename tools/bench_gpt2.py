@@ -45,6 +45,7 @@ class GPT2BenchTrial(det_ds.DeepSpeedTrial):
             "gradient_clipping": 1.0,
             "bf16": {"enabled": True},
             "zero_optimization": {"stage": int(hp["stage"]), "overlap_comm": True,
+                                  "overlap_param_gather": True,
                                   "reduce_bucket_size": int(hp.get("bucket_elems", 5e7))},
         }
         engine, _, _, _ = det_ds.initialize(model=self.model, config=ds_config)
