@@ -1,0 +1,958 @@
+"""Expconf v0 schema engine: sanity / completeness validation, defaults, merging.
+
+Reference: the JSON-schema dialect of ``schemas/expconf/v0/*.json`` (draft-07 plus the custom
+keywords ``eventuallyRequired``, ``checks``, ``compareProperties``, ``union``, ``optionalRef``,
+``disallowProperties``) and the Go structs that consume it (``master/pkg/schemas/expconf``:
+``schemas.WithDefaults`` / ``schemas.Merge`` / JSON marshalling with ``omitempty``). No JSON-schema
+library is installed here, so the schema is expressed as a tree of small Python spec objects, each
+able to
+
+* ``check(value, path, errors, complete)`` -- SANITY (``complete=False``: types, ranges, patterns,
+  custom checks, hard ``required``) or COMPLETENESS (``complete=True``: additionally every
+  ``eventuallyRequired`` field present and the ``eventually`` checks);
+* ``defaults(value)`` -- fill schema defaults the way ``schemas.WithDefaults`` fills nil pointers
+  (legacy shapes such as a plain image string or ``gpu:`` keys normalised on the way);
+* ``marshal(value)`` -- the JSON the Go struct would produce (all struct fields, ``omitempty``
+  ones dropped when nil; unknown/ignored keys such as ``data_layer`` gone);
+* ``merge(obj, src)`` -- ``schemas.Merge``: ``obj`` wins, nil fields come from ``src``, structs
+  merge recursively, bind mounts / devices append unique container paths, unions merge only
+  within the same member (plus their common fields).
+
+Error strings follow the reference's rendering (``<config>.a.b[2]: message``) so the reference's
+shared test vectors (``schemas/test_cases/v0``, ported in ``tests/fixtures/expconf_v0``) apply
+unchanged. ``URLS`` maps each schema URL the vectors name to its spec.
+"""
+import copy
+import posixpath
+import re
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
+
+PREFIX = "http://determined.ai/schemas/expconf/v0/"
+MISSING = object()
+
+
+def _tname(v: Any) -> str:
+    if v is None:
+        return "null"
+    if isinstance(v, bool):
+        return "boolean"
+    if isinstance(v, int):
+        return "integer"
+    if isinstance(v, float):
+        return "number"
+    if isinstance(v, str):
+        return "string"
+    if isinstance(v, list):
+        return "array"
+    if isinstance(v, dict):
+        return "object"
+    return type(v).__name__
+
+
+def _is(v: Any, t: str) -> bool:
+    if t == "null":
+        return v is None
+    if t == "boolean":
+        return isinstance(v, bool)
+    if t == "integer":
+        return (isinstance(v, int) and not isinstance(v, bool)) or (isinstance(v, float) and v.is_integer())
+    if t == "number":
+        return isinstance(v, (int, float)) and not isinstance(v, bool)
+    if t == "string":
+        return isinstance(v, str)
+    if t == "array":
+        return isinstance(v, list)
+    if t == "object":
+        return isinstance(v, dict)
+    return True
+
+
+def _sub(path: str, key: Any) -> str:
+    return f"{path}[{key}]" if isinstance(key, int) else f"{path}.{key}"
+
+
+Check = Tuple[str, Callable[[Any], bool]]  # (message, predicate that is True when VALID)
+
+
+class Spec:
+    def check(self, v: Any, path: str, errs: List[str], complete: bool) -> None:
+        raise NotImplementedError
+
+    def defaults(self, v: Any) -> Any:
+        return v
+
+    def marshal(self, v: Any) -> Any:
+        return v
+
+    def merge(self, obj: Any, src: Any) -> Any:
+        return src if obj is None else obj
+
+
+class AnyV(Spec):
+    def check(self, v, path, errs, complete):
+        pass
+
+
+class Scalar(Spec):
+    """A leaf value: JSON types (``"null"`` allowed iff listed), numeric bounds, enum, checks."""
+
+    def __init__(self, *types: str, minimum: Optional[float] = None, xminimum: Optional[float] = None,
+                 maximum: Optional[float] = None, enum: Optional[Sequence[Any]] = None,
+                 checks: Sequence[Check] = ()) -> None:
+        self.types = types or ("string",)
+        self.minimum, self.xminimum, self.maximum = minimum, xminimum, maximum
+        self.enum = enum
+        self.checks = list(checks)
+
+    def check(self, v, path, errs, complete):
+        if self.enum is not None:
+            if v not in self.enum:
+                errs.append(f"{path}: must be one of {', '.join(repr(e) for e in self.enum if e is not None)}")
+            return
+        if not any(_is(v, t) for t in self.types):
+            errs.append(f"{path}: expected {' or '.join(self.types)}, but got {_tname(v)}")
+            return
+        if v is None:
+            return
+        if self.minimum is not None and _is(v, "number") and v < self.minimum:
+            errs.append(f"{path}: must be >= {self.minimum} but found {v}")
+        if self.xminimum is not None and _is(v, "number") and v <= self.xminimum:
+            errs.append(f"{path}: must be > {self.xminimum} but found {v}")
+        if self.maximum is not None and _is(v, "number") and v > self.maximum:
+            errs.append(f"{path}: must be <= {self.maximum} but found {v}")
+        for msg, ok in self.checks:
+            if not ok(v):
+                errs.append(f"{path}: {msg}")
+
+
+def S(*types, **kw) -> Scalar:
+    return Scalar(*types, **kw)
+
+
+class ListOf(Spec):
+    def __init__(self, item: Spec, nullable: bool = True, unique_key: Optional[str] = None) -> None:
+        self.item, self.nullable, self.unique_key = item, nullable, unique_key
+
+    def check(self, v, path, errs, complete):
+        if v is None and self.nullable:
+            return
+        if not isinstance(v, list):
+            errs.append(f"{path}: expected array, but got {_tname(v)}")
+            return
+        for i, x in enumerate(v):
+            self.item.check(x, _sub(path, i), errs, complete)
+
+    def defaults(self, v):
+        return None if v is None else [self.item.defaults(x) for x in v]
+
+    def marshal(self, v):
+        return None if v is None else [self.item.marshal(x) for x in v]
+
+    def merge(self, obj, src):
+        """Bind mounts / devices: src entries whose ``unique_key`` obj does not use are appended
+        (reference bind_mounts / devices Merge)."""
+        if obj is None:
+            return copy.deepcopy(src)
+        if src is None or self.unique_key is None:
+            return obj
+        norm = getattr(self.item, "normalize", lambda x: x)
+        seen = {norm(x).get(self.unique_key) for x in obj}
+        return list(obj) + [x for x in src if norm(x).get(self.unique_key) not in seen]
+
+
+class MapOf(Spec):
+    """Object whose every value matches ``value`` (hyperparameters, ports)."""
+
+    def __init__(self, value: Spec) -> None:
+        self.value = value
+
+    def check(self, v, path, errs, complete):
+        if v is None:
+            return
+        if not isinstance(v, dict):
+            errs.append(f"{path}: expected object, but got {_tname(v)}")
+            return
+        for k, x in v.items():
+            self.value.check(x, _sub(path, k), errs, complete)
+
+    def defaults(self, v):
+        return None if v is None else {k: self.value.defaults(x) for k, x in v.items()}
+
+    def marshal(self, v):
+        return None if v is None else {k: self.value.marshal(x) for k, x in v.items()}
+
+    def merge(self, obj, src):
+        if obj is None:
+            return copy.deepcopy(src)
+        if src is None:
+            return obj
+        out = dict(obj)
+        for k, x in src.items():
+            out[k] = self.value.merge(out[k], x) if k in out else copy.deepcopy(x)
+        return out
+
+
+class F:
+    """One struct field. ``default``: the schema default (MISSING = none); ``omitempty``: the Go
+    field is dropped from the marshalled JSON when nil; ``go=False``: accepted by the schema but
+    not part of the struct (never marshalled); ``runtime``: filled at runtime by the master
+    (e.g. a random experiment name), rendered as a non-null placeholder by :meth:`Obj.defaults`."""
+
+    def __init__(self, name: str, spec: Spec, default: Any = MISSING, omitempty: bool = False,
+                 go: bool = True, runtime: Any = MISSING) -> None:
+        self.name, self.spec, self.default = name, spec, default
+        self.omitempty, self.go, self.runtime = omitempty, go, runtime
+
+
+class Obj(Spec):
+    def __init__(self, fields: Sequence[F], required: Sequence[str] = (),
+                 eventually: Sequence[str] = (), checks: Sequence[Check] = (),
+                 eventually_checks: Sequence[Check] = (), extra: bool = False,
+                 nullable: bool = True, disallow: Optional[Dict[str, str]] = None) -> None:
+        self.fields = {f.name: f for f in fields}
+        self.required, self.eventually = list(required), list(eventually)
+        self.checks, self.eventually_checks = list(checks), list(eventually_checks)
+        self.extra, self.nullable, self.disallow = extra, nullable, disallow or {}
+
+    def check(self, v, path, errs, complete):
+        if v is None and self.nullable:
+            return
+        if not isinstance(v, dict):
+            errs.append(f"{path}: expected object, but got {_tname(v)}")
+            return
+        for k in v:
+            if k in self.disallow:
+                errs.append(f"{_sub(path, k)}: {self.disallow[k]}")
+            elif k not in self.fields and not self.extra:
+                errs.append(f"{path}: additional property {k} is not allowed")
+        for k in self.required:
+            if k not in v:
+                errs.append(f"{path}: {k} is a required property")
+        if complete:
+            for k in self.eventually:
+                if v.get(k) is None:
+                    errs.append(f"{path}: {k} is a required property")
+            for msg, ok in self.eventually_checks:
+                if not ok(v):
+                    errs.append(f"{path}: {msg}")
+        for k, x in v.items():
+            f = self.fields.get(k)
+            if f is not None:
+                f.spec.check(x, _sub(path, k), errs, complete)
+        for msg, ok in self.checks:
+            if not ok(v):
+                errs.append(f"{path}: {msg}")
+
+    def defaults(self, v):
+        if v is None:
+            return None
+        out = {}
+        for name, f in self.fields.items():
+            x = v.get(name)
+            if x is None and f.default is not MISSING:
+                x = copy.deepcopy(f.default)
+            if x is None and f.runtime is not MISSING:
+                x = f.runtime() if callable(f.runtime) else copy.deepcopy(f.runtime)
+            out[name] = f.spec.defaults(x) if x is not None else None
+        if self.extra:
+            out.update({k: x for k, x in v.items() if k not in self.fields})
+        return out
+
+    def marshal(self, v):
+        if v is None:
+            return None
+        out = {}
+        for name, f in self.fields.items():
+            if not f.go:
+                continue
+            x = v.get(name)
+            if x is None and f.omitempty:
+                continue
+            out[name] = f.spec.marshal(x) if x is not None else None
+        if self.extra:
+            out.update({k: x for k, x in v.items() if k not in self.fields})
+        return out
+
+    def merge(self, obj, src):
+        if obj is None:
+            return copy.deepcopy(src)
+        if not isinstance(src, dict):
+            return obj
+        out = dict(obj)
+        for name, f in self.fields.items():
+            o, s = obj.get(name), src.get(name)
+            if s is None:
+                continue
+            out[name] = copy.deepcopy(s) if o is None else f.spec.merge(o, s)
+        return out
+
+
+class Union(Spec):
+    """Discriminated union on ``key`` (searcher ``name``, storage ``type``, ...). Without the key,
+    only the union's common properties are validated (reference ``if: required: [key]``);
+    merging keeps obj's member and takes ``common`` fields from any src."""
+
+    def __init__(self, key: str, members: Dict[str, Obj], message: str, common: Sequence[str] = (),
+                 all_props: Sequence[str] = (), common_specs: Optional[Dict[str, F]] = None,
+                 eventually: Sequence[str] = ()) -> None:
+        self.key, self.members, self.message = key, members, message
+        self.common = list(common)
+        self.all_props = set(all_props) | {key}
+        for m in members.values():
+            self.all_props |= set(m.fields)
+        self.common_specs = common_specs or {}
+        self.eventually = list(eventually) or [key]
+
+    def member(self, v: Any) -> Optional[Obj]:
+        return self.members.get(v.get(self.key)) if isinstance(v, dict) else None
+
+    def check(self, v, path, errs, complete):
+        if v is None:
+            return
+        if not isinstance(v, dict):
+            errs.append(f"{path}: expected object, but got {_tname(v)}")
+            return
+        for k in v:
+            if k not in self.all_props:
+                errs.append(f"{path}: additional property {k} is not allowed")
+        if complete:
+            for k in self.eventually:
+                if v.get(k) is None:
+                    errs.append(f"{path}: {k} is a required property")
+        if self.key in v:
+            m = self.member(v)
+            if m is None:
+                errs.append(f"{path}: {self.message}")
+            else:
+                m.check(v, path, errs, complete)
+        else:
+            for k, f in self.common_specs.items():
+                if k in v:
+                    f.spec.check(v[k], _sub(path, k), errs, complete)
+
+    def defaults(self, v):
+        m = self.member(v)
+        return m.defaults(v) if m is not None else v
+
+    def marshal(self, v):
+        m = self.member(v)
+        if m is None:
+            return v
+        out = m.marshal(v)
+        return out
+
+    def merge(self, obj, src):
+        if obj is None:
+            return copy.deepcopy(src)
+        if not isinstance(src, dict):
+            return obj
+        m = self.member(obj)
+        if m is None:
+            return obj
+        if src.get(self.key) in (None, obj.get(self.key)):
+            return m.merge(obj, src)
+        return m.merge(obj, {k: src[k] for k in self.common if k in src})
+
+
+# ----------------------------------------------------------------------------------- checks
+def _compare(a: str, b: str, op: str) -> Callable[[Dict[str, Any]], bool]:
+    def ok(v: Dict[str, Any]) -> bool:
+        x, y = v.get(a), v.get(b)
+        if not (_is(x, "number") and _is(y, "number")):
+            return True
+        return x < y if op == "<" else x <= y
+    return ok
+
+
+def _subdir_ok(v: Dict[str, Any]) -> bool:
+    """``storage_path`` is relative without escaping, or absolute inside ``host_path``."""
+    sp, hp = v.get("storage_path"), v.get("host_path")
+    if not isinstance(sp, str):
+        return True
+    if sp.startswith("/"):
+        if not isinstance(hp, str):
+            return True
+        rel = posixpath.relpath(posixpath.normpath(sp), posixpath.normpath(hp))
+        return rel != ".." and not rel.startswith("../")
+    n = posixpath.normpath(sp)
+    return n != ".." and not n.startswith("../")
+
+
+_PREFIX_BAD = re.compile(r"/\.\./|^\.\./|/\.\.$|^\.\.$")
+
+
+def _prefix_ok(p: Any) -> bool:
+    return not (isinstance(p, str) and _PREFIX_BAD.search(p))
+
+
+_MEM = re.compile(r"^([0-9]*[.])?[0-9]+ ?(([kmgtpKMGTP]([iI]?[bB])?)|[bB])?$")
+
+
+def memory_size_ok(v: Any) -> bool:
+    return not isinstance(v, str) or bool(_MEM.match(v))
+
+
+def parse_memory_size(v: Any) -> Optional[int]:
+    """``shm_size`` in bytes: an integer is bytes; strings like ``1.5 gb`` / ``512Mi`` / ``10 b``."""
+    if v is None:
+        return None
+    if isinstance(v, (int, float)) and not isinstance(v, bool):
+        return int(v)
+    m = _MEM.match(str(v))
+    if not m:
+        raise ValueError(f"invalid memory size {v!r}")
+    num = float(str(v)[:m.start(2)] if m.group(2) else str(v))
+    unit = (m.group(2) or "").lower()
+    if unit in ("", "b"):
+        return int(num)
+    mult = {"k": 1, "m": 2, "g": 3, "t": 4, "p": 5}[unit[0]]
+    base = 1024 if "i" in unit else 1000
+    return int(num * base ** mult)
+
+
+# ----------------------------------------------------------------------------------- leaves
+Str, NStr = S("string"), S("string", "null")
+NInt, NBool, NNum = S("integer", "null"), S("boolean", "null"), S("number", "null")
+
+
+def NIntMin(m: float) -> Scalar:
+    return S("integer", "null", minimum=m)
+
+
+SAVE_FIELDS = [F("save_experiment_best", NIntMin(0), 0), F("save_trial_best", NIntMin(0), 1),
+               F("save_trial_latest", NIntMin(0), 1)]
+
+# ----------------------------------------------------------------------------------- length
+LENGTH_MSG = 'a length object must have one attribute named "batches", "records", or "epochs"'
+LENGTH_UNITS = ("batches", "records", "epochs")
+
+
+class Length(Spec):
+    """``{batches|records|epochs: N}`` (exactly one key), N >= ``minimum``."""
+
+    def __init__(self, minimum: int = 0) -> None:
+        self.minimum = minimum
+
+    def check(self, v, path, errs, complete):
+        if v is None:
+            return
+        if not isinstance(v, dict) or len(v) != 1 or next(iter(v)) not in LENGTH_UNITS:
+            errs.append(f"{path}: {LENGTH_MSG}")
+            return
+        (k, n), = v.items()
+        S("integer", minimum=self.minimum).check(n, _sub(path, k), errs, complete)
+
+
+class SearcherLength(Spec):
+    """``max_length``: a Length (each value >= 1) or a bare integer >= 0 (legacy, unitless)."""
+
+    def check(self, v, path, errs, complete):
+        if v is None or (isinstance(v, dict)):
+            Length(1).check(v, path, errs, complete)
+        else:
+            S("integer", minimum=0).check(v, path, errs, complete)
+
+
+# ----------------------------------------------------------------------------------- hparams
+HP_TYPES = ("int", "double", "log", "const", "categorical")
+
+HP_MEMBERS = {
+    "int": Obj([F("type", Str), F("minval", S("integer")), F("maxval", S("integer")),
+                F("count", NIntMin(1), omitempty=True)], required=("type", "minval", "maxval"),
+               checks=[("minval must be less than maxval", _compare("minval", "maxval", "<"))],
+               nullable=False),
+    "double": Obj([F("type", Str), F("minval", S("number")), F("maxval", S("number")),
+                   F("count", NIntMin(1), omitempty=True)], required=("type", "minval", "maxval"),
+                  checks=[("minval must be less than maxval", _compare("minval", "maxval", "<"))],
+                  nullable=False),
+    "log": Obj([F("type", Str), F("minval", S("number")), F("maxval", S("number")),
+                F("base", S("number", xminimum=0)), F("count", NIntMin(1), omitempty=True)],
+               required=("type", "minval", "maxval", "base"),
+               checks=[("minval must be less than maxval", _compare("minval", "maxval", "<"))],
+               nullable=False),
+    "const": Obj([F("type", Str), F("val", AnyV())], required=("type", "val"), nullable=False),
+    "categorical": Obj([F("type", Str), F("vals", ListOf(AnyV(), nullable=False))],
+                       required=("type", "vals"),
+                       checks=[("vals must not be empty", lambda v: not isinstance(v.get("vals"), list)
+                                or len(v["vals"]) > 0)], nullable=False),
+}
+
+
+class Hyperparameter(Spec):
+    """A hyperparameter: typed (``type`` one of HP_TYPES), a nested group (an object without
+    ``type``) or an implicit constant (anything else)."""
+
+    def check(self, v, path, errs, complete):
+        if not isinstance(v, dict):
+            return  # implicit const
+        if "type" not in v:
+            for k, x in v.items():
+                self.check(x, _sub(path, k), errs, complete)
+            return
+        m = HP_MEMBERS.get(v["type"]) if isinstance(v["type"], str) else None
+        if m is None:
+            errs.append(f"{path}: if a hyperparameter object's [\"type\"] is set, it must be one of "
+                        "\"int\", \"double\", \"log\", const\", or \"categorical\"")
+            return
+        m.check(v, path, errs, complete)
+
+    @staticmethod
+    def normalize(v: Any) -> Any:
+        if not isinstance(v, dict):
+            return {"type": "const", "val": v}
+        if "type" not in v:
+            return {k: Hyperparameter.normalize(x) for k, x in v.items()}
+        return v
+
+    def defaults(self, v):
+        return self.normalize(v)
+
+    def marshal(self, v):
+        v = self.normalize(v)
+        if "type" not in v or not isinstance(v.get("type"), str):
+            return {k: self.marshal(x) for k, x in v.items()}
+        m = HP_MEMBERS.get(v["type"])
+        return m.marshal(v) if m is not None else v
+
+    def merge(self, obj, src):
+        o, s = self.normalize(obj), self.normalize(src)
+        nested = lambda x: isinstance(x, dict) and "type" not in x  # noqa: E731
+        if nested(o) and nested(s):
+            out = dict(o)
+            for k, x in s.items():
+                out[k] = self.merge(out[k], x) if k in out else x
+            return out
+        return o
+
+
+class GridCheck(Spec):
+    """check-grid-hyperparameter: under grid search every int/double/log needs ``count``."""
+
+    def check(self, v, path, errs, complete):
+        if isinstance(v, list):
+            for i, x in enumerate(v):
+                self.check(x, _sub(path, i), errs, complete)
+        elif isinstance(v, dict):
+            if "type" not in v:
+                for k, x in v.items():
+                    self.check(x, _sub(path, k), errs, complete)
+            elif v.get("type") in ("double", "log", "int") and v.get("count") is None:
+                errs.append(f"{path}: grid search is in use but count was not provided")
+
+
+# ----------------------------------------------------------------------------------- storage
+def _storage(t: str, fields: List[F], eventually: Sequence[str] = (), checks: Sequence[Check] = (),
+             eventually_checks: Sequence[Check] = ()) -> Obj:
+    return Obj([F("type", S("string"))] + fields + SAVE_FIELDS, required=("type",),
+               eventually=eventually, checks=checks, eventually_checks=eventually_checks,
+               nullable=False)
+
+
+PREFIX_CHECK: Check = ("prefix cannot contain /../", _prefix_ok)
+SHARED_FS = _storage("shared_fs", [
+    F("host_path", NStr), F("container_path", NStr, omitempty=True),
+    F("checkpoint_path", NStr, omitempty=True), F("tensorboard_path", NStr, omitempty=True),
+    F("storage_path", NStr), F("propagation", NStr, "rprivate")], eventually=("host_path",),
+    checks=[("storage_path must either be a relative directory or a subdirectory of host_path",
+             _subdir_ok)])
+S3 = _storage("s3", [F("bucket", NStr), F("access_key", NStr), F("secret_key", NStr),
+                     F("endpoint_url", NStr), F("prefix", S("string", "null", checks=[PREFIX_CHECK]))],
+              eventually=("bucket",))
+GCS = _storage("gcs", [F("bucket", NStr), F("prefix", S("string", "null", checks=[PREFIX_CHECK]))],
+               eventually=("bucket",))
+AZURE = _storage("azure", [
+    F("container", NStr), F("connection_string", NStr, omitempty=True),
+    F("account_url", NStr, omitempty=True), F("credential", NStr, omitempty=True)],
+    eventually=("container",),
+    checks=[("credential and connection_string must not both be set",
+             lambda v: not (isinstance(v.get("connection_string"), str) and isinstance(v.get("credential"), str)))],
+    eventually_checks=[("Exactly one of connection_string or account_url must be set",
+                        lambda v: (v.get("connection_string") is not None) != (v.get("account_url") is not None))])
+DIRECTORY = _storage("directory", [F("container_path", NStr)], eventually=("container_path",))
+STORAGE_MEMBERS = {"shared_fs": SHARED_FS, "directory": DIRECTORY, "s3": S3, "gcs": GCS, "azure": AZURE}
+CHECKPOINT_STORAGE = Union(
+    "type", STORAGE_MEMBERS,
+    "is not an object where object[\"type\"] is one of 'shared_fs', 'directory', 's3', 'gcs', or 'azure'",
+    common=[f.name for f in SAVE_FIELDS], all_props=("user",),
+    common_specs={f.name: f for f in SAVE_FIELDS})
+
+
+class TensorboardStorage(Spec):
+    """Deprecated and ignored (reference tensorboard-storage.json): shared_fs / s3 / gcs shapes
+    are accepted, the save_* keys are disallowed."""
+
+    def check(self, v, path, errs, complete):
+        if v is None:
+            return
+        if not isinstance(v, dict):
+            errs.append(f"{path}: expected object, but got {_tname(v)}")
+            return
+        for k in ("save_experiment_best", "save_trial_best", "save_trial_latest"):
+            if k in v:
+                errs.append(f"{_sub(path, k)}: this field is deprecated and will be ignored")
+        m = {"shared_fs": SHARED_FS, "s3": S3, "gcs": GCS}.get(v.get("type"))
+        if m is None:
+            errs.append(f"{path}: this field is deprecated and will be ignored")
+
+
+# ----------------------------------------------------------------------------------- searcher
+SEARCHER_COMMON = [F("metric", NStr), F("smaller_is_better", NBool, True),
+                   F("source_trial_id", NInt), F("source_checkpoint_uuid", NStr)]
+MODE = S(enum=(None, "aggressive", "standard", "conservative"))
+DIVISOR = S("number", "null", xminimum=1)
+
+
+def _searcher(name: str, fields: List[F], eventually: Sequence[str], extra: bool = False) -> Obj:
+    return Obj([F("name", S("string"))] + fields + SEARCHER_COMMON, required=("name",),
+               eventually=eventually, extra=extra, nullable=False)
+
+
+POS_LENGTH = Length(1)
+SEARCHER_MEMBERS = {
+    "single": _searcher("single", [F("max_length", SearcherLength())], ("max_length", "metric")),
+    "random": _searcher("random", [F("max_trials", NIntMin(1)), F("max_length", SearcherLength()),
+                                   F("max_concurrent_trials", NIntMin(0), 16)],
+                        ("max_trials", "max_length", "metric")),
+    "grid": _searcher("grid", [F("max_length", SearcherLength()),
+                               F("max_concurrent_trials", NIntMin(0), 16)], ("max_length", "metric")),
+    "async_halving": _searcher("async_halving", [
+        F("num_rungs", NIntMin(1)), F("max_length", POS_LENGTH), F("max_trials", NIntMin(1)),
+        F("divisor", DIVISOR, 4), F("max_concurrent_trials", NIntMin(0), 16),
+        F("stop_once", NBool, False)], ("num_rungs", "max_length", "max_trials", "metric")),
+    "adaptive_asha": _searcher("adaptive_asha", [
+        F("max_length", SearcherLength()), F("max_trials", NIntMin(1)),
+        F("bracket_rungs", ListOf(S("integer")), []), F("divisor", DIVISOR, 4), F("mode", MODE, "standard"),
+        F("max_rungs", NIntMin(1), 5), F("max_concurrent_trials", NIntMin(0), 16),
+        F("stop_once", NBool, False)], ("max_length", "max_trials", "metric")),
+    "custom": Obj([F("name", S("string")), F("metric", NStr), F("smaller_is_better", NBool, True),
+                   F("unit", S(enum=("batches", "records", "epochs", None)))],
+                  required=("name",), eventually=("metric",), extra=True, nullable=False),
+    # end-of-life searchers: still parsed (old experiments), not runnable
+    "sync_halving": _searcher("sync_halving", [
+        F("num_rungs", NIntMin(1)), F("max_length", POS_LENGTH), F("budget", POS_LENGTH),
+        F("divisor", DIVISOR, 4), F("train_stragglers", NBool, True)],
+        ("num_rungs", "max_length", "budget", "metric")),
+    "adaptive": _searcher("adaptive", [
+        F("max_length", POS_LENGTH), F("budget", Length(0)), F("bracket_rungs", ListOf(S("integer")), []),
+        F("divisor", DIVISOR, 4), F("train_stragglers", NBool, True), F("mode", MODE, "standard"),
+        F("max_rungs", NIntMin(1), 5)], ("budget", "max_length", "metric")),
+    "adaptive_simple": _searcher("adaptive_simple", [
+        F("max_length", POS_LENGTH), F("max_trials", S("integer", "null", minimum=1, maximum=2000)),
+        F("max_rungs", NIntMin(1), 5), F("divisor", DIVISOR, 4), F("mode", MODE, "standard")],
+        ("max_trials", "max_length", "metric")),
+}
+SEARCHER = Union(
+    "name", SEARCHER_MEMBERS,
+    "is not an object where object[\"name\"] is one of 'single', 'random', 'grid', 'custom', or 'adaptive_asha'",
+    common=[f.name for f in SEARCHER_COMMON], common_specs={f.name: f for f in SEARCHER_COMMON},
+    eventually=("name", "metric"))
+
+# ----------------------------------------------------------------------------------- environment
+GPU_FLAVOURS = ("cpu", "cuda", "rocm")
+# runtime default images (the master's task-container defaults fill them; MI355X: ROCm 7)
+DEFAULT_IMAGES = {"cpu": "determined-clone-amd/environments:py-3.10-cpu",
+                  "cuda": "determined-clone-amd/environments:py-3.10-rocm-7.2-gfx950",
+                  "rocm": "determined-clone-amd/environments:py-3.10-rocm-7.2-gfx950"}
+
+
+class EnvImage(Spec):
+    """A string (every flavour) or ``{cpu, cuda, rocm}`` (legacy ``gpu`` = cuda)."""
+
+    MAP = Obj([F(k, NStr) for k in GPU_FLAVOURS + ("gpu",)], eventually=GPU_FLAVOURS, nullable=False)
+
+    def check(self, v, path, errs, complete):
+        if v is None or isinstance(v, str):
+            return
+        if not isinstance(v, dict):
+            errs.append(f"{path}: is neither a string nor a map of cpu, cuda, or rocm to strings")
+            return
+        self.MAP.check(v, path, errs, False)
+
+    @staticmethod
+    def normalize(v: Any) -> Dict[str, Any]:
+        if isinstance(v, str):
+            return {k: v for k in GPU_FLAVOURS}
+        v = dict(v or {})
+        if v.get("cuda") is None and v.get("gpu") is not None:
+            v["cuda"] = v["gpu"]
+        return {k: v.get(k) for k in GPU_FLAVOURS}
+
+    def defaults(self, v):
+        out = self.normalize(v)
+        for k in GPU_FLAVOURS:
+            if out[k] is None:
+                out[k] = DEFAULT_IMAGES[k]
+        return out
+
+    def marshal(self, v):
+        return self.normalize(v)
+
+    def merge(self, obj, src):
+        if obj is None:
+            return copy.deepcopy(src)
+        o = self.normalize(obj)
+        s = self.normalize(src) if src is not None else {}
+        return {k: o[k] if o[k] is not None else s.get(k) for k in GPU_FLAVOURS}
+
+
+class EnvVars(Spec):
+    """A list of ``NAME=value`` strings (every flavour) or ``{cpu, cuda, rocm}`` lists (legacy
+    ``gpu`` = cuda)."""
+
+    MAP = Obj([F(k, ListOf(S("string"))) for k in GPU_FLAVOURS + ("gpu",)], nullable=False)
+
+    def check(self, v, path, errs, complete):
+        if v is None:
+            return
+        if isinstance(v, list):
+            ListOf(S("string")).check(v, path, errs, complete)
+        elif isinstance(v, dict):
+            self.MAP.check(v, path, errs, complete)
+        else:
+            errs.append(f"{path}: is neither a list of strings nor a map of cpu, cuda, or rocm to lists of strings")
+
+    @staticmethod
+    def normalize(v: Any) -> Dict[str, List[str]]:
+        if v is None:
+            return {k: [] for k in GPU_FLAVOURS}
+        if isinstance(v, list):
+            return {k: list(v) for k in GPU_FLAVOURS}
+        v = dict(v)
+        if v.get("cuda") is None and v.get("gpu") is not None:
+            v["cuda"] = v["gpu"]
+        return {k: list(v.get(k) or []) for k in GPU_FLAVOURS}
+
+    def defaults(self, v):
+        return self.normalize(v)
+
+    def marshal(self, v):
+        return self.normalize(v)
+
+    def merge(self, obj, src):
+        """Append: src's entries first, obj's after (later entries override when applied)."""
+        if obj is None:
+            return copy.deepcopy(src)
+        o, s = self.normalize(obj), self.normalize(src)
+        return {k: s[k] + o[k] for k in GPU_FLAVOURS}
+
+
+REGISTRY_AUTH = Obj([F(k, NStr, omitempty=True) for k in (
+    "username", "password", "auth", "email", "serveraddress", "identitytoken", "registrytoken")])
+PROXY_PORT = Obj([F("proxy_port", S("number")), F("proxy_tcp", NBool, False),
+                  F("unauthenticated", NBool, False), F("default_service_id", NBool, False)],
+                 required=("proxy_port",), nullable=False)
+_CONTAINER_DISALLOW = {
+    "image": "container Image is not configurable, set it in the experiment config",
+    "command": "container Command is not configurable", "args": "container Args are not configurable",
+    "working_dir": "container WorkingDir is not configurable", "ports": "container Ports are not configurable",
+    "liveness_probe": "container LivenessProbe is not configurable",
+    "readiness_probe": "container ReadinessProbe is not configurable",
+    "startup_probe": "container StartupProbe is not configurable",
+    "lifecycle": "container Lifecycle is not configurable",
+    "termination_message_path": "container TerminationMessagePath is not configurable",
+    "termination_message_policy": "container TerminationMessagePolicy is not configurable",
+    "image_pull_policy": "container ImagePullPolicy is not configurable, set it in the experiment config",
+    "security_context": "container SecurityContext is not configurable, set it in the experiment config"}
+POD_SPEC = Obj([F("spec", Obj([F("containers", ListOf(Obj([], extra=True, nullable=False,
+                                                               disallow=_CONTAINER_DISALLOW)))],
+                              extra=True))],
+               extra=True, disallow={"name": "pod Name is not a configurable option",
+                                     "name_space": "pod NameSpace is not a configurable option"})
+ENVIRONMENT = Obj([
+    F("image", EnvImage(), {}), F("environment_variables", EnvVars(), []),
+    F("proxy_ports", ListOf(PROXY_PORT), []), F("ports", MapOf(S("integer")), {}),
+    F("force_pull_image", NBool, False), F("registry_auth", REGISTRY_AUTH),
+    F("add_capabilities", ListOf(S("string")), []), F("drop_capabilities", ListOf(S("string")), []),
+    F("pod_spec", POD_SPEC)], eventually=("image",))
+
+# ----------------------------------------------------------------------------------- resources
+_DEVICE_STR = re.compile(r"^/[^:]*:/[^:]*(:[rwm]*)?")
+
+
+class Device(Spec):
+    OBJ = Obj([F("host_path", S("string")), F("container_path", S("string")), F("mode", NStr, "mrw")],
+              required=("host_path", "container_path"), nullable=False)
+
+    def check(self, v, path, errs, complete):
+        if isinstance(v, str):
+            if not _DEVICE_STR.match(v):
+                errs.append(f"{path}: is neither a list of --device strings nor a map containing "
+                            "host_path, container_path, and mode")
+        elif isinstance(v, dict):
+            self.OBJ.check(v, path, errs, complete)
+        else:
+            errs.append(f"{path}: is neither a list of --device strings nor a map containing "
+                        "host_path, container_path, and mode")
+
+    @staticmethod
+    def normalize(v: Any) -> Dict[str, Any]:
+        if isinstance(v, str):
+            parts = v.split(":")
+            return {"host_path": parts[0], "container_path": parts[1],
+                    "mode": parts[2] if len(parts) > 2 else None}
+        return dict(v)
+
+    def defaults(self, v):
+        return self.OBJ.defaults(self.normalize(v))
+
+    def marshal(self, v):
+        return self.OBJ.marshal(self.normalize(v))
+
+
+BIND_MOUNT = Obj([
+    F("host_path", S("string", checks=[("host_path must be an absolute path", lambda p: p.startswith("/"))])),
+    F("container_path", S("string", checks=[('container_path must not be "."', lambda p: p != ".")])),
+    F("read_only", NBool, False), F("propagation", NStr, "rprivate")],
+    required=("host_path", "container_path"), nullable=False)
+BIND_MOUNTS = ListOf(BIND_MOUNT, unique_key="container_path")
+DEVICES = ListOf(Device(), unique_key="container_path")
+
+RESOURCES = Obj([
+    F("slots", NInt, omitempty=True), F("max_slots", NInt), F("slots_per_trial", NInt, 1),
+    F("weight", NNum, 1), F("native_parallel", NBool, False, omitempty=True),
+    F("shm_size", S("integer", "string", "null", checks=[("must be a valid memory size", memory_size_ok)])),
+    F("resource_pool", NStr, ""), F("priority", NInt), F("devices", DEVICES, []),
+    F("agent_label", NStr, go=False), F("is_single_node", NBool, omitempty=True)])
+
+# ----------------------------------------------------------------------------------- the rest
+OPTIMIZATIONS = Obj([
+    F("aggregation_frequency", NIntMin(1), 1), F("average_aggregated_gradients", NBool, True),
+    F("average_training_metrics", NBool, True), F("gradient_compression", NBool, False),
+    F("grad_updates_size_file", NStr), F("mixed_precision", S(enum=(None, "O0", "O1", "O2", "O3")), "O0",
+                                         omitempty=True),
+    F("tensor_fusion_threshold", NIntMin(0), 64), F("tensor_fusion_cycle_time", NIntMin(0), 1),
+    F("auto_tune_tensor_fusion", NBool, False),
+    # MI355X extension: capture the training step as a HIP graph after N eager warm-up steps
+    F("hip_graph", NBool, go=False), F("hip_graph_warmup_steps", NIntMin(1), go=False)])
+PROFILING = Obj([F("enabled", NBool, False), F("begin_on_batch", NIntMin(0), 0),
+                 F("end_after_batch", NIntMin(0)), F("sync_timings", NBool, True)],
+                checks=[("begin_on_batch must be less than end_after_batch",
+                         _compare("begin_on_batch", "end_after_batch", "<="))])
+REPRODUCIBILITY = Obj([F("experiment_seed", NIntMin(0), runtime=lambda: _random_seed())],
+                      eventually=("experiment_seed",))
+KERBEROS = Obj([F("config_file", S("string"))], required=("config_file",))
+SECURITY = Obj([F("kerberos", KERBEROS)])
+SLURM = Obj([F("slots_per_node", NIntMin(1), omitempty=True), F("gpu_type", NStr, omitempty=True),
+             F("sbatch_args", ListOf(S("string")), omitempty=True)])
+PBS = Obj([F("slots_per_node", NIntMin(1), omitempty=True),
+           F("pbsbatch_args", ListOf(S("string")), omitempty=True)])
+LOG_ACTION = Union("type", {"cancel_retries": Obj([F("type", S("string"))], required=("type",), nullable=False),
+                            "exclude_node": Obj([F("type", S("string"))], required=("type",), nullable=False)},
+                   "is not an object where object[\"type\"] is one of 'cancel_retries' or 'exclude_node'")
+LOG_POLICY = Obj([F("pattern", S("string")), F("action", LOG_ACTION)], required=("pattern", "action"),
+                 nullable=False)
+
+
+class Entrypoint(Spec):
+    def check(self, v, path, errs, complete):
+        if v is None or isinstance(v, str):
+            return
+        ListOf(S("string"), nullable=False).check(v, path, errs, complete)
+
+
+def _random_seed() -> int:
+    import random
+
+    return random.randint(0, 2 ** 31 - 1)
+
+
+def _random_name() -> str:
+    import uuid
+
+    return f"Experiment ({uuid.uuid4().hex[:8]})"
+
+
+class Experiment(Obj):
+    """experiment.json; under grid search every hyperparameter is grid-checked."""
+
+    def check(self, v, path, errs, complete):
+        super().check(v, path, errs, complete)
+        if isinstance(v, dict) and isinstance(v.get("searcher"), dict) and \
+                v["searcher"].get("name") == "grid" and isinstance(v.get("hyperparameters"), dict):
+            for k, hp in v["hyperparameters"].items():
+                GridCheck().check(hp, _sub(_sub(path, "hyperparameters"), k), errs, complete)
+
+
+EXPERIMENT = Experiment([
+    F("bind_mounts", BIND_MOUNTS, []), F("checkpoint_policy", S(enum=(None, "best", "all", "none")), "best"),
+    F("checkpoint_storage", CHECKPOINT_STORAGE, None), F("data", S("object", "null"), {}),
+    F("data_layer", S("object", "null"), go=False), F("debug", NBool, False),
+    F("description", NStr), F("entrypoint", Entrypoint()), F("environment", ENVIRONMENT, {}),
+    F("hyperparameters", MapOf(Hyperparameter()), {}), F("internal", S("null"), go=False),
+    F("labels", ListOf(S("string")), []), F("log_policies", ListOf(LOG_POLICY), []),
+    F("max_restarts", NIntMin(0), 5), F("min_checkpoint_period", Length(0), {"batches": 0}),
+    F("min_validation_period", Length(0), {"batches": 0}), F("name", NStr, runtime=_random_name),
+    F("optimizations", OPTIMIZATIONS, {}), F("perform_initial_validation", NBool, False),
+    F("profiling", PROFILING, {}), F("project", NStr, ""), F("records_per_epoch", NInt, 0),
+    F("reproducibility", REPRODUCIBILITY, {}), F("resources", RESOURCES, {}),
+    F("scheduling_unit", NIntMin(1), 100), F("searcher", SEARCHER, None),
+    F("security", SECURITY, None, omitempty=True), F("slurm", SLURM, {}, omitempty=True),
+    F("pbs", PBS, {}, omitempty=True), F("tensorboard_storage", TensorboardStorage(), omitempty=True),
+    F("workspace", NStr, "")],
+    eventually=("checkpoint_storage", "name", "hyperparameters", "reproducibility", "searcher"))
+
+# test-only structs of the reference's schema test suite (test-root / test-union)
+TEST_UNION = Union("type", {
+    "a": Obj([F("type", S("string")), F("val_a", S("integer")), F("common_val", NStr, "default-common-val")],
+             required=("type", "val_a"), nullable=False),
+    "b": Obj([F("type", S("string")), F("val_b", S("integer")), F("common_val", NStr, "default-common-val")],
+             required=("type", "val_b"), nullable=False)}, "bad test union", common=["common_val"])
+TEST_ROOT = Obj([F("val_x", S("integer")), F("sub_obj", Obj([F("val_y", NStr, "default_y")]), {}),
+                 F("sub_union", TEST_UNION), F("runtime_defaultable", NInt, runtime=lambda: 42),
+                 F("defaulted_array", ListOf(S("string")), []), F("nodefault_array", ListOf(S("string")))],
+                required=("val_x",))
+
+URLS: Dict[str, Spec] = {PREFIX + k: v for k, v in {
+    "experiment.json": EXPERIMENT, "bind-mount.json": BIND_MOUNT, "bind-mounts.json": BIND_MOUNTS,
+    "device.json": Device(), "devices.json": DEVICES, "environment.json": ENVIRONMENT,
+    "environment-image.json": EnvImage(), "environment-variables.json": EnvVars(),
+    "resources.json": RESOURCES, "optimizations.json": OPTIMIZATIONS, "profiling.json": PROFILING,
+    "reproducibility.json": REPRODUCIBILITY, "security.json": SECURITY, "kerberos.json": KERBEROS,
+    "checkpoint-storage.json": CHECKPOINT_STORAGE, "shared-fs.json": SHARED_FS, "s3.json": S3,
+    "gcs.json": GCS, "azure.json": AZURE, "directory.json": DIRECTORY,
+    "tensorboard-storage.json": TensorboardStorage(), "searcher.json": SEARCHER,
+    **{f"searcher-{k.replace('_', '-')}.json": m for k, m in SEARCHER_MEMBERS.items()},
+    "searcher-length.json": SearcherLength(), "length.json": Length(0),
+    "check-positive-length.json": Length(1), "hyperparameter.json": Hyperparameter(),
+    "hyperparameters.json": MapOf(Hyperparameter()),
+    **{f"hyperparameter-{k}.json": m for k, m in HP_MEMBERS.items()},
+    "check-grid-hyperparameter.json": GridCheck(), "log-action.json": LOG_ACTION,
+    "log-action-cancel-retries.json": LOG_ACTION.members["cancel_retries"],
+    "log-action-exclude-node.json": LOG_ACTION.members["exclude_node"], "log-policy.json": LOG_POLICY,
+    "hpc-cluster-slurm.json": SLURM, "hpc-cluster-pbs.json": PBS, "registry-auth.json": REGISTRY_AUTH,
+    "proxy-port.json": PROXY_PORT, "proxy-ports.json": ListOf(PROXY_PORT),
+    "test-root.json": TEST_ROOT, "test-union.json": TEST_UNION,
+    "test-union-a.json": TEST_UNION.members["a"], "test-union-b.json": TEST_UNION.members["b"],
+}.items()}
+
+
+def spec_for(url: str) -> Spec:
+    if not url.startswith(PREFIX):
+        url = PREFIX + url
+    try:
+        return URLS[url]
+    except KeyError:
+        raise KeyError(f"no schema for {url}") from None
+
+
+def sanity_errors(url: str, value: Any) -> List[str]:
+    errs: List[str] = []
+    spec_for(url).check(value, "<config>", errs, False)
+    return errs
+
+
+def completeness_errors(url: str, value: Any) -> List[str]:
+    errs: List[str] = []
+    spec_for(url).check(value, "<config>", errs, True)
+    return errs
+
+
+def with_defaults(url: str, value: Any) -> Any:
+    """Defaults filled, marshalled the way the reference's Go struct would serialise it."""
+    spec = spec_for(url)
+    return spec.marshal(spec.defaults(copy.deepcopy(value)))
+
+
+def merge(url: str, obj: Any, src: Any) -> Any:
+    spec = spec_for(url)
+    return spec.marshal(spec.merge(copy.deepcopy(obj), copy.deepcopy(src)))

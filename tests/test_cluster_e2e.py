@@ -113,7 +113,7 @@ def test_single_experiment_completes_with_metrics_and_checkpoint(cluster):
 
 def test_asha_search_runs_concurrent_trials(cluster):
     m, s, ctx, _ = cluster
-    cfg = BASE.replace("lr: 0.01", "lr: {type: log, minval: -3, maxval: -1}") + \
+    cfg = BASE.replace("lr: 0.01", "lr: {type: log, minval: -3, maxval: -1, base: 10}") + \
         "searcher: {name: adaptive_asha, metric: val_loss, max_length: {batches: 16}, max_trials: 6, " \
         "max_rungs: 2, divisor: 2, mode: aggressive, max_concurrent_trials: 4}\n"
     eid = _create(s, ctx, cfg)
@@ -269,7 +269,7 @@ def test_webui_visualization_compare_and_workloads_render(cluster):
     if shutil.which("node") is None:
         pytest.skip("node not installed")
     m, s, ctx, _ = cluster
-    cfg = BASE.replace("lr: 0.01", "lr: {type: log, minval: -3, maxval: -1}\n  width: {type: categorical, vals: [8, 16]}") + \
+    cfg = BASE.replace("lr: 0.01", "lr: {type: log, minval: -3, maxval: -1, base: 10}\n  width: {type: categorical, vals: [8, 16]}") + \
         "searcher: {name: random, metric: val_loss, max_length: {batches: 8}, max_trials: 3, max_concurrent_trials: 3}\n"
     eid = _create(s, ctx, cfg)
     assert _wait(s, eid, timeout=400) == "COMPLETED"
