@@ -37,7 +37,7 @@ def main() -> None:
                cluster_name=cfg.get("cluster_name", "default"),
                authz=args.authz or ((cfg.get("security") or {}).get("authz") or {}).get("type", "basic"),
                resource_manager=cfg.get("resource_manager"), resource_pools=cfg.get("resource_pools"),
-               logging_config=cfg.get("logging"))
+               logging_config=cfg.get("logging"), webhooks_config=cfg.get("webhooks"))
     m.sso_providers = [{"name": str(p["name"]), "sso_url": str(p["sso_url"])}
                        for p in cfg.get("sso_providers") or []]
     srv = MasterServer(m, cfg.get("host", args.host), int(cfg.get("port", args.port)),

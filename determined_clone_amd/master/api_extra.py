@@ -988,18 +988,14 @@ def workspace_pools(r: Req) -> Any:
 # =========================================================================== webhooks
 @route("POST", "/api/v1/webhooks/{wid}/test")
 def test_webhook(r: Req) -> Any:
+    """A signed test event to the webhook's URL (reference api_webhook.go TestWebhook)."""
     require(r, "EDIT_WEBHOOKS")
     row = r.m.db.one("SELECT * FROM webhooks WHERE id=?", [_int(r.p["wid"])])
     if row is None:
         raise HTTPError(404, "webhook not found")
-    import urllib.request
-
-    body = json.dumps({"event_type": "TEST", "event_data": {"message": "test webhook"},
-                       "timestamp": int(now())}).encode()
     try:
-        urllib.request.urlopen(urllib.request.Request(row["url"], data=body, method="POST",
-                                                      headers={"Content-Type": "application/json"}), timeout=10)
-        return {"completed": True}
+        code = r.m.webhooks.post(row["url"], r.m.webhooks.test_payload(row["webhook_type"]))
+        return {"completed": code < 400}
     except Exception as e:
         return {"completed": False, "error": str(e)}
 

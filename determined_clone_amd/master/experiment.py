@@ -154,7 +154,6 @@ class Experiment:
             t.latest_checkpoint = op.checkpoint
         self.trials[op.request_id] = t
         self._process(self.searcher.trial_created(op.request_id))
-        self.master.webhooks.trial_event(self, t, "ACTIVE")
 
     # ------------------------------------------------------------------ unmanaged trials
     def add_unmanaged_trial(self, hparams: Optional[Dict[str, Any]] = None,
@@ -283,7 +282,6 @@ class Experiment:
         t.state = state
         self.master.db.update("trials", "id", t.id, {"state": state, "end_time": now()})
         self.master.checkpoint_gc_trial(self, t)
-        self.master.webhooks.trial_event(self, t, state)
 
     # ------------------------------------------------------------------ user actions
     def _set_state(self, state: str) -> None:
@@ -291,7 +289,7 @@ class Experiment:
             logger.info(f"experiment {self.id}: {self.state} -> {state}")
         self.state = state
         self.master.db.update("experiments", "id", self.id, {"state": state})
-        self.master.webhooks.experiment_event(self, state)
+        self.master.webhooks.experiment_state_changed(self, state)
 
     def pause(self) -> None:
         with self.lock:

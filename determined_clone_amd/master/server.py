@@ -1300,22 +1300,46 @@ def move_experiment(r: Req) -> Any:
 # =========================================================================== webhooks
 @route("GET", "/api/v1/webhooks")
 def list_webhooks(r: Req) -> Any:
-    return {"webhooks": [dict(x, triggers=dec(x["triggers"], [])) for x in r.m.db.all("SELECT * FROM webhooks")]}
+    return {"webhooks": [_webhook_out(x) for x in r.m.webhooks.hooks()]}
+
+
+def _webhook_out(row: Dict[str, Any]) -> Dict[str, Any]:
+    """webhookv1.Webhook: proto enum names for the webhook and trigger types."""
+    from determined_clone_amd.master import webhooks as wh
+
+    out = dict(row)
+    out["webhook_type"] = "WEBHOOK_TYPE_" + wh.norm_webhook_type(row.get("webhook_type"))
+    out["triggers"] = [dict(t, trigger_type="TRIGGER_TYPE_" + wh.norm_trigger_type(t.get("trigger_type")),
+                            webhook_id=row.get("id"))
+                       for t in row.get("triggers") or []]
+    return out
 
 
 @route("POST", "/api/v1/webhooks")
 def post_webhook(r: Req) -> Any:
+    from determined_clone_amd.master import webhooks as wh
+
     require(r, "EDIT_WEBHOOKS")
-    wid = r.m.db.insert("webhooks", {"url": r.body["url"], "webhook_type": r.body.get("webhook_type", "DEFAULT"),
-                                     "triggers": r.body.get("triggers", []), "mode": r.body.get("mode", "WORKSPACE"),
-                                     "name": r.body.get("name"), "workspace_id": r.body.get("workspace_id")})
-    return {"webhook": dict(r.m.db.one("SELECT * FROM webhooks WHERE id=?", [wid]), triggers=r.body.get("triggers", []))}
+    try:
+        triggers = wh.validate_triggers(r.body.get("triggers", []))
+    except ValueError as e:
+        raise HTTPError(400, str(e))
+    wtype = wh.norm_webhook_type(r.body.get("webhook_type"))
+    if wtype not in (wh.DEFAULT, wh.SLACK):
+        raise HTTPError(400, f"unknown webhook type {r.body.get('webhook_type')!r}")
+    wid = r.m.db.insert("webhooks", {"url": r.body["url"], "webhook_type": wtype, "triggers": triggers,
+                                     "mode": r.body.get("mode", "WORKSPACE"), "name": r.body.get("name"),
+                                     "workspace_id": r.body.get("workspace_id")})
+    r.m.webhooks.reload_triggers()
+    row = r.m.db.one("SELECT * FROM webhooks WHERE id=?", [wid])
+    return {"webhook": _webhook_out(dict(row, triggers=triggers))}
 
 
 @route("DELETE", "/api/v1/webhooks/{wid}")
 def delete_webhook(r: Req) -> Any:
     require(r, "EDIT_WEBHOOKS")
     r.m.db.execute("DELETE FROM webhooks WHERE id=?", [_int(r.p["wid"])])
+    r.m.webhooks.reload_triggers()
     return {}
 
 
@@ -1685,6 +1709,7 @@ class MasterServer:
         self.httpd.shutdown()
         self.httpd.server_close()
         self.master.rm.close()
+        self.master.webhooks.close()  # undelivered events stay queued for the next master
 
 
 # routes that live in their own modules register on import

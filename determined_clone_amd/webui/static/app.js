@@ -666,12 +666,14 @@ async function pageWebhooks() {
   const url = h("input", { placeholder: "https://…", style: "width:320px" });
   const type = h("select", {}, h("option", {}, "DEFAULT"), h("option", {}, "SLACK"));
   const states = h("input", { placeholder: "trigger states, e.g. COMPLETED,ERROR", style: "width:260px" });
+  const regex = h("input", { placeholder: "task log regex (optional)", style: "width:200px" });
   const create = () => act(() => api.post("/api/v1/webhooks", { url: url.value, webhook_type: type.value,
-    triggers: states.value.split(",").map((s) => s.trim()).filter(Boolean).map((s) => ({ trigger_type: "TRIGGER_TYPE_EXPERIMENT_STATE_CHANGE", condition: { state: s } })) }));
-  return h("div", {}, h("h1", {}, "Webhooks"), h("div", { class: "toolbar" }, url, type, states, h("button", { class: "primary", onclick: create }, "Create")),
+    triggers: states.value.split(",").map((s) => s.trim()).filter(Boolean).map((s) => ({ trigger_type: "TRIGGER_TYPE_EXPERIMENT_STATE_CHANGE", condition: { state: s } }))
+      .concat(regex.value ? [{ trigger_type: "TRIGGER_TYPE_TASK_LOG", condition: { regex: regex.value } }] : []) }));
+  return h("div", {}, h("h1", {}, "Webhooks"), h("div", { class: "toolbar" }, url, type, states, regex, h("button", { class: "primary", onclick: create }, "Create")),
     table([
       { key: "id", label: "ID" }, { key: "url", label: "URL" }, { key: "webhook_type", label: "Type" },
-      { key: "triggers", label: "Triggers", render: (w) => (w.triggers || []).map((t) => (t.condition || {}).state || t.trigger_type).join(", ") },
+      { key: "triggers", label: "Triggers", render: (w) => (w.triggers || []).map((t) => (t.condition || {}).state || ((t.condition || {}).regex ? "log /" + t.condition.regex + "/" : t.trigger_type)).join(", ") },
       { key: "act", label: "", render: (w) => [h("button", { onclick: () => act(() => api.post(`/api/v1/webhooks/${w.id}/test`)) }, "Test"),
         h("button", { onclick: () => act(() => api.del(`/api/v1/webhooks/${w.id}`)) }, "Delete")] },
     ], webhooks, { sortKey: "id", desc: false }));
