@@ -49,6 +49,17 @@ def share_devices(devs: List[Dict[str, Any]], slots_per_gpu: int) -> List[Dict[s
     return out
 
 
+def pci_address(domain: Any, location_id: Any) -> Optional[str]:
+    """KFD topology ``domain`` + ``location_id`` (bus << 8 | device << 3 | function) ->
+    ``dddd:bb:dd.f``, the form of ``/dev/dri/by-path/pci-<address>-{card,render}``."""
+    try:
+        loc = int(location_id)
+        dom = int(domain or 0)
+    except (TypeError, ValueError):
+        return None
+    return f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 0x7:x}"
+
+
 def detect_devices(artificial_slots: int = 0, slots_per_gpu: int = 1,
                    max_gpus: int = 0) -> List[Dict[str, Any]]:
     devs = _detect_physical(artificial_slots)
@@ -69,7 +80,11 @@ def _detect_physical(artificial_slots: int = 0) -> List[Dict[str, Any]]:
             devs.append({"id": int(g["index"]), "uuid": g.get("unique_id") or g["index"],
                          "type": "rocm", "brand": "AMD", "gfx_target": g.get("gfx_target"),
                          "cu_count": int(g.get("cu_count") or 0),
-                         "vram_bytes": int(g.get("vram_bytes") or 0)})
+                         "vram_bytes": int(g.get("vram_bytes") or 0),
+                         # PCI address + DRM render minor: which /dev/dri nodes a container of
+                         # this slot gets (agent/containers.py rocm_device_paths)
+                         "pci_bus": pci_address(g.get("domain"), g.get("location_id")),
+                         "render_minor": int(g["drm_render_minor"]) if g.get("drm_render_minor") else None})
     except Exception as e:  # pragma: no cover - no native module / no KFD
         logger.debug(f"KFD detection failed: {e}")
     if not devs and shutil.which("rocm-smi"):
@@ -103,7 +118,8 @@ class Agent:
     def __init__(self, master_url: str, agent_id: Optional[str] = None, pool: str = "default",
                  artificial_slots: int = 0, label: str = "", username: str = "admin",
                  password: str = "", workdir: Optional[str] = None, slots_per_gpu: int = 1,
-                 max_gpus: int = 0) -> None:
+                 max_gpus: int = 0, container_runtime: str = "process",
+                 container_socket: Optional[str] = None, dev_root: str = "/dev") -> None:
         self.session = Session(master_url)
         tok = self.session.post("/api/v1/auth/login", {"username": username, "password": password})["token"]
         self.session.token = tok
@@ -117,6 +133,11 @@ class Agent:
         os.makedirs(self.workdir, exist_ok=True)  # the zygote binds its socket here right away
         self._stop = threading.Event()
         self._lock = threading.Lock()
+        # container runtime (agent/containers.py): Docker / Podman / Apptainer, or None = tasks
+        # run as process groups (also the fallback of "auto" when no daemon answers)
+        from determined_clone_amd.agent import containers
+
+        self.containers = containers.make_runtime(container_runtime, self.id, container_socket, dev_root)
         # pre-warmed fork server for task processes (exec/zygote.py), started in the background
         self.zygote = None
         self._zygote_done = threading.Event()
@@ -143,6 +164,9 @@ class Agent:
         wd = os.path.join(self.workdir, alloc.replace("/", "_"))
         ctx_dir = os.path.join(wd, "context")
         runtime.fetch_context(self.session, spec["task_id"], ctx_dir)
+        if self.containers is not None:
+            self._start_container(spec, wd, ctx_dir)
+            return
         cmd, env = runtime.build_task(spec, self.master_url, self.id, self.devices, ctx_dir)
         if "MIOPEN_USER_DB_PATH" not in env:
             # one writable MIOpen find DB + kernel cache per agent, seeded from the shipped MI355X
@@ -177,31 +201,88 @@ class Agent:
         self._event(alloc, "RUNNING")
         threading.Thread(target=self._pump, args=(t,), daemon=True).start()
 
+    def _start_container(self, spec: Dict[str, Any], wd: str, ctx_dir: str) -> None:
+        """Run the task in a container (agent/containers.py): same command and DET_* environment
+        as the process runtime, seen through the container's mounts and device mapping."""
+        alloc = spec["allocation_id"]
+        base = {k: v for k, v in os.environ.items() if k.startswith("DET_MASTER_CERT")}
+        cmd, env = runtime.build_task(spec, self.master_url, self.id, self.devices, ctx_dir, base_env=base)
+        mine = runtime.assigned_devices(spec, self.devices)
+        proc = self.containers.launch(spec, cmd, env, ctx_dir, mine, runtime.FRAMEWORK_ROOT)
+        t = _Task(spec, proc, wd)
+        with self._lock:
+            self.tasks[alloc] = t
+        self._event(alloc, "RUNNING")
+        threading.Thread(target=self._pump, args=(t,), daemon=True).start()
+
+    def _reattach(self) -> None:
+        """After an agent restart: follow this agent's containers that are still running and
+        report the exit of those that ended while no agent watched them (reference
+        docker.go ReattachContainer)."""
+        if self.containers is None:
+            return
+        for labels, proc, code in self.containers.reattach():
+            from determined_clone_amd.agent import containers
+
+            alloc = labels.get(containers.LABEL_ALLOC)
+            if not alloc or alloc in self.tasks:
+                continue
+            if code is not None:
+                logger.info(f"container of {alloc} exited ({code}) while the agent was down")
+                self._event(alloc, "TERMINATED", code)
+                proc.remove()
+                continue
+            logger.info(f"re-attached to the running container of {alloc}")
+            spec = {"allocation_id": alloc, "task_id": labels.get(containers.LABEL_TASK, alloc)}
+            t = _Task(spec, proc, os.path.join(self.workdir, alloc.replace("/", "_")))
+            with self._lock:
+                self.tasks[alloc] = t
+            self._event(alloc, "RUNNING")
+            threading.Thread(target=self._pump, args=(t,), daemon=True).start()
+
     def _pump(self, t: _Task) -> None:
         alloc = t.spec["allocation_id"]
         code = runtime.pump_logs(t.proc, self.session, t.spec, self.id)
         with self._lock:
             self.tasks.pop(alloc, None)
         self._event(alloc, "TERMINATED", code if not t.killed else (code or 137))
+        remove = getattr(t.proc, "remove", None)
+        if remove is not None:  # container: delete it once its exit is reported
+            try:
+                remove()
+            except Exception as e:
+                logger.warning(f"removing the container of {alloc}: {e}")
         shutil.rmtree(t.workdir, ignore_errors=True)
+
+    def _signal(self, t: _Task, sig: int) -> bool:
+        """SIGTERM / SIGKILL the task: its process group, or its container."""
+        from determined_clone_amd.agent import containers
+
+        if isinstance(t.proc, containers.ContainerProcess):  # Docker / Podman: via the daemon
+            try:
+                t.proc.send_signal(signal.Signals(sig).name)
+            except Exception as e:
+                logger.warning(f"signalling container: {e}")
+                return False
+            return True
+        try:
+            os.killpg(t.proc.pid, sig)
+        except ProcessLookupError:
+            return False
+        return True
 
     def _kill(self, alloc: str, grace: float = 10.0) -> None:
         t = self.tasks.get(alloc)
         if t is None:
             return
         t.killed = True
-        try:
-            os.killpg(t.proc.pid, signal.SIGTERM)
-        except ProcessLookupError:
+        if not self._signal(t, signal.SIGTERM):
             return
 
         def hard() -> None:
             time.sleep(grace)
             if t.proc.poll() is None:
-                try:
-                    os.killpg(t.proc.pid, signal.SIGKILL)
-                except ProcessLookupError:
-                    pass
+                self._signal(t, signal.SIGKILL)
 
         threading.Thread(target=hard, daemon=True).start()
 
@@ -215,6 +296,7 @@ class Agent:
     # ------------------------------------------------------------------ main loop
     def run(self) -> None:
         self.register()
+        self._reattach()
         while not self._stop.is_set():
             try:
                 acts = self.session.get(f"/api/v1/agents/{self.id}/actions",
@@ -240,6 +322,7 @@ class Agent:
 
     def start_background(self) -> "Agent":
         self.register()
+        self._reattach()
         threading.Thread(target=self.run, daemon=True, name=f"agent-{self.id}").start()
         return self
 
@@ -261,6 +344,11 @@ def main() -> None:
     ap.add_argument("--slots-per-gpu", type=int, default=1,
                     help="expose each MI355X as this many slots (HP-search trials sharing a GPU)")
     ap.add_argument("--max-gpus", type=int, default=0, help="use only the first N GPUs (0 = all)")
+    ap.add_argument("--container-runtime", default="auto",
+                    choices=["auto", "docker", "podman", "apptainer", "process"],
+                    help="run tasks in containers (auto: Docker or Podman when its socket answers, "
+                         "else process groups)")
+    ap.add_argument("--container-socket", default=None, help="Docker / Podman API unix socket")
     ap.add_argument("--master-cert-file", default=None,
                     help="CA / self-signed cert of an HTTPS master, or 'noverify'")
     ap.add_argument("--master-cert-name", default=None,
@@ -275,7 +363,8 @@ def main() -> None:
     if args.master_cert_name:
         os.environ["DET_MASTER_CERT_NAME"] = args.master_cert_name
     Agent(args.master_url, args.agent_id, args.resource_pool, args.artificial_slots, args.label,
-          slots_per_gpu=args.slots_per_gpu, max_gpus=args.max_gpus).run()
+          slots_per_gpu=args.slots_per_gpu, max_gpus=args.max_gpus,
+          container_runtime=args.container_runtime, container_socket=args.container_socket).run()
 
 
 if __name__ == "__main__":

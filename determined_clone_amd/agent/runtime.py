@@ -20,6 +20,17 @@ from typing import Any, Dict, List, Optional, Tuple
 logger = logging.getLogger("determined_clone_amd.agent")
 
 FRAMEWORK_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# sources the context directory's startup-hook.sh, then execs the task (reference entrypoint.sh)
+ENTRYPOINT_SH = os.path.join(FRAMEWORK_ROOT, "determined_clone_amd", "exec", "entrypoint.sh")
+STARTUP_HOOK = "startup-hook.sh"
+
+
+def with_startup_hook(cmd: List[str], ctx_dir: str, entrypoint_sh: str = ENTRYPOINT_SH) -> List[str]:
+    """``cmd`` run through the entrypoint wrapper when the context directory has a
+    ``startup-hook.sh`` (for trials and every NTSC task, like the reference's entrypoints)."""
+    if os.path.isfile(os.path.join(ctx_dir, STARTUP_HOOK)):
+        return ["bash", entrypoint_sh] + list(cmd)
+    return list(cmd)
 
 
 def fetch_context(session: Any, task_id: str, ctx_dir: str) -> None:
@@ -43,6 +54,12 @@ def _user_env(spec: Dict[str, Any]) -> Dict[str, str]:
         user_env = dict(x.split("=", 1) for x in (user_env.get("rocm") or user_env.get("cpu") or [])
                         if "=" in x)
     return {str(k): str(v) for k, v in user_env.items()}
+
+
+def assigned_devices(spec: Dict[str, Any], devices: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
+    """The agent's devices given to this container (``spec["slots"]``; all when absent)."""
+    slot_ids = spec.get("slots")
+    return list(devices) if slot_ids is None else [d for d in devices if d["id"] in set(slot_ids)]
 
 
 def build_task(spec: Dict[str, Any], master_url: str, agent_id: str,
@@ -99,7 +116,7 @@ def build_task(spec: Dict[str, Any], master_url: str, agent_id: str,
         cmd = list(spec.get("entrypoint") or ["true"])
         if cmd and cmd[0] in ("python", "python3"):
             cmd[0] = sys.executable
-    return cmd, env
+    return with_startup_hook(cmd, ctx_dir), env
 
 
 def pump_logs(proc: subprocess.Popen, session: Any, spec: Dict[str, Any], agent_id: str) -> int:

@@ -55,6 +55,27 @@ class Allocation:
         self.proxy_address: Optional[str] = None
 
 
+def container_spec(cfg: Dict[str, Any]) -> Dict[str, Any]:
+    """What an agent's container runtime needs from a task's config (reference
+    master/pkg/tasks/task.go ToDockerSpec): image (per-flavour map), pull policy + registry auth,
+    bind mounts (defaults filled), shm_size in bytes, extra devices, capabilities."""
+    from determined_clone_amd.config import schema
+
+    env = cfg.get("environment") or {}
+    res = cfg.get("resources") or {}
+    image = env.get("image")
+    image = schema.EnvImage.normalize(image) if image else None
+    mounts = [dict(m, read_only=bool(m.get("read_only")), propagation=m.get("propagation") or "rprivate")
+              for m in cfg.get("bind_mounts") or [] if isinstance(m, dict)]
+    devices = [schema.Device.normalize(d) for d in res.get("devices") or []]
+    return {"image": image, "force_pull_image": bool(env.get("force_pull_image")),
+            "registry_auth": env.get("registry_auth"), "bind_mounts": mounts,
+            "shm_size": schema.parse_memory_size(res.get("shm_size")),
+            "devices": [dict(d, mode=d.get("mode") or "mrw") for d in devices],
+            "add_capabilities": list(env.get("add_capabilities") or []),
+            "drop_capabilities": list(env.get("drop_capabilities") or [])}
+
+
 class MasterLogBuffer(logging.Handler):
     """Last ``capacity`` log records of the master process, served by ``GET /api/v1/master/logs``
     (reference: ``det master logs`` / MasterLogs)."""
@@ -378,7 +399,7 @@ class Master:
         ep = cfg.get("entrypoint")
         return {"kind": "TRIAL", "cluster_info": info, "entrypoint": ep,
                 "environment": cfg.get("environment", {}), "experiment_id": exp.id,
-                "slots_per_trial": exp.slots_per_trial}
+                "slots_per_trial": exp.slots_per_trial, "container": container_spec(cfg)}
 
     def _task_token(self) -> str:
         u = self.db.one("SELECT id FROM users WHERE username='determined'") or {"id": 1}
@@ -390,7 +411,7 @@ class Master:
     def launch_command(self, kind: str, entrypoint: List[str], slots: int = 0,
                        priority: int = 42, pool: str = "default", env: Optional[Dict[str, str]] = None,
                        owner_id: int = 1, context: Optional[bytes] = None,
-                       name: Optional[str] = None) -> Dict[str, Any]:
+                       name: Optional[str] = None, config: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
         task_id = str(uuid.uuid4())
         alloc_id = f"{task_id}.0"
         # per-task secret the service (shell / notebook / tensorboard) demands on every request:
@@ -399,7 +420,7 @@ class Master:
         secret = secrets.token_urlsafe(24)
         self.db.kv_set(f"proxy_secret:{task_id}", secret)
         spec = {"kind": kind, "entrypoint": entrypoint, "environment": {"environment_variables": env or {}},
-                "proxy_secret": secret,
+                "proxy_secret": secret, "container": container_spec(config or {}),
                 "cluster_info": {"master_url": self.master_url, "cluster_id": self.cluster_id,
                                  "agent_id": "", "slot_ids": [], "task_id": task_id,
                                  "allocation_id": alloc_id, "session_token": self._task_token(),

@@ -859,7 +859,7 @@ for _kind, _path in (("COMMAND", "commands"), ("SHELL", "shells"), ("NOTEBOOK", 
                 env[f"DET_{kind}_IDLE_TIMEOUT"] = str(_seconds(idle))
             t = r.m.launch_command(kind, ep, int(res.get("slots", 0)), int(res.get("priority") or 42),
                                    res.get("resource_pool") or "default", env,
-                                   r.user["id"], ctx, cfg.get("description"))
+                                   r.user["id"], ctx, cfg.get("description"), config=cfg)
             return {path[:-1]: t}
 
         @route("GET", f"/api/v1/{path}")

@@ -598,6 +598,7 @@ std::vector<std::map<std::string, std::string>> detect_kfd_gpus(const std::strin
                                    std::max(1L, std::atol(kv["simd_per_cu"].c_str())));
     g["unique_id"] = kv["unique_id"];
     g["location_id"] = kv["location_id"];
+    g["domain"] = kv["domain"];  // PCI domain: with location_id, the device's PCI address
     g["drm_render_minor"] = kv["drm_render_minor"];
     g["vendor_id"] = kv["vendor_id"];
     g["device_id"] = kv["device_id"];

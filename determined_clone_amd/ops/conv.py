@@ -80,6 +80,65 @@ _CHOICE = {}
 AUTOTUNE = os.environ.get("DCA_CONV_AUTOTUNE", "1") != "0"
 DUAL = os.environ.get("DCA_PW_DUAL", "1") != "0"  # pointwise_dual for downsampling blocks
 
+# Shipped decisions (like the MIOpen find DB and the TunableOp CSV in ops/tuned/): every
+# (direction, shape) this chooser met in the ResNet-50 bench (bs 1024, 256), the SD UNet bench and
+# the CIFAR ASHA trials, timed on an MI355X by ``tools/dump_conv_choices.py`` and stored in
+# ``ops/tuned/conv_choices_gfx950.json``. Shapes found there are never timed again: no timing
+# noise between processes (16 ASHA trials on one GPU timing against each other's load) and
+# identical decisions on every DDP rank. ``DCA_CONV_CHOICES=0`` ignores the file,
+# ``DCA_CONV_CHOICES=<path>`` reads another one.
+TIMINGS = 0  # candidates timed by this process (0 in a bench run whose shapes are all shipped)
+_SHIPPED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned", "conv_choices_gfx950.json")
+
+
+def _key_to_json(key) -> list:
+    return [str(k) if isinstance(k, torch.dtype) else (list(k) if isinstance(k, tuple) else k) for k in key]
+
+
+def _key_from_json(raw) -> tuple:
+    out = []
+    for k in raw:
+        if isinstance(k, list):
+            out.append(tuple(k))
+        elif isinstance(k, str) and k.startswith("torch."):
+            out.append(getattr(torch, k[len("torch."):]))
+        else:
+            out.append(k)
+    return tuple(out)
+
+
+def load_choices(path: Optional[str] = None) -> int:
+    """Merge a decisions file into the cache (entries already decided in-process win)."""
+    import json
+
+    env = os.environ.get("DCA_CONV_CHOICES", "1")
+    if path is None:
+        if env == "0":
+            return 0
+        path = _SHIPPED_PATH if env == "1" else env
+    if not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        data = json.load(f)
+    n = 0
+    for e in data.get("choices", []):
+        key = _key_from_json(e["key"])
+        if key not in _CHOICE:
+            _CHOICE[key] = int(e["choice"])
+            n += 1
+    return n
+
+
+def dump_choices(path: str, device_name: str = "") -> None:
+    import json
+
+    rows = [{"key": _key_to_json(k), "choice": v} for k, v in sorted(_CHOICE.items(), key=lambda kv: str(kv[0]))]
+    with open(path, "w") as f:
+        json.dump({"device": device_name, "choices": rows}, f, indent=1)
+
+
+load_choices()
+
 
 def _time_us(fn, reps: int = 5) -> float:
     fn()
@@ -92,15 +151,40 @@ def _time_us(fn, reps: int = 5) -> float:
     return s.elapsed_time(e) * 1e3 / reps
 
 
+def _world() -> int:
+    import torch.distributed as dist
+
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+# Multi-rank runs: a shape missing from the shipped decisions takes candidate 0 (the library) on
+# every rank without timing, so ranks cannot disagree and no collective is needed inside the
+# forward (pipeline stages meet different shapes). DCA_CONV_AUTOTUNE_DIST=1 instead times on every
+# rank and adopts rank 0's pick (broadcast_object_list; all ranks must meet the same shapes).
+AUTOTUNE_DIST = os.environ.get("DCA_CONV_AUTOTUNE_DIST", "0") == "1"
+
+
 def _choose(key, candidates) -> int:
-    """Index of the fastest candidate for ``key`` (timed once per process, then cached)."""
+    """Index of the fastest candidate for ``key`` (shipped, else timed once per process)."""
     got = _CHOICE.get(key)
     if got is not None:
         return got
-    if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
+    if not AUTOTUNE or (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
         return 0
+    world = _world()
+    if world > 1 and not AUTOTUNE_DIST:
+        _CHOICE[key] = 0
+        return 0
+    global TIMINGS
     times = [_time_us(fn) for fn in candidates]
+    TIMINGS += len(candidates)
     best = min(range(len(times)), key=times.__getitem__)
+    if world > 1:
+        import torch.distributed as dist
+
+        obj = [best]
+        dist.broadcast_object_list(obj, src=0)
+        best = int(obj[0])
     _CHOICE[key] = best
     if os.environ.get("DCA_CONV_DEBUG") == "1":
         print(f"[conv chooser] {key[0]} {key[1:]} us={[round(t, 1) for t in times]} -> {best}",

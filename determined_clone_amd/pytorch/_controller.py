@@ -296,11 +296,13 @@ class _PyTorchTrialController:
                     if st.exists():
                         self.start_from_batch = int(json.loads(st.read_text()).get("batches_trained", 0))
             self._set_data_loaders()
+            util.startup_mark("data loaders built")
             it = iter(self.training_loader)
             if self.context.experimental._auto_to_device and self.context.device.type == "cuda":
                 it = _data.DevicePrefetcher(it, self.context.device)
             self.training_iterator = it
             self.training_enumerator = enumerate(self._timed_iter(it), start=self.start_from_batch)
+            util.startup_mark("training iterator ready")
 
             def cleanup() -> None:
                 del self.training_iterator
@@ -327,6 +329,7 @@ class _PyTorchTrialController:
             else:
                 ops = self.core_context.searcher.operations()
             for op in ops:
+                util.startup_mark("first searcher operation")
                 train_unit = self.max_length if self.local_training else TrainUnit._from_searcher_unit(
                     op.length, self.searcher_unit, self.global_batch_size)
                 self._train_for_op(op, [
@@ -486,6 +489,7 @@ class _PyTorchTrialController:
             torch.cuda.empty_cache()
 
     def _train_batch(self, batch: Any, epoch_idx: int, batch_idx: int) -> Dict[str, Any]:
+        util.startup_mark("first batch fetched")
         self.context._loss_ids = {}
         t0 = time.time()
         self.prof.update_batch_idx(batch_idx)

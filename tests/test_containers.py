@@ -1,0 +1,284 @@
+"""Agent container runtime (agent/containers.py) against a fake Docker daemon on a unix socket
+(tests/fake_docker.py), and startup-hook.sh for every task (reference: agent/pkg/docker,
+agent/internal/containers/spec.go:99-142, master/pkg/tasks/mounts.go, entrypoint.sh)."""
+import base64
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import pytest
+
+from determined_clone_amd.agent import containers, runtime
+from determined_clone_amd.agent.agent import Agent
+from determined_clone_amd.common.api import Session
+from determined_clone_amd.master import Master, MasterServer
+from determined_clone_amd.util import tar_directory
+
+from tests.fake_docker import FakeDocker
+
+
+@pytest.fixture()
+def docker():
+    d = tempfile.mkdtemp(prefix="fd-", dir="/tmp")  # short path: unix sockets cap at 108 bytes
+    fake = FakeDocker(os.path.join(d, "docker.sock"))
+    yield fake
+    fake.close()
+
+
+def _dev_tree(root):
+    """/dev with kfd and two GPUs' DRM nodes + by-path links (bus c1 -> card1/renderD129,
+    bus c2 -> card2/renderD130)."""
+    os.makedirs(os.path.join(root, "dri", "by-path"))
+    open(os.path.join(root, "kfd"), "w").close()
+    for card, render, bus in ((1, 129, "0000:c1:00.0"), (2, 130, "0000:c2:00.0")):
+        for name in (f"card{card}", f"renderD{render}"):
+            open(os.path.join(root, "dri", name), "w").close()
+        os.symlink(f"../card{card}", os.path.join(root, "dri", "by-path", f"pci-{bus}-card"))
+        os.symlink(f"../renderD{render}", os.path.join(root, "dri", "by-path", f"pci-{bus}-render"))
+
+
+def test_engine_config_maps_rocm_devices_mounts_and_shm(tmp_path):
+    dev = str(tmp_path / "dev")
+    _dev_tree(dev)
+    devices = [{"id": 3, "uuid": "GPU-a", "type": "rocm", "pci_bus": "0000:C1:00.0", "device_index": 0}]
+    spec = {"allocation_id": "7.1.0", "task_id": "7.1", "container": {
+        "image": {"cpu": "img-cpu", "rocm": "img-rocm"}, "shm_size": 2 ** 31,
+        "bind_mounts": [{"host_path": "/datasets", "container_path": "/data", "read_only": True,
+                         "propagation": "rprivate"},
+                        {"host_path": "/scratch", "container_path": "scratch", "read_only": False,
+                         "propagation": "rshared"}],
+        "devices": [{"host_path": "/dev/infiniband", "container_path": "/dev/infiniband", "mode": "rwm"}],
+        "add_capabilities": ["IPC_LOCK"], "drop_capabilities": ["NET_RAW"]}}
+    env = {"DET_CONTEXT_DIR": "/host/ctx", "PYTHONPATH": "/host/ctx:/fw", "HIP_VISIBLE_DEVICES": "0",
+           "DET_MASTER": "http://127.0.0.1:8080"}
+    cfg = containers.engine_config(spec, [sys.executable, "-m", "determined_clone_amd.exec.launch"], env,
+                                   "/host/ctx", devices, "agent-0", "/fw", dev_root=dev)
+    host = cfg["HostConfig"]
+    paths = [d["PathOnHost"] for d in host["Devices"]]
+    assert paths == ["/dev/infiniband", f"{dev}/kfd", f"{dev}/dri/card1", f"{dev}/dri/renderD129"]
+    assert host["GroupAdd"] == ["video"] and host["SecurityOpt"] == ["seccomp=unconfined"]
+    assert host["ShmSize"] == 2 ** 31 and host["CapAdd"] == ["IPC_LOCK"] and host["CapDrop"] == ["NET_RAW"]
+    mounts = {m["Target"]: m for m in host["Mounts"]}
+    assert mounts[containers.WORKDIR]["Source"] == "/host/ctx"
+    assert mounts[containers.FRAMEWORK_MOUNT]["ReadOnly"]
+    assert mounts["/data"]["ReadOnly"] and mounts["/data"]["Source"] == "/datasets"
+    assert mounts[containers.WORKDIR + "/scratch"]["BindOptions"]["Propagation"] == "rshared"
+    assert cfg["Image"] == "img-rocm"
+    env_in = dict(e.split("=", 1) for e in cfg["Env"])
+    assert "HIP_VISIBLE_DEVICES" not in env_in  # the device mapping confines the container
+    assert env_in["DET_CONTEXT_DIR"] == containers.WORKDIR and env_in["DET_SLOT_IDS"] == "[3]"
+    assert cfg["Cmd"][:2] == ["bash", f"{containers.FRAMEWORK_MOUNT}/determined_clone_amd/exec/entrypoint.sh"]
+    assert cfg["Cmd"][2] == "python3"
+    assert cfg["Labels"][containers.LABEL_ALLOC] == "7.1.0"
+    # a second slot of the same GPU maps the same nodes once; an unknown bus is an error
+    two = devices + [dict(devices[0], id=4)]
+    assert containers.rocm_device_paths(two, dev).count(f"{dev}/dri/renderD129") == 1
+    with pytest.raises(RuntimeError):
+        containers.rocm_device_paths([{"type": "rocm", "pci_bus": "0000:ff:00.0", "uuid": "x"}], dev)
+
+
+def test_pull_uses_registry_auth_and_force_pull(docker):
+    rt = containers.EngineRuntime("agent-0", docker.sock_path)
+    assert rt.available()
+    auth = {"username": "u", "password": "p", "serveraddress": "registry.example:5000"}
+    spec = {"container": {"registry_auth": auth}}
+    rt.ensure_image(spec, "registry.example:5000/team/img:1.0")
+    assert docker.pulls == [{"image": "registry.example:5000/team/img:1.0", "auth": auth}]
+    rt.ensure_image(spec, "registry.example:5000/team/img:1.0")  # present: no second pull
+    assert len(docker.pulls) == 1
+    rt.ensure_image({"container": {"force_pull_image": True}}, "registry.example:5000/team/img:1.0")
+    assert len(docker.pulls) == 2
+    assert containers.split_image("ubuntu") == ("ubuntu", "latest")
+    assert containers.split_image("a/b@sha256:00") == ("a/b@sha256:00", "")
+
+
+MODEL_DEF = '''
+import os
+import torch
+from determined_clone_amd import pytorch
+
+class Ones(torch.utils.data.Dataset):
+    def __len__(self):
+        return 16
+    def __getitem__(self, i):
+        return torch.tensor([1.0]), torch.tensor([1.0])
+
+class HookTrial(pytorch.PyTorchTrial):
+    def __init__(self, context):
+        self.context = context
+        print("hook variable:", os.environ.get("HOOK_VAR"), flush=True)
+        print("context dir:", os.environ.get("DET_CONTEXT_DIR"), flush=True)
+        self.model = context.wrap_model(torch.nn.Linear(1, 1, bias=False))
+        self.opt = context.wrap_optimizer(torch.optim.SGD(self.model.parameters(), lr=0.1))
+    def train_batch(self, batch, epoch_idx, batch_idx):
+        x, y = batch
+        loss = torch.nn.functional.mse_loss(self.model(x), y)
+        self.context.backward(loss)
+        self.context.step_optimizer(self.opt)
+        return {"loss": loss}
+    def evaluate_batch(self, batch, batch_idx):
+        x, y = batch
+        return {"val_loss": torch.nn.functional.mse_loss(self.model(x), y)}
+    def build_training_data_loader(self):
+        return pytorch.DataLoader(Ones(), batch_size=4)
+    def build_validation_data_loader(self):
+        return pytorch.DataLoader(Ones(), batch_size=4)
+'''
+
+CONFIG = """
+name: in-a-container
+entrypoint: model_def:HookTrial
+hyperparameters: {global_batch_size: 4}
+max_restarts: 0
+searcher: {name: single, metric: val_loss, max_length: {batches: 4}}
+environment:
+  image: {cpu: "registry.example/det/cpu-img:2", rocm: "registry.example/det/rocm-img:2"}
+  registry_auth: {username: robot, password: hunter2}
+  force_pull_image: true
+bind_mounts:
+  - {host_path: /tmp, container_path: /shared, read_only: true}
+resources: {shm_size: 4 gb}
+"""
+
+
+def _cluster(tmp, **agent_kw):
+    m = Master(os.path.join(tmp, "m.db"), checkpoint_storage={"type": "shared_fs", "host_path": os.path.join(tmp, "ckpt")})
+    srv = MasterServer(m, "127.0.0.1", 0).start()
+    agent = Agent(m.master_url, "agent-c", artificial_slots=2, **agent_kw).start_background()
+    s = Session(m.master_url)
+    s.token = s.post("/api/v1/auth/login", {"username": "admin", "password": ""})["token"]
+    return m, srv, agent, s
+
+
+def _run_experiment(s, ctx, cfg, timeout=240):
+    body = {"config": cfg, "model_definition": base64.b64encode(tar_directory(ctx)).decode()}
+    eid = s.post("/api/v1/experiments", body)["experiment"]["id"]
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        st = s.get(f"/api/v1/experiments/{eid}")["experiment"]["state"]
+        if st in ("COMPLETED", "CANCELED", "ERROR"):
+            break
+        time.sleep(0.5)
+    tid = s.get(f"/api/v1/experiments/{eid}/trials")["trials"][0]["id"]
+    logs = [x["log"] for x in s.get(f"/api/v1/trials/{tid}/logs")["logs"]]
+    return st, logs
+
+
+def _ctx(tmp):
+    ctx = os.path.join(tmp, "ctx")
+    os.makedirs(ctx)
+    with open(os.path.join(ctx, "model_def.py"), "w") as f:
+        f.write(MODEL_DEF)
+    with open(os.path.join(ctx, "startup-hook.sh"), "w") as f:
+        f.write('export HOOK_VAR="set-by-startup-hook"\necho "startup hook ran"\n')
+    return ctx
+
+
+def test_managed_trial_runs_in_a_container_with_startup_hook(docker):
+    tmp = tempfile.mkdtemp(prefix="det-ct-")
+    m, srv, agent, s = _cluster(tmp, container_runtime="docker", container_socket=docker.sock_path)
+    try:
+        assert isinstance(agent.containers, containers.EngineRuntime)
+        st, logs = _run_experiment(s, _ctx(tmp), CONFIG)
+        assert st == "COMPLETED", logs[-30:]
+        assert any("hook variable: set-by-startup-hook" in x for x in logs), logs[:40]
+        assert any("startup hook ran" in x for x in logs)
+        create = docker.creates[-1]
+        # the task environment is expressed in the container's paths (the fake daemon maps the
+        # mount targets back to host paths when it runs the "container" as a process)
+        env_in = dict(e.split("=", 1) for e in create["Env"])
+        assert env_in["DET_CONTEXT_DIR"] == containers.WORKDIR and create["WorkingDir"] == containers.WORKDIR
+        assert create["Image"] == "registry.example/det/cpu-img:2"
+        host = create["HostConfig"]
+        assert host["ShmSize"] == 4 * 1000 ** 3
+        assert {"Type": "bind", "Source": "/tmp", "Target": "/shared", "ReadOnly": True,
+                "BindOptions": {"Propagation": "rprivate"}} in host["Mounts"]
+        assert docker.pulls and docker.pulls[-1]["auth"] == {"username": "robot", "password": "hunter2"}
+        assert create["Labels"][containers.LABEL_AGENT] == "agent-c"
+        time.sleep(0.5)
+        assert not docker.containers  # removed once its exit was reported
+    finally:
+        agent.stop()
+        srv.stop()
+
+
+def test_process_runtime_sources_the_startup_hook_too():
+    tmp = tempfile.mkdtemp(prefix="det-ph-")
+    m, srv, agent, s = _cluster(tmp, container_runtime="process")
+    try:
+        assert agent.containers is None
+        st, logs = _run_experiment(s, _ctx(tmp), CONFIG)
+        assert st == "COMPLETED", logs[-30:]
+        assert any("hook variable: set-by-startup-hook" in x for x in logs)
+    finally:
+        agent.stop()
+        srv.stop()
+
+
+def test_restarted_agent_reattaches_to_its_running_container(docker):
+    tmp = tempfile.mkdtemp(prefix="det-ra-")
+    m = Master(os.path.join(tmp, "m.db"))
+    srv = MasterServer(m, "127.0.0.1", 0).start()
+    try:
+        rt = containers.EngineRuntime("agent-r", docker.sock_path)
+        docker.images.add(containers.DEFAULT_IMAGES["cpu"])
+        ctx = os.path.join(tmp, "ctx")
+        os.makedirs(ctx)
+        spec = {"allocation_id": "task-9.0", "task_id": "task-9", "container": {}}
+        code = "import time\nfor i in range(30):\n    print('tick', i, flush=True)\n    time.sleep(0.1)\n"
+        rt.launch(spec, [sys.executable, "-c", code], {}, ctx, [], runtime.FRAMEWORK_ROOT)
+        time.sleep(0.5)
+        # a new agent process with the same id finds the container by its labels
+        events = []
+        agent = Agent(m.master_url, "agent-r", artificial_slots=1, container_runtime="docker",
+                      container_socket=docker.sock_path)
+        agent._event = lambda alloc, state, exit_code=None: events.append((alloc, state, exit_code))
+        agent._reattach()
+        assert "task-9.0" in agent.tasks and ("task-9.0", "RUNNING", None) in events
+        t0 = time.time()
+        while ("task-9.0", "TERMINATED", 0) not in events and time.time() - t0 < 15:
+            time.sleep(0.1)
+        assert ("task-9.0", "TERMINATED", 0) in events
+        time.sleep(0.3)
+        assert not docker.containers
+        # a container that exited while no agent watched is reported and removed
+        rt.launch(spec, [sys.executable, "-c", "raise SystemExit(3)"], {}, ctx, [], runtime.FRAMEWORK_ROOT)
+        time.sleep(1.0)
+        events.clear()
+        agent._reattach()
+        assert events == [("task-9.0", "TERMINATED", 3)] and not docker.containers
+    finally:
+        srv.stop()
+
+
+def test_auto_runtime_falls_back_to_processes_without_a_daemon(tmp_path):
+    assert containers.make_runtime("auto", "a", socket_path=str(tmp_path / "none.sock")) is None
+    with pytest.raises(RuntimeError):
+        containers.make_runtime("docker", "a", socket_path=str(tmp_path / "none.sock"))
+
+
+def test_apptainer_command_line():
+    rt = containers.ApptainerRuntime(binary="apptainer")
+    spec = {"allocation_id": "1.1.0", "task_id": "1.1", "container": {
+        "image": "registry.example/det/rocm-img:2",
+        "bind_mounts": [{"host_path": "/datasets", "container_path": "/data", "read_only": True}]}}
+    devices = [{"id": 0, "type": "rocm", "device_index": 2}, {"id": 1, "type": "rocm", "device_index": 5}]
+    argv, env = rt.argv(spec, [sys.executable, "-m", "determined_clone_amd.exec.launch"],
+                        {"DET_MASTER": "http://m:8080", "HIP_VISIBLE_DEVICES": "2,5"}, "/ctx", devices, "/fw")
+    assert argv[:2] == ["apptainer", "exec"] and "--rocm" in argv
+    assert "/datasets:/data:ro" in argv and f"/ctx:{containers.WORKDIR}" in argv
+    assert "docker://registry.example/det/rocm-img:2" in argv
+    assert env["APPTAINERENV_ROCR_VISIBLE_DEVICES"] == "2,5" and env["APPTAINERENV_DET_MASTER"] == "http://m:8080"
+    assert "APPTAINERENV_HIP_VISIBLE_DEVICES" not in env
+
+
+def test_entrypoint_sources_hook(tmp_path):
+    (tmp_path / "startup-hook.sh").write_text("export FROM_HOOK=42\n")
+    cmd = runtime.with_startup_hook([sys.executable, "-c", "import os; print(os.environ['FROM_HOOK'])"],
+                                    str(tmp_path))
+    assert cmd[:2] == ["bash", runtime.ENTRYPOINT_SH]
+    out = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, check=True).stdout
+    assert out.strip() == "42"
+    assert runtime.with_startup_hook(["true"], str(tmp_path / "nohook")) == ["true"]

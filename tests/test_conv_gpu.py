@@ -162,6 +162,7 @@ def test_pointwise_library_choice_matches_fp32(shape, stride, choice):
         _close(c.weight.grad, w2.grad, 2e-2, "wgrad")
     finally:
         conv._CHOICE.clear()
+        conv.load_choices()  # back to the shipped decisions for later tests
 
 
 @pytest.mark.parametrize("dgrad_choice", [None, 0, 1])
@@ -187,6 +188,7 @@ def test_pointwise_dual_matches_two_convs(stride, dgrad_choice):
         torch.autograd.backward([y1, yp], [g1, gp])
     finally:
         conv._CHOICE.clear()
+        conv.load_choices()  # back to the shipped decisions for later tests
     x2 = x.float().clone().requires_grad_(True)
     w1 = c1.weight.detach().float().clone().requires_grad_(True)
     wp = cp.weight.detach().float().clone().requires_grad_(True)
