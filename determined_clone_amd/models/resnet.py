@@ -16,8 +16,13 @@ architecture is defined here. It is laid out for MI355X rather than copied:
 * 1x1/stride-1 convolutions go through ``ops.conv.pointwise_conv``: MIOpen by default (measured
   faster), or with ``DCA_CONV1X1=1`` hand-written MFMA GEMM kernels (``ops/csrc/conv1x1.hip``)
   whose forward epilogue also reduces the next BatchNorm's statistics;
+* a downsampling block's tail ``relu(bn3(conv3(..)) + bn_ds(proj(x)))`` is ONE fused op
+  (``ops.batchnorm.batch_norm_act_dual``): the projection shortcut's BatchNorm is applied inside
+  bn3's apply pass (its output is never written) and both BatchNorms' backward share one
+  statistics pass and one apply pass (``DCA_BN_DUAL=0`` keeps two separate BatchNorms);
 * the classifier is a plain PyTorch op (<2 % of step time).
 """
+import os
 from typing import List, Optional, Type
 
 import torch
@@ -27,6 +32,8 @@ import torch.nn.functional as F
 from determined_clone_amd.ops import batchnorm as bn_ops
 from determined_clone_amd.ops import conv as conv_ops
 from determined_clone_amd.ops.conv import pointwise_conv, pointwise_dual
+
+BN_DUAL = os.environ.get("DCA_BN_DUAL", "1") != "0"
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -96,8 +103,13 @@ class Bottleneck(nn.Module):
                 yd = pointwise_conv(ds_conv, x, ds_bn.training)
             else:
                 y1, yd = pointwise_dual(self.conv1, ds_conv, x, self.bn1.training)
-            identity = ds_bn(yd)
             out = self.bn1(y1)
+            if BN_DUAL and self.bn3.relu and not ds_bn.relu:
+                out = self.bn2(conv_ops.spatial_conv(self.conv2, out, self.bn2.training))
+                # relu(bn3(conv3) + bn_ds(proj)): one fused op, the shortcut BN never written
+                return bn_ops.batch_norm_act_dual(pointwise_conv(self.conv3, out, self.bn3.training),
+                                                  self.bn3, yd, ds_bn)
+            identity = ds_bn(yd)
         # 3x3: implicit-GEMM MFMA kernel whose epilogue also reduces bn2's statistics
         out = self.bn2(conv_ops.spatial_conv(self.conv2, out, self.bn2.training))
         # identity shortcut: x also feeds conv1, so its gradient can be summed inside the

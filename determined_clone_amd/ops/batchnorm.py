@@ -159,6 +159,109 @@ def batch_norm_act(x: torch.Tensor, weight: Optional[torch.Tensor], bias: Option
     return _ext.load().bn_fwd_affine(x, residual, scale, shift, relu)
 
 
+# ----------------------------------------------------------------------------- dual (shortcut) fusion
+def reference_batch_norm_act_dual(x, bn, x2, bn2, relu=True):
+    """fp32 / CPU oracle: ``act(bn(x) + bn2(x2))`` with two ``nn.BatchNorm2d``-like modules."""
+    y = F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.training,
+                     bn.momentum if bn.momentum is not None else 0.0, bn.eps)
+    y2 = F.batch_norm(x2, bn2.running_mean, bn2.running_var, bn2.weight, bn2.bias, bn2.training,
+                      bn2.momentum if bn2.momentum is not None else 0.0, bn2.eps)
+    y = y + y2
+    return F.relu(y) if relu else y
+
+
+class _BNActDualTrain(torch.autograd.Function):
+    """``act(bn(x) + bn2(x2))``: the main-branch BatchNorm of a downsampling ResNet block and its
+    projection shortcut's BatchNorm in one apply pass forward (the shortcut's normalised tensor is
+    never written) and one statistics + one apply pass backward (both inputs' gradients from the
+    shared masked gradient) -- ``csrc/batchnorm.hip`` ``bn_*_train_dual``."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, x2, weight2, bias2, running_mean, running_var, num_batches,
+                running_mean2, running_var2, num_batches2, momentum, eps, relu, out_sink,
+                partials, partials2):
+        y, m1, i1, mask, m2, i2 = _ext.load().bn_fwd_train_dual(
+            x, weight, bias, running_mean, running_var, num_batches, x2, weight2, bias2,
+            running_mean2, running_var2, num_batches2, momentum, eps, relu, partials, partials2)
+        ctx.save_for_backward(x, x2, mask if relu else None, weight, weight2, m1, i1, m2, i2)
+        ctx.relu = relu
+        ctx.out_sink = out_sink
+        ctx.params = (weight, bias, weight2, bias2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, x2, mask, weight, weight2, m1, i1, m2, i2 = ctx.saved_tensors
+        n = ctx.needs_input_grad
+        need_w = any(n[i] for i in (1, 2, 4, 5))
+        dy2 = ctx.out_sink.grad if ctx.out_sink is not None else None
+        if ctx.out_sink is not None:
+            ctx.out_sink.grad = None
+        acc = []
+        if need_w:
+            t1, t2 = _direct_grad_targets(ctx.params[0], ctx.params[1])
+            t3, t4 = _direct_grad_targets(ctx.params[2], ctx.params[3])
+            if all(t is not None for t in (t1, t2, t3, t4)):
+                acc = [t1, t2, t3, t4]
+        dx, dx2, dg, db, dg2, db2 = _ext.load().bn_bwd_train_dual(
+            dy, x, mask, weight, m1, i1, x2, weight2, m2, i2, ctx.relu, need_w, dy2, acc)
+        if acc:
+            dg = db = dg2 = db2 = None  # accumulated into the parameters' .grad views
+        return (dx, dg if n[1] else None, db if n[2] else None, dx2, dg2 if n[4] else None,
+                db2 if n[5] else None) + (None,) * 12
+
+
+def batch_norm_act_dual(x: torch.Tensor, bn: torch.nn.BatchNorm2d, x2: torch.Tensor,
+                        bn2: torch.nn.BatchNorm2d, relu: bool = True) -> torch.Tensor:
+    """``act(bn(x) + bn2(x2))`` -- e.g. ``relu(bn3(conv3(...)) + bn_ds(conv_ds(x)))``, a ResNet
+    downsampling block's tail, with torch BatchNorm semantics for both (running statistics,
+    ``num_batches_tracked``). GPU: fused kernels (see :class:`_BNActDualTrain`); the statistics
+    partials a convolution epilogue attached to ``x`` / ``x2`` are used. Elsewhere: the plain
+    PyTorch composition."""
+    training = bn.training or bn.running_mean is None
+    ok = (_hip_ok(x) and x.dim() == 4 and x2.shape == x.shape and x2.dtype == x.dtype
+          and bn.momentum is not None and bn2.momentum is not None and training == (bn2.training or bn2.running_mean is None)
+          and bn.eps == bn2.eps and bn.momentum == bn2.momentum)
+    if not ok:
+        for m in (bn, bn2):
+            if m.training and m.num_batches_tracked is not None:
+                m.num_batches_tracked.add_(1)
+        return reference_batch_norm_act_dual(x, bn, x2, bn2, relu)
+    p1 = getattr(x, "_dca_bn_partials", None)
+    p2 = getattr(x2, "_dca_bn_partials", None)
+    x = x.contiguous(memory_format=torch.channels_last)
+    x2 = x2.contiguous(memory_format=torch.channels_last)
+    if not training:  # inference: y = act(x*s + t + x2*s2 + t2)
+        def affine(m):
+            scale = torch.rsqrt(m.running_var.float() + m.eps)
+            if m.weight is not None:
+                scale = scale * m.weight.float()
+            shift = -m.running_mean.float() * scale
+            if m.bias is not None:
+                shift = shift + m.bias.float()
+            return scale, shift
+        (s1, t1), (s2, t2) = affine(bn), affine(bn2)
+        if torch.is_grad_enabled() and (x.requires_grad or x2.requires_grad):
+            shape = (1, -1, 1, 1)
+            y = x * s1.view(shape).to(x.dtype) + t1.view(shape).to(x.dtype) + \
+                x2 * s2.view(shape).to(x.dtype) + t2.view(shape).to(x.dtype)
+            return F.relu(y) if relu else y
+        C = _ext.load()
+        return C.bn_fwd_affine(x, C.bn_fwd_affine(x2, None, s2, t2, False), s1, t1, relu)
+    out_sink = ResidualGradSink() if torch.is_grad_enabled() else None
+    y = _BNActDualTrain.apply(x, bn.weight, bn.bias, x2, bn2.weight, bn2.bias,
+                              bn.running_mean if bn.training else None,
+                              bn.running_var if bn.training else None,
+                              bn.num_batches_tracked if bn.training else None,
+                              bn2.running_mean if bn2.training else None,
+                              bn2.running_var if bn2.training else None,
+                              bn2.num_batches_tracked if bn2.training else None,
+                              float(bn.momentum), float(bn.eps), relu, out_sink, p1, p2)
+    if out_sink is not None:
+        y._dca_grad_sink = out_sink
+    return y
+
+
 # ----------------------------------------------------------------------------- stem fusion
 def reference_bn_relu_maxpool(x, weight, bias, running_mean, running_var, training=True,
                               momentum=0.1, eps=1e-5):

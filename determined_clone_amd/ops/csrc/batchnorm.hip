@@ -104,12 +104,17 @@ __device__ __forceinline__ void st8(void* base, int64_t elem_off, const float (&
 // the tensors' producer (a convolution, or the previous pass) wrote/read them ascending, so the
 // rows it touched last are still in the 256 MB Infinity Cache when the first chunks run here;
 // the apply pass then walks ascending and starts on the rows this pass read last.
-template <typename T, bool BWD, int U, bool NT = false>
+// DUAL (backward only): a second BatchNorm input x2 whose output was ADDED before the ReLU
+// (relu(bn(x) + bn2(x2)), the projection shortcut of a downsampling block) shares the masked
+// upstream gradient dy'; the pass also reduces sum dy'*(x2-mean2) into partial2 (whose first
+// statistic, sum dy', is the same as partial's).
+template <typename T, bool BWD, int U, bool NT = false, bool DUAL = false>
 __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
     const void* __restrict__ x, const void* __restrict__ dy, const void* __restrict__ dy2,
     const uint8_t* __restrict__ mask, const float* __restrict__ mean, int64_t M, int C, int tpr,
-    int rpi, bool relu, float* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][tpr*16]
+    int rpi, bool relu, float* __restrict__ partial, const void* __restrict__ x2,
+    const float* __restrict__ mean2, float* __restrict__ partial2) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [rpi][tpr*(DUAL ? 24 : 16)]
   const int tid = threadIdx.x;
   const int lc = tid % tpr, r0 = tid / tpr;
   const int c = (blockIdx.y * tpr + lc) * 8;
@@ -119,15 +124,21 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
   float s[8], q[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; }
-  float mu[8];
+  float mu[8], mu2[8], q2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) q2[k] = 0.f;
   if (BWD && active) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) mu[k] = mean[c + k];
+    if (DUAL) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mu2[k] = mean2[c + k];
+    }
   }
   if (active) {
     int64_t r = rr.begin + r0;
     for (; r + (U - 1) * rpi < rr.end; r += U * rpi) {
-      Raw8<T> rx[U], rg[U], rg2[U];
+      Raw8<T> rx[U], rg[U], rg2[U], rx2[U];
       uint32_t mk[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -136,6 +147,7 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
         if (BWD) {
           rg[u] = NT ? ld8nt<T>(dy, off) : ld8<T>(dy, off);
           if (dy2) rg2[u] = NT ? ld8nt<T>(dy2, off) : ld8<T>(dy2, off);
+          if (DUAL) rx2[u] = NT ? ld8nt<T>(x2, off) : ld8<T>(x2, off);
           mk[u] = relu ? mask[off >> 3] : 0xffu;
         }
       }
@@ -155,11 +167,14 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
 #pragma unroll
             for (int k = 0; k < 8; ++k) g[k] += g2[k];
           }
+          float x2v[8];
+          if (DUAL) unpack8<T>(rx2[u], x2v);
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             const float gk = ((mk[u] >> k) & 1u) ? g[k] : 0.f;
             s[k] += gk;
             q[k] = fmaf(gk, xv[k] - mu[k], q[k]);
+            if (DUAL) q2[k] = fmaf(gk, x2v[k] - mu2[k], q2[k]);
           }
         }
       }
@@ -187,21 +202,37 @@ __global__ __launch_bounds__(kBlock) void bn_reduce_kernel(
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) { s[k] += g[k]; q[k] = fmaf(g[k], xv[k] - mu[k], q[k]); }
+        if (DUAL) {
+          float x2v[8];
+          unpack8<T>(ld8<T>(x2, off), x2v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) q2[k] = fmaf(g[k], x2v[k] - mu2[k], q2[k]);
+        }
       }
     }
   }
-  // Combine the rpi row-groups that share channels through LDS.
-  const int width = tpr * 16;
-  float* mine = lds + r0 * width + lc * 16;
+  // Combine the rpi row-groups that share channels through LDS: per lane 8 channels x
+  // (sum, sum2 [, dual sum2]).
+  constexpr int W = DUAL ? 24 : 16;
+  const int width = tpr * W;
+  float* mine = lds + r0 * width + lc * W;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { mine[k] = s[k]; mine[8 + k] = q[k]; }
+  for (int k = 0; k < 8; ++k) {
+    mine[k] = s[k];
+    mine[8 + k] = q[k];
+    if (DUAL) mine[16 + k] = q2[k];
+  }
   __syncthreads();
   for (int o = tid; o < width; o += kBlock) {
     float acc = 0.f;
     for (int r = 0; r < rpi; ++r) acc += lds[r * width + o];
-    const int lco = o / 16, k = o % 16;
+    const int lco = o / W, k = o % W, stat = k >> 3;
     const int ch = (blockIdx.y * tpr + lco) * 8 + (k & 7);
-    if (ch < C) partial[(static_cast<int64_t>(bx) * 2 + (k >> 3)) * C + ch] = acc;
+    if (ch >= C) continue;
+    const int64_t b2 = static_cast<int64_t>(bx) * 2;
+    if (stat < 2) partial[(b2 + stat) * C + ch] = acc;
+    if (DUAL && stat == 0) partial2[b2 * C + ch] = acc;
+    if (DUAL && stat == 2) partial2[(b2 + 1) * C + ch] = acc;
   }
 }
 
@@ -302,11 +333,14 @@ __global__ __launch_bounds__(kBlock) void bn_finalize_bwd_kernel(
 
 // y = act(x*scale + shift [+ res]) (+ ReLU bitmask), row-tile mapping, U rows in flight per lane.
 // Bit k of mask byte (row*C + c)/8 is the ReLU decision of channel c+k.
+// res2_scale / res2_shift (optional): the residual is itself normalised in this pass,
+// res -> res*res2_scale + res2_shift (a projection shortcut's BatchNorm, never materialised).
 template <typename T, int U>
 __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
     const void* __restrict__ x, const void* __restrict__ res, void* __restrict__ y,
     const float* __restrict__ scale, const float* __restrict__ shift, int64_t M, int C, int tpr,
-    int rpi, bool relu, uint8_t* __restrict__ mask) {
+    int rpi, bool relu, uint8_t* __restrict__ mask, const float* __restrict__ res2_scale,
+    const float* __restrict__ res2_shift) {
   const int tid = threadIdx.x;
   const int lc = tid % tpr, r0 = tid / tpr;
   const BlkMap bm = apply_block_map(C, tpr);
@@ -321,6 +355,12 @@ __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
     const float4 b1 = *reinterpret_cast<const float4*>(shift + c + 4);
     a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
     b[0] = b0.x; b[1] = b0.y; b[2] = b0.z; b[3] = b0.w; b[4] = b1.x; b[5] = b1.y; b[6] = b1.z; b[7] = b1.w;
+  }
+  float a2[8], b2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a2[k] = res2_scale ? res2_scale[c + k] : 1.f;
+    b2[k] = res2_shift ? res2_shift[c + k] : 0.f;
   }
   auto finish = [&](int64_t off, float (&o)[8]) {
     if (relu) {
@@ -354,7 +394,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
         float rv[8];
         unpack8<T>(rres[u], rv);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] += rv[k];
+        for (int k = 0; k < 8; ++k) o[k] += fmaf(rv[k], a2[k], b2[k]);
       }
       finish(off, o);
     }
@@ -369,7 +409,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
       float rv[8];
       unpack8<T>(ld8<T>(res, off), rv);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] += rv[k];
+      for (int k = 0; k < 8; ++k) o[k] += fmaf(rv[k], a2[k], b2[k]);
     }
     finish(off, o);
   }
@@ -377,21 +417,28 @@ __global__ __launch_bounds__(kBlock) void bn_apply_fwd_kernel(
 
 // dx = k1*dy' + k2*x + k3 with dy' = (dy [+ dy2]) masked by the ReLU bit; dres = dy' when the
 // forward fused a residual add. Row-tile mapping, coefficients held in registers.
-template <typename T, int U>
+// DUAL: also dx2 = k1b*dy' + k2b*x2 + k3b for the second BatchNorm input that was added before
+// the ReLU (coef2 = its [3][C] coefficients); dres is not written then (dy' is consumed here).
+template <typename T, int U, bool DUAL = false>
 __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
     const void* __restrict__ dy, const void* __restrict__ dy2, const uint8_t* __restrict__ mask,
     const void* __restrict__ x, const float* __restrict__ coef, void* __restrict__ dx,
-    void* __restrict__ dres, int64_t M, int C, int tpr, int rpi, bool relu) {
+    void* __restrict__ dres, int64_t M, int C, int tpr, int rpi, bool relu,
+    const void* __restrict__ x2, const float* __restrict__ coef2, void* __restrict__ dx2) {
   const int tid = threadIdx.x;
   const int lc = tid % tpr, r0 = tid / tpr;
   const BlkMap bm = apply_block_map(C, tpr);
   const int c = (bm.cg * tpr + lc) * 8;
   if (c >= C) return;
   const RowRange rr = chunk_rows(M, rpi, bm.bx, bm.nb);
-  float k1[8], k2[8], k3[8];
+  float k1[8], k2[8], k3[8], j1[8], j2[8], j3[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { k1[k] = coef[c + k]; k2[k] = coef[C + c + k]; k3[k] = coef[2 * C + c + k]; }
-  auto body = [&](int64_t off, float (&g)[8], const float (&xv)[8], uint32_t m) {
+  if (DUAL) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { j1[k] = coef2[c + k]; j2[k] = coef2[C + c + k]; j3[k] = coef2[2 * C + c + k]; }
+  }
+  auto body = [&](int64_t off, float (&g)[8], const float (&xv)[8], const float (&x2v)[8], uint32_t m) {
     if (relu) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] = ((m >> k) & 1u) ? g[k] : 0.f;
@@ -400,11 +447,17 @@ __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], g[k], fmaf(k2[k], xv[k], k3[k]));
     st8<T>(dx, off, o);
-    if (dres) st8<T>(dres, off, g);
+    if (DUAL) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = fmaf(j1[k], g[k], fmaf(j2[k], x2v[k], j3[k]));
+      st8<T>(dx2, off, o);
+    } else if (dres) {
+      st8<T>(dres, off, g);
+    }
   };
   int64_t r = rr.begin + r0;
   for (; r + (U - 1) * rpi < rr.end; r += U * rpi) {
-    Raw8<T> rg[U], rg2[U], rx[U];
+    Raw8<T> rg[U], rg2[U], rx[U], rx2[U];
     uint32_t mk[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -412,12 +465,13 @@ __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
       rg[u] = ld8<T>(dy, off);
       if (dy2) rg2[u] = ld8<T>(dy2, off);
       rx[u] = ld8<T>(x, off);
+      if (DUAL) rx2[u] = ld8<T>(x2, off);
       mk[u] = relu ? mask[off >> 3] : 0xffu;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t off = (r + u * rpi) * C + c;
-      float g[8], xv[8];
+      float g[8], xv[8], x2v[8];
       unpack8<T>(rg[u], g);
       if (dy2) {
         float g2[8];
@@ -426,12 +480,13 @@ __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
         for (int k = 0; k < 8; ++k) g[k] += g2[k];
       }
       unpack8<T>(rx[u], xv);
-      body(off, g, xv, mk[u]);
+      if (DUAL) unpack8<T>(rx2[u], x2v);
+      body(off, g, xv, x2v, mk[u]);
     }
   }
   for (; r < rr.end; r += rpi) {
     const int64_t off = r * C + c;
-    float g[8], xv[8];
+    float g[8], xv[8], x2v[8];
     unpack8<T>(ld8<T>(dy, off), g);
     if (dy2) {
       float g2[8];
@@ -440,7 +495,8 @@ __global__ __launch_bounds__(kBlock) void bn_apply_bwd_kernel(
       for (int k = 0; k < 8; ++k) g[k] += g2[k];
     }
     unpack8<T>(ld8<T>(x, off), xv);
-    body(off, g, xv, relu ? mask[off >> 3] : 0xffu);
+    if (DUAL) unpack8<T>(ld8<T>(x2, off), x2v);
+    body(off, g, xv, x2v, relu ? mask[off >> 3] : 0xffu);
   }
 }
 
@@ -550,21 +606,25 @@ template <typename T>
 void launch_reduce(bool bwd, const void* x, const void* dy, const void* dy2, const uint8_t* y,
                    const float* mean,
                    int64_t M, int C, bool relu, float* partial, int B, const ReduceGeom& g,
-                   hipStream_t st) {
+                   hipStream_t st, const void* x2 = nullptr, const float* mean2 = nullptr,
+                   float* partial2 = nullptr) {
   dim3 grid(B, g.cgroups);
-  size_t lds = static_cast<size_t>(g.rpi) * g.tpr * 16 * sizeof(float);
+  const bool dual = bwd && x2 != nullptr;
+  size_t lds = static_cast<size_t>(g.rpi) * g.tpr * (dual ? 24 : 16) * sizeof(float);
   const ReduceVar& v = reduce_var();
-#define DCA_RED(BW, UU, NTT)                                                                       \
-  hipLaunchKernelGGL((bn_reduce_kernel<T, BW, UU, NTT>), grid, dim3(kBlock), lds, st, x, dy, dy2, y, \
-                     mean, M, C, g.tpr, g.rpi, relu, partial)
-  if (bwd) {
+#define DCA_RED(BW, UU, NTT, DU)                                                                     \
+  hipLaunchKernelGGL((bn_reduce_kernel<T, BW, UU, NTT, DU>), grid, dim3(kBlock), lds, st, x, dy, dy2, \
+                     y, mean, M, C, g.tpr, g.rpi, relu, partial, x2, mean2, partial2)
+  if (dual) {
+    if (v.nt) DCA_RED(true, kUReduceBwd, true, true); else DCA_RED(true, kUReduceBwd, false, true);
+  } else if (bwd) {
     if (v.u_bwd == 8) {
-      if (v.nt) DCA_RED(true, 8, true); else DCA_RED(true, 8, false);
+      if (v.nt) DCA_RED(true, 8, true, false); else DCA_RED(true, 8, false, false);
     } else {
-      if (v.nt) DCA_RED(true, kUReduceBwd, true); else DCA_RED(true, kUReduceBwd, false);
+      if (v.nt) DCA_RED(true, kUReduceBwd, true, false); else DCA_RED(true, kUReduceBwd, false, false);
     }
   } else {
-    if (v.nt) DCA_RED(false, kUReduceFwd, true); else DCA_RED(false, kUReduceFwd, false);
+    if (v.nt) DCA_RED(false, kUReduceFwd, true, false); else DCA_RED(false, kUReduceFwd, false, false);
   }
 #undef DCA_RED
 }
@@ -572,28 +632,34 @@ void launch_reduce(bool bwd, const void* x, const void* dy, const void* dy2, con
 template <typename T>
 void launch_apply_fwd(const void* x, const void* res, void* y, const float* scale,
                       const float* shift, int64_t M, int C, bool relu, uint8_t* mask,
-                      hipStream_t st) {
+                      hipStream_t st, const float* res_scale = nullptr,
+                      const float* res_shift = nullptr) {
   const RowGeom g = row_geom(C);
   const ApplyTuning t = apply_tuning(M * C);
   const dim3 grid = apply_grid(M, g, t);
   switch (t.u) {
-    case 2: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, 2>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
-    case 8: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, 8>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
-    default: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask); break;
+    case 2: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, 2>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask, res_scale, res_shift); break;
+    case 8: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, 8>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask, res_scale, res_shift); break;
+    default: hipLaunchKernelGGL((bn_apply_fwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, x, res, y, scale, shift, M, C, g.tpr, g.rpi, relu, mask, res_scale, res_shift); break;
   }
 }
 
 template <typename T>
 void launch_apply_bwd(const void* dy, const void* dy2, const uint8_t* mask, const void* x,
                       const float* coef, void* dx, void* dres, int64_t M, int C, bool relu,
-                      hipStream_t st) {
+                      hipStream_t st, const void* x2 = nullptr, const float* coef2 = nullptr,
+                      void* dx2 = nullptr) {
   const RowGeom g = row_geom(C);
   const ApplyTuning t = apply_tuning(M * C);
   const dim3 grid = apply_grid(M, g, t);
+  if (x2 != nullptr) {  // dual: fixed 2 rows in flight (three 16-B loads + two stores per row)
+    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 2, true>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu, x2, coef2, dx2);
+    return;
+  }
   switch (t.u) {
-    case 2: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 2>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
-    case 8: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 8>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
-    default: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu); break;
+    case 2: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 2>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu, x2, coef2, dx2); break;
+    case 8: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, 8>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu, x2, coef2, dx2); break;
+    default: hipLaunchKernelGGL((bn_apply_bwd_kernel<T, kUApply>), grid, dim3(kBlock), 0, st, dy, dy2, mask, x, coef, dx, dres, M, C, g.tpr, g.rpi, relu, x2, coef2, dx2); break;
   }
 }
 
@@ -821,17 +887,21 @@ int64_t bn_workspace_floats(int64_t M, int C) {
   return static_cast<int64_t>(B) * 2 * C + 4 * static_cast<int64_t>(C);
 }
 
-void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
-                      const float* gamma, const float* beta, float* running_mean,
-                      float* running_var, float momentum, float eps, bool relu, float* save_mean,
-                      float* save_invstd, int64_t* num_batches, uint8_t* mask, float* workspace,
-                      const float* given_partials, int given_blocks, hipStream_t st) {
+// Per-channel (scale, shift) of a training-mode forward: statistics pass over x (unless the
+// producer already reduced them into given_partials, e.g. a convolution epilogue in the same
+// [B][2][C] layout), then the fp64 finalize (running stats, saved mean / invstd). Returns the
+// scale pointer inside workspace; shift = scale + C.
+static float* forward_affine_from_stats(BnDtype dt, const void* x, int64_t M, int C,
+                                        const float* gamma, const float* beta,
+                                        float* running_mean, float* running_var, float momentum,
+                                        float eps, float* save_mean, float* save_invstd,
+                                        int64_t* num_batches, float* workspace,
+                                        const float* given_partials, int given_blocks,
+                                        hipStream_t st) {
   const float* partial = given_partials;
   int B = given_blocks;
   float* scale = workspace;
   if (given_partials == nullptr) {
-    // statistics pass over x; with given_partials the producer (e.g. the pointwise-convolution
-    // GEMM epilogue, conv1x1.hip) already reduced them in the same [B][2][C] layout
     ReduceGeom g = reduce_geom(C);
     B = reduce_blocks(M, C, g);
     float* part = workspace;
@@ -847,10 +917,48 @@ void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64
   hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
                      C, M, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
                      save_invstd, scale, shift, num_batches);
+  return scale;
+}
+
+void bn_forward_train(BnDtype dt, const void* x, const void* res, void* y, int64_t M, int C,
+                      const float* gamma, const float* beta, float* running_mean,
+                      float* running_var, float momentum, float eps, bool relu, float* save_mean,
+                      float* save_invstd, int64_t* num_batches, uint8_t* mask, float* workspace,
+                      const float* given_partials, int given_blocks, hipStream_t st) {
+  const float* scale = forward_affine_from_stats(dt, x, M, C, gamma, beta, running_mean, running_var,
+                                                 momentum, eps, save_mean, save_invstd, num_batches,
+                                                 workspace, given_partials, given_blocks, st);
+  const float* shift = scale + C;
   switch (dt) {
     case BnDtype::kBF16: launch_apply_fwd<BF16>(x, res, y, scale, shift, M, C, relu, mask, st); break;
     case BnDtype::kF16: launch_apply_fwd<F16>(x, res, y, scale, shift, M, C, relu, mask, st); break;
     default: launch_apply_fwd<F32>(x, res, y, scale, shift, M, C, relu, mask, st); break;
+  }
+}
+
+// act(bn(x) + bn2(x2)): a downsampling ResNet block's main-branch BatchNorm and its projection
+// shortcut's BatchNorm in ONE apply pass -- the shortcut's normalised tensor is never written
+// (both statistics are finalised first; x2 is read once, inside the apply).
+void bn_forward_train_dual(BnDtype dt, const void* x, const void* x2, void* y, int64_t M, int C,
+                           const float* gamma, const float* beta, float* running_mean,
+                           float* running_var, const float* gamma2, const float* beta2,
+                           float* running_mean2, float* running_var2, float momentum, float eps,
+                           bool relu, float* save_mean, float* save_invstd, float* save_mean2,
+                           float* save_invstd2, int64_t* num_batches, int64_t* num_batches2,
+                           uint8_t* mask, float* workspace, float* workspace2,
+                           const float* given_partials, int given_blocks,
+                           const float* given_partials2, int given_blocks2, hipStream_t st) {
+  const float* scale = forward_affine_from_stats(dt, x, M, C, gamma, beta, running_mean, running_var,
+                                                 momentum, eps, save_mean, save_invstd, num_batches,
+                                                 workspace, given_partials, given_blocks, st);
+  const float* scale2 = forward_affine_from_stats(dt, x2, M, C, gamma2, beta2, running_mean2,
+                                                  running_var2, momentum, eps, save_mean2,
+                                                  save_invstd2, num_batches2, workspace2,
+                                                  given_partials2, given_blocks2, st);
+  switch (dt) {
+    case BnDtype::kBF16: launch_apply_fwd<BF16>(x, x2, y, scale, scale + C, M, C, relu, mask, st, scale2, scale2 + C); break;
+    case BnDtype::kF16: launch_apply_fwd<F16>(x, x2, y, scale, scale + C, M, C, relu, mask, st, scale2, scale2 + C); break;
+    default: launch_apply_fwd<F32>(x, x2, y, scale, scale + C, M, C, relu, mask, st, scale2, scale2 + C); break;
   }
 }
 
@@ -885,6 +993,39 @@ void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_
     case BnDtype::kBF16: launch_apply_bwd<BF16>(dy, dy2, y, x, coef, dx, dres, M, C, relu, st); break;
     case BnDtype::kF16: launch_apply_bwd<F16>(dy, dy2, y, x, coef, dx, dres, M, C, relu, st); break;
     default: launch_apply_bwd<F32>(dy, dy2, y, x, coef, dx, dres, M, C, relu, st); break;
+  }
+}
+
+// Backward of act(bn(x) + bn2(x2)): one statistics pass (the masked upstream gradient dy' is
+// shared; sum dy' * (x - mean) and sum dy' * (x2 - mean2) reduced together), two finalizes, one
+// apply pass writing dx and dx2 -- instead of two reduce + two apply passes and the dres tensor.
+void bn_backward_train_dual(BnDtype dt, const void* dy, const void* dy2, const uint8_t* mask,
+                            const void* x, const void* x2, int64_t M, int C, const float* gamma,
+                            const float* save_mean, const float* save_invstd,
+                            const float* gamma2, const float* save_mean2,
+                            const float* save_invstd2, bool relu, void* dx, void* dx2,
+                            float* dgamma, float* dbeta, float* dgamma2, float* dbeta2,
+                            bool accumulate_dw, float* workspace, float* workspace2,
+                            hipStream_t st) {
+  ReduceGeom g = reduce_geom(C);
+  int B = reduce_blocks(M, C, g);
+  float* partial = workspace;
+  float* coef = workspace + static_cast<int64_t>(B) * 2 * C;
+  float* partial2 = workspace2;
+  float* coef2 = workspace2 + static_cast<int64_t>(B) * 2 * C;
+  switch (dt) {
+    case BnDtype::kBF16: launch_reduce<BF16>(true, x, dy, dy2, mask, save_mean, M, C, relu, partial, B, g, st, x2, save_mean2, partial2); break;
+    case BnDtype::kF16: launch_reduce<F16>(true, x, dy, dy2, mask, save_mean, M, C, relu, partial, B, g, st, x2, save_mean2, partial2); break;
+    default: launch_reduce<F32>(true, x, dy, dy2, mask, save_mean, M, C, relu, partial, B, g, st, x2, save_mean2, partial2); break;
+  }
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
+                     C, M, gamma, save_mean, save_invstd, dgamma, dbeta, accumulate_dw, coef);
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial2, B,
+                     C, M, gamma2, save_mean2, save_invstd2, dgamma2, dbeta2, accumulate_dw, coef2);
+  switch (dt) {
+    case BnDtype::kBF16: launch_apply_bwd<BF16>(dy, dy2, mask, x, coef, dx, nullptr, M, C, relu, st, x2, coef2, dx2); break;
+    case BnDtype::kF16: launch_apply_bwd<F16>(dy, dy2, mask, x, coef, dx, nullptr, M, C, relu, st, x2, coef2, dx2); break;
+    default: launch_apply_bwd<F32>(dy, dy2, mask, x, coef, dx, nullptr, M, C, relu, st, x2, coef2, dx2); break;
   }
 }
 

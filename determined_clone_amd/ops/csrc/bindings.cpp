@@ -34,6 +34,24 @@ void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_
                        bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
                        bool accumulate_dw, float* workspace, hipStream_t st);
 
+void bn_forward_train_dual(BnDtype dt, const void* x, const void* x2, void* y, int64_t M, int C,
+                           const float* gamma, const float* beta, float* running_mean,
+                           float* running_var, const float* gamma2, const float* beta2,
+                           float* running_mean2, float* running_var2, float momentum, float eps,
+                           bool relu, float* save_mean, float* save_invstd, float* save_mean2,
+                           float* save_invstd2, int64_t* num_batches, int64_t* num_batches2,
+                           uint8_t* mask, float* workspace, float* workspace2,
+                           const float* given_partials, int given_blocks,
+                           const float* given_partials2, int given_blocks2, hipStream_t st);
+void bn_backward_train_dual(BnDtype dt, const void* dy, const void* dy2, const uint8_t* mask,
+                            const void* x, const void* x2, int64_t M, int C, const float* gamma,
+                            const float* save_mean, const float* save_invstd,
+                            const float* gamma2, const float* save_mean2,
+                            const float* save_invstd2, bool relu, void* dx, void* dx2,
+                            float* dgamma, float* dbeta, float* dgamma2, float* dbeta2,
+                            bool accumulate_dw, float* workspace, float* workspace2,
+                            hipStream_t st);
+
 void spatial_mean_backward(BnDtype dt, const void* g, void* dx, int N, int HW, int C,
                            hipStream_t st);
 
@@ -210,6 +228,100 @@ std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const Opt
                          ws.data_ptr<float>(), cur_stream());
   if (acc) return {dx, Tensor(), Tensor(), dres};
   return {dx, dgamma, dbeta, dres};
+}
+
+static void check_partials(const OptT& p, int64_t C, const Tensor& x) {
+  if (p.has_value() && p->defined())
+    TORCH_CHECK(p->scalar_type() == at::kFloat && p->is_contiguous() && p->dim() == 3 &&
+                    p->size(1) == 2 && p->size(2) == C && p->device() == x.device(),
+                "batchnorm: partial statistics must be contiguous fp32 [blocks, 2, C]");
+}
+
+static bool has(const OptT& t) { return t.has_value() && t->defined(); }
+
+// act(bn(x) + bn2(x2)) training forward (downsampling block: main branch + projection shortcut).
+// Returns (y, mean, invstd, mask, mean2, invstd2).
+std::vector<Tensor> bn_fwd_train_dual(const Tensor& x, const OptT& weight, const OptT& bias,
+                                      const OptT& running_mean, const OptT& running_var,
+                                      const OptT& num_batches, const Tensor& x2,
+                                      const OptT& weight2, const OptT& bias2,
+                                      const OptT& running_mean2, const OptT& running_var2,
+                                      const OptT& num_batches2, double momentum, double eps,
+                                      bool relu, const OptT& partials, const OptT& partials2) {
+  CHECK_DEV(x);
+  CHECK_DEV(x2);
+  const c10::DeviceGuard guard(x.device());
+  auto [M, C] = rows_channels(x);
+  const bool same_layout = x.dim() == 4 ? x2.is_contiguous(at::MemoryFormat::ChannelsLast) : x2.is_contiguous();
+  TORCH_CHECK(x2.sizes() == x.sizes() && same_layout && x2.scalar_type() == x.scalar_type(),
+              "batchnorm dual: second input must match the first's shape/layout/dtype");
+  check_partials(partials, C, x);
+  check_partials(partials2, C, x);
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor y = torch::empty_like(x);
+  Tensor m1 = torch::empty({C}, fopt), i1 = torch::empty({C}, fopt);
+  Tensor m2 = torch::empty({C}, fopt), i2 = torch::empty({C}, fopt);
+  Tensor ws = torch::empty({has(partials) ? 2 * C : dca::bn_workspace_floats(M, C)}, fopt);
+  Tensor ws2 = torch::empty({has(partials2) ? 2 * C : dca::bn_workspace_floats(M, C)}, fopt);
+  Tensor mask = relu ? torch::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
+  dca::bn_forward_train_dual(
+      bn_dtype(x), x.data_ptr(), x2.data_ptr(), y.data_ptr(), M, C, ptr_or_null<float>(weight),
+      ptr_or_null<float>(bias), ptr_or_null<float>(running_mean), ptr_or_null<float>(running_var),
+      ptr_or_null<float>(weight2), ptr_or_null<float>(bias2), ptr_or_null<float>(running_mean2),
+      ptr_or_null<float>(running_var2), static_cast<float>(momentum), static_cast<float>(eps), relu,
+      m1.data_ptr<float>(), i1.data_ptr<float>(), m2.data_ptr<float>(), i2.data_ptr<float>(),
+      ptr_or_null<int64_t>(num_batches), ptr_or_null<int64_t>(num_batches2),
+      relu ? mask.data_ptr<uint8_t>() : nullptr, ws.data_ptr<float>(), ws2.data_ptr<float>(),
+      has(partials) ? partials->data_ptr<float>() : nullptr,
+      has(partials) ? static_cast<int>(partials->size(0)) : 0,
+      has(partials2) ? partials2->data_ptr<float>() : nullptr,
+      has(partials2) ? static_cast<int>(partials2->size(0)) : 0, cur_stream());
+  return {y, m1, i1, mask, m2, i2};
+}
+
+// Backward of bn_fwd_train_dual. Returns (dx, dx2, dgamma, dbeta, dgamma2, dbeta2); the four
+// parameter gradients are accumulated into the given .grad targets instead when all four are
+// passed (then returned undefined).
+std::vector<Tensor> bn_bwd_train_dual(const Tensor& dy_in, const Tensor& x, const OptT& mask,
+                                      const OptT& weight, const Tensor& mean, const Tensor& invstd,
+                                      const Tensor& x2, const OptT& weight2, const Tensor& mean2,
+                                      const Tensor& invstd2, bool relu, bool need_dweight,
+                                      const OptT& dy2_in, const std::vector<Tensor>& acc) {
+  CHECK_DEV(x);
+  const c10::DeviceGuard guard(x.device());
+  auto [M, C] = rows_channels(x);
+  Tensor dy = dy_in.dim() == 4 ? dy_in.contiguous(at::MemoryFormat::ChannelsLast) : dy_in.contiguous();
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && x2.sizes() == x.sizes() &&
+                  x2.scalar_type() == x.scalar_type(), "batchnorm dual bwd: shape/dtype mismatch");
+  Tensor dy2;
+  if (has(dy2_in)) {
+    dy2 = dy2_in->dim() == 4 ? dy2_in->contiguous(at::MemoryFormat::ChannelsLast) : dy2_in->contiguous();
+    TORCH_CHECK(dy2.sizes() == x.sizes() && dy2.scalar_type() == x.scalar_type(), "batchnorm dual bwd: dy2 mismatch");
+  }
+  TORCH_CHECK(!relu || (has(mask) && mask->numel() == M * C / 8),
+              "batchnorm dual bwd: relu needs the forward's ReLU bitmask");
+  const bool accumulate = need_dweight && acc.size() == 4;
+  if (accumulate)
+    for (const Tensor& t : acc)
+      TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C &&
+                  t.device() == x.device(), "batchnorm dual bwd: accumulation target must be fp32 [C]");
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor dx = torch::empty_like(x), dx2 = torch::empty_like(x);
+  std::vector<Tensor> dw(4);
+  for (int i = 0; i < 4; ++i)
+    dw[i] = accumulate ? acc[i] : need_dweight ? torch::empty({C}, fopt) : Tensor();
+  Tensor ws = torch::empty({dca::bn_workspace_floats(M, C)}, fopt);
+  Tensor ws2 = torch::empty({dca::bn_workspace_floats(M, C)}, fopt);
+  auto p = [&](int i) { return need_dweight ? dw[i].data_ptr<float>() : nullptr; };
+  dca::bn_backward_train_dual(bn_dtype(x), dy.data_ptr(), dy2.defined() ? dy2.data_ptr() : nullptr,
+                              relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(), x2.data_ptr(),
+                              M, C, ptr_or_null<float>(weight), mean.data_ptr<float>(),
+                              invstd.data_ptr<float>(), ptr_or_null<float>(weight2),
+                              mean2.data_ptr<float>(), invstd2.data_ptr<float>(), relu,
+                              dx.data_ptr(), dx2.data_ptr(), p(0), p(1), p(2), p(3), accumulate,
+                              ws.data_ptr<float>(), ws2.data_ptr<float>(), cur_stream());
+  if (accumulate) return {dx, dx2, Tensor(), Tensor(), Tensor(), Tensor()};
+  return {dx, dx2, dw[0], dw[1], dw[2], dw[3]};
 }
 
 // Stem fusion: act(bn(x)) -> max_pool2d(3, 2, 1) without materialising the pre-pool tensor.
@@ -464,6 +576,8 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("running_var"), pybind11::arg("num_batches"), pybind11::arg("momentum"),
         pybind11::arg("eps"), pybind11::arg("relu"), pybind11::arg("partials") = pybind11::none());
   m.def("bn_fwd_affine", &bn_fwd_affine);
+  m.def("bn_fwd_train_dual", &bn_fwd_train_dual);
+  m.def("bn_bwd_train_dual", &bn_bwd_train_dual);
   m.def("bn_bwd_train", &bn_bwd_train, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("mask"),
         pybind11::arg("weight"), pybind11::arg("save_mean"), pybind11::arg("save_invstd"),
         pybind11::arg("relu"), pybind11::arg("need_dres"), pybind11::arg("need_dweight"),

@@ -263,3 +263,86 @@ def test_global_avg_pool_matches_torch():
     y2.backward(g)
     assert x1.grad.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(x1.grad.float(), x2.grad, atol=1e-3, rtol=1e-2)
+
+
+def _bn_pair(C, dev, seed):
+    from determined_clone_amd.models.resnet import BatchNormAct2d
+
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    a = BatchNormAct2d(C, relu=True).to(dev)
+    b = BatchNormAct2d(C, relu=False).to(dev)
+    with torch.no_grad():
+        for m in (a, b):
+            m.weight.copy_(torch.rand(C, generator=g) + 0.5)
+            m.bias.copy_(torch.randn(C, generator=g))
+    return a, b
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 256, 14, 14), (4, 512, 7, 7), (2, 2048, 3, 3), (3, 64, 17, 19)])
+@pytest.mark.parametrize("with_partials,with_dy2", [(False, False), (True, True)])
+def test_bn_act_dual_matches_fp32(dtype, shape, with_partials, with_dy2):
+    """relu(bn3(x) + bn_ds(x2)) (a downsampling block's tail, csrc/batchnorm.hip *_dual) against
+    two fp32 BatchNorms + add + ReLU: output, running statistics of BOTH BatchNorms, gradients of
+    both inputs and all four affine parameters; with statistics partials supplied by a producer
+    and an extra upstream gradient deposited by a consumer (dy2)."""
+    _ext_loaded()
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    dev = "cuda"
+    x = (torch.randn(shape, device=dev) * 2 + 0.5).to(dtype).contiguous(memory_format=torch.channels_last)
+    x2 = (torch.randn(shape, device=dev) * 0.7 - 0.3).to(dtype).contiguous(memory_format=torch.channels_last)
+    bn, bnd = _bn_pair(C, dev, 1)
+    rbn, rbnd = _bn_pair(C, dev, 1)
+    xa, x2a = x.clone().requires_grad_(True), x2.clone().requires_grad_(True)
+    if with_partials:  # the convolution epilogue's [blocks, 2, C] (sum, sum^2) layout
+        for t, src in ((xa, x), (x2a, x2)):
+            rows = src.float().permute(0, 2, 3, 1).reshape(-1, C)
+            parts = torch.stack([torch.stack([r.sum(0), (r * r).sum(0)]) for r in rows.chunk(3)])
+            t._dca_bn_partials = parts.contiguous()
+    y = batchnorm.batch_norm_act_dual(xa, bn, x2a, bnd)
+    xr, x2r = x.float().clone().requires_grad_(True), x2.float().clone().requires_grad_(True)
+    yr = batchnorm.reference_batch_norm_act_dual(xr, rbn, x2r, rbnd)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol * 4, rtol=tol)
+    for m, r in ((bn, rbn), (bnd, rbnd)):
+        torch.testing.assert_close(m.running_mean, r.running_mean, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(m.running_var, r.running_var, atol=1e-3, rtol=1e-3)
+        assert int(m.num_batches_tracked) == 1
+    g = torch.randn_like(yr)
+    extra = torch.randn_like(yr) if with_dy2 else None
+    if with_dy2:  # a consumer deposits a second upstream gradient into the output's sink
+        y._dca_grad_sink.deposit(extra.to(dtype).contiguous(memory_format=torch.channels_last))
+    y.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
+    yr.backward(g + extra if with_dy2 else g)
+    torch.testing.assert_close(xa.grad.float(), xr.grad, atol=tol * 10, rtol=tol * 5)
+    torch.testing.assert_close(x2a.grad.float(), x2r.grad, atol=tol * 10, rtol=tol * 5)
+    for m, r in ((bn, rbn), (bnd, rbnd)):
+        torch.testing.assert_close(m.weight.grad, r.weight.grad, atol=tol * 50, rtol=tol * 5)
+        torch.testing.assert_close(m.bias.grad, r.bias.grad, atol=tol * 50, rtol=tol * 5)
+
+
+def test_resnet_downsample_block_dual_bn_matches_separate(monkeypatch):
+    """A bf16 ResNet stage whose downsampling block runs the fused dual BatchNorm gives the same
+    output and gradients as the same block with two separate BatchNorms (DCA_BN_DUAL=0 path)."""
+    from determined_clone_amd.models import resnet
+
+    _ext_loaded()
+    torch.manual_seed(0)
+    blk = resnet.Bottleneck(256, 128, stride=2)
+    blk = resnet.to_mi355x_layout(blk).cuda()
+    x = torch.randn(8, 256, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for dual in (True, False):
+        monkeypatch.setattr(resnet, "BN_DUAL", dual)
+        for p in blk.parameters():
+            p.grad = None
+        xi = x.clone().requires_grad_(True)
+        y = blk(xi)
+        y.float().square().mean().backward()
+        outs.append((y.float(), xi.grad.float(), {n: p.grad.float().clone() for n, p in blk.named_parameters()}))
+    (y1, g1, p1), (y2, g2, p2) = outs
+    torch.testing.assert_close(y1, y2, atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(g1, g2, atol=5e-3, rtol=5e-2)
+    for n in p1:
+        torch.testing.assert_close(p1[n], p2[n], atol=5e-3, rtol=5e-2, msg=n)

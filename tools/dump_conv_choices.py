@@ -1,11 +1,13 @@
 """Measure the ops/conv.py chooser decisions on this GPU and write them to
 ``ops/tuned/conv_choices_gfx950.json`` (shipped, so bench / trial processes never time them).
 
-Runs two training steps of every shipped workload with the shipped file ignored
-(``DCA_CONV_CHOICES=0``): ResNet-50 at bs 1024 (the headline bench) and 256, and the SD-2-shaped
-UNet at bs 8 / 512^2 (``tools/bench_diffusion.py``). GPU only.
+The headline shapes are best recorded from the real bench process, whose step conditions
+(flat .grad views, side-stream weight gradients) the timings depend on:
+``DCA_CONV_CHOICES=0 DCA_CONV_DUMP=<file> python bench.py`` (ops/conv.py dumps its decisions at
+exit, merging into the file). This tool adds the remaining workloads to the same file -- ResNet-50
+at bs 256 and the SD-2-shaped UNet at bs 8 / 512^2 -- with the shipped file ignored. GPU only.
 
-Usage: python tools/dump_conv_choices.py [--out PATH]
+Usage: python tools/dump_conv_choices.py [--out PATH] [--batches 256] [--skip-unet]
 """
 import argparse
 import os
@@ -19,6 +21,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--skip-unet", action="store_true")
+    ap.add_argument("--batches", default="1024,256", help="ResNet-50 batch sizes to run")
     a = ap.parse_args()
     import torch
     import torch.nn.functional as F
@@ -28,7 +31,10 @@ def main() -> None:
     from determined_clone_amd.ops import optim as fopt
 
     dev = torch.device("cuda")
-    for bs in (1024, 256):
+    out = a.out or conv_ops._SHIPPED_PATH
+    if os.path.exists(out):  # keep decisions already recorded (e.g. by the bench process)
+        conv_ops.load_choices(out)
+    for bs in [int(b) for b in a.batches.split(",") if b]:
         torch.manual_seed(0)
         model = resnet.to_mi355x_layout(resnet.resnet50()).to(dev)
         opt = fopt.FusedSGD(model.parameters(), lr=0.1, momentum=0.9)
@@ -57,7 +63,6 @@ def main() -> None:
             opt.zero_grad()
         torch.cuda.synchronize()
         print(f"unet: {len(conv_ops._CHOICE)} decisions so far", flush=True)
-    out = a.out or conv_ops._SHIPPED_PATH
     conv_ops.dump_choices(out, torch.cuda.get_device_name(0))
     print(f"wrote {len(conv_ops._CHOICE)} decisions ({conv_ops.TIMINGS} candidate timings) to {out}")
 
