@@ -238,13 +238,22 @@ def _run_rank(args: argparse.Namespace) -> None:
                 "diagnostics": {"alloc_retries": int(ms_stats.get("num_alloc_retries", 0)) if on_gpu else 0,
                                 "device_free_gb_at_start": round(free0 / 2**30, 1) if on_gpu else None,
                                 "max_reserved_gb": round(torch.cuda.max_memory_reserved() / 2**30, 1) if on_gpu else None,
-                                "max_allocated_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else None},
+                                "max_allocated_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if on_gpu else None,
+                                # candidates timed by the convolution chooser in this process
+                                # (0: every decision came from ops/tuned/conv_choices_gfx950.json)
+                                "conv_chooser_timings": _conv_timings()},
                 "config": {"model": "resnet50", "global_batch": args.batch * world, "seq_len": None,
                            "image_size": 224, "parallelism": f"dp{world}",
                            "trial": "PyTorchTrial", "optimizer": f"SGD momentum ({opt_name})",
                            "slots_per_trial": world},
             }
             print(json.dumps(out), flush=True)
+
+
+def _conv_timings() -> int:
+    from determined_clone_amd.ops import conv as conv_ops
+
+    return int(conv_ops.TIMINGS)
 
 
 def main() -> None:

@@ -13,9 +13,9 @@ architecture is defined here. It is laid out for MI355X rather than copied:
 * 3x3 convolutions run on the hand-written implicit-GEMM MFMA kernel (``ops/csrc/conv_igemm.hip``,
   forward + stride-1 data gradient), whose forward epilogue also reduces the following
   BatchNorm's statistics;
-* 1x1/stride-1 convolutions go through ``ops.conv.pointwise_conv``: MIOpen by default (measured
-  faster), or with ``DCA_CONV1X1=1`` hand-written MFMA GEMM kernels (``ops/csrc/conv1x1.hip``)
-  whose forward epilogue also reduces the next BatchNorm's statistics;
+* 1x1 convolutions go through ``ops.conv.pointwise_conv``: per shape and direction the fastest of
+  MIOpen, hipBLASLt and the implicit GEMM (whose forward epilogue also reduces the next
+  BatchNorm's statistics);
 * a downsampling block's tail ``relu(bn3(conv3(..)) + bn_ds(proj(x)))`` is ONE fused op
   (``ops.batchnorm.batch_norm_act_dual``): the projection shortcut's BatchNorm is applied inside
   bn3's apply pass (its output is never written) and both BatchNorms' backward share one
@@ -98,7 +98,7 @@ class Bottleneck(nn.Module):
             # conv1 and the projection shortcut read the same x: one op, one input gradient
             # (the shortcut's strided backward-data is accumulated in place, ops/conv.py)
             ds_conv, ds_bn = self.downsample
-            if conv_ops.ENABLED or not conv_ops.DUAL:
+            if not conv_ops.DUAL:
                 y1 = pointwise_conv(self.conv1, x, self.bn1.training)
                 yd = pointwise_conv(ds_conv, x, ds_bn.training)
             else:

@@ -1,72 +1,28 @@
-"""Pointwise (1x1, stride 1) NHWC convolution on the MFMA GEMM kernels of ``csrc/conv1x1.hip``.
-
-GPU path: forward GEMM (optionally emitting the per-block (sum, sum^2) statistics the following
-fused BatchNorm consumes instead of re-reading the output), dgrad GEMM and split-m wgrad, the
-weight gradient accumulated straight into the parameter's persistent ``.grad`` view when the
-optimizer's flat buffers own it (``ops/_grad.py``).
+"""NHWC convolutions for the ResNet / UNet hot path: the hand-written implicit-GEMM MFMA kernels of
+``csrc/conv_igemm.hip`` (3x3 forward with the next BatchNorm's statistics in its epilogue, stride-1
+data gradient -- optionally with the preceding BatchNorm's backward statistics in its epilogue --
+and weight gradient) and, for 1x1 convolutions, a per-shape, per-direction choice between MIOpen,
+hipBLASLt GEMMs on the NHWC row view and the implicit GEMM (decisions shipped in
+``ops/tuned/conv_choices_gfx950.json``). Weight gradients accumulate straight into the parameters'
+persistent ``.grad`` views when the optimizer's flat buffers own them (``ops/_grad.py``).
 CPU / unsupported shapes: ``torch.nn.functional.conv2d`` (also the fp32 oracle of the GPU tests).
 
-The partial statistics ride on the output tensor as ``y._dca_bn_partials`` and
+Fused statistics ride on the output tensor as ``y._dca_bn_partials`` and
 ``ops.batchnorm.batch_norm_act`` picks them up when it normalises exactly that tensor.
 
-Status: OPT-IN (``DCA_CONV1X1=1``). Measured on MI355X at ResNet-50 bs256 shapes
-(``tools/bench_pointwise.py``, ``profiles/r8_pointwise_conv_study.txt``), MIOpen's NHWC 1x1
-kernels already stream the memory-bound layer1/layer2 shapes at ~5-6 TB/s and reach 500-650
-TFLOP/s on layer3/layer4; these kernels win only the layer3/4 weight gradients (6-25 %), lose the
-forward/dgrad by 1.3-2.4x, so the end-to-end step is slower (7.8k vs 9.2k img/s) even with the
-BatchNorm statistics pass removed. The model therefore keeps MIOpen by default.
+(An earlier hand-written pointwise GEMM family lost to the libraries on the forward / data
+gradient by 1.3-2.4x at ResNet-50 shapes -- ``profiles/r8_pointwise_conv_study.txt`` -- and was
+removed; the implicit GEMM covers 1x1 where it wins.)
 """
 import os
 import sys
-from typing import Optional, Tuple
+from typing import Optional
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from determined_clone_amd.ops import _ext, _grad
-
-ENABLED = os.environ.get("DCA_CONV1X1", "0") == "1"
-
-
-class _Conv1x1(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, weight, stats):
-        y, partial = _ext.load().conv1x1_fwd(x, weight, stats)
-        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
-        ctx.save_for_backward(x, weight)
-        if partial is not None:
-            ctx.mark_non_differentiable(partial)
-        return y, partial
-
-    @staticmethod
-    def backward(ctx, dy, _dpartial):
-        x, w = ctx.saved_tensors
-        C = _ext.load()
-        dx = dw = None
-        if ctx.needs_input_grad[0]:
-            dx = C.conv1x1_dgrad(dy, w)
-        if ctx.needs_input_grad[1]:
-            acc = _grad.target(w)
-            dw = C.conv1x1_wgrad(dy, x, w, acc)
-            if acc is not None:
-                dw = None  # already accumulated into w.grad
-        return dx, dw, None
-
-
-def supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
-    """True when ``conv(x)`` can run on the HIP pointwise kernels."""
-    if not (ENABLED and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16):
-        return False
-    if conv.kernel_size != (1, 1) or conv.stride != (1, 1) or conv.padding != (0, 0):
-        return False
-    if conv.groups != 1 or conv.dilation != (1, 1) or conv.bias is not None:
-        return False
-    w = conv.weight
-    if w.dtype != torch.bfloat16 or conv.in_channels % 64 or conv.out_channels % 64:
-        return False
-    return w.stride(0) == conv.in_channels and w.stride(1) == 1
-
 
 # ----------------------------------------------------------------------------- library chooser
 # Measured per direction on MI355X (tools/bench_conv_ops.py, profiles/s2_conv_ops_miopen_vs_gemm.txt):
@@ -431,7 +387,7 @@ class _PointwiseDual(torch.autograd.Function):
 def pointwise_dual(conv1: nn.Conv2d, proj: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False):
     """``(conv1(x), proj(x))`` for a downsampling bottleneck (see :class:`_PointwiseDual`); with
     ``bn_stats`` each output may carry its BatchNorm's partial statistics (``_ig1x1_wins``)."""
-    if (not supported(conv1, x) and _lib_supported(conv1, x) and _lib_supported(proj, x)
+    if (_lib_supported(conv1, x) and _lib_supported(proj, x)
             and conv1.stride == (1, 1)):
         x = x.contiguous(memory_format=torch.channels_last)
         s1 = bool(bn_stats) and _ig1x1_ok(x, conv1.weight) and _ig1x1_wins(x, conv1.weight, 1)
@@ -625,6 +581,11 @@ def stem_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
 # stride-1 data gradient 4.16 vs 5.56 ms. Stride-2 data gradients and every weight gradient stay
 # on MIOpen (the latter on the side stream). DCA_IGEMM=0 routes everything back to MIOpen.
 IGEMM = os.environ.get("DCA_IGEMM", "1") != "0"
+# stride-1 k x k data gradient whose input came from a fused BN+ReLU: with DCA_FUSE_BN_BWD_STATS=1
+# that BatchNorm's backward statistics pass runs in the dgrad epilogue (conv_igemm_dgrad_bn).
+# OFF by default: it saves one read of the gradient but lengthens the MFMA kernel's epilogue, and
+# measured -0.4 % on the ResNet-50 step (profiles/round5_dgrad_bn_stats_epilogue_ab.txt).
+FUSE_BN_BWD_STATS = os.environ.get("DCA_FUSE_BN_BWD_STATS", "0") == "1"
 
 
 def igemm_supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -650,11 +611,12 @@ class _IgemmConv(torch.autograd.Function):
     """k x k convolution on conv_igemm.hip; returns ``(y, bn_partials)``."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, stats):
+    def forward(ctx, x, weight, stride, pad, stats, bn_src=None):
         y, partial = _ext.load().conv_igemm_fwd(x, weight, stride, pad, stats)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         ctx.save_for_backward(x, weight)
         ctx.stride, ctx.pad = stride, pad
+        ctx.bn_src = bn_src  # autograd node of the BN(+ReLU) producing x (see backward)
         if partial is not None:
             ctx.mark_non_differentiable(partial)
         return y, partial
@@ -668,11 +630,19 @@ class _IgemmConv(torch.autograd.Function):
         dw = _wgrad(args, w) if ctx.needs_input_grad[1] else None
         dx = None
         if ctx.needs_input_grad[0]:
-            if st == 1:
+            node = ctx.bn_src
+            if st == 1 and node is not None:
+                # x = relu(bn(x_bn)): the dgrad epilogue also reduces that BatchNorm's backward
+                # statistics (sum g*m, sum g*m*(x_bn - mean)) and hands them to its backward,
+                # which then skips its own statistics pass over dy and x_bn
+                x_bn, mask, _w, mean, _invstd = node.saved_tensors
+                dx, part = _ext.load().conv_igemm_dgrad_bn(dy, w, pad, x_bn, mask, mean)
+                node._dca_given_partials = (part, dx)
+            elif st == 1:
                 dx = _ext.load().conv_igemm_dgrad(dy, w, pad)
             else:
                 dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def spatial_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> torch.Tensor:
@@ -680,8 +650,13 @@ def spatial_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> to
     ``bn_stats`` the output carries the following BatchNorm's partial statistics), others on
     MIOpen with the weight (and bias) gradient on the side stream (``ops/_grad.py``)."""
     if igemm_supported(conv, x):
+        from determined_clone_amd.ops import batchnorm as bn_ops
+
+        src = bn_ops.fused_bwd_stats_source(x) if FUSE_BN_BWD_STATS and conv.stride[0] == 1 else None
         x = x.contiguous(memory_format=torch.channels_last)
-        y, partial = _IgemmConv.apply(x, conv.weight, conv.stride[0], conv.padding[0], bool(bn_stats))
+        if src is not None and not x.is_contiguous(memory_format=torch.channels_last):
+            src = None
+        y, partial = _IgemmConv.apply(x, conv.weight, conv.stride[0], conv.padding[0], bool(bn_stats), src)
         if partial is not None:
             y._dca_bn_partials = partial
         return y
@@ -705,16 +680,9 @@ def _lib_supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
 
 
 def pointwise_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> torch.Tensor:
-    """``conv(x)`` for a 1x1 convolution in NHWC. With ``DCA_CONV1X1=1`` (stride 1, bf16) the
-    hand-written MFMA kernels run and, with ``bn_stats``, the output carries the partial BatchNorm
-    statistics of the forward epilogue; otherwise each direction runs on the faster of MIOpen and
-    hipBLASLt for its shape."""
-    if supported(conv, x):
-        x = x.contiguous(memory_format=torch.channels_last)
-        y, partial = _Conv1x1.apply(x, conv.weight, bool(bn_stats))
-        if partial is not None:
-            y._dca_bn_partials = partial
-        return y
+    """``conv(x)`` for a 1x1 convolution in NHWC: each direction runs on the fastest of MIOpen,
+    hipBLASLt and the implicit GEMM for its shape; with ``bn_stats`` and the implicit-GEMM forward
+    the output carries the next BatchNorm's partial statistics from its epilogue."""
     if _lib_supported(conv, x):
         x = x.contiguous(memory_format=torch.channels_last)
         stats = bool(bn_stats) and _ig1x1_ok(x, conv.weight) and _ig1x1_wins(x, conv.weight, conv.stride[0])
@@ -731,10 +699,3 @@ def take_bn_partials(x: torch.Tensor) -> Optional[torch.Tensor]:
     if p is not None:
         x._dca_bn_partials = None
     return p
-
-
-def reference_conv1x1(x: torch.Tensor, weight: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """fp32 oracle: ``(y, per-channel [sum, sum^2])`` of the convolution output."""
-    y = F.conv2d(x.float(), weight.float())
-    yc = y.permute(0, 2, 3, 1).reshape(-1, y.shape[1])
-    return y, torch.stack([yc.sum(0), (yc * yc).sum(0)])

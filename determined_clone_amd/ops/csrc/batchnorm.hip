@@ -977,17 +977,24 @@ void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_
                        int64_t M, int C,
                        const float* gamma, const float* save_mean, const float* save_invstd,
                        bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
-                       bool accumulate_dw, float* workspace, hipStream_t st) {
+                       bool accumulate_dw, float* workspace, hipStream_t st,
+                       const float* given_partials, int given_blocks) {
   ReduceGeom g = reduce_geom(C);
   int B = reduce_blocks(M, C, g);
   float* partial = workspace;
   float* coef = workspace + static_cast<int64_t>(B) * 2 * C;  // [3][C]
-  switch (dt) {
-    case BnDtype::kBF16: launch_reduce<BF16>(true, x, dy, dy2, y, save_mean, M, C, relu, partial, B, g, st); break;
-    case BnDtype::kF16: launch_reduce<F16>(true, x, dy, dy2, y, save_mean, M, C, relu, partial, B, g, st); break;
-    default: launch_reduce<F32>(true, x, dy, dy2, y, save_mean, M, C, relu, partial, B, g, st); break;
+  if (given_partials != nullptr) {  // statistics reduced by dy's producer (conv dgrad epilogue)
+    B = given_blocks;
+    coef = workspace;
+  } else {
+    switch (dt) {
+      case BnDtype::kBF16: launch_reduce<BF16>(true, x, dy, dy2, y, save_mean, M, C, relu, partial, B, g, st); break;
+      case BnDtype::kF16: launch_reduce<F16>(true, x, dy, dy2, y, save_mean, M, C, relu, partial, B, g, st); break;
+      default: launch_reduce<F32>(true, x, dy, dy2, y, save_mean, M, C, relu, partial, B, g, st); break;
+    }
   }
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
+  const float* stats = given_partials != nullptr ? given_partials : partial;
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, stats, B,
                      C, M, gamma, save_mean, save_invstd, dgamma, dbeta, accumulate_dw, coef);
   switch (dt) {
     case BnDtype::kBF16: launch_apply_bwd<BF16>(dy, dy2, y, x, coef, dx, dres, M, C, relu, st); break;

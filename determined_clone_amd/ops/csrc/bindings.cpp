@@ -32,7 +32,8 @@ void bn_relu_pool_backward(BnDtype dt, const void* dyp, const uint8_t* idx, cons
 void bn_backward_train(BnDtype dt, const void* dy, const void* dy2, const uint8_t* mask, const void* x,
                        int64_t M, int C, const float* gamma, const float* save_mean, const float* save_invstd,
                        bool relu, void* dx, void* dres, float* dgamma, float* dbeta,
-                       bool accumulate_dw, float* workspace, hipStream_t st);
+                       bool accumulate_dw, float* workspace, hipStream_t st,
+                       const float* given_partials, int given_blocks);
 
 void bn_forward_train_dual(BnDtype dt, const void* x, const void* x2, void* y, int64_t M, int C,
                            const float* gamma, const float* beta, float* running_mean,
@@ -130,6 +131,15 @@ std::pair<int64_t, int> rows_channels(const Tensor& x) {
   return {M, C};
 }
 
+static void check_partials(const OptT& p, int64_t C, const Tensor& x) {
+  if (p.has_value() && p->defined())
+    TORCH_CHECK(p->scalar_type() == at::kFloat && p->is_contiguous() && p->dim() == 3 &&
+                    p->size(1) == 2 && p->size(2) == C && p->device() == x.device(),
+                "batchnorm: partial statistics must be contiguous fp32 [blocks, 2, C]");
+}
+
+static bool has(const OptT& t) { return t.has_value() && t->defined(); }
+
 std::vector<Tensor> bn_fwd_train(const Tensor& x, const OptT& residual, const OptT& weight,
                                  const OptT& bias, const OptT& running_mean,
                                  const OptT& running_var, const OptT& num_batches, double momentum,
@@ -189,7 +199,7 @@ std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const Opt
                                  const OptT& weight, const Tensor& save_mean,
                                  const Tensor& save_invstd, bool relu, bool need_dres,
                                  bool need_dweight, const OptT& dy2_in, const OptT& dweight_acc,
-                                 const OptT& dbias_acc) {
+                                 const OptT& dbias_acc, const OptT& partials) {
   CHECK_DEV(x);
   const c10::DeviceGuard guard(x.device());
   auto [M, C] = rows_channels(x);
@@ -217,6 +227,10 @@ std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const Opt
   }
   Tensor dgamma = acc ? *dweight_acc : need_dweight ? torch::empty({C}, fopt) : Tensor();
   Tensor dbeta = acc ? *dbias_acc : need_dweight ? torch::empty({C}, fopt) : Tensor();
+  // partials: the statistics pass already done by the producer of dy (a data-gradient epilogue)
+  const bool given = has(partials);
+  check_partials(partials, C, x);
+  TORCH_CHECK(!given || !dy2.defined(), "batchnorm bwd: given partials exclude a second gradient");
   Tensor ws = torch::empty({dca::bn_workspace_floats(M, C)}, fopt);
   dca::bn_backward_train(bn_dtype(x), dy.data_ptr(), dy2.defined() ? dy2.data_ptr() : nullptr,
                          relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(),
@@ -225,19 +239,12 @@ std::vector<Tensor> bn_bwd_train(const Tensor& dy_in, const Tensor& x, const Opt
                          need_dres ? dres.data_ptr() : nullptr,
                          need_dweight ? dgamma.data_ptr<float>() : nullptr,
                          need_dweight ? dbeta.data_ptr<float>() : nullptr, acc,
-                         ws.data_ptr<float>(), cur_stream());
+                         ws.data_ptr<float>(), cur_stream(),
+                         given ? partials->data_ptr<float>() : nullptr,
+                         given ? static_cast<int>(partials->size(0)) : 0);
   if (acc) return {dx, Tensor(), Tensor(), dres};
   return {dx, dgamma, dbeta, dres};
 }
-
-static void check_partials(const OptT& p, int64_t C, const Tensor& x) {
-  if (p.has_value() && p->defined())
-    TORCH_CHECK(p->scalar_type() == at::kFloat && p->is_contiguous() && p->dim() == 3 &&
-                    p->size(1) == 2 && p->size(2) == C && p->device() == x.device(),
-                "batchnorm: partial statistics must be contiguous fp32 [blocks, 2, C]");
-}
-
-static bool has(const OptT& t) { return t.has_value() && t->defined(); }
 
 // act(bn(x) + bn2(x2)) training forward (downsampling block: main branch + projection shortcut).
 // Returns (y, mean, invstd, mask, mean2, invstd2).
@@ -582,7 +589,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("weight"), pybind11::arg("save_mean"), pybind11::arg("save_invstd"),
         pybind11::arg("relu"), pybind11::arg("need_dres"), pybind11::arg("need_dweight"),
         pybind11::arg("dy2") = pybind11::none(), pybind11::arg("dweight_acc") = pybind11::none(),
-        pybind11::arg("dbias_acc") = pybind11::none());
+        pybind11::arg("dbias_acc") = pybind11::none(), pybind11::arg("partials") = pybind11::none());
   m.def("bn_pool_fwd_train", &bn_pool_fwd_train);
   m.def("bn_pool_fwd_affine", &bn_pool_fwd_affine);
   m.def("bn_pool_bwd", &bn_pool_bwd);

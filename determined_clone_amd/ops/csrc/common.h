@@ -135,6 +135,23 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
   return v;
 }
+// Wave-wide sum on the VALU, no LDS round trips: DPP quad / half-row / row mirrors give every lane
+// its 16-lane row sum, then the gfx950 permlane16 / permlane32 half swaps add the other rows
+// (r[0] + r[1] of a swap of v with itself = v + the partner lane's v).
+template <int kCtrl>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), kCtrl, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f32<0xB1>(v);   // quad_perm [1,0,3,2]: + lane ^ 1
+  v += dpp_f32<0x4E>(v);   // quad_perm [2,3,0,1]: + lane ^ 2
+  v += dpp_f32<0x141>(v);  // row_half_mirror: + the other quad of the 8-lane half row
+  v += dpp_f32<0x140>(v);  // row_mirror: + the other half row
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));

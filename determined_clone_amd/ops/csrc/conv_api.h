@@ -1,24 +1,10 @@
-// Host API of the pointwise-convolution family (conv1x1.hip), shared by the kernels' translation
-// unit and the PyTorch bindings (conv_bindings.cpp). Activations are NHWC bf16 viewed as
-// [M = N*H*W][C] row-major matrices; weights are bf16 [Cout][Cin]. Channel counts are multiples of
-// 64.
+// Host API of the implicit-GEMM convolution family (conv_igemm.hip), shared by the kernels'
+// translation unit and the PyTorch bindings (conv_bindings.cpp).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace dca {
-// Number of row blocks of the forward GEMM = first dimension of its BatchNorm partial-statistics
-// output ([blocks][2][Cout] fp32: per-block sum and sum of squares of the bf16 outputs).
-int conv1x1_fwd_row_blocks(int64_t M, int Cout);
-void conv1x1_fwd(const void* x, const void* w, void* y, float* partial, int64_t M, int Cin,
-                 int Cout, hipStream_t st);
-// wt: Cin*Cout bf16 scratch for the transposed weight.
-void conv1x1_dgrad(const void* dy, const void* w, void* wt, void* dx, int64_t M, int Cin, int Cout,
-                   hipStream_t st);
-int64_t conv1x1_wgrad_ws_floats(int64_t M, int Cin, int Cout);
-void conv1x1_wgrad(const void* dy, const void* x, float* ws, void* dw, bool dw_f32,
-                   bool accumulate, int64_t M, int Cin, int Cout, hipStream_t st);
-
 // ---- k x k implicit-GEMM convolutions (conv_igemm.hip). x [N][H][W][C], w [K][R][S][C],
 // y [N][P][Q][K], all bf16; C and K multiples of 64; N*H*W*C and N*P*Q*K below 2^31.
 struct ConvGeom {
@@ -26,8 +12,12 @@ struct ConvGeom {
 };
 // Row blocks of the forward = first dimension of its [blocks][2][K] BatchNorm partial statistics.
 int conv_igemm_row_blocks(const ConvGeom& g);
+// With bn_x / bn_mask / bn_mean (data gradient of a convolution whose input was relu(bn(bn_x)),
+// y laid out like bn_x): partial receives that BatchNorm's BACKWARD statistics instead,
+// (sum g*m, sum g*m*(bn_x - bn_mean)) of the bf16 output g masked by the ReLU bits m.
 void conv_igemm_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                    hipStream_t st);
+                    hipStream_t st, const void* bn_x = nullptr, const uint8_t* bn_mask = nullptr,
+                    const float* bn_mean = nullptr);
 // Weight gradient dW (bf16 or fp32; accumulate adds into it) from dy [M][K] and x, stored
 // [K][R][S][C] (channels_last) or, with dw_kcrs, [K][C][R][S]; ws: conv_igemm_wgrad_ws_floats(g)
 // fp32 scratch.

@@ -1,4 +1,4 @@
-// Bindings for the pointwise-convolution family (conv1x1.hip).
+// Bindings for the implicit-GEMM convolution family (conv_igemm.hip).
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
@@ -24,77 +24,9 @@ int64_t nhwc_rows(const Tensor& t, const char* what) {
   return M;
 }
 
-void check_weight(const Tensor& w, int64_t cout, int64_t cin) {
-  TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(0) == cout &&
-                  w.size(1) == cin && w.size(2) == 1 && w.size(3) == 1,
-              "conv1x1: weight must be bf16 [Cout, Cin, 1, 1]");
-  TORCH_CHECK(w.stride(0) == cin && w.stride(1) == 1, "conv1x1: weight must be dense [Cout][Cin]");
-}
-
 Tensor nhwc_empty(const Tensor& like, int64_t c) {
   return torch::empty({like.size(0), c, like.size(2), like.size(3)},
                       like.options().memory_format(at::MemoryFormat::ChannelsLast));
-}
-
-std::vector<Tensor> conv1x1_fwd(const Tensor& x, const Tensor& w, bool stats) {
-  const c10::DeviceGuard g(x.device());
-  const int64_t M = nhwc_rows(x, "conv1x1_fwd");
-  const int64_t cin = x.size(1), cout = w.size(0);
-  check_weight(w, cout, cin);
-  TORCH_CHECK(cout % 64 == 0, "conv1x1_fwd: Cout must be a multiple of 64");
-  Tensor y = nhwc_empty(x, cout);
-  Tensor partial;
-  if (stats) {
-    const int B = dca::conv1x1_fwd_row_blocks(M, static_cast<int>(cout));
-    partial = torch::empty({B, 2, cout}, x.options().dtype(at::kFloat));
-  }
-  dca::conv1x1_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(),
-                   stats ? partial.data_ptr<float>() : nullptr, M, static_cast<int>(cin),
-                   static_cast<int>(cout), stream());
-  return {y, partial};
-}
-
-Tensor conv1x1_dgrad(const Tensor& dy_in, const Tensor& w) {
-  const Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
-  const c10::DeviceGuard g(dy.device());
-  const int64_t M = nhwc_rows(dy, "conv1x1_dgrad");
-  const int64_t cout = dy.size(1), cin = w.size(1);
-  check_weight(w, cout, cin);
-  TORCH_CHECK(cin % 64 == 0, "conv1x1_dgrad: Cin must be a multiple of 64");
-  Tensor wt = torch::empty({cin, cout}, w.options().memory_format(at::MemoryFormat::Contiguous));
-  Tensor dx = nhwc_empty(dy, cin);
-  dca::conv1x1_dgrad(dy.data_ptr(), w.data_ptr(), wt.data_ptr(), dx.data_ptr(), M,
-                     static_cast<int>(cin), static_cast<int>(cout), stream());
-  return dx;
-}
-
-// Returns the weight gradient; with `acc` (the parameter's persistent .grad view) the result is
-// added into it in place and `acc` is returned.
-Tensor conv1x1_wgrad(const Tensor& dy_in, const Tensor& x, const Tensor& w, const OptT& acc) {
-  const Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
-  const c10::DeviceGuard g(dy.device());
-  const int64_t M = nhwc_rows(dy, "conv1x1_wgrad");
-  TORCH_CHECK(nhwc_rows(x, "conv1x1_wgrad") == M, "conv1x1_wgrad: dy / x row mismatch");
-  const int64_t cout = dy.size(1), cin = x.size(1);
-  check_weight(w, cout, cin);
-  Tensor ws = torch::empty({dca::conv1x1_wgrad_ws_floats(M, static_cast<int>(cin), static_cast<int>(cout))},
-                           dy.options().dtype(at::kFloat));
-  Tensor out;
-  bool accumulate = false;
-  if (acc.has_value() && acc->defined()) {
-    out = *acc;
-    TORCH_CHECK(out.numel() == cout * cin && out.device() == dy.device() && out.dim() == 4 &&
-                    (out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16) &&
-                    out.stride(0) == cin && out.stride(1) == 1,
-                "conv1x1_wgrad: accumulation target must be a dense fp32/bf16 [Cout, Cin, 1, 1]");
-    accumulate = true;
-  } else {
-    out = torch::empty({cout, cin, 1, 1}, w.options().memory_format(at::MemoryFormat::Contiguous));
-  }
-  dca::conv1x1_wgrad(dy.data_ptr(), x.data_ptr(), ws.data_ptr<float>(), out.data_ptr(),
-                     out.scalar_type() == at::kFloat, accumulate, M, static_cast<int>(cin),
-                     static_cast<int>(cout), stream());
-  return out;
 }
 
 // ---------------------------------------------------------------- k x k implicit GEMM
@@ -167,6 +99,39 @@ Tensor conv_igemm_dgrad(const Tensor& dy_in, const Tensor& w, int64_t pad) {
   return dx;
 }
 
+// dx of a stride-1 convolution whose input was relu(bn(bn_x)) (bn_mask: that BatchNorm's ReLU
+// bits, bn_mean its saved mean): also returns the BatchNorm backward's [blocks][2][C] statistics
+// partials, reduced in the data-gradient epilogue (batchnorm bwd then skips its statistics pass).
+std::vector<Tensor> conv_igemm_dgrad_bn(const Tensor& dy_in, const Tensor& w, int64_t pad,
+                                        const Tensor& bn_x, const Tensor& bn_mask,
+                                        const Tensor& bn_mean) {
+  const Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
+  const c10::DeviceGuard dg(dy.device());
+  check_nhwc(dy, "conv_igemm_dgrad_bn");
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == dy.size(1) && w.size(1) % 64 == 0 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.scalar_type() == at::kBFloat16,
+              "conv_igemm_dgrad_bn: weight must be bf16 channels_last [K, C, R, S], C a multiple of 64");
+  const int64_t K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(R == S && pad <= R - 1, "conv_igemm_dgrad_bn: square kernels, padding < kernel");
+  Tensor wt = torch::empty({C, K, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dca::conv_flip_transpose(w.data_ptr(), wt.data_ptr(), static_cast<int>(K), static_cast<int>(C),
+                           static_cast<int>(R * S), stream());
+  const dca::ConvGeom g = geom(dy, wt, 1, R - 1 - pad);
+  check_nhwc(bn_x, "conv_igemm_dgrad_bn (bn_x)");
+  TORCH_CHECK(bn_x.size(0) == g.N && bn_x.size(1) == g.K && bn_x.size(2) == g.P && bn_x.size(3) == g.Q,
+              "conv_igemm_dgrad_bn: bn_x must have the data gradient's shape");
+  TORCH_CHECK(bn_mask.scalar_type() == at::kByte && bn_mask.is_contiguous() &&
+                  bn_mask.numel() == static_cast<int64_t>(g.M) * g.K / 8 && bn_mask.device() == dy.device(),
+              "conv_igemm_dgrad_bn: bn_mask must be the BatchNorm's ReLU bitmask");
+  TORCH_CHECK(bn_mean.scalar_type() == at::kFloat && bn_mean.is_contiguous() && bn_mean.numel() == g.K,
+              "conv_igemm_dgrad_bn: bn_mean must be fp32 [C]");
+  Tensor dx = torch::empty({g.N, g.K, g.P, g.Q}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor partial = torch::empty({dca::conv_igemm_row_blocks(g), 2, g.K}, dy.options().dtype(at::kFloat));
+  dca::conv_igemm_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), partial.data_ptr<float>(), g,
+                      stream(), bn_x.data_ptr(), bn_mask.data_ptr<uint8_t>(), bn_mean.data_ptr<float>());
+  return {dx, partial};
+}
+
 // Weight gradient of y = conv2d(x, w, stride, pad) given dy; with `acc` (the parameter's
 // persistent .grad view, fp32 or bf16, [K, C, R, S] channels_last) it is added in place and
 // returned.
@@ -229,8 +194,6 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stats"));
   m.def("conv_igemm_dgrad", &conv_igemm_dgrad, pybind11::arg("dy"), pybind11::arg("w"),
         pybind11::arg("pad"));
-  m.def("conv1x1_fwd", &conv1x1_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stats"));
-  m.def("conv1x1_dgrad", &conv1x1_dgrad);
-  m.def("conv1x1_wgrad", &conv1x1_wgrad, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"),
-        pybind11::arg("acc") = pybind11::none());
+  m.def("conv_igemm_dgrad_bn", &conv_igemm_dgrad_bn, pybind11::arg("dy"), pybind11::arg("w"),
+        pybind11::arg("pad"), pybind11::arg("bn_x"), pybind11::arg("bn_mask"), pybind11::arg("bn_mean"));
 }

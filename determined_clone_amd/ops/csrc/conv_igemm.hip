@@ -84,10 +84,17 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rsrc, uint32_t vof
       rsrc, (__attribute__((address_space(3))) void*)(lds_dst), 16, voff, soff, 0, 0);
 }
 
-template <int BM, int BN, int WM, int WN, int NSTAGE, bool STATS>
+// STATS (epilogue statistics into partial[mt][2][K], batchnorm.hip's layout):
+//   0 = none;
+//   1 = forward: (sum y, sum y^2) of the bf16 outputs -- the following BatchNorm's statistics;
+//   2 = backward: this launch is the DATA GRADIENT of a convolution whose input was
+//       relu(bn(bnx)); with g = the bf16 output and m = that BatchNorm's ReLU bit (bnmask),
+//       (sum g*m, sum g*m*(bnx - bnmean)) -- the BatchNorm backward's statistics pass, fused.
+template <int BM, int BN, int WM, int WN, int NSTAGE, int STATS>
 __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-    float* __restrict__ partial, ConvGeom g) {
+    float* __restrict__ partial, ConvGeom g, const uint16_t* __restrict__ bnx,
+    const uint8_t* __restrict__ bnmask, const float* __restrict__ bnmean) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM / WM, TN = BN / WN;  // wave tile: pixels x channels
   constexpr int FM = TM / 32, FN = TN / 32;
@@ -269,18 +276,32 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
   constexpr int CPR = BN / 8;          // 16-B chunks per output row
   constexpr int RPP = kThreads / CPR;  // rows per pass
   const int cc = tid % CPR, rr = tid / CPR;
-  float s8[8], q8[8];
+  float s8[8], q8[8], mu[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
+  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; mu[k] = STATS == 2 ? bnmean[n0 + cc * 8 + k] : 0.f; }
   for (int row = rr; row < BM; row += RPP) {
     if (m0 + row >= g.M) break;
     const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CS + cc * 8);
-    *reinterpret_cast<uint4*>(y + static_cast<int64_t>(m0 + row) * g.K + n0 + cc * 8) = v;
+    const int64_t off = static_cast<int64_t>(m0 + row) * g.K + n0 + cc * 8;
+    *reinterpret_cast<uint4*>(y + off) = v;
     if (STATS) {
       const float f[8] = {bf16_lo(v.x), bf16_hi(v.x), bf16_lo(v.y), bf16_hi(v.y),
                           bf16_lo(v.z), bf16_hi(v.z), bf16_lo(v.w), bf16_hi(v.w)};
+      if (STATS == 1) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] = fmaf(f[k], f[k], q8[k]); }
+        for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] = fmaf(f[k], f[k], q8[k]); }
+      } else {
+        const uint4 xv = *reinterpret_cast<const uint4*>(bnx + off);
+        const uint32_t mk = bnmask[off >> 3];
+        const float xf[8] = {bf16_lo(xv.x), bf16_hi(xv.x), bf16_lo(xv.y), bf16_hi(xv.y),
+                             bf16_lo(xv.z), bf16_hi(xv.z), bf16_lo(xv.w), bf16_hi(xv.w)};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float gk = ((mk >> k) & 1u) ? f[k] : 0.f;
+          s8[k] += gk;
+          q8[k] = fmaf(gk, xf[k] - mu[k], q8[k]);
+        }
+      }
     }
   }
   if (STATS) {
@@ -628,9 +649,15 @@ int stages() {
   return v;
 }
 
-template <int BM, int BN, int NSTAGE, bool STATS>
+struct BnSrc {
+  const void* x;
+  const uint8_t* mask;
+  const float* mean;
+};
+
+template <int BM, int BN, int NSTAGE, int STATS>
 void launch_fwd_n(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                  hipStream_t st) {
+                  hipStream_t st, const BnSrc& bn) {
   constexpr int WM = BN >= 128 ? 2 : 4, WN = 4 / WM;
   constexpr size_t stage = static_cast<size_t>(BM + BN) * kBK * 2 * NSTAGE;
   constexpr size_t epi = static_cast<size_t>(BM) * (BN + 8) * 2;
@@ -645,26 +672,27 @@ void launch_fwd_n(const void* x, const void* w, void* y, float* partial, const C
   (void)attr;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, st,
                      static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w),
-                     static_cast<uint16_t*>(y), partial, g);
+                     static_cast<uint16_t*>(y), partial, g, static_cast<const uint16_t*>(bn.x),
+                     bn.mask, bn.mean);
 }
 
-template <int BM, int BN, bool STATS>
+template <int BM, int BN, int STATS>
 void launch_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                hipStream_t st) {
-  if (stages() == 3) launch_fwd_n<BM, BN, 3, STATS>(x, w, y, partial, g, st);
-  else launch_fwd_n<BM, BN, 2, STATS>(x, w, y, partial, g, st);
+                hipStream_t st, const BnSrc& bn) {
+  if (stages() == 3) launch_fwd_n<BM, BN, 3, STATS>(x, w, y, partial, g, st, bn);
+  else launch_fwd_n<BM, BN, 2, STATS>(x, w, y, partial, g, st, bn);
 }
 
-template <bool STATS>
+template <int STATS>
 void fwd_dispatch(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                  hipStream_t st) {
+                  hipStream_t st, const BnSrc& bn) {
   const Cfg c = pick(g);
   if (c.bn == 128) {
-    if (c.bm == 256) launch_fwd<256, 128, STATS>(x, w, y, partial, g, st);
-    else launch_fwd<128, 128, STATS>(x, w, y, partial, g, st);
+    if (c.bm == 256) launch_fwd<256, 128, STATS>(x, w, y, partial, g, st, bn);
+    else launch_fwd<128, 128, STATS>(x, w, y, partial, g, st, bn);
   } else {
-    if (c.bm == 256) launch_fwd<256, 64, STATS>(x, w, y, partial, g, st);
-    else launch_fwd<128, 64, STATS>(x, w, y, partial, g, st);
+    if (c.bm == 256) launch_fwd<256, 64, STATS>(x, w, y, partial, g, st, bn);
+    else launch_fwd<128, 64, STATS>(x, w, y, partial, g, st, bn);
   }
 }
 
@@ -677,9 +705,11 @@ int conv_igemm_row_blocks(const ConvGeom& g) {
 }
 
 void conv_igemm_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                    hipStream_t st) {
-  if (partial) fwd_dispatch<true>(x, w, y, partial, g, st);
-  else fwd_dispatch<false>(x, w, y, nullptr, g, st);
+                    hipStream_t st, const void* bn_x, const uint8_t* bn_mask, const float* bn_mean) {
+  const BnSrc bn{bn_x, bn_mask, bn_mean};
+  if (partial && bn_x) fwd_dispatch<2>(x, w, y, partial, g, st, bn);
+  else if (partial) fwd_dispatch<1>(x, w, y, partial, g, st, bn);
+  else fwd_dispatch<0>(x, w, y, nullptr, g, st, bn);
 }
 
 int64_t conv_igemm_wgrad_ws_floats(const ConvGeom& g) {

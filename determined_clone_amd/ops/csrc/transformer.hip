@@ -22,6 +22,7 @@ namespace {
 
 constexpr int kWaves = 4;             // rows (LN) handled concurrently per block
 constexpr int kBlock = kWaves * 64;
+constexpr int kLnColsumMaxD = 2048;    // LN backward reduces dx's column sums in-pass up to this width
 
 // 8 consecutive fp32 affine parameters (gamma or beta) from c, or `fill` when absent / out of range.
 __device__ __forceinline__ void load_affine8(const float* __restrict__ p, int c, bool ok, float fill,
@@ -107,20 +108,24 @@ __global__ __launch_bounds__(kBlock) void ln_fwd_kernel(
 
 // dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) [+ dres passthrough handled by caller]
 // Per-block partial dgamma/dbeta: partial[blockIdx.x][2][D] (fp32).
-template <typename T, int NV>
+// COLSUM: also the per-block column sums of dx itself (partial[blockIdx.x][3][D], third row): in a
+// pre-LN transformer the residual branch that fed this LayerNorm ends in a linear layer whose
+// output gradient IS dx, so its bias gradient comes out of this pass (no separate reduction).
+template <typename T, int NV, bool COLSUM = false>
 __global__ __launch_bounds__(kBlock) void ln_bwd_kernel(
     const void* __restrict__ dy, const void* __restrict__ x, const float* __restrict__ gamma,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const void* __restrict__ dsum, void* __restrict__ dx, float* __restrict__ partial,
     int64_t rows, int D) {
+  constexpr int NP = COLSUM ? 3 : 2;  // partial rows per block
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nvec = D / 8;
-  float dg[NV][8], db[NV][8], gam[NV][8];
+  float dg[NV][8], db[NV][8], gam[NV][8], cs[NV][8];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { dg[i][k] = 0.f; db[i][k] = 0.f; }
+    for (int k = 0; k < 8; ++k) { dg[i][k] = 0.f; db[i][k] = 0.f; cs[i][k] = 0.f; }
     const int c = (lane + i * 64) * 8;
     load_affine8(gamma, c, c < D, 1.f, gam[i]);
   }
@@ -193,28 +198,170 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_kernel(
 #pragma unroll
           for (int k = 0; k < 8; ++k) o[k] += r[k];
         }
+        if (COLSUM) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) cs[i][k] += o[k];
+        }
         Vec8<T>::store(reinterpret_cast<char*>(dx) + (base + c) * Vec8<T>::bytes, o);
       }
     }
   }
   // block-level combine of the kWaves waves' column partials through LDS
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [kWaves][2][D]
+  // cross-wave reduction, one partial row at a time through a [kWaves][D] LDS buffer (<= 128 KB
+  // at D = 8192)
+  extern __shared__ __attribute__((aligned(16))) float lds[];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int vi = lane + i * 64;
-    if (vi < nvec)
+  for (int which = 0; which < NP; ++which) {
+    if (which) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = lane + i * 64;
+      if (vi < nvec)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          lds[wid * D + vi * 8 + k] = which == 0 ? dg[i][k] : which == 1 ? db[i][k] : cs[i][k];
+    }
+    __syncthreads();
+    for (int col = threadIdx.x; col < D; col += kBlock) {
+      float a = 0.f;
+      for (int w = 0; w < kWaves; ++w) a += lds[w * D + col];
+      partial[(static_cast<int64_t>(blockIdx.x) * NP + which) * D + col] = a;
+    }
+  }
+}
+
+// Row-group LayerNorm backward for D <= 2048 (the transformer widths). A row is covered by a group
+// of W = ceil(D / 512) waves -- 8 columns per lane, one 16-B nontemporal load per tensor -- so a
+// lane keeps only 8 columns of dgamma / dbeta (/ dx column sum) accumulators and gamma: ~1/2 the
+// registers of the one-row-per-wave kernel above, hence twice the waves per CU to keep HBM busy.
+// A 512-thread block runs G = 8 / W groups; each group takes R rows per step, all their loads
+// issued before the first use. The per-row sums (g.gamma, g.gamma.xhat) cross the W waves of a
+// group through a double-buffered LDS slot (one barrier per step; none when W == 1), and at the
+// end the G groups' column partials combine through LDS into ONE partial row set per block
+// (partial[blockIdx.x][NP][D]), so the partial traffic stays ~1-2 % of the pass.
+constexpr int kLnRgThreads = 512;
+template <typename T, int W, int R, bool COLSUM>
+__global__ __launch_bounds__(kLnRgThreads) void ln_bwd_rg_kernel(
+    const void* __restrict__ dy, const void* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const void* __restrict__ dsum, void* __restrict__ dx, float* __restrict__ partial,
+    int64_t rows, int D) {
+  constexpr int G = 8 / W;
+  constexpr int NP = COLSUM ? 3 : 2;
+  __shared__ float red[2][G][R][W][2];
+  __shared__ __attribute__((aligned(16))) float comb[G][W * 512];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar row math
+  const int grp = wid / W, wg = wid % W;
+  const int cl = (wg * 64 + lane) * 8;  // first of this lane's 8 columns
+  const bool ok = cl < D;
+  const int clc = ok ? cl : 0;          // loads stay in bounds; !ok lanes never store
+  float gam[8], dg[8], db[8], cs[8];
+  load_affine8(gamma, cl, ok, 1.f, gam);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { dg[k] = 0.f; db[k] = 0.f; cs[k] = 0.f; }
+  int par = 0;
+  // block-uniform trip count (every wave reaches every barrier); rows past the end load the last
+  // row again and are masked out of the sums and stores
+  for (int64_t b0 = static_cast<int64_t>(blockIdx.x) * G * R; b0 < rows;
+       b0 += static_cast<int64_t>(gridDim.x) * G * R) {
+    const int64_t r0 = b0 + static_cast<int64_t>(grp) * R;
+    Raw8<T> rx[R], rg[R], rr[R];
+    float mu[R], rs[R], s1[R], s2[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int64_t row = r0 + j < rows ? r0 + j : rows - 1;
+      mu[j] = mean_in[row];
+      rs[j] = rstd_in[row];
+      rx[j] = ld8nt<T>(x, row * D + clc);
+      rg[j] = ld8nt<T>(dy, row * D + clc);
+      rr[j] = {};
+      if (dsum) rr[j] = ld8nt<T>(dsum, row * D + clc);
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      float xv[8], g[8];
+      unpack8<T>(rx[j], xv);
+      unpack8<T>(rg[j], g);
+      const float live = (r0 + j < rows && ok) ? 1.f : 0.f;
+      float a = 0.f, b = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        lds[(wid * 2 + 0) * D + vi * 8 + k] = dg[i][k];
-        lds[(wid * 2 + 1) * D + vi * 8 + k] = db[i][k];
+        const float gk = g[k] * live;
+        const float xh = (xv[k] - mu[j]) * rs[j];
+        dg[k] = fmaf(gk, xh, dg[k]);
+        db[k] += gk;
+        const float gg = gk * gam[k];
+        a += gg;
+        b = fmaf(gg, xh, b);
       }
+      s1[j] = wave_sum_dpp(a);
+      s2[j] = wave_sum_dpp(b);
+    }
+    if constexpr (W > 1) {
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          red[par][grp][j][wg][0] = s1[j];
+          red[par][grp][j][wg][1] = s2[j];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          a += red[par][grp][j][w][0];
+          b += red[par][grp][j][w][1];
+        }
+        s1[j] = a;
+        s2[j] = b;
+      }
+      par ^= 1;
+    }
+    const float inv_d = 1.f / static_cast<float>(D);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int64_t row = r0 + j;
+      if (row < rows && ok) {
+        float xv[8], g[8], o[8];
+        unpack8<T>(rx[j], xv);
+        unpack8<T>(rg[j], g);
+        const float m1 = s1[j] * inv_d, m2 = s2[j] * inv_d;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float xh = (xv[k] - mu[j]) * rs[j];
+          o[k] = rs[j] * (g[k] * gam[k] - m1 - xh * m2);
+        }
+        if (dsum) {
+          float r[8];
+          unpack8<T>(rr[j], r);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] += r[k];
+        }
+        if (COLSUM) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) cs[k] += o[k];
+        }
+        Vec8<T>::store(reinterpret_cast<char*>(dx) + (row * D + cl) * Vec8<T>::bytes, o);
+      }
+    }
   }
-  __syncthreads();
-  for (int c = threadIdx.x; c < 2 * D; c += kBlock) {
-    const int which = c / D, col = c % D;
-    float a = 0.f;
-    for (int w = 0; w < kWaves; ++w) a += lds[(w * 2 + which) * D + col];
-    partial[(static_cast<int64_t>(blockIdx.x) * 2 + which) * D + col] = a;
+  // the G groups' column partials -> one partial row per quantity
+#pragma unroll
+  for (int which = 0; which < NP; ++which) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      comb[grp][cl + k] = which == 0 ? dg[k] : which == 1 ? db[k] : cs[k];  // cl < W * 512
+    __syncthreads();
+    for (int col = threadIdx.x; col < D; col += kLnRgThreads) {
+      float a = 0.f;
+#pragma unroll
+      for (int g2 = 0; g2 < G; ++g2) a += comb[g2][col];
+      partial[(static_cast<int64_t>(blockIdx.x) * NP + which) * D + col] = a;
+    }
   }
 }
 
@@ -235,9 +382,12 @@ __device__ __forceinline__ void column_store(const ColumnOut& o, int64_t j, floa
   }
 }
 
+// Columns j >= n0 land in out2 (at j - n0): one launch reduces several quantities whose partial
+// rows sit side by side (LayerNorm backward: dgamma | dbeta | dx column sums).
 __global__ __launch_bounds__(kColWaves * 64) void column_reduce_kernel(const float* __restrict__ partial,
                                                                       int nparts, int64_t ncols,
-                                                                      ColumnOut out) {
+                                                                      ColumnOut out, int64_t pstride,
+                                                                      ColumnOut out2, int64_t n0) {
   __shared__ float red[kColWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + lane;
@@ -245,12 +395,12 @@ __global__ __launch_bounds__(kColWaves * 64) void column_reduce_kernel(const flo
   if (j < ncols) {
     int b = w;
     for (; b + 3 * kColWaves < nparts; b += 4 * kColWaves) {
-      a0 += partial[static_cast<int64_t>(b) * ncols + j];
-      a1 += partial[static_cast<int64_t>(b + kColWaves) * ncols + j];
-      a2 += partial[static_cast<int64_t>(b + 2 * kColWaves) * ncols + j];
-      a3 += partial[static_cast<int64_t>(b + 3 * kColWaves) * ncols + j];
+      a0 += partial[static_cast<int64_t>(b) * pstride + j];
+      a1 += partial[static_cast<int64_t>(b + kColWaves) * pstride + j];
+      a2 += partial[static_cast<int64_t>(b + 2 * kColWaves) * pstride + j];
+      a3 += partial[static_cast<int64_t>(b + 3 * kColWaves) * pstride + j];
     }
-    for (; b < nparts; b += kColWaves) a0 += partial[static_cast<int64_t>(b) * ncols + j];
+    for (; b < nparts; b += kColWaves) a0 += partial[static_cast<int64_t>(b) * pstride + j];
   }
   red[w][lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
@@ -258,7 +408,10 @@ __global__ __launch_bounds__(kColWaves * 64) void column_reduce_kernel(const flo
     if (w < s) red[w][lane] += red[w + s][lane];
     __syncthreads();
   }
-  if (w == 0 && j < ncols) column_store(out, j, red[0][lane]);
+  if (w == 0 && j < ncols) {
+    if (j < n0) column_store(out, j, red[0][lane]);
+    else column_store(out2, j - n0, red[0][lane]);
+  }
 }
 
 // Per-block column partial sums of dy [rows][N] (bias gradient of a linear layer). Block = 4 waves;
@@ -411,9 +564,10 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
     float g[4][8], a[4][8];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int64_t off = ((r + u * step) * N + c) * Vec8<T>::bytes;
-      Vec8<T>::load(reinterpret_cast<const char*>(dy) + off, g[u]);
-      Vec8<T>::load(reinterpret_cast<const char*>(x) + off, a[u]);
+      // streamed once: nontemporal loads (profiles/round4_hbm_streaming_ceilings.txt)
+      const int64_t e = (r + u * step) * N + c;
+      unpack8<T>(ld8nt<T>(dy, e), g[u]);
+      unpack8<T>(ld8nt<T>(x, e), a[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -542,24 +696,95 @@ void layernorm_fwd(TDtype dt, const void* x, const void* res, void* sum_out, voi
   });
 }
 
+// Row-group kernel launch shape (D <= kLnColsumMaxD): W waves per row, R rows per group step.
+int ln_rg_waves(int D) { return D <= 512 ? 1 : D <= 1024 ? 2 : 4; }
+int ln_rg_rows() {
+  static const int r = [] {
+    const char* e = std::getenv("DCA_LN_BWD_ROWS");
+    return e && std::atoi(e) == 4 ? 4 : 2;
+  }();
+  return r;
+}
+int ln_rg_blocks(int64_t rows, int D) {
+  // DCA_LN_BWD_BLOCKS overrides (tuning); the default fills every CU with two 8-wave blocks
+  static const int cap = [] {
+    const char* e = std::getenv("DCA_LN_BWD_BLOCKS");
+    return e ? std::atoi(e) : 512;
+  }();
+  const int64_t per = static_cast<int64_t>(8 / ln_rg_waves(D)) * ln_rg_rows();
+  const int64_t g = (rows + per - 1) / per;
+  return static_cast<int>(g < cap ? (g < 1 ? 1 : g) : cap);
+}
+bool ln_rg_path(int D) {
+  static const bool off = [] {
+    const char* e = std::getenv("DCA_LN_BWD_RG");
+    return e && e[0] == '0';
+  }();
+  return !off && D <= kLnColsumMaxD;
+}
+
+int64_t ln_bwd_partial_floats(int64_t rows, int D, bool colsum) {
+  const int blocks = ln_rg_path(D) ? ln_rg_blocks(rows, D) : ln_bwd_blocks(rows);
+  const int64_t n = static_cast<int64_t>(blocks) * (colsum && D <= kLnColsumMaxD ? 3 : 2) * D;
+  const int64_t r = colsum && D > kLnColsumMaxD ? static_cast<int64_t>(row_sum_blocks(rows, D)) * D : 0;
+  return n > r ? n : r;
+}
+
 void layernorm_bwd(TDtype dt, const void* dy, const void* x, const float* gamma, const float* mean,
                    const float* rstd, const void* dsum, void* dx, float* partial,
-                   const ColumnOut* dgamma_dbeta, int64_t rows, int D, hipStream_t st) {
-  const int blocks = ln_bwd_blocks(rows);
+                   const ColumnOut* dgamma_dbeta, int64_t rows, int D, hipStream_t st,
+                   const ColumnOut* dx_colsum) {
+  const bool rg = ln_rg_path(D);
+  const int blocks = rg ? ln_rg_blocks(rows, D) : ln_bwd_blocks(rows);
+  const bool fused_colsum = dx_colsum && D <= kLnColsumMaxD;
+  const int np = fused_colsum ? 3 : 2;
   dispatch_t(dt, [&](auto t) {
     using T = decltype(t);
+    if (rg) {
+      const int W = ln_rg_waves(D), R = ln_rg_rows();
+      auto go = [&](auto wt, auto rt) {
+        constexpr int Wc = decltype(wt)::value, Rc = decltype(rt)::value;
+        if (fused_colsum)
+          hipLaunchKernelGGL((ln_bwd_rg_kernel<T, Wc, Rc, true>), dim3(blocks), dim3(kLnRgThreads), 0, st,
+                             dy, x, gamma, mean, rstd, dsum, dx, partial, rows, D);
+        else
+          hipLaunchKernelGGL((ln_bwd_rg_kernel<T, Wc, Rc, false>), dim3(blocks), dim3(kLnRgThreads), 0, st,
+                             dy, x, gamma, mean, rstd, dsum, dx, partial, rows, D);
+      };
+      auto by_rows = [&](auto wt) {
+        if (R == 4) go(wt, NVTag<4>{}); else go(wt, NVTag<2>{});
+      };
+      if (W == 1) by_rows(NVTag<1>{});
+      else if (W == 2) by_rows(NVTag<2>{});
+      else by_rows(NVTag<4>{});
+      return;
+    }
     dispatch_nv<T>(D, [&](auto nvt) {
       constexpr int NV = decltype(nvt)::value;
-      const size_t lds = static_cast<size_t>(kWaves) * 2 * D * sizeof(float);
-      hipLaunchKernelGGL((ln_bwd_kernel<T, NV>), dim3(blocks), dim3(kBlock), lds, st, dy, x, gamma,
+      const size_t lds = static_cast<size_t>(kWaves) * D * sizeof(float);
+      if constexpr (NV <= 4) {  // D <= 2048: the extra accumulators fit in registers
+        if (fused_colsum) {
+          hipLaunchKernelGGL((ln_bwd_kernel<T, NV, true>), dim3(blocks), dim3(kBlock), lds, st, dy, x,
+                             gamma, mean, rstd, dsum, dx, partial, rows, D);
+          return;
+        }
+      }
+      hipLaunchKernelGGL((ln_bwd_kernel<T, NV, false>), dim3(blocks), dim3(kBlock), lds, st, dy, x, gamma,
                          mean, rstd, dsum, dx, partial, rows, D);
     });
   });
-  if (dgamma_dbeta) {
-    const int64_t ncols = 2 * static_cast<int64_t>(D);
+  const int64_t pstride = static_cast<int64_t>(np) * D;
+  if (dgamma_dbeta || fused_colsum) {
+    // one launch: dgamma | dbeta (2D columns) and the dx column sums (D more) when fused
+    const int64_t n0 = dgamma_dbeta ? 2 * static_cast<int64_t>(D) : 0;
+    const int64_t ncols = n0 + (fused_colsum ? D : 0);
+    const float* src = dgamma_dbeta ? partial : partial + 2 * D;
     hipLaunchKernelGGL(column_reduce_kernel, dim3((ncols + 63) / 64), dim3(kColWaves * 64), 0, st,
-                       partial, blocks, ncols, *dgamma_dbeta);
+                       src, blocks, ncols, dgamma_dbeta ? *dgamma_dbeta : ColumnOut{}, pstride,
+                       fused_colsum ? *dx_colsum : ColumnOut{}, n0);
   }
+  if (dx_colsum && !fused_colsum)  // wide rows: a separate column reduction of dx (see ln_bwd_partial_floats)
+    row_sum(dt, dx, partial, *dx_colsum, rows, D, st);
 }
 
 void bias_gelu_fwd(TDtype dt, const void* x, const void* bias, bool bias_bf16, void* y,
@@ -572,7 +797,14 @@ void bias_gelu_fwd(TDtype dt, const void* x, const void* bias, bool bias_bf16, v
   });
 }
 
-int bias_gelu_bwd_row_blocks(int64_t rows) { return static_cast<int>(rows < 256 ? (rows < 1 ? 1 : rows) : 256); }
+int bias_gelu_bwd_row_blocks(int64_t rows) {
+  // row slabs (grid.y); DCA_BGB_BLOCKS overrides (tuning)
+  static const int cap = [] {
+    const char* e = std::getenv("DCA_BGB_BLOCKS");
+    return e ? std::atoi(e) : 256;
+  }();
+  return static_cast<int>(rows < cap ? (rows < 1 ? 1 : rows) : cap);
+}
 
 void bias_gelu_bwd(TDtype dt, const void* dy, const void* x, const void* bias, bool bias_bf16,
                    void* dx, float* partial, const ColumnOut* dbias, int64_t rows, int N,
@@ -586,7 +818,8 @@ void bias_gelu_bwd(TDtype dt, const void* dy, const void* x, const void* bias, b
   });
   if (dbias)
     hipLaunchKernelGGL(column_reduce_kernel, dim3((N + 63) / 64), dim3(kColWaves * 64), 0, st,
-                       partial, rb, static_cast<int64_t>(N), *dbias);
+                       partial, rb, static_cast<int64_t>(N), *dbias, static_cast<int64_t>(N), ColumnOut{},
+                       static_cast<int64_t>(N));
 }
 
 int row_sum_blocks(int64_t rows, int N) {
@@ -607,7 +840,8 @@ void row_sum(TDtype dt, const void* dy, float* partial, const ColumnOut& out, in
     hipLaunchKernelGGL(row_sum_kernel<T>, grid, dim3(kRsWaves * 64), 0, st, dy, partial, rows, N);
   });
   hipLaunchKernelGGL(column_reduce_kernel, dim3((N + 63) / 64), dim3(kColWaves * 64), 0, st,
-                     partial, rb, static_cast<int64_t>(N), out);
+                     partial, rb, static_cast<int64_t>(N), out, static_cast<int64_t>(N), ColumnOut{},
+                     static_cast<int64_t>(N));
 }
 
 void rope(TDtype dt, const void* x, void* y, const float* cosT, const float* sinT, int64_t rows,

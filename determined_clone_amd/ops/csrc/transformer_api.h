@@ -22,9 +22,14 @@ int ln_bwd_blocks(int64_t rows);
 void layernorm_fwd(TDtype dt, const void* x, const void* res, void* sum_out, void* y,
                    const float* gamma, const float* beta, float* mean, float* rstd, int64_t rows,
                    int D, float eps, hipStream_t st);
+// floats of `partial` layernorm_bwd needs
+int64_t ln_bwd_partial_floats(int64_t rows, int D, bool colsum);
+// dx_colsum (optional): column sums of dx (the bias gradient of the linear layer whose output fed
+// the LayerNorm as its residual); partial then holds [blocks][3][D].
 void layernorm_bwd(TDtype dt, const void* dy, const void* x, const float* gamma, const float* mean,
                    const float* rstd, const void* dsum, void* dx, float* partial,
-                   const ColumnOut* dgamma_dbeta, int64_t rows, int D, hipStream_t st);
+                   const ColumnOut* dgamma_dbeta, int64_t rows, int D, hipStream_t st,
+                   const ColumnOut* dx_colsum = nullptr);
 void bias_gelu_fwd(TDtype dt, const void* x, const void* bias, bool bias_bf16, void* y,
                    int64_t rows, int N, hipStream_t st);
 int bias_gelu_bwd_row_blocks(int64_t rows);

@@ -58,15 +58,23 @@ void check_acc(const Tensor& t, int64_t n, const Tensor& like, const char* what)
 
 std::vector<Tensor> ln_bwd(const Tensor& dy_in, const Tensor& x, const OptT& gamma,
                            const Tensor& mean, const Tensor& rstd, const OptT& dsum,
-                           bool need_param_grads, const OptT& dgamma_acc, const OptT& dbeta_acc) {
+                           bool need_param_grads, const OptT& dgamma_acc, const OptT& dbeta_acc,
+                           const OptT& colsum_acc) {
   const c10::DeviceGuard g(x.device());
   Tensor dy = dy_in.contiguous();
   const int D = static_cast<int>(x.size(-1));
   const int64_t rows = x.numel() / D;
   Tensor dx = torch::empty_like(x);
   auto fo = x.options().dtype(at::kFloat);
-  const int blocks = dca::ln_bwd_blocks(rows);
-  Tensor partial = torch::empty({static_cast<int64_t>(blocks) * 2 * D}, fo);
+  // colsum_acc (+)= dx.sum(rows): the bias gradient of the linear layer that produced the
+  // residual input, reduced in this pass (partial grows a third [D] row per block)
+  const bool colsum = want_acc(colsum_acc);
+  dca::ColumnOut cs;
+  if (colsum) {
+    check_acc(*colsum_acc, D, x, "ln_bwd colsum");
+    cs = {colsum_acc->data_ptr(), nullptr, D, colsum_acc->scalar_type() == at::kBFloat16, true};
+  }
+  Tensor partial = torch::empty({dca::ln_bwd_partial_floats(rows, D, colsum)}, fo);
   const bool acc = need_param_grads && want_acc(dgamma_acc) && want_acc(dbeta_acc);
   Tensor dgb;
   dca::ColumnOut out;
@@ -83,7 +91,8 @@ std::vector<Tensor> ln_bwd(const Tensor& dy_in, const Tensor& x, const OptT& gam
   Tensor ds = dsum.has_value() && dsum->defined() ? dsum->contiguous() : Tensor();
   dca::layernorm_bwd(tdt(x), dy.data_ptr(), x.data_ptr(), fp(gamma), mean.data_ptr<float>(),
                      rstd.data_ptr<float>(), ds.defined() ? ds.data_ptr() : nullptr, dx.data_ptr(),
-                     partial.data_ptr<float>(), need_param_grads ? &out : nullptr, rows, D, stream());
+                     partial.data_ptr<float>(), need_param_grads ? &out : nullptr, rows, D, stream(),
+                     colsum ? &cs : nullptr);
   if (!need_param_grads || acc) return {dx, Tensor(), Tensor()};
   return {dx, dgb[0], dgb[1]};
 }
@@ -308,7 +317,7 @@ void register_transformer_ops(pybind11::module& m) {
   m.def("ln_bwd", &ln_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("gamma"),
         pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("dsum"),
         pybind11::arg("need_param_grads"), pybind11::arg("dgamma_acc") = pybind11::none(),
-        pybind11::arg("dbeta_acc") = pybind11::none());
+        pybind11::arg("dbeta_acc") = pybind11::none(), pybind11::arg("colsum_acc") = pybind11::none());
   m.def("bias_grad", &bias_grad, pybind11::arg("dy"), pybind11::arg("acc") = pybind11::none());
   m.def("bias_gelu", &bias_gelu);
   m.def("splitk_accumulate", &splitk_accumulate, pybind11::arg("part"), pybind11::arg("acc"),

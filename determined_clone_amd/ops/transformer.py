@@ -91,6 +91,15 @@ def _f32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return t if t.dtype == torch.float32 and t.is_contiguous() else t.float().contiguous()
 
 
+# DCA_FUSE_LN_BIAS_GRAD=1: the out-projection bias gradients come out of the LayerNorm backward
+# (its dx column sums, +0.6 us per call in isolation) instead of a separate column reduction. OFF by
+# default: the GPT-2-medium step measured 0.6 % slower with it (381.6k vs 383.9k tok/s, same box,
+# profiles/round5_ln_bwd_bias_grad_fusion_ab.txt) -- on the main stream the separate memory-bound
+# reduction pairs better with the side stream's weight-gradient GEMMs than the next dX GEMM does.
+FUSE_LN_BIAS_GRAD = os.environ.get("DCA_FUSE_LN_BIAS_GRAD", "0") == "1"
+LN_BIAS_GRAD_HITS = [0]
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, eps):
@@ -105,6 +114,11 @@ class _LayerNorm(torch.autograd.Function):
         ctx.has_res = res is not None
         ctx.w_dtype = weight.dtype if weight is not None else None
         ctx.params = (weight, bias)
+        # pre-LN block: the residual input is the output of a ``linear`` (attention / MLP out
+        # projection) whose dy is exactly this LayerNorm's dx -- its bias gradient is reduced in
+        # the LN backward pass instead of by a separate column sum (``_Linear.backward``)
+        ctx.bias_node = residual.grad_fn if (FUSE_LN_BIAS_GRAD and res is not None and res is residual and
+                                             type(residual.grad_fn).__name__ == "_LinearBackward") else None
         if res is not None:
             return y, s
         return y
@@ -116,8 +130,16 @@ class _LayerNorm(torch.autograd.Function):
         acc_g, acc_b = (_grad.target(ctx.params[0]), _grad.target(ctx.params[1])) if need_w else (None, None)
         if acc_g is None or acc_b is None or acc_g.dtype != acc_b.dtype:
             acc_g = acc_b = None
+        node, acc_cs = ctx.bias_node, None
+        ctx.bias_node = None
+        if node is not None and ctx.needs_input_grad[1] and node.needs_input_grad[2] and \
+                node.params[1] is not None:
+            acc_cs = _grad.target(node.params[1])
         dx, dg, db = _ext.load().ln_bwd(dy, xin, _f32(weight), mean, rstd,
-                                        dsum if ctx.has_res else None, need_w, acc_g, acc_b)
+                                        dsum if ctx.has_res else None, need_w, acc_g, acc_b, acc_cs)
+        if acc_cs is not None:
+            node._dca_bias_given = dx  # (+)= dx.sum(rows) is already in the bias .grad
+            LN_BIAS_GRAD_HITS[0] += 1
         if acc_g is not None:
             need_w = False  # accumulated into .grad in-kernel
         if need_w:
@@ -230,6 +252,13 @@ class _Linear(torch.autograd.Function):
                 dw = dy2.t() @ x2
         if ctx.needs_input_grad[0]:
             dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
+        given = getattr(ctx, "_dca_bias_given", None)
+        if given is not None:
+            ctx._dca_bias_given = None
+            if dy.data_ptr() == given.data_ptr() and dy.shape == given.shape and dy.stride() == given.stride():
+                return dx, dw, None  # bias gradient reduced by the consuming LayerNorm's backward
+            # dy also carries gradient from another consumer: add only that part
+            dy2 = (dy - given).reshape(-1, dy.shape[-1])
         if b_param is not None and ctx.needs_input_grad[2]:
             acc = _grad.target(b_param)
             if dy2.shape[-1] % 8 == 0 and dy2.is_cuda:

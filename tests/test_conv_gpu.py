@@ -1,4 +1,5 @@
-"""Numerics of the pointwise-convolution MFMA kernels (ops/csrc/conv1x1.hip) vs fp32 PyTorch."""
+"""Numerics of the convolution paths (ops/conv.py: library 1x1 choices, implicit-GEMM MFMA kernels of
+ops/csrc/conv_igemm.hip, fused BatchNorm statistics) vs fp32 PyTorch."""
 import copy
 
 import pytest
@@ -10,128 +11,10 @@ from determined_clone_amd.ops import _ext, batchnorm, conv
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [
-    # (N, Cin, H, W, Cout): ResNet-50 bottleneck pointwise shapes (small batch) + ragged row counts
-    (2, 64, 56, 56, 64),
-    (2, 256, 56, 56, 64),
-    (2, 64, 56, 56, 256),
-    (4, 512, 28, 28, 128),
-    (4, 128, 28, 28, 512),
-    (8, 1024, 14, 14, 256),
-    (8, 256, 14, 14, 1024),
-    (3, 2048, 7, 7, 512),
-    (3, 512, 7, 7, 2048),
-    (1, 128, 3, 5, 64),
-]
-
-
 def _close(got, ref, tol, what):
     err = (got.float() - ref).abs().max().item()
     scale = ref.abs().max().item() + 1e-6
     assert err <= tol * scale, f"{what}: max abs err {err:.3e} vs scale {scale:.3e}"
-
-
-def _inputs(n, cin, h, w, cout, seed=0):
-    g = torch.Generator(device="cpu").manual_seed(seed)
-    x = torch.randn(n, cin, h, w, generator=g).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
-    wt = (torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5).cuda().bfloat16()
-    dy = torch.randn(n, cout, h, w, generator=g).cuda().bfloat16().contiguous(memory_format=torch.channels_last)
-    return x, wt, dy
-
-
-@pytest.mark.parametrize("shape", SHAPES)
-def test_conv1x1_forward_and_stats(shape):
-    C = _ext.load()
-    n, cin, h, w, cout = shape
-    x, wt, _ = _inputs(*shape)
-    y, partial = C.conv1x1_fwd(x, wt, True)
-    assert y.is_contiguous(memory_format=torch.channels_last) and y.dtype == torch.bfloat16
-    ref, stats = conv.reference_conv1x1(x, wt)
-    _close(y, ref, 1e-2, "y")
-    # the fused statistics are of the bf16-rounded output
-    yc = y.float().permute(0, 2, 3, 1).reshape(-1, cout)
-    got = partial.sum(0)
-    torch.testing.assert_close(got[0], yc.sum(0), atol=1e-2 * yc.shape[0] ** 0.5, rtol=1e-3)
-    torch.testing.assert_close(got[1], (yc * yc).sum(0), atol=1e-2, rtol=1e-3)
-    y2, p2 = C.conv1x1_fwd(x, wt, False)
-    assert p2 is None
-    torch.testing.assert_close(y2, y, atol=0, rtol=0)
-
-
-@pytest.mark.parametrize("shape", SHAPES)
-def test_conv1x1_dgrad_wgrad(shape):
-    C = _ext.load()
-    x, wt, dy = _inputs(*shape, seed=1)
-    xr = x.float().requires_grad_(True)
-    wr = wt.float().requires_grad_(True)
-    F.conv2d(xr, wr).backward(dy.float())
-    dx = C.conv1x1_dgrad(dy, wt)
-    assert dx.is_contiguous(memory_format=torch.channels_last)
-    _close(dx, xr.grad, 1e-2, "dx")
-    dw = C.conv1x1_wgrad(dy, x, wt)
-    assert dw.shape == wt.shape and dw.dtype == torch.bfloat16
-    _close(dw, wr.grad, 1e-2, "dw")
-    # accumulate into an existing fp32 and bf16 .grad
-    for dt in (torch.float32, torch.bfloat16):
-        acc = torch.full(wt.shape, 0.5, device="cuda", dtype=dt)
-        out = C.conv1x1_wgrad(dy, x, wt, acc)
-        assert out.data_ptr() == acc.data_ptr()
-        _close(acc, wr.grad + 0.5, 1e-2, f"dw accumulate {dt}")
-
-
-@pytest.fixture
-def pointwise_on(monkeypatch):
-    monkeypatch.setattr(conv, "ENABLED", True)
-
-
-def test_pointwise_conv_autograd_and_bn_fusion(pointwise_on):
-    """Module path: pointwise conv -> fused BN(+ReLU) consuming the epilogue statistics, against
-    the same bf16 layers unfused (MIOpen conv + BN with its own statistics pass); the output is
-    also checked against fp32 torch."""
-    torch.manual_seed(0)
-    conv_m = nn.Conv2d(256, 128, 1, bias=False).cuda().bfloat16().to(memory_format=torch.channels_last)
-    x0 = torch.randn(4, 256, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    dout = torch.randn(4, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-
-    def run(fused):
-        bn = nn.BatchNorm2d(128).cuda()
-        w = conv_m.weight.detach().clone().requires_grad_(True)
-        x = x0.detach().clone().requires_grad_(True)
-        if fused:
-            conv_m.weight.grad = None
-            y = conv.pointwise_conv(conv_m, x, bn_stats=True)
-            assert getattr(y, "_dca_bn_partials", None) is not None
-        else:
-            y = F.conv2d(x, w)
-        out = batchnorm.batch_norm_act(y, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                       training=True, relu=True)
-        out.backward(dout)
-        dw = conv_m.weight.grad if fused else w.grad
-        return out, x.grad, dw, bn
-
-    out, dx, dw, bn = run(True)
-    out_r, dx_r, dw_r, bn_r = run(False)
-    _close(out, out_r.float(), 2e-2, "bn(conv(x))")
-    _close(dx, dx_r.float(), 2e-2, "dx")
-    _close(dw, dw_r.float(), 2e-2, "dW")
-    torch.testing.assert_close(bn.running_mean, bn_r.running_mean, atol=1e-3, rtol=1e-2)
-    torch.testing.assert_close(bn.running_var, bn_r.running_var, atol=1e-3, rtol=1e-2)
-    ref = F.relu(F.batch_norm(F.conv2d(x0.float(), conv_m.weight.float()), None, None, None, None,
-                              True, 0.1, 1e-5))
-    _close(out, ref, 3e-2, "vs fp32")
-
-
-def test_resnet_bottleneck_uses_pointwise_kernels(pointwise_on):
-    from determined_clone_amd.models import resnet
-
-    torch.manual_seed(0)
-    m = resnet.to_mi355x_layout(resnet.resnet18_bottleneck_tiny(num_classes=10)).cuda()
-    blk = m.layer1[0]
-    x = torch.randn(2, 64, 16, 16, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    assert conv.supported(blk.conv1, x) and conv.supported(blk.conv3, torch.empty(2, 64, 16, 16, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last))
-    out = m(torch.randn(2, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last))
-    out.float().sum().backward()
-    assert torch.isfinite(blk.conv1.weight.grad.float()).all()
 
 
 @pytest.mark.parametrize("choice", [0, 1])
@@ -499,3 +382,59 @@ def test_strided_accumulate_matches_strided_add(shape):
     want[:, :, ::s, ::s] += small
     _ext.load().strided_accumulate(dx, small, s)
     torch.testing.assert_close(dx, want, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 56, 56), (2, 128, 28, 28), (8, 256, 14, 14), (4, 512, 7, 7)])
+def test_igemm_dgrad_bn_statistics_epilogue(shape):
+    """conv_igemm_dgrad_bn: the stride-1 3x3 data gradient plus, from its epilogue, the backward
+    statistics of the BN+ReLU that produced the convolution input -- (sum g*m, sum g*m*(x - mean))
+    over the bf16 gradient g -- against the same sums in fp32 over the returned gradient."""
+    from determined_clone_amd.ops import _ext
+
+    C = _ext.load()
+    torch.manual_seed(0)
+    N, c, H, W = shape
+    k = c
+    dy = torch.randn(N, k, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(k, c, 3, 3, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
+    x_bn = torch.randn(N, c, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    mean = torch.randn(c, device="cuda") * 0.1
+    keep = torch.rand(N, c, H, W, device="cuda") > 0.4
+    rows = keep.permute(0, 2, 3, 1).reshape(-1, c)
+    bits = (rows.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1)
+    mask = bits.to(torch.uint8).contiguous()
+    dx_ref = C.conv_igemm_dgrad(dy, w, 1)
+    dx, part = C.conv_igemm_dgrad_bn(dy, w, 1, x_bn, mask, mean)
+    assert torch.equal(dx, dx_ref)  # the epilogue statistics leave the gradient untouched
+    g = dx.float().permute(0, 2, 3, 1).reshape(-1, c) * rows
+    xr = x_bn.float().permute(0, 2, 3, 1).reshape(-1, c)
+    want_s, want_q = g.sum(0), (g * (xr - mean)).sum(0)
+    got = part.sum(0)
+    torch.testing.assert_close(got[0], want_s, atol=2e-2, rtol=1e-3)
+    torch.testing.assert_close(got[1], want_q, atol=5e-2, rtol=1e-3)
+
+
+def test_bottleneck_bn1_backward_statistics_fused_in_conv2_dgrad(monkeypatch):
+    """In a stride-1 bottleneck, bn1's backward takes its statistics from conv2's dgrad epilogue
+    (counted) and the block's gradients match the unfused path (DCA_FUSE_BN_BWD_STATS=0)."""
+    from determined_clone_amd.models import resnet
+    from determined_clone_amd.ops import batchnorm as bn_ops
+
+    torch.manual_seed(0)
+    blk = resnet.to_mi355x_layout(resnet.Bottleneck(256, 64, stride=1)).cuda()
+    x = torch.randn(8, 256, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setattr(conv, "FUSE_BN_BWD_STATS", fused)
+        for p in blk.parameters():
+            p.grad = None
+        before = bn_ops.FUSED_BWD_STATS_HITS
+        xi = x.clone().requires_grad_(True)
+        y = blk(xi)
+        y.float().square().mean().backward()
+        assert (bn_ops.FUSED_BWD_STATS_HITS - before) == (1 if fused else 0)
+        outs.append((xi.grad.float(), {n: p.grad.float().clone() for n, p in blk.named_parameters()}))
+    (g1, p1), (g2, p2) = outs
+    torch.testing.assert_close(g1, g2, atol=2e-3, rtol=2e-2)
+    for n in p1:
+        torch.testing.assert_close(p1[n], p2[n], atol=2e-3, rtol=2e-2, msg=n)

@@ -300,6 +300,11 @@ def test_asha_on_deepspeed_trial_example(cluster, capsys):
                         session=s)
     assert rc == 0
     out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    if out["best"] is None:  # show why the profiling trials produced nothing
+        for t in s.get(f"/api/v1/experiments/{out['experiment_id']}/trials")["trials"]:
+            lines = [e["log"] for e in s.get(f"/api/v1/trials/{t['id']}/logs")["logs"]]
+            first = next((i for i, ln in enumerate(lines) if "Traceback" in ln), 0)
+            print(t["id"], t["state"], "\n".join(lines[first:first + 40]))
     assert out["best"] is not None and out["best"]["train_micro_batch_size_per_gpu"] >= 1
     assert len(out["trials"]) == 4  # + the model-profile trial = max_trials
     trials = s.get(f"/api/v1/experiments/{out['experiment_id']}/trials")["trials"]

@@ -417,3 +417,70 @@ def test_layer_norm_and_bias_gelu_direct_grad_accumulation():
     assert _rel(lw1.grad, lw2.grad) < 1e-4
     assert _rel(lb1.grad, lb2.grad) < 1e-4
     assert _rel(gb1.grad, gb2.grad) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("acc_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,D", [(333, 64), (8192, 768), (4096, 2048), (1024, 4096)])
+def test_ln_bwd_dx_column_sums(dtype, acc_dtype, rows, D):
+    """ln_bwd(colsum_acc=...) adds dx.sum(rows) into the target in the same pass (D <= 2048; a
+    separate column reduction past that) and leaves dx / dgamma / dbeta unchanged."""
+    C = _C()
+    torch.manual_seed(0)
+    x = torch.randn(rows, D, device="cuda").to(dtype)
+    dy = torch.randn(rows, D, device="cuda").to(dtype)
+    ds = torch.randn(rows, D, device="cuda").to(dtype)
+    w = torch.rand(D, device="cuda") + 0.5
+    b = torch.randn(D, device="cuda")
+    _, _, mean, rstd = C.ln_fwd(x, None, w, b, 1e-5, False)
+    dx0, dg0, db0 = C.ln_bwd(dy, x, w, mean, rstd, ds, True)
+    acc = torch.randn(D, device="cuda").to(acc_dtype)
+    want = acc.float() + dx0.float().sum(0)
+    dx1, dg1, db1 = C.ln_bwd(dy, x, w, mean, rstd, ds, True, None, None, acc)
+    # same math; the two instantiations may contract multiply-adds differently (an ulp)
+    ulp = 1e-5 if dtype == torch.float32 else 2 ** -7
+    torch.testing.assert_close(dx1, dx0, atol=ulp * 4, rtol=ulp)
+    torch.testing.assert_close(dg1, dg0, atol=1e-4 * math.sqrt(rows), rtol=1e-5)
+    torch.testing.assert_close(db1, db0, atol=1e-4 * math.sqrt(rows), rtol=1e-5)
+    # the kernel sums dx before its bf16 rounding: allow that rounding's random walk
+    tol = 1e-3 * math.sqrt(rows) + (0.05 if acc_dtype == torch.bfloat16 else 0)
+    if dtype == torch.bfloat16:
+        tol += 2 ** -8 * math.sqrt(rows) * dx0.float().abs().max().item()
+    torch.testing.assert_close(acc.float(), want, atol=tol, rtol=1e-2)
+
+
+@pytest.mark.parametrize("extra_consumer", [False, True])
+def test_out_projection_bias_grad_reduced_in_layer_norm_backward(extra_consumer, monkeypatch):
+    """Pre-LN block pattern ``LN(resid + linear(h))``: the linear's bias gradient comes out of the
+    LayerNorm backward (no separate column sum) and equals the unfused path's -- also when the
+    linear output has a second consumer (only that consumer's share is reduced separately)."""
+    _C()
+    torch.manual_seed(0)
+    D, N = 768, 1024
+    h = torch.randn(4, 256, N, device="cuda").bfloat16()
+    resid = torch.randn(4, 256, D, device="cuda").bfloat16()
+    g = torch.randn(4, 256, D, device="cuda").bfloat16()
+    w = torch.randn(D, N, device="cuda").bfloat16() * 0.03
+    bias = torch.randn(D, device="cuda").bfloat16()
+    lw = torch.rand(D, device="cuda") + 0.5
+    lb = torch.randn(D, device="cuda")
+    grads = {}
+    for fused in (True, False):
+        monkeypatch.setattr(T, "FUSE_LN_BIAS_GRAD", fused)
+        ps = [torch.nn.Parameter(t.clone()) for t in (w, bias, lw, lb)]
+        space, _ = _flat(ps)
+        hits = T.LN_BIAS_GRAD_HITS[0]
+        for _ in range(2):
+            out = T.linear(h, ps[0], ps[1])
+            y, s = T.layer_norm(resid, ps[2], ps[3], 1e-5, residual=out)
+            loss = (y.float() * g.float()).sum() + s.float().square().mean()
+            if extra_consumer:
+                loss = loss + (out.float() * 0.5).sum()
+            loss.backward()
+        from determined_clone_amd.ops import _grad
+
+        _grad.join()
+        assert T.LN_BIAS_GRAD_HITS[0] - hits == (2 if fused else 0)
+        grads[fused] = [p.grad.float().clone() for p in ps]
+    for a, b in zip(grads[True], grads[False]):
+        assert _rel(a, b) < 2e-2
