@@ -187,10 +187,10 @@ __device__ __forceinline__ Blk xcd_block(int order) {
 // tail tile, padded keys) come back as zeros from the hardware range check -- no per-chunk
 // branches, and 32-bit lane offsets computed once instead of 64-bit addresses per tile (the
 // host checks that (Sk + ROWS) * row stride stays below 2^31 bytes).
-template <int D, int ROWS = 64, int VPAD = kPad>
+template <int D, int ROWS = 64, int VPAD = kPad, int NT = 256>
 struct KVPrefetch {
   static constexpr int CPR = D / 8;
-  static constexpr int PER = ROWS * CPR / 256;  // 16-B chunks per thread per tensor
+  static constexpr int PER = ROWS * CPR / NT;  // 16-B chunks per thread per tensor
   static constexpr int N = 2 * PER;
   uint4 reg[N];
   uint32_t voff[N];  // byte offset of this lane's chunk j in a tile starting at row 0
@@ -206,7 +206,7 @@ struct KVPrefetch {
                                            static_cast<int>((n_rows - 1) * vstep + 2u * D), 0x00020000);
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      const int cc = threadIdx.x + 256 * (j % PER);
+      const int cc = threadIdx.x + NT * (j % PER);
       const int rr = cc / CPR, d0 = (cc % CPR) * 8;
       voff[j] = static_cast<uint32_t>(rr) * (j < PER ? kstep : vstep) + 2u * d0;
     }
@@ -223,9 +223,94 @@ struct KVPrefetch {
   __device__ __forceinline__ void store(uint16_t* Ks, uint16_t* Vs) const {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      const int cc = threadIdx.x + 256 * (j % PER);
+      const int cc = threadIdx.x + NT * (j % PER);
       const int rr = cc / CPR, d0 = (cc % CPR) * 8;
       *reinterpret_cast<uint4*>(j >= PER ? Vs + rr * (D + VPAD) + d0 : Ks + rr * (D + kPad) + d0) = reg[j];
+    }
+  }
+};
+
+// Direct-to-LDS staging of the K / V (Q / dO) tiles (buffer_load_dwordx4 ... lds, guide §5
+// "glds"): no VGPR round trip, no ds_write, and a 2-stage LDS ring so the next tile streams in
+// during the current tile's MFMAs with ONE barrier per tile. A wave instruction writes 1 KB of LDS
+// (lane l at +16 l), so rows are unpadded and conflict-free reads come from an XOR swizzle of the
+// 16-B chunks instead: the chunk stored at (row, p) is source chunk p ^ f(row), and readers address
+// chunk c of a row at c ^ f(row). One f serves both read patterns of a tile:
+//  * ds_read_b128 row reads (16 lanes = 16 consecutive rows at one chunk) need 16 distinct bank
+//    positions: f(row) must be a permutation over 16 rows (per row parity on 128-B rows);
+//  * ds_read_b64_tr_b16 (32 lanes = 4 consecutive rows x a 4-chunk quad) need the 4 rows' quads
+//    apart: f's bit 2 (D 64: rows 0/2 and 1/3 share a bank line) or bits 2-3 (D 128) must differ.
+// D 64 (128-B rows): f = 4 ((row >> 1) & 1) + ((row >> 2) & 3); D 128 (256-B rows):
+// f = 4 (row & 3) + ((row >> 2) & 3).
+// Issued as inline asm: with the builtin, hipcc treats every later ds_read_b64_tr_b16 as possibly
+// reading the in-flight DMA bytes and puts an s_waitcnt vmcnt(0) in front of the V reads, which
+// serialises the next tile's loads with this tile's MFMAs. hipcc does not count these loads: the
+// loop waits for them itself (vmcnt(0) + barrier). M0 is saved and restored inside the statement.
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff, void* lds_dst) {
+  const uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) void*)(lds_dst)));
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(la), "s"(rsrc)
+      : "memory");
+}
+template <int D>
+__device__ __forceinline__ int swz(int row) {
+  return D == 128 ? 4 * (row & 3) + ((row >> 2) & 3) : 4 * ((row >> 1) & 1) + ((row >> 2) & 3);
+}
+// element offset of 16-B chunk c of `row` in a swizzled tile row
+template <int D>
+__device__ __forceinline__ int swz_off(int row, int c) { return 8 * (c ^ swz<D>(row)); }
+// this lane's ds_read_b64_tr_b16 element offset in column block n of a transposed fragment read
+// whose rows start at a multiple of 16 (the lane reads row 4 hf + tr_row, +8 for the second half)
+template <int D>
+__device__ __forceinline__ int tr_off(int lane, int n, bool plus8) {
+  const int r = lane & 31, hf = lane >> 5, tr_row = (r & 15) >> 2;
+  return swz_off<D>(4 * hf + tr_row + (plus8 ? 8 : 0), 4 * n + 2 * (r >> 4) + ((r & 3) >> 1)) + 4 * (r & 1);
+}
+
+template <int D, int ROWS, int NW = 4>
+struct KVDma {
+  static constexpr int CPR = D / 8;           // 16-B chunks per row
+  static constexpr int RPI = 64 / CPR;        // rows per wave instruction (1 KB)
+  static constexpr int IPW = ROWS / RPI / NW; // instructions per wave per tensor per tile
+  __amdgpu_buffer_rsrc_t kr, vr;
+  uint32_t kstep, vstep;
+  uint32_t ko[IPW], vo[IPW];
+  __device__ __forceinline__ void init(const uint16_t* __restrict__ kb, Strides ks,
+                                       const uint16_t* __restrict__ vb, Strides vs, int n_rows,
+                                       int w, int lane) {
+    kstep = static_cast<uint32_t>(ks.s) * 2u;
+    vstep = static_cast<uint32_t>(vs.s) * 2u;
+    // rows past n_rows read as zeros (buffer range check)
+    kr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(kb), 0,
+                                           static_cast<int>((n_rows - 1) * kstep + 2u * D), 0x00020000);
+    vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(vb), 0,
+                                           static_cast<int>((n_rows - 1) * vstep + 2u * D), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int row = (w * IPW + i) * RPI + lane / CPR, pc = lane % CPR;
+      ko[i] = static_cast<uint32_t>(row) * kstep + 16u * static_cast<uint32_t>(pc ^ swz<D>(row));
+      vo[i] = static_cast<uint32_t>(row) * vstep + 16u * static_cast<uint32_t>(pc ^ swz<D>(row));
+    }
+  }
+  // new tensor bases (same strides): the dK/dV kernel moves on to the next query head
+  __device__ __forceinline__ void set_base(const uint16_t* __restrict__ kb, const uint16_t* __restrict__ vb,
+                                           int n_rows) {
+    kr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(kb), 0,
+                                           static_cast<int>((n_rows - 1) * kstep + 2u * D), 0x00020000);
+    vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(vb), 0,
+                                           static_cast<int>((n_rows - 1) * vstep + 2u * D), 0x00020000);
+  }
+  __device__ __forceinline__ void issue(uint16_t* Kst, uint16_t* Vst, int r0, int w) const {
+    const uint32_t kb0 = static_cast<uint32_t>(r0) * kstep, vb0 = static_cast<uint32_t>(r0) * vstep;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      blds16(kr, ko[i] + kb0, Kst + (w * IPW + i) * 512);
+      blds16(vr, vo[i] + vb0, Vst + (w * IPW + i) * 512);
     }
   }
 };
@@ -242,7 +327,10 @@ struct KVPrefetch {
 // sub-tile: one more O^T-shaped MFMA pair per sub-tile with an all-ones A operand, whose every
 // row is sum_k P^T[k][q] (the same bf16 P the O product uses), rescaled with O by the deferred max.
 // The MFMA pipe runs at ~30% here while VALU issue and its dependency chains bound the loop.
-template <int D, bool CAUSAL, int KT, bool PIPE, bool MSUM = false>
+// ABL (timing-only ablations, wrong outputs; DCA_ATTN_ABL, never a default): bit 0 skips the
+// scale/max FMA before each exp, bit 1 the row-sum adds, bit 2 the exps, bit 3 the row max, bit 4
+// the K/V tile HBM loads after the first, bit 5 the LDS tile stores and their barriers.
+template <int D, bool CAUSAL, int KT, bool PIPE, bool MSUM = false, int ABL = 0, bool DMA = false>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
@@ -288,14 +376,46 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   // tr-read lane address pieces (see T10: lane 4q+p of a 16-lane group -> row q, cols 4p..4p+3)
   const int tr_row = (r & 15) >> 2;
   const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
+  // LDS fragment addresses: padded rows (register-staged tiles) or the swizzled unpadded rows of
+  // the DMA ring (KVDma); kx / vx: this lane's element offsets inside a row
+  constexpr int KRS = DMA ? D : RS, VRS = DMA ? D : RSV;
+  int kx[D / 16], vx[D / 32], vx8[D / 32];
+#pragma unroll
+  for (int s2 = 0; s2 < D / 16; ++s2) kx[s2] = DMA ? swz_off<D>(r, 2 * s2 + hf) : 16 * s2 + 8 * hf;
+#pragma unroll
+  for (int n = 0; n < D / 32; ++n) {
+    vx[n] = DMA ? tr_off<D>(lane, n, false) : 32 * n + tr_col;
+    vx8[n] = DMA ? tr_off<D>(lane, n, true) : 32 * n + tr_col;
+  }
   KVPrefetch<D, KT, VPAD> pf;
-  pf.init(kb, ks, vb, vs, Sk);
-  pf.fetch(0);
+  KVDma<D, KT> dma;
+  if constexpr (DMA) {
+    dma.init(kb, ks, vb, vs, Sk, w, lane);
+    dma.issue(smem, smem + KT * D, 0, w);
+  } else {
+    pf.init(kb, ks, vb, vs, Sk);
+    pf.fetch(0);
+  }
+  int stage = 0;
   for (int kt = 0; kt < k_end; kt += KT) {
-    __syncthreads();
-    pf.store(Ks, Vs);
-    __syncthreads();
-    if (kt + KT < k_end) pf.fetch(kt + KT);
+    if constexpr (DMA) {
+      // this tile's loads (issued one tile ago) landed for this wave; the barrier publishes every
+      // wave's part and retires the previous tile's reads of the other stage
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      Ks = smem + stage * 2 * KT * D;
+      Vs = Ks + KT * D;
+      if (kt + KT < k_end) dma.issue(smem + (stage ^ 1) * 2 * KT * D, smem + (stage ^ 1) * 2 * KT * D + KT * D, kt + KT, w);
+      stage ^= 1;
+    } else {
+      if constexpr ((ABL & 32) == 0) {
+        __syncthreads();
+        pf.store(Ks, Vs);
+        __syncthreads();
+      }
+      if ((ABL & 16) == 0 && kt + KT < k_end) pf.fetch(kt + KT);
+    }
     if constexpr (PIPE) {
       // online softmax of one sub-tile's scores and O^T += V^T P^T
       auto softmax_pv = [&](f32x16 sc, const int sub, const int kb0, const bool need_mask) {
@@ -310,9 +430,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
           }
         }
         float mx = -INFINITY;
+        if constexpr ((ABL & 8) != 0) {
+          mx = sc[0];
+        } else {
   #pragma unroll
-        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[i]);
-        mx = half_max(mx);
+          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[i]);
+          mx = half_max(mx);
+        }
         // deferred max (T13): the running max m moves only when a score exceeds it by more than
         // kRescaleLog2 (p <= 2^kRescaleLog2 meanwhile: exact in the fp32 accumulators, 8 bits of
         // headroom in the bf16 P), so the D/2-multiply rescale of O and l runs on a few sub-tiles
@@ -326,9 +450,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         float rs = 0.f;
   #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = fast_exp2(fmaf(sc[i], scale_log2, -mref));
+          const float t = (ABL & 1) ? sc[i] : fmaf(sc[i], scale_log2, -mref);
+          const float p = (ABL & 4) ? t : fast_exp2(t);
           sc[i] = p;
-          if constexpr (!MSUM) rs += p;
+          if constexpr (!MSUM && (ABL & 2) == 0) rs += p;
         }
         if constexpr (!MSUM) {
           rs = half_sum(rs);
@@ -349,8 +474,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         for (int n = 0; n < D / 32; ++n) {
   #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
-            const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RSV + 32 * n + tr_col;
-            oacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RSV)), s2 ? p1 : p0, oacc[n]);
+            const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * VRS;
+            oacc[n] = mfma32(cat8(tr_read(base + vx[n]), tr_read(base + 8 * VRS + vx8[n])), s2 ? p1 : p0, oacc[n]);
           }
         }
       };
@@ -365,8 +490,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
           bf16x8 ka[D / 16], kb2[D / 16];
   #pragma unroll
           for (int s = 0; s < D / 16; ++s) {
-            ka[s] = load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf);
-            kb2[s] = load8(Ks + (32 * sub + 32 + r) * RS + 16 * s + 8 * hf);
+            ka[s] = load8(Ks + (32 * sub + r) * KRS + kx[s]);
+            kb2[s] = load8(Ks + (32 * sub + 32 + r) * KRS + kx[s]);
           }
           f32x16 sa = zero16(), sb = zero16();
   #pragma unroll
@@ -391,7 +516,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       // every K fragment read issued before the first MFMA: one LDS wait instead of one per MFMA
       bf16x8 kf[D / 16];
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) kf[s] = load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf);
+      for (int s = 0; s < D / 16; ++s) kf[s] = load8(Ks + (32 * sub + r) * KRS + kx[s]);
       f32x16 sc = zero16();
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) sc = mfma32(kf[s], qf[s], sc);
@@ -450,8 +575,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       for (int n = 0; n < D / 32; ++n) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RSV + 32 * n + tr_col;
-          oacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RSV)), s2 ? p1 : p0, oacc[n]);
+          const uint16_t* base = Vs + (32 * sub + 16 * s2 + 4 * hf + tr_row) * VRS;
+          oacc[n] = mfma32(cat8(tr_read(base + vx[n]), tr_read(base + 8 * VRS + vx8[n])), s2 ? p1 : p0, oacc[n]);
         }
       }
     }
@@ -476,6 +601,176 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   }
 }
 
+// ------------------------------------------------------------------ forward, 64 query rows per wave
+// NW waves x 64 queries = 64 NW query rows per workgroup. Each wave runs TWO 32-query groups over
+// the same key sub-tile: the K fragments (ds_read_b128) and V^T fragments (ds_read_b64_tr_b16) are
+// read from LDS once and feed both groups' MFMAs (half the LDS reads per FLOP of attn_fwd_kernel),
+// and the two groups' softmax chains are independent, so inside ONE wave group 0's softmax (VALU)
+// issues under group 1's score MFMAs and group 1's softmax under group 0's P.V MFMAs -- the
+// MFMA / softmax ping-pong without relying on a co-resident wave. D = 128 needs ~490 VGPRs: one wave
+// per SIMD (NW = 4, one workgroup per CU). Same math, masks, deferred max and outputs as
+// attn_fwd_kernel (DCA_ATTN_FWD_W64=1 selects it). Measured 10-24 % SLOWER than attn_fwd_kernel
+// (2 / 1 waves per SIMD instead of 3-4 hide less latency; profiles/round5_attention_pmc_baseline.txt):
+// kept opt-in as the measured negative of the one-wave-per-SIMD structure.
+template <int D, bool CAUSAL, int NW>
+__global__ __launch_bounds__(NW * 64, (D == 128 ? 1 : 2)) void attn_fwd_w64_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
+    uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
+    Strides ks, Strides vs, Strides os, float scale_log2, int order, const int* __restrict__ kvlen, int G) {
+  constexpr int KT = 64;
+  constexpr int QB = 64 * NW;
+  constexpr int NT = 64 * NW;
+  constexpr int RS = D + kPad;
+  constexpr int VPAD = D == 128 ? kTrPad : kPad;
+  constexpr int RSV = D + VPAD;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Ks = smem;
+  uint16_t* Vs = Ks + KT * RS;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const Blk blk = xcd_block(order);
+  const int b = blk.z, h = blk.y;
+  if (kvlen) Sk = min(Sk, max(kvlen[b], 1));
+  const int q_blk = (CAUSAL ? (gridDim.x - 1 - blk.x) : blk.x) * QB;
+  const int q0 = q_blk + w * 64;  // group g: queries q0 + 32 g + r
+  const uint16_t* qb = q + b * qs.b + h * qs.h;
+  const uint16_t* kb = k + b * ks.b + (h / G) * ks.h;
+  const uint16_t* vb = v + b * vs.b + (h / G) * vs.h;
+
+  bf16x8 qf[2][D / 16];
+  f32x16 oacc[2][D / 32];
+  float m[2], l[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int my_q = q0 + 32 * g + r;
+#pragma unroll
+    for (int s2 = 0; s2 < D / 16; ++s2)
+      qf[g][s2] = my_q < Sq ? load8(qb + static_cast<int64_t>(my_q) * qs.s + 16 * s2 + 8 * hf) : zero8();
+#pragma unroll
+    for (int n = 0; n < D / 32; ++n) oacc[g][n] = zero16();
+    m[g] = -INFINITY;
+    l[g] = 0.f;
+  }
+  const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
+  const int tr_row = (r & 15) >> 2;
+  const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
+
+  // online softmax of one group's 32-key sub-tile scores -> P fragments (and O rescale)
+  auto softmax = [&](f32x16& sc, const int g, const int kb0, const bool need_mask, bf16x8& p0, bf16x8& p1) {
+    const int my_q = q0 + 32 * g + r;
+    if (need_mask) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+        sc[i] = (key >= Sk || (CAUSAL && key > my_q)) ? -INFINITY : sc[i];
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[i]);
+    mx = half_max(mx);
+    const float mcand = mx * scale_log2;
+    const bool upd = mcand > m[g] + kRescaleLog2;
+    const float mnew = upd ? mcand : m[g];
+    const float mref = mnew == -INFINITY ? 0.f : mnew;
+    const float alpha = upd ? fast_exp2(m[g] - mref) : 1.f;
+    float rs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = fast_exp2(fmaf(sc[i], scale_log2, -mref));
+      sc[i] = p;
+      rs += p;
+    }
+    rs = half_sum(rs);
+    l[g] = l[g] * alpha + rs;
+    m[g] = mnew;
+    if (__any(upd)) {
+#pragma unroll
+      for (int n = 0; n < D / 32; ++n) rescale16(oacc[g][n], alpha);
+    }
+    p0 = pack8(sc, 0);
+    p1 = pack8(sc, 8);
+  };
+
+  KVPrefetch<D, KT, VPAD, NT> pf;
+  pf.init(kb, ks, vb, vs, Sk);
+  pf.fetch(0);
+  for (int kt = 0; kt < k_end; kt += KT) {
+    __syncthreads();
+    pf.store(Ks, Vs);
+    __syncthreads();
+    if (kt + KT < k_end) pf.fetch(kt + KT);
+#pragma unroll
+    for (int sub = 0; sub < KT / 32; ++sub) {
+      const int kb0 = kt + 32 * sub;
+      if (kb0 >= k_end) break;
+      if (CAUSAL && kb0 > q0 + 63) break;  // wave-uniform: both groups fully masked from here
+      // group g needs any work (causal): its last query reaches this sub-tile
+      const bool live1 = !CAUSAL || kb0 <= q0 + 63;
+      const bool live0 = !CAUSAL || kb0 <= q0 + 31;
+      bf16x8 kf[D / 16];
+#pragma unroll
+      for (int s2 = 0; s2 < D / 16; ++s2) kf[s2] = load8(Ks + (32 * sub + r) * RS + 16 * s2 + 8 * hf);
+      // group 0's score chain first, then group 1's: group 0's softmax below issues while group
+      // 1's MFMAs are still in the matrix pipe
+      f32x16 s0 = zero16(), s1 = zero16();
+      if (live0) {
+#pragma unroll
+        for (int s2 = 0; s2 < D / 16; ++s2) s0 = mfma32(kf[s2], qf[0][s2], s0);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < D / 16; ++s2) s1 = mfma32(kf[s2], qf[1][s2], s1);
+      (void)live1;
+      const bool mask0 = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0);
+      const bool mask1 = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0 + 32);
+      bf16x8 a0, a1, c0, c1;
+      // V^T fragments of this sub-tile, shared by both groups
+      bf16x8 vf[D / 32][2];
+#pragma unroll
+      for (int n = 0; n < D / 32; ++n)
+#pragma unroll
+        for (int s3 = 0; s3 < 2; ++s3) {
+          const uint16_t* base = Vs + (32 * sub + 16 * s3 + 4 * hf + tr_row) * RSV + 32 * n + tr_col;
+          vf[n][s3] = cat8(tr_read(base), tr_read(base + 8 * RSV));
+        }
+      if (live0) {
+        softmax(s0, 0, kb0, mask0, a0, a1);  // VALU under group 1's score MFMAs
+#pragma unroll
+        for (int n = 0; n < D / 32; ++n) {
+          oacc[0][n] = mfma32(vf[n][0], a0, oacc[0][n]);
+          oacc[0][n] = mfma32(vf[n][1], a1, oacc[0][n]);
+        }
+      }
+      softmax(s1, 1, kb0, mask1, c0, c1);  // VALU under group 0's P.V MFMAs
+#pragma unroll
+      for (int n = 0; n < D / 32; ++n) {
+        oacc[1][n] = mfma32(vf[n][0], c0, oacc[1][n]);
+        oacc[1][n] = mfma32(vf[n][1], c1, oacc[1][n]);
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int my_q = q0 + 32 * g + r;
+    if (my_q < Sq) {
+      const float inv = l[g] > 0.f ? 1.f / l[g] : 0.f;
+      uint16_t* orow = o + b * os.b + h * os.h + static_cast<int64_t>(my_q) * os.s;
+#pragma unroll
+      for (int n = 0; n < D / 32; ++n)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          uint2 pk;
+          pk.x = pack_bf16x2(oacc[g][n][4 * gg] * inv, oacc[g][n][4 * gg + 1] * inv);
+          pk.y = pack_bf16x2(oacc[g][n][4 * gg + 2] * inv, oacc[g][n][4 * gg + 3] * inv);
+          *reinterpret_cast<uint2*>(orow + 32 * n + 8 * gg + 4 * hf) = pk;
+        }
+      if (hf == 0)
+        lse[(static_cast<int64_t>(b) * H + h) * Sq + my_q] = l[g] > 0.f ? m[g] + log2f(l[g]) : INFINITY;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------ backward
 // Two kernels, no atomics (FlashAttention-2 style split, MI355X layouts):
 //  * attn_bwd_dq_kernel: one workgroup = 128 queries (4 waves x 32). Computes delta = rowsum(dO*O)
@@ -487,7 +782,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
 //    next tile's HBM loads overlap the current tile's MFMAs). S and dP have the key on the lane, so
 //    P and dS are directly the B operands of dV^T += dO^T P and dK^T += Q^T dS (A operands by
 //    transposed LDS reads of the row-major Q / dO tiles).
-template <int D, bool CAUSAL, int KT, bool PIPE>
+template <int D, bool CAUSAL, int KT, bool PIPE, bool DMA = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     const uint16_t* __restrict__ o, const uint16_t* __restrict__ dO, const float* __restrict__ lse,
@@ -539,14 +834,42 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
   const int tr_row = (r & 15) >> 2;
   const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
   const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
+  // LDS fragment addresses (see attn_fwd_kernel): padded rows or the swizzled DMA ring
+  constexpr int KRS = DMA ? D : RS;
+  int kx[D / 16], tx[D / 32], tx8[D / 32];
+#pragma unroll
+  for (int s2 = 0; s2 < D / 16; ++s2) kx[s2] = DMA ? swz_off<D>(r, 2 * s2 + hf) : 16 * s2 + 8 * hf;
+#pragma unroll
+  for (int n = 0; n < D / 32; ++n) {
+    tx[n] = DMA ? tr_off<D>(lane, n, false) : 32 * n + tr_col;
+    tx8[n] = DMA ? tr_off<D>(lane, n, true) : 32 * n + tr_col;
+  }
   KVPrefetch<D, KT> pf;
-  pf.init(kb, ks, vb, vs, Sk);
-  pf.fetch(0);
+  KVDma<D, KT> dma;
+  if constexpr (DMA) {
+    dma.init(kb, ks, vb, vs, Sk, w, lane);
+    dma.issue(smem, smem + KT * D, 0, w);
+  } else {
+    pf.init(kb, ks, vb, vs, Sk);
+    pf.fetch(0);
+  }
+  int stage = 0;
   for (int kt = 0; kt < k_end; kt += KT) {
-    __syncthreads();
-    pf.store(Ks, Vs);
-    __syncthreads();
-    if (kt + KT < k_end) pf.fetch(kt + KT);
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of tile kt landed
+      __builtin_amdgcn_s_barrier();                       // everyone's; the other stage is free
+      asm volatile("" ::: "memory");
+      Ks = smem + stage * 2 * KT * D;
+      Vs = Ks + KT * D;
+      if (kt + KT < k_end)
+        dma.issue(smem + (stage ^ 1) * 2 * KT * D, smem + (stage ^ 1) * 2 * KT * D + KT * D, kt + KT, w);
+      stage ^= 1;
+    } else {
+      __syncthreads();
+      pf.store(Ks, Vs);
+      __syncthreads();
+      if (kt + KT < k_end) pf.fetch(kt + KT);
+    }
     // S^T = K Q^T and dP^T = V dO^T for the 32-key sub-tile `sub` of the staged tile
     auto sdp = [&](const int sub, f32x16& sc, f32x16& dp) {
       sc = zero16();
@@ -555,8 +878,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
         bf16x8 kfr[D / 16], vfr[D / 16];
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          kfr[s] = load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf);
-          vfr[s] = load8(Vs + (32 * sub + r) * RS + 16 * s + 8 * hf);
+          kfr[s] = load8(Ks + (32 * sub + r) * KRS + kx[s]);
+          vfr[s] = load8(Vs + (32 * sub + r) * KRS + kx[s]);
         }
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
@@ -566,8 +889,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
       } else {
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          sc = mfma32(load8(Ks + (32 * sub + r) * RS + 16 * s + 8 * hf), qf[s], sc);
-          dp = mfma32(load8(Vs + (32 * sub + r) * RS + 16 * s + 8 * hf), dof[s], dp);
+          sc = mfma32(load8(Ks + (32 * sub + r) * KRS + kx[s]), qf[s], sc);
+          dp = mfma32(load8(Vs + (32 * sub + r) * KRS + kx[s]), dof[s], dp);
         }
       }
     };
@@ -587,8 +910,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
       for (int n = 0; n < D / 32; ++n)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const uint16_t* base = Ks + (32 * sub + 16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
-          dqacc[n] = mfma32(cat8(tr_read(base), tr_read(base + 8 * RS)), s2 ? s1 : s0, dqacc[n]);
+          const uint16_t* base = Ks + (32 * sub + 16 * s2 + 4 * hf + tr_row) * KRS;
+          dqacc[n] = mfma32(cat8(tr_read(base + tx[n]), tr_read(base + 8 * KRS + tx8[n])), s2 ? s1 : s0, dqacc[n]);
         }
     };
     auto sub_tile = [&](auto masked, const int sub, const int kb0) {
@@ -824,6 +1147,243 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
   store_rows<D>(dv + b * dvs.b + h * dvs.h + static_cast<int64_t>(my_key) * dvs.s, dvacc, 1.f, hf, my_key < SkT);
 }
 
+// The dK/dV kernel with the Q / dO tiles (and the LSE / delta rows) through the 2-stage
+// direct-to-LDS ring (KVDma): one flat (query head, query tile) sequence, one barrier per tile.
+template <int D, bool CAUSAL, int QT, bool DMA = true>
+__global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_dma_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
+    const uint16_t* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
+    uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int Sq, int Sk, int H, Strides qs,
+    Strides ks, Strides vs, Strides dos, Strides dks, Strides dvs, float scale_log2, float scale,
+    int order, const int* __restrict__ kvlen, int G) {
+  constexpr int KB = 128;
+  static_assert(QT == 32 || QT == 64, "query tile");
+  constexpr int RS = D + kPad;
+  constexpr int CPR = D / 8;                 // 16-byte chunks per row
+  constexpr int NPF = 2 * QT * CPR / 256;    // prefetched chunks per thread (Q and dO tiles)
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  // register-staged: [QT][RS] Q | [QT][RS] dO | lse[QT] | delta[QT]; DMA: two such stages of
+  // [QT][D] swizzled rows (see KVDma) -- QRS is the row stride either way
+  constexpr int QRS = DMA ? D : RS;
+  constexpr int STG = 2 * QT * QRS + 4 * QT;  // stage size in uint16 elements
+  uint16_t* Qs = smem;
+  uint16_t* dOs = Qs + QT * QRS;
+  float* lse_s = reinterpret_cast<float*>(dOs + QT * QRS);
+  float* del_s = lse_s + QT;
+  const int lane = threadIdx.x & 63;
+  // wave index in an SGPR: every per-wave condition below (causal extents, masking) is a
+  // uniform branch instead of per-lane exec masking
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const Blk blk = xcd_block(order);
+  const int b = blk.z, h = blk.y;
+  const int SkT = Sk;  // rows of dK/dV to write (padded keys get zeros)
+  // key padding: keys at or past kvlen[b] are masked like keys past Sk (>= 1 key kept)
+  if (kvlen) Sk = min(Sk, max(kvlen[b], 1));
+  const int k_blk = blk.x * KB;
+  const int kw0 = k_blk + 32 * w;
+  const int my_key = kw0 + r;
+  // h is the K/V head (grid y runs over H / G of them); its G query heads h*G .. h*G+G-1 are swept
+  // one after another below, dK / dV summing over all of them in the same registers
+  const uint16_t* qb = q;
+  const uint16_t* dob = dO;
+  int64_t bh = 0;
+
+  bf16x8 kf[D / 16], vf[D / 16];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    const bool ok = my_key < Sk;
+    kf[s] = ok ? load8(k + b * ks.b + h * ks.h + static_cast<int64_t>(my_key) * ks.s + 16 * s + 8 * hf) : zero8();
+    vf[s] = ok ? load8(v + b * vs.b + h * vs.h + static_cast<int64_t>(my_key) * vs.s + 16 * s + 8 * hf) : zero8();
+  }
+  f32x16 dkacc[D / 32], dvacc[D / 32];
+#pragma unroll
+  for (int n = 0; n < D / 32; ++n) {
+    dkacc[n] = zero16();
+    dvacc[n] = zero16();
+  }
+  // register double buffer for the next query tile
+  uint4 pf[NPF];
+  float pl = 0.f, pd = 0.f;
+  constexpr bool ROWC = D == 128;
+  const float inv_sl2 = 1.f / scale_log2;
+  // Q / dO tiles through buffer descriptors ending after row Sq - 1: rows past it load as zeros
+  // (hardware range check; see KVPrefetch), 32-bit lane offsets computed once
+  constexpr int PER = NPF / 2;  // chunks per thread per tensor (j < PER: Q, else dO)
+  const uint32_t qstep = static_cast<uint32_t>(qs.s) * 2u, dstep = static_cast<uint32_t>(dos.s) * 2u;
+  __amdgpu_buffer_rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(qb), 0, static_cast<int>((Sq - 1) * qstep + 2u * D), 0x00020000);
+  __amdgpu_buffer_rsrc_t dr = qr;
+  auto set_head = [&](int hq) {
+    qb = q + b * qs.b + hq * qs.h;
+    dob = dO + b * dos.b + hq * dos.h;
+    bh = static_cast<int64_t>(b) * H + hq;
+    qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(qb), 0,
+                                           static_cast<int>((Sq - 1) * qstep + 2u * D), 0x00020000);
+    dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(dob), 0,
+                                           static_cast<int>((Sq - 1) * dstep + 2u * D), 0x00020000);
+  };
+  uint32_t pvo[NPF];
+#pragma unroll
+  for (int j = 0; j < NPF; ++j) {
+    const int cc = threadIdx.x + 256 * (j % PER);
+    pvo[j] = static_cast<uint32_t>(cc / CPR) * (j < PER ? qstep : dstep) + 2u * ((cc % CPR) * 8);
+  }
+  auto fetch = [&](int qt) {
+    const uint32_t qo = static_cast<uint32_t>(qt) * qstep, dof = static_cast<uint32_t>(qt) * dstep;
+#pragma unroll
+    for (int j = 0; j < NPF; ++j)
+      pf[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            j < PER ? qr : dr, pvo[j] + (j < PER ? qo : dof), 0, 0));
+    if (threadIdx.x < QT) {
+      const int qi = qt + threadIdx.x;
+      if constexpr (ROWC) {
+        // staged as the accumulators' initial values (see the tile below): -LSE/scale_log2, -delta
+        pl = qi < Sq ? -lse[bh * Sq + qi] * inv_sl2 : -INFINITY;
+        pd = qi < Sq ? -delta[bh * Sq + qi] : 0.f;
+      } else {
+        pl = qi < Sq ? lse[bh * Sq + qi] : INFINITY;
+        pd = qi < Sq ? delta[bh * Sq + qi] : 0.f;
+      }
+    }
+  };
+  const int tr_row = (r & 15) >> 2;
+  const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
+  const int q_start = CAUSAL ? (k_blk / QT) * QT : 0;
+  // the MFMA work on the staged query tile qt (Qs / dOs / lse_s / del_s)
+  auto process = [&](const int qt) {
+    // one 32-query MFMA sub-tile at LDS row offset 32*half (queries qs0 .. qs0+31)
+    auto tile = [&](auto masked, const int half) {
+      const int qs0 = qt + 32 * half;
+      const uint16_t* Qh = Qs + 32 * half * QRS;
+      const uint16_t* dOh = dOs + 32 * half * QRS;
+      // ROWC (D = 128): row constants as the initial accumulators (guide: attention backward):
+      // S' = Q K^T - LSE/scale_log2 and dP' = dO V^T - delta come out of the MFMA chains, so
+      // p = exp2(S' * scale_log2) and dS = p * dP' need no per-element subtraction and no
+      // registers for the constants (D = 128: +6%; D = 64: neutral, so off there --
+      // profiles/round3_attention_bwd_ab.txt). This lane's 16 queries are 4 runs of 4 consecutive
+      // rows: 16-B LDS reads straight into the accumulator registers.
+      auto rows16 = [&](const float* base) {
+        const f32x4* b4 = reinterpret_cast<const f32x4*>(base + 32 * half + 4 * hf);
+        const f32x4 a0 = b4[0], a1 = b4[2], a2 = b4[4], a3 = b4[6];  // rows +0, +8, +16, +24
+        return __builtin_shufflevector(__builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7),
+                                       __builtin_shufflevector(a2, a3, 0, 1, 2, 3, 4, 5, 6, 7),
+                                       0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+      };
+      f32x16 sacc = ROWC ? rows16(lse_s) : zero16(), dpacc = ROWC ? rows16(del_s) : zero16();
+      f32x16 lrow, drow;  // !ROWC: the same constants, subtracted per element below
+      if constexpr (!ROWC) {
+        lrow = rows16(lse_s);
+        drow = rows16(del_s);
+      }
+      if constexpr (D == 64) {  // fragments preloaded (see the forward)
+        bf16x8 qfr[D / 16], dofr[D / 16];
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          qfr[s] = load8(Qh + r * QRS + swz_off<D>(r, 2 * s + hf));
+          dofr[s] = load8(dOh + r * QRS + swz_off<D>(r, 2 * s + hf));
+        }
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          sacc = mfma32(qfr[s], kf[s], sacc);
+          dpacc = mfma32(dofr[s], vf[s], dpacc);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          sacc = mfma32(load8(Qh + r * QRS + swz_off<D>(r, 2 * s + hf)), kf[s], sacc);
+          dpacc = mfma32(load8(dOh + r * QRS + swz_off<D>(r, 2 * s + hf)), vf[s], dpacc);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = ROWC ? fast_exp2(sacc[i] * scale_log2) : fast_exp2(fmaf(sacc[i], scale_log2, -lrow[i]));
+        if constexpr (decltype(masked)::value) {
+          const int qi = qs0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          p = (qi >= Sq || my_key >= Sk || (CAUSAL && my_key > qi)) ? 0.f : p;
+        }
+        sacc[i] = p;
+        dpacc[i] = ROWC ? p * dpacc[i] : p * (dpacc[i] - drow[i]);  // scale applied once to dK at the end
+      }
+      const bf16x8 p0 = pack8(sacc, 0), p1 = pack8(sacc, 8);
+      const bf16x8 s0 = pack8(dpacc, 0), s1 = pack8(dpacc, 8);
+#pragma unroll
+      for (int n = 0; n < D / 32; ++n) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int off = (16 * s2 + 4 * hf + tr_row) * QRS + tr_off<D>(lane, n, false);
+          const int off8 = (16 * s2 + 4 * hf + tr_row + 8) * QRS + tr_off<D>(lane, n, true);
+          dvacc[n] = mfma32(cat8(tr_read(dOh + off), tr_read(dOh + off8)), s2 ? p1 : p0, dvacc[n]);
+          dkacc[n] = mfma32(cat8(tr_read(Qh + off), tr_read(Qh + off8)), s2 ? s1 : s0, dkacc[n]);
+        }
+      }
+    };
+#pragma unroll
+    for (int half = 0; half < QT / 32; ++half) {
+      const int qs0 = qt + 32 * half;
+      // wave-uniform: causal (keys after every query of the sub-tile), past Sq / Sk
+      if (qs0 >= Sq || (CAUSAL && kw0 > qs0 + 31) || kw0 >= Sk) continue;
+      // a key block straddling Sk only exists in the last workgroup
+      if (D == 128 || (qs0 + 32 > Sq) || (kw0 + 32 > Sk) || (CAUSAL && kw0 + 31 > qs0))
+        tile(std::true_type{}, half);
+      else
+        tile(std::false_type{}, half);
+    }
+  };
+  if constexpr (DMA) {
+    // one flat sequence of (query head, query tile) through the 2-stage ring
+    const int tph = q_start < Sq ? (Sq - q_start + QT - 1) / QT : 0;  // tiles per query head
+    const int ntiles = G * tph;
+    KVDma<D, QT> dma;
+    auto rows_of = [&](int hq, int qt) {  // this tile's -LSE/scale_log2, -delta (ROWC) or LSE, delta
+      if (threadIdx.x < QT) {
+        const int qi = qt + threadIdx.x;
+        const int64_t bq = static_cast<int64_t>(b) * H + hq;
+        if constexpr (ROWC) {
+          pl = qi < Sq ? -lse[bq * Sq + qi] * inv_sl2 : -INFINITY;
+          pd = qi < Sq ? -delta[bq * Sq + qi] : 0.f;
+        } else {
+          pl = qi < Sq ? lse[bq * Sq + qi] : INFINITY;
+          pd = qi < Sq ? delta[bq * Sq + qi] : 0.f;
+        }
+      }
+    };
+    if (ntiles > 0) {
+      dma.init(q + b * qs.b + (h * G) * qs.h, qs, dO + b * dos.b + (h * G) * dos.h, dos, Sq, w, lane);
+      dma.issue(smem, smem + QT * D, q_start, w);
+      rows_of(h * G, q_start);
+    }
+    int stage = 0, cur_g = 0;
+    for (int t = 0; t < ntiles; ++t) {
+      const int qt = q_start + (t % tph) * QT;
+      Qs = smem + stage * STG;
+      dOs = Qs + QT * D;
+      lse_s = reinterpret_cast<float*>(dOs + QT * D);
+      del_s = lse_s + QT;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of the tile landed
+      if (threadIdx.x < QT) {
+        lse_s[threadIdx.x] = pl;
+        del_s[threadIdx.x] = pd;
+      }
+      __syncthreads();  // everyone's tile + row constants; the other stage is free
+      if (t + 1 < ntiles) {
+        const int g1 = (t + 1) / tph, qt1 = q_start + ((t + 1) % tph) * QT;
+        if (g1 != cur_g) {
+          cur_g = g1;
+          dma.set_base(q + b * qs.b + (h * G + g1) * qs.h, dO + b * dos.b + (h * G + g1) * dos.h, Sq);
+        }
+        uint16_t* nq = smem + (stage ^ 1) * STG;
+        dma.issue(nq, nq + QT * D, qt1, w);
+        rows_of(h * G + g1, qt1);
+      }
+      process(qt);
+      stage ^= 1;
+    }
+  }
+  store_rows<D>(dk + b * dks.b + h * dks.h + static_cast<int64_t>(my_key) * dks.s, dkacc, scale, hf, my_key < SkT);
+  store_rows<D>(dv + b * dvs.b + h * dvs.h + static_cast<int64_t>(my_key) * dvs.s, dvacc, 1.f, hf, my_key < SkT);
+}
+
 size_t fwd_lds(int D, int KT = 64) {  // K tile + V tile (see attn_fwd_kernel's VPAD)
   return static_cast<size_t>(KT) * ((D + kPad) + (D + (D == 128 ? kTrPad : kPad))) * 2;
 }
@@ -911,11 +1471,72 @@ int dkdv_qt() {
   return qt;
 }
 
+// timing-only forward ablation bits (attn_fwd_kernel ABL): DCA_ATTN_ABL
+int fwd_ablation() {
+  static const int a = [] {
+    const char* e = std::getenv("DCA_ATTN_ABL");
+    return e ? std::atoi(e) : 0;
+  }();
+  return a;
+}
+
+// forward K / V tiles through the direct-to-LDS ring (KVDma): +1.5-8 % causal, +3-5 % full over the
+// register-staged tiles (profiles/round5_attention_dma_ring_ab.txt); DCA_ATTN_FWD_DMA=0 restores them
+bool fwd_dma() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCA_ATTN_FWD_DMA");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
+// backward tiles through the direct-to-LDS ring at D = 128 (dQ: K / V, dK/dV: Q / dO; bwd +2 %,
+// profiles/round5_attention_dma_ring_ab.txt): DCA_ATTN_BWD_DMA=0 disables. At D = 64 the dK/dV
+// kernel sits at 246 of its 256 registers and the swizzled offsets spill it (-50 %), and the dQ
+// kernel alone measured -1.5 % on the backward: both keep register staging unless
+// DCA_ATTN_BWD_DMA64=1 (dQ only)
+bool bwd_dma64() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCA_ATTN_BWD_DMA64");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+bool bwd_dma() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCA_ATTN_BWD_DMA");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
+// forward with 64 query rows per wave (attn_fwd_w64_kernel): DCA_ATTN_FWD_W64=1
+bool fwd_w64() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCA_ATTN_FWD_W64");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
 template <int D, bool C>
 void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse,
                 int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs, Strides os,
                 float scale_log2, const int* kvlen, int G, hipStream_t st) {
   dim3 grid((Sq + 127) / 128, H, B);
+  if (fwd_w64()) {
+    // D = 64: 2 waves x 64 queries = the same 128-query blocks; D = 128: 4 waves (256-query
+    // blocks) so the K/V staging registers per thread halve (one wave per SIMD either way)
+    constexpr int NW = D == 128 ? 4 : 2;
+    grid.x = (Sq + 64 * NW - 1) / (64 * NW);
+    auto kern = attn_fwd_w64_kernel<D, C, NW>;
+    const size_t lds = fwd_lds(D, 64);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
+                       scale_log2, attn_order(C), kvlen, G);
+    return;
+  }
   auto go = [&](auto ktag) {
     constexpr int KT = decltype(ktag)::value;
     const size_t lds = fwd_lds(D, KT);
@@ -926,8 +1547,36 @@ void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_
                          scale_log2, attn_order(C), kvlen, G);
     };
     const bool ms = fwd_msum();
+    if constexpr (KT == 64) {
+      if (fwd_dma() && !ms && fwd_ablation() == 0) {
+        // K / V tiles through the 2-stage direct-to-LDS ring (KVDma)
+        const size_t lds2 = 2 * 2 * static_cast<size_t>(KT) * D * 2;
+        auto launch2 = [&](auto kern) {
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds2));
+          hipLaunchKernelGGL(kern, grid, dim3(256), lds2, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
+                             scale_log2, attn_order(C), kvlen, G);
+        };
+        if (fwd_pipe() && (D == 64 || fwd_pipe128())) launch2(attn_fwd_kernel<D, C, KT, true, false, 0, true>);
+        else launch2(attn_fwd_kernel<D, C, KT, false, false, 0, true>);
+        return;
+      }
+    }
     // D = 128: the pipelined form fits without spills only without MSUM (246 VGPRs)
     if (fwd_pipe() && (D == 64 || (!ms && fwd_pipe128()))) {
+      if constexpr (C && KT == 64) {
+        switch (fwd_ablation()) {
+          case 1: launch(attn_fwd_kernel<D, C, KT, true, false, 1>); return;
+          case 2: launch(attn_fwd_kernel<D, C, KT, true, false, 2>); return;
+          case 4: launch(attn_fwd_kernel<D, C, KT, true, false, 4>); return;
+          case 8: launch(attn_fwd_kernel<D, C, KT, true, false, 8>); return;
+          case 15: launch(attn_fwd_kernel<D, C, KT, true, false, 15>); return;
+          case 16: launch(attn_fwd_kernel<D, C, KT, true, false, 16>); return;
+          case 48: launch(attn_fwd_kernel<D, C, KT, true, false, 48>); return;
+          case 63: launch(attn_fwd_kernel<D, C, KT, true, false, 63>); return;
+          default: break;
+        }
+      }
       if constexpr (D == 64) {
         if (ms) launch(attn_fwd_kernel<D, C, KT, true, true>);
         else launch(attn_fwd_kernel<D, C, KT, true>);
@@ -961,8 +1610,20 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
                        delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2, scale, attn_order(C), kvlen, G);
   };
   bool dq_done = false;
+  if (bwd_dma() && (D == 128 || bwd_dma64())) {
+    // K / V tiles through the direct-to-LDS ring (KVDma)
+    const size_t l2 = 2 * 2 * static_cast<size_t>(64) * D * 2;
+    if constexpr (D == 64) {
+      if (dq_pipe()) dq_go(attn_bwd_dq_kernel<D, C, 64, true, true>, l2);
+      else dq_go(attn_bwd_dq_kernel<D, C, 64, false, true>, l2);
+    } else {
+      dq_go(attn_bwd_dq_kernel<D, C, 64, false, true>, l2);
+    }
+    dq_done = true;
+  }
   if constexpr (D == 64) {
-    if (dq_kt() == 128) {
+    if (dq_done) {
+    } else if (dq_kt() == 128) {
       dq_go(attn_bwd_dq_kernel<D, C, 128, false>, bwd_dq_lds(D, 128));
       dq_done = true;
     } else if (dq_pipe()) {
@@ -971,7 +1632,21 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
     }
   }
   if (!dq_done) dq_go(attn_bwd_dq_kernel<D, C, 64, false>, bwd_dq_lds(D, 64));
-  if (dkdv_qt() == 64) {
+  bool dkdv_done = false;
+  if constexpr (D == 128) {
+    if (bwd_dma() && dkdv_qt() == 64) {
+      const size_t l2 = 2 * (2 * static_cast<size_t>(64) * D * 2 + 2 * 64 * sizeof(float));
+      auto kern = attn_bwd_dkdv_dma_kernel<D, C, 64>;
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l2));
+      hipLaunchKernelGGL(kern, dim3((Sk + 127) / 128, H / G, B), dim3(256), l2, st, q, k, v, dO, lse,
+                         delta, dk, dv, Sq, Sk, H, qs, ks, vs, dos, dks, dvs, scale_log2, scale,
+                         attn_order(C), kvlen, G);
+      dkdv_done = true;
+    }
+  }
+  if (dkdv_done) {
+  } else if (dkdv_qt() == 64) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H / G, B), dim3(256),
                        bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
                        vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen, G);
