@@ -952,7 +952,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
 
 // QT = queries staged per LDS tile (one barrier pair per tile); each wave consumes it in 32-query
 // MFMA sub-tiles, so QT = 64 halves the barriers and staging passes per MFMA of QT = 32.
-template <int D, bool CAUSAL, int QT>
+template <int D, bool CAUSAL, int QT, bool SWZ = false>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     const uint16_t* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
@@ -961,7 +961,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     int order, const int* __restrict__ kvlen, int G) {
   constexpr int KB = 128;
   static_assert(QT == 32 || QT == 64, "query tile");
-  constexpr int RS = D + kPad;
+  // SWZ: unpadded rows with the XOR chunk swizzle of KVDma (zero bank conflicts on both the row and
+  // the transposed reads; the padded rows measured 0.92 conflict cycles per LDS instruction)
+  constexpr int RS = SWZ ? D : D + kPad;
   constexpr int CPR = D / 8;                 // 16-byte chunks per row
   constexpr int NPF = 2 * QT * CPR / 256;    // prefetched chunks per thread (Q and dO tiles)
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -1057,7 +1059,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
     for (int j = 0; j < NPF; ++j) {
       const int cc = threadIdx.x + 256 * (j % PER);
-      *reinterpret_cast<uint4*>((j >= PER ? dOs : Qs) + (cc / CPR) * RS + (cc % CPR) * 8) = pf[j];
+      const int row = cc / CPR, ch = cc % CPR;
+      *reinterpret_cast<uint4*>((j >= PER ? dOs : Qs) + row * RS + (SWZ ? swz_off<D>(row, ch) : ch * 8)) = pf[j];
     }
     if (threadIdx.x < QT) {
       lse_s[threadIdx.x] = pl;
@@ -1093,8 +1096,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
         bf16x8 qfr[D / 16], dofr[D / 16];
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          qfr[s] = load8(Qh + r * RS + 16 * s + 8 * hf);
-          dofr[s] = load8(dOh + r * RS + 16 * s + 8 * hf);
+          const int c = SWZ ? swz_off<D>(r, 2 * s + hf) : 16 * s + 8 * hf;
+          qfr[s] = load8(Qh + r * RS + c);
+          dofr[s] = load8(dOh + r * RS + c);
         }
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
@@ -1104,8 +1108,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
       } else {
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          sacc = mfma32(load8(Qh + r * RS + 16 * s + 8 * hf), kf[s], sacc);
-          dpacc = mfma32(load8(dOh + r * RS + 16 * s + 8 * hf), vf[s], dpacc);
+          const int c = SWZ ? swz_off<D>(r, 2 * s + hf) : 16 * s + 8 * hf;
+          sacc = mfma32(load8(Qh + r * RS + c), kf[s], sacc);
+          dpacc = mfma32(load8(dOh + r * RS + c), vf[s], dpacc);
         }
       }
 #pragma unroll
@@ -1124,9 +1129,10 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
       for (int n = 0; n < D / 32; ++n) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const int off = (16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
-          dvacc[n] = mfma32(cat8(tr_read(dOh + off), tr_read(dOh + off + 8 * RS)), s2 ? p1 : p0, dvacc[n]);
-          dkacc[n] = mfma32(cat8(tr_read(Qh + off), tr_read(Qh + off + 8 * RS)), s2 ? s1 : s0, dkacc[n]);
+          const int off = (16 * s2 + 4 * hf + tr_row) * RS + (SWZ ? tr_off<D>(lane, n, false) : 32 * n + tr_col);
+          const int off8 = (16 * s2 + 4 * hf + tr_row + 8) * RS + (SWZ ? tr_off<D>(lane, n, true) : 32 * n + tr_col);
+          dvacc[n] = mfma32(cat8(tr_read(dOh + off), tr_read(dOh + off8)), s2 ? p1 : p0, dvacc[n]);
+          dkacc[n] = mfma32(cat8(tr_read(Qh + off), tr_read(Qh + off8)), s2 ? s1 : s0, dkacc[n]);
         }
       }
     };
@@ -1495,6 +1501,16 @@ bool fwd_dma() {
 // kernel sits at 246 of its 256 registers and the swizzled offsets spill it (-50 %), and the dQ
 // kernel alone measured -1.5 % on the backward: both keep register staging unless
 // DCA_ATTN_BWD_DMA64=1 (dQ only)
+// dK/dV register-staged tiles in the swizzled unpadded layout (DCA_ATTN_DKDV_SWZ=1): removes the
+// padded layout's 0.92 bank-conflict cycles per LDS instruction but measured neutral (D64 S1024 -1 %,
+// S2048 +2 %, GPT-2 step +0.1 %: profiles/round5_attention_dma_ring_ab.txt), so off by default
+bool dkdv_swz() {
+  static const bool on = [] {
+    const char* e = std::getenv("DCA_ATTN_DKDV_SWZ");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
 bool bwd_dma64() {
   static const bool on = [] {
     const char* e = std::getenv("DCA_ATTN_BWD_DMA64");
@@ -1646,6 +1662,10 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
     }
   }
   if (dkdv_done) {
+  } else if (dkdv_qt() == 64 && dkdv_swz()) {
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64, true>), dim3((Sk + 127) / 128, H / G, B), dim3(256),
+                       bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
+                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen, G);
   } else if (dkdv_qt() == 64) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H / G, B), dim3(256),
                        bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
