@@ -89,7 +89,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> pathlib.
     if cmds or force or not TARGET.exists():
         link = [_hipcc(), "-shared", "-fPIC", "-o", str(TARGET)] + [str(o) for o in objs] + [
             f"--offload-arch={ARCH}", f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
-            "-ltorch_hip", "-ltorch_python", "-lamdhip64", f"-Wl,-rpath,{lib}"]
+            "-ltorch_hip", "-ltorch_python", "-lamdhip64", "-lhipblaslt", f"-Wl,-rpath,{lib}"]
         if verbose:
             print(" ".join(link), flush=True)
         _compile(link)

@@ -575,6 +575,7 @@ void scale_(const Tensor& x, double s, const OptT& dev_scale) {
 void register_transformer_ops(pybind11::module& m);
 void register_conv_ops(pybind11::module& m);
 void register_groupnorm_ops(pybind11::module& m);
+void register_lt_ops(pybind11::module& m);
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "determined_clone_amd MI355X (gfx950) HIP kernels";
@@ -613,4 +614,5 @@ PYBIND11_MODULE(_C, m) {
   register_transformer_ops(m);
   register_conv_ops(m);
   register_groupnorm_ops(m);
+  register_lt_ops(m);
 }

@@ -216,6 +216,34 @@ def _wgrad_split_k(acc: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, s: in
     _ext.load().splitk_accumulate(torch.bmm(a, b, out_dtype=torch.float32), acc)
 
 
+def _weight_grad(w_param: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> Optional[torch.Tensor]:
+    """dW = dy2^T x2, accumulated into the parameter's flat ``.grad`` view on the side stream
+    (split-K batched GEMM at >= 8k tokens; returns None) or returned when there is no such view."""
+    acc = _grad.target(w_param)
+    if acc is None:
+        return dy2.t() @ x2
+    s = _wgrad_splits(dy2.shape[0], dy2.shape[1], x2.shape[1])
+    side = _grad.side_stream_for(w_param) if LINEAR_SIDE_STREAM else None
+    if side is not None:
+        _grad.fork(side, (dy2, x2))
+    with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+        if s > 1:
+            _wgrad_split_k(acc, dy2, x2, s)
+        else:
+            acc.addmm_(dy2.t(), x2)
+    return None
+
+
+def _bias_grad(b_param: torch.Tensor, dy2: torch.Tensor) -> Optional[torch.Tensor]:
+    """db = dy2.sum(0): the fused column reduction straight into the flat ``.grad`` view (returns
+    None) or a returned gradient."""
+    acc = _grad.target(b_param)
+    if dy2.shape[-1] % 8 == 0 and dy2.is_cuda:
+        out = _ext.load().bias_grad(dy2, acc)
+        return None if acc is not None else out.to(b_param.dtype)
+    return dy2.sum(0).to(b_param.dtype)
+
+
 class _Linear(torch.autograd.Function):
     """``y = x @ w.T + b`` whose backward accumulates straight into the parameters' flat
     ``.grad`` views: dW by a GEMM with beta = 1 (``grad.addmm_``), db by the fused column
@@ -236,20 +264,7 @@ class _Linear(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = dw = db = None
         if ctx.needs_input_grad[1]:  # first: on the side stream it overlaps the data gradient
-            x2 = x.reshape(-1, x.shape[-1])
-            acc = _grad.target(w_param)
-            if acc is not None:
-                s = _wgrad_splits(dy2.shape[0], dy2.shape[1], x2.shape[1])
-                side = _grad.side_stream_for(w_param) if LINEAR_SIDE_STREAM else None
-                if side is not None:
-                    _grad.fork(side, (dy2, x2))
-                with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-                    if s > 1:
-                        _wgrad_split_k(acc, dy2, x2, s)
-                    else:
-                        acc.addmm_(dy2.t(), x2)
-            else:
-                dw = dy2.t() @ x2
+            dw = _weight_grad(w_param, dy2, x.reshape(-1, x.shape[-1]))
         if ctx.needs_input_grad[0]:
             dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
         given = getattr(ctx, "_dca_bias_given", None)
@@ -260,12 +275,7 @@ class _Linear(torch.autograd.Function):
             # dy also carries gradient from another consumer: add only that part
             dy2 = (dy - given).reshape(-1, dy.shape[-1])
         if b_param is not None and ctx.needs_input_grad[2]:
-            acc = _grad.target(b_param)
-            if dy2.shape[-1] % 8 == 0 and dy2.is_cuda:
-                out = _ext.load().bias_grad(dy2, acc)
-                db = None if acc is not None else out.to(b_param.dtype)
-            else:
-                db = dy2.sum(0).to(b_param.dtype)
+            db = _bias_grad(b_param, dy2)
         return dx, dw, db
 
 

@@ -484,3 +484,11 @@ def test_out_projection_bias_grad_reduced_in_layer_norm_backward(extra_consumer,
         grads[fused] = [p.grad.float().clone() for p in ps]
     for a, b in zip(grads[True], grads[False]):
         assert _rel(a, b) < 2e-2
+
+
+def test_hipblaslt_epilogue_probe_runs():
+    """tools/lt_probe.py's entry point: the plain GEMM and the BIAS epilogue have kernels."""
+    C = _C()
+    torch.zeros(1, device="cuda")
+    assert C.lt_probe(1, 1024, 4096, 1024, True, False, -1, -1, False) > 0
+    assert C.lt_probe(4, 1024, 4096, 1024, True, False, 0, -1, True) > 0
