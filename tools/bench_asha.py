@@ -54,6 +54,8 @@ def search_config(args: argparse.Namespace) -> dict:
     cfg["hyperparameters"]["global_batch_size"] = args.batch
     cfg["checkpoint_storage"] = {"save_trial_latest": 1, "save_trial_best": 0, "save_experiment_best": 1}
     cfg["max_restarts"] = 0
+    if args.hip_graph is not None:  # A/B of the trials' HIP-graph-captured training step
+        cfg.setdefault("optimizations", {})["hip_graph"] = bool(args.hip_graph)
     return cfg
 
 
@@ -103,6 +105,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--timeout", type=float, default=3000.0)
     ap.add_argument("--cpu", action="store_true", help="artificial CPU slots (plumbing check)")
+    ap.add_argument("--hip-graph", type=int, default=None, choices=(0, 1),
+                    help="override the example's optimizations.hip_graph (A/B)")
     ap.add_argument("--trace", action="store_true",
                     help="also print mean start-up phase times to stderr")
     args = ap.parse_args()
