@@ -70,6 +70,7 @@ OPTIMIZATIONS = {
     # MI355X extension: capture the training step as a HIP graph after N eager warm-up steps
     "hip_graph": ((bool,), False),
     "hip_graph_warmup_steps": ((int,), 3),
+    "hip_graph_deterministic_convs": ((bool,), False),
     "mixed_precision": ((str,), "O0"),
     "tensor_fusion_cycle_time": ((int,), 1),
     "tensor_fusion_threshold": ((int,), 64),

@@ -823,7 +823,8 @@ OPTIMIZATIONS = Obj([
     F("tensor_fusion_threshold", NIntMin(0), 64), F("tensor_fusion_cycle_time", NIntMin(0), 1),
     F("auto_tune_tensor_fusion", NBool, False),
     # MI355X extension: capture the training step as a HIP graph after N eager warm-up steps
-    F("hip_graph", NBool, go=False), F("hip_graph_warmup_steps", NIntMin(1), go=False)])
+    F("hip_graph", NBool, go=False), F("hip_graph_warmup_steps", NIntMin(1), go=False),
+    F("hip_graph_deterministic_convs", NBool, go=False)])
 PROFILING = Obj([F("enabled", NBool, False), F("begin_on_batch", NIntMin(0), 0),
                  F("end_after_batch", NIntMin(0)), F("sync_timings", NBool, True)],
                 checks=[("begin_on_batch must be less than end_after_batch",

@@ -105,6 +105,7 @@ class PyTorchTrialContext(_PyTorchReducerContext):
         self._average_training_metrics = bool(opts.get("average_training_metrics", True))
         self._hip_graph = bool(opts.get("hip_graph", False))
         self._hip_graph_warmup = int(opts.get("hip_graph_warmup_steps", 3) or 3)
+        self._hip_graph_det_convs = bool(opts.get("hip_graph_deterministic_convs", False))
         fusion_mb = opts.get("tensor_fusion_threshold")
         self._bucket_mb = float(fusion_mb) if fusion_mb and fusion_mb != 64 else 32.0
 

@@ -467,8 +467,9 @@ class _PyTorchTrialController:
                 logger.warning(f"optimizations.hip_graph disabled: {reason}")
                 self.context._hip_graph = False
                 return None
-            self._graphed = _graph.GraphedTrainStep(self.context, self.trial.train_batch,
-                                                    self.context._hip_graph_warmup)
+            self._graphed = _graph.GraphedTrainStep(
+                self.context, self.trial.train_batch, self.context._hip_graph_warmup,
+                deterministic_convs=getattr(self.context, "_hip_graph_det_convs", False))
         return self._graphed
 
     _scratch_released = False

@@ -20,16 +20,18 @@ optimizer, and a ``train_batch`` without host synchronisation or data-dependent 
 flow. Transformer trials (fused LayerNorm / attention / bias-GELU / cross-entropy, hipBLASLt
 GEMMs, fused AdamW with device-side clipping) and ResNets replay bit-exactly.
 
-MIOpen convolutions: for models with convolutions, every call of the step function made by the
-graph runner (warm-up, capture, eager fallbacks) runs with MIOpen's deterministic solvers
-(``torch.backends.cudnn.deterministic = True`` for the duration of the call only, restored after
-it, so evaluation and other models keep the default solvers). Root cause of the
-eager-vs-replay divergence measured in earlier rounds (profiles/round4_hip_graph_miopen_root_cause.txt):
-nothing was missing from the graph -- MIOpen's default solver for small strided 1x1 NHWC
-convolutions (ConvAsmImplicitGemmGTCDynamicFwdXdlopsNHWC, a split-K kernel accumulating with
-atomics) is nondeterministic run to run (relative 4e-5 between two EAGER calls), and the replay
-merely ran it with a different atomic order; a few SGD steps amplified that. With deterministic
-solvers eager and replay agree bit for bit. The reference has no equivalent (its step is eager).
+MIOpen convolutions: the eager-vs-replay difference measured in earlier rounds
+(profiles/round4_hip_graph_miopen_root_cause.txt) was not a capture bug -- MIOpen's default solver
+for small strided 1x1 NHWC convolutions (ConvAsmImplicitGemmGTCDynamicFwdXdlopsNHWC, a split-K
+kernel accumulating with atomics) is nondeterministic run to run (relative 4e-5 between two EAGER
+calls), and the replay merely ran it with a different atomic order. With
+``optimizations.hip_graph_deterministic_convs: true`` every call of the step function made by the
+runner (warm-up, capture, eager fallbacks) runs MIOpen's deterministic solvers
+(``torch.backends.cudnn.deterministic = True`` for the duration of the call only), and eager and
+replay agree bit for bit. It is OFF by default: the deterministic solvers made the CIFAR ASHA
+trial's step ~10x slower (79.6 s vs 8.1 s for 300 batches, tools/probe_cifar_graph.py,
+profiles/round5_asha_hip_graph_attempt.txt) -- a price only bitwise reproducibility should pay.
+The reference has no equivalent (its step is eager).
 """
 import contextlib
 import logging
@@ -64,7 +66,8 @@ def _has_convs(context: Any) -> bool:
 
 
 class GraphedTrainStep:
-    def __init__(self, context: Any, fn: Callable[..., Any], warmup_steps: int = 3) -> None:
+    def __init__(self, context: Any, fn: Callable[..., Any], warmup_steps: int = 3,
+                 deterministic_convs: bool = False) -> None:
         self.context = context
         self.fn = fn
         self.warmup_steps = max(1, int(warmup_steps))
@@ -76,12 +79,12 @@ class GraphedTrainStep:
         self.replays = 0
         for opt in context.optimizers:
             opt.enable_device_hparams()
-        # MIOpen runs its deterministic solvers for every call of the step function this object
-        # makes (warm-up, capture, eager fallbacks), so warm-up, capture and replay run the same
-        # solvers; the process-wide flag is restored after each call, so evaluation, other
-        # models and later trials in the process keep the fastest (split-K atomic) solvers.
-        self._deterministic = (torch.backends.cudnn.enabled and not torch.backends.cudnn.deterministic
-                               and _has_convs(context))
+        # deterministic_convs: MIOpen runs its deterministic solvers for every call of the step
+        # function this object makes (warm-up, capture, eager fallbacks), so warm-up, capture and
+        # replay run the same solvers; the process-wide flag is restored after each call, so
+        # evaluation, other models and later trials in the process keep the fastest solvers.
+        self._deterministic = (deterministic_convs and torch.backends.cudnn.enabled
+                               and not torch.backends.cudnn.deterministic and _has_convs(context))
         if self._deterministic:
             logger.info("hip_graph: MIOpen runs deterministic convolution solvers inside the "
                         "graphed training step")

@@ -76,8 +76,8 @@ class _GPTTrial(_ResNetTrial):
         return pytorch.DataLoader(pytorch.DeviceBatchDataset(batches, 64), batch_size=None)
 
 
-def _run(trial_cls, graph, tmp_path):
-    opts = {"hip_graph": graph, "hip_graph_warmup_steps": 3}
+def _run(trial_cls, graph, tmp_path, det_convs=False):
+    opts = {"hip_graph": graph, "hip_graph_warmup_steps": 3, "hip_graph_deterministic_convs": det_convs}
     with pytorch.init(hparams={"global_batch_size": 8}, exp_conf={"optimizations": opts}) as ctx:
         ctx._core.checkpoint._storage_manager = __import__(
             "determined_clone_amd.common.storage", fromlist=["x"]).SharedFSStorageManager(str(tmp_path / f"ck{graph}"))
@@ -106,10 +106,13 @@ def test_graph_step_matches_eager(trial_cls, tmp_path, monkeypatch):
 
 
 def test_graph_with_miopen_convolutions_switches_to_deterministic_solvers(tmp_path, monkeypatch):
-    """The runner's own step calls use the deterministic solvers; the process-wide flag is back
-    to its previous value afterwards (evaluation and other models keep the default solvers)."""
+    """With hip_graph_deterministic_convs the runner's own step calls use the deterministic solvers;
+    the process-wide flag is back to its previous value afterwards (evaluation and other models keep
+    the default solvers). Without it (the default) the runner leaves the solvers alone."""
     monkeypatch.setattr(torch.backends.cudnn, "deterministic", False)
-    _, runner, _, step = _run(_ResNetTrial, True, tmp_path)
+    _, runner0, _, _ = _run(_ResNetTrial, True, tmp_path / "default")
+    assert runner0 is not None and not runner0._deterministic
+    _, runner, _, step = _run(_ResNetTrial, True, tmp_path, det_convs=True)
     assert runner is not None and runner.replays == STEPS - 3 and step == STEPS
     assert runner._deterministic
     assert not torch.backends.cudnn.deterministic
