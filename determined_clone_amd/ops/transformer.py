@@ -187,6 +187,8 @@ class _BiasGelu(torch.autograd.Function):
 
 
 _WGRAD_SPLITK = os.environ.get("DCA_WGRAD_SPLITK", "1") != "0"
+# K-slices of the split-K weight gradient (A/B knob; 4 measured best in isolation)
+_WGRAD_SPLITS = int(os.environ.get("DCA_WGRAD_SPLITS", "4"))
 # linear-layer weight gradients on the side stream (ops/_grad.py); A/B switch
 LINEAR_SIDE_STREAM = os.environ.get("DCA_LINEAR_WGRAD_STREAM", "1") != "0"
 
@@ -201,9 +203,9 @@ def _wgrad_splits(tokens: int, m: int, n: int) -> int:
     3072x1024 166 -> 115 us, 4096x1024 166 -> 145 us, 1024x4096 161 -> 143 us."""
     if not _WGRAD_SPLITK or tokens < 8192 or tokens % 4 or m * n > 16 * 2 ** 20:
         return 1
-    if (m * n) % 8:  # splitk_accumulate streams 8 elements per thread (16-B aligned buffers)
+    if (m * n) % 8 or tokens % _WGRAD_SPLITS:  # splitk_accumulate: 8 elements per thread
         return 1
-    return 4
+    return _WGRAD_SPLITS
 
 
 def _wgrad_split_k(acc: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, s: int) -> None:
