@@ -503,9 +503,16 @@ def _bgrad(dy: torch.Tensor, bias: torch.Tensor) -> Optional[torch.Tensor]:
 STEM_S2D = os.environ.get("DCA_STEM_S2D", "1") != "0"
 
 
+# the stem image's pad + space-to-depth as one HIP pass (csrc/conv_igemm.hip stem_s2d_kernel);
+# DCA_STEM_S2D_KERNEL=0 keeps ATen's pad + reshape copies (A/B only).
+STEM_S2D_KERNEL = os.environ.get("DCA_STEM_S2D_KERNEL", "1") != "0"
+
+
 def _s2d_input(x: torch.Tensor) -> torch.Tensor:
     """[N, 3, H, W] (NHWC memory) -> [N, 12, (H+6)/2, (W+6)/2] channels_last, channel (dy, dx, c)."""
     n, c, h, w = x.shape
+    if STEM_S2D_KERNEL and x.is_cuda and x.dtype == torch.bfloat16 and c == 3:
+        return _ext.load().stem_s2d(x)  # one pass, padding folded in (csrc/conv_igemm.hip)
     xn = F.pad(x.permute(0, 2, 3, 1), (0, 0, 3, 3, 3, 3))  # [N, H+6, W+6, C]
     hh, ww = (h + 6) // 2, (w + 6) // 2
     xs = xn.view(n, hh, 2, ww, 2, c).permute(0, 1, 3, 2, 4, 5).reshape(n, hh, ww, 4 * c)

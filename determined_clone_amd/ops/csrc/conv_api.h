@@ -26,6 +26,8 @@ void conv_igemm_wgrad(const void* dy, const void* x, float* ws, void* dw, bool d
                       bool accumulate, bool dw_kcrs, const ConvGeom& g, hipStream_t st);
 // w [K][RS][C] -> wt [C][RS][K] with the taps reversed (stride-1 data-gradient weight).
 void conv_flip_transpose(const void* w, void* wt, int K, int C, int RS, hipStream_t st);
+// ResNet stem space-to-depth with zero padding 3: x [N][H][W][3] -> [N][(H+6)/2][(W+6)/2][12] bf16.
+void stem_s2d(const void* x, void* xs, int N, int H, int W, hipStream_t st);
 // dx [N][H][W][C] += small [N][Ho][Wo][C] at rows s*i, columns s*j (bf16, C a multiple of 8).
 void strided_accumulate(void* dx, const void* small, int N, int H, int W, int C, int Ho, int Wo,
                         int s, hipStream_t st);

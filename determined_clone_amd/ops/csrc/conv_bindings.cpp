@@ -184,7 +184,26 @@ void strided_accumulate(Tensor& dx, const Tensor& small, int64_t s) {
                           static_cast<int>(Wo), static_cast<int>(s), stream());
 }
 
+// [N, 3, H, W] channels_last bf16 image -> [N, 12, (H+6)/2, (W+6)/2] channels_last (ops/conv.py
+// _s2d_input: the space-to-depth form of the 7x7/2 padding-3 stem convolution).
+Tensor stem_s2d(const Tensor& x) {
+  const c10::DeviceGuard dg(x.device());
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3,
+              "stem_s2d: bf16 [N, 3, H, W] GPU tensor required");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "stem_s2d: channels_last layout required");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "stem_s2d: even H and W required");
+  TORCH_CHECK(N * (H + 6) * (W + 6) * 3 < (int64_t{1} << 40), "stem_s2d: too large");
+  Tensor xs = torch::empty({N, 12, (H + 6) / 2, (W + 6) / 2},
+                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (xs.numel() == 0) return xs;
+  dca::stem_s2d(x.data_ptr(), xs.data_ptr(), static_cast<int>(N), static_cast<int>(H),
+                static_cast<int>(W), stream());
+  return xs;
+}
+
 void register_conv_ops(pybind11::module& m) {
+  m.def("stem_s2d", &stem_s2d, pybind11::arg("x"));
   m.def("strided_accumulate", &strided_accumulate, pybind11::arg("dx"), pybind11::arg("small"),
         pybind11::arg("stride"));
   m.def("conv_igemm_wgrad", &conv_igemm_wgrad, pybind11::arg("dy"), pybind11::arg("x"),

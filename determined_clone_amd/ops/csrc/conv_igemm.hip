@@ -774,6 +774,99 @@ void strided_accumulate(void* dx, const void* small, int N, int H, int W, int C,
                      Ho, W, H, s);
 }
 
+// Space-to-depth of the 3-channel stem image with its 3-pixel zero padding in the same pass:
+// x [N][H][W][3] (NHWC bf16) -> xs [N][(H+6)/2][(W+6)/2][12], channel (dy, dx, c) of output pixel
+// (i, j) = x[2i+dy-3][2j+dx-3][c] or 0 outside the image. Replaces ATen's pad (fill + copy) and
+// the strided reshape copy (423 us of the ResNet-50 bs-1024 step, profiles/round5_stem_s2d_kernel.txt).
+// Row kernel: each half-block (128 lanes) owns one output row; its two input rows (contiguous,
+// 6W bytes each) come in with 16-byte nontemporal loads into LDS, then every lane emits 8-byte
+// chunks (4 of an output pixel's 12 channels) so the stores are one contiguous run per row.
+// Needs 6W % 16 == 0 (W % 8 == 0); other widths take the per-pixel kernel below.
+constexpr int kS2dMaxW = 1024;
+__global__ __launch_bounds__(256) void stem_s2d_rows_kernel(const uint16_t* __restrict__ x,
+                                                            uint16_t* __restrict__ xs, int rows_out,
+                                                            int Wo, int Ho, int W, int H) {
+  __shared__ uint4 tile[2][2][kS2dMaxW * 3 / 8];
+  const int h = threadIdx.x >> 7, lt = threadIdx.x & 127;
+  const int g = blockIdx.x * 2 + h;  // output row n * Ho + i
+  const bool live = g < rows_out;
+  const int n = live ? g / Ho : 0, i = live ? g - n * Ho : 0;
+  const int row_vec = W * 3 / 8;  // 16-byte vectors per input row
+  if (live) {
+    for (int idx = lt; idx < 2 * row_vec; idx += 128) {
+      const int dy = idx >= row_vec, v = idx - dy * row_vec;
+      const int r = 2 * i + dy - 3;
+      tile[h][dy][v] = (r >= 0 && r < H)
+                           ? ldnt16(x + (static_cast<int64_t>(n) * H + r) * W * 3 + v * 8)
+                           : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  const uint16_t* t16 = reinterpret_cast<const uint16_t*>(&tile[h][0][0]);
+  const int row16 = kS2dMaxW * 3;  // LDS row stride in bf16
+  uint2* out = reinterpret_cast<uint2*>(xs + static_cast<int64_t>(g) * Wo * 12);
+  for (int k = lt; k < Wo * 3; k += 128) {
+    const int j = k / 3, q = k - 3 * j;
+    uint32_t v[4];
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      const int e = 4 * q + e4;  // channel (dy, dx, c) of output pixel j
+      const int dy = e / 6, dx = (e / 3) & 1, c = e % 3;
+      const int col = 2 * j + dx - 3;
+      v[e4] = (col >= 0 && col < W) ? t16[dy * row16 + col * 3 + c] : 0u;
+    }
+    out[k] = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+  }
+}
+
+// Per-pixel fallback for widths the row kernel does not take: one lane per output pixel.
+__global__ __launch_bounds__(256) void stem_s2d_kernel(const uint16_t* __restrict__ x,
+                                                       uint16_t* __restrict__ xs, int64_t n_pix,
+                                                       int Wo, int Ho, int W, int H) {
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < n_pix;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int j = static_cast<int>(t % Wo);
+    const int64_t ni = t / Wo;
+    const int i = static_cast<int>(ni % Ho);
+    const int64_t n = ni / Ho;
+    uint16_t v[12];
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      const int r = 2 * i + dy - 3;
+      const bool row_ok = r >= 0 && r < H;
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const int c0 = 2 * j + dx - 3;
+        const bool ok = row_ok && c0 >= 0 && c0 < W;
+        const uint16_t* src = x + ((n * H + r) * W + c0) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[(dy * 2 + dx) * 3 + c] = ok ? __builtin_nontemporal_load(src + c) : 0;
+      }
+    }
+    uint2* dst = reinterpret_cast<uint2*>(xs + t * 12);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      dst[q] = make_uint2(v[4 * q] | (static_cast<uint32_t>(v[4 * q + 1]) << 16),
+                          v[4 * q + 2] | (static_cast<uint32_t>(v[4 * q + 3]) << 16));
+  }
+}
+
+void stem_s2d(const void* x, void* xs, int N, int H, int W, hipStream_t st) {
+  const int Ho = (H + 6) / 2, Wo = (W + 6) / 2;
+  const int64_t rows_out = static_cast<int64_t>(N) * Ho;
+  if (W % 8 == 0 && W <= kS2dMaxW && rows_out < (int64_t{1} << 31)) {
+    hipLaunchKernelGGL(stem_s2d_rows_kernel, dim3(static_cast<unsigned>((rows_out + 1) / 2)), dim3(256), 0,
+                       st, static_cast<const uint16_t*>(x), static_cast<uint16_t*>(xs),
+                       static_cast<int>(rows_out), Wo, Ho, W, H);
+    return;
+  }
+  const int64_t n_pix = rows_out * Wo;
+  const int64_t blocks = std::min<int64_t>((n_pix + 255) / 256, 256 * 64);
+  hipLaunchKernelGGL(stem_s2d_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st,
+                     static_cast<const uint16_t*>(x), static_cast<uint16_t*>(xs), n_pix, Wo, Ho, W, H);
+}
+
 void conv_flip_transpose(const void* w, void* wt, int K, int C, int RS, hipStream_t st) {
   hipLaunchKernelGGL(flip_transpose_kernel, dim3((C + 63) / 64, (K + 63) / 64, RS), dim3(kThreads),
                      0, st, static_cast<const uint16_t*>(w), static_cast<uint16_t*>(wt), K, C, RS);

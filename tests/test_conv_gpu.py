@@ -189,6 +189,22 @@ def test_side_stream_inputs_released_without_optimizer_step(monkeypatch):
     assert not _grad.pending() and not _grad._keep
 
 
+@pytest.mark.parametrize("hw", [(224, 224), (64, 48), (2, 8), (6, 10)])
+def test_stem_s2d_kernel_matches_pad_and_reshape(hw):
+    """The HIP space-to-depth (padding folded in) is a pure data movement: bit-equal to the ATen
+    pad + permute + reshape it replaces, including images smaller than the padding."""
+    from determined_clone_amd.ops import _ext
+
+    torch.manual_seed(0)
+    x = torch.randn(3, 3, *hw, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xs = _ext.load().stem_s2d(x)
+    n, c, h, w = x.shape
+    ref = F.pad(x.permute(0, 2, 3, 1), (0, 0, 3, 3, 3, 3)).view(n, (h + 6) // 2, 2, (w + 6) // 2, 2, c)
+    ref = ref.permute(0, 1, 3, 2, 4, 5).reshape(n, (h + 6) // 2, (w + 6) // 2, 4 * c).permute(0, 3, 1, 2)
+    assert xs.is_contiguous(memory_format=torch.channels_last) and xs.shape == ref.shape
+    assert torch.equal(xs, ref)
+
+
 @pytest.mark.parametrize("side", [True, False])
 @pytest.mark.parametrize("hw", [(224, 224), (64, 48)])
 def test_stem_space_to_depth_matches_fp32(monkeypatch, side, hw):
