@@ -152,8 +152,9 @@ class ResNet(nn.Module):
         # stem: conv -> fused BN + ReLU + 3x3/2 max-pool (the 112x112 pre-pool activation is never
         # written; its gradient is gathered inside the BN backward)
         bn = self.bn1
-        x = bn_ops.batch_norm_relu_maxpool(conv_ops.stem_conv(self.conv1, x), bn.weight, bn.bias, bn.running_mean,
-                                           bn.running_var, training=bn.training,
+        # (the stem kernel reduces the BatchNorm's batch statistics in its epilogue)
+        x = conv_ops.stem_conv(self.conv1, x, bn_stats=bn.training)
+        x = bn_ops.batch_norm_relu_maxpool(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, training=bn.training,
                                            momentum=bn.momentum, eps=bn.eps,
                                            num_batches_tracked=bn.num_batches_tracked)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))

@@ -300,9 +300,11 @@ def reference_bn_relu_maxpool(x, weight, bias, running_mean, running_var, traini
 
 class _BNReLUPoolTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, num_batches, momentum, eps):
+    def forward(ctx, x, weight, bias, running_mean, running_var, num_batches, momentum, eps,
+                partials=None):
         y, mean, invstd, idx = _ext.load().bn_pool_fwd_train(x, weight, bias, running_mean,
-                                                             running_var, num_batches, momentum, eps)
+                                                             running_var, num_batches, momentum, eps,
+                                                             partials)
         ctx.save_for_backward(x, idx, weight, mean, invstd)
         return y
 
@@ -311,7 +313,7 @@ class _BNReLUPoolTrain(torch.autograd.Function):
         x, idx, weight, mean, invstd = ctx.saved_tensors
         need_w = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         dx, dg, db = _ext.load().bn_pool_bwd(dy, x, idx, weight, mean, invstd, need_w)
-        return dx, dg if need_w else None, db if need_w else None, None, None, None, None, None
+        return dx, dg if need_w else None, db if need_w else None, None, None, None, None, None, None
 
 
 def batch_norm_relu_maxpool(x: torch.Tensor, weight: Optional[torch.Tensor],
@@ -320,7 +322,10 @@ def batch_norm_relu_maxpool(x: torch.Tensor, weight: Optional[torch.Tensor],
                             momentum: Optional[float] = 0.1, eps: float = 1e-5,
                             num_batches_tracked: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``max_pool2d(relu(batch_norm(x)), 3, 2, 1)`` -- the ResNet stem -- without writing the
-    pre-pool activation; backward gathers the pooled gradient inside the BN-backward passes."""
+    pre-pool activation; backward gathers the pooled gradient inside the BN-backward passes.
+    Training statistics come from ``x._dca_bn_partials`` when the stem convolution's epilogue
+    reduced them (``ops.conv.stem_conv(..., bn_stats=True)``)."""
+    partials = getattr(x, "_dca_bn_partials", None)
     if not (_hip_ok(x) and x.dim() == 4) or momentum is None:
         if training and num_batches_tracked is not None:
             num_batches_tracked.add_(1)
@@ -328,12 +333,13 @@ def batch_norm_relu_maxpool(x: torch.Tensor, weight: Optional[torch.Tensor],
                 momentum = 1.0 / float(num_batches_tracked.item())
         return reference_bn_relu_maxpool(x, weight, bias, running_mean, running_var, training,
                                          momentum if momentum is not None else 0.0, eps)
-    x = x.contiguous(memory_format=torch.channels_last)
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x, partials = x.contiguous(memory_format=torch.channels_last), None
     if training or running_mean is None:
         return _BNReLUPoolTrain.apply(x, weight, bias, running_mean if training else None,
                                       running_var if training else None,
                                       num_batches_tracked if training else None, float(momentum),
-                                      float(eps))
+                                      float(eps), partials)
     scale = torch.rsqrt(running_var.float() + eps)
     if weight is not None:
         scale = scale * weight.float()

@@ -506,6 +506,12 @@ STEM_S2D = os.environ.get("DCA_STEM_S2D", "1") != "0"
 # the stem image's pad + space-to-depth as one HIP pass (csrc/conv_igemm.hip stem_s2d_kernel);
 # DCA_STEM_S2D_KERNEL=0 keeps ATen's pad + reshape copies (A/B only).
 STEM_S2D_KERNEL = os.environ.get("DCA_STEM_S2D_KERNEL", "1") != "0"
+# the stem convolution itself on the hand-written kernel (stem_conv_kernel, BatchNorm statistics in
+# its epilogue). OFF by default: standalone it runs the bs-1024 stem in 0.84 ms against MIOpen's
+# 1.94 ms (+0.28 ms statistics pass), but in the step the kernels around it ran 1-8 % slower and
+# the step measured -0.3..-2 % in five same-box A/Bs (profiles/round5_stem_conv_kernel_ab.txt).
+# DCA_STEM_KERNEL=1 opts in.
+STEM_KERNEL = os.environ.get("DCA_STEM_KERNEL", "0") == "1"
 
 
 def _s2d_input(x: torch.Tensor) -> torch.Tensor:
@@ -519,11 +525,14 @@ def _s2d_input(x: torch.Tensor) -> torch.Tensor:
     return xs.permute(0, 3, 1, 2)
 
 
-def _s2d_weight(w: torch.Tensor) -> torch.Tensor:
-    """[K, C, 7, 7] -> [K, 4C, 4, 4] (channels_last), channel (dy, dx, c), tap (i, j) = (2i+dy, 2j+dx)."""
+def _s2d_weight(w: torch.Tensor, channels: int = 0) -> torch.Tensor:
+    """[K, C, 7, 7] -> [K, 4C, 4, 4] (channels_last), channel (dy, dx, c), tap (i, j) = (2i+dy, 2j+dx);
+    ``channels`` > 4C appends zero channels (the stem kernel's 16-channel pixels)."""
     k, c = w.shape[:2]
-    wp = F.pad(w, (0, 1, 0, 1)).view(k, c, 4, 2, 4, 2).permute(0, 3, 5, 1, 2, 4)
-    return wp.reshape(k, 4 * c, 4, 4).contiguous(memory_format=torch.channels_last)
+    wp = F.pad(w, (0, 1, 0, 1)).view(k, c, 4, 2, 4, 2).permute(0, 3, 5, 1, 2, 4).reshape(k, 4 * c, 4, 4)
+    if channels > 4 * c:
+        wp = F.pad(wp, (0, 0, 0, 0, 0, channels - 4 * c))
+    return wp.contiguous(memory_format=torch.channels_last)
 
 
 def _s2d_weight_grad(dw2: torch.Tensor, c: int) -> torch.Tensor:
@@ -535,47 +544,71 @@ def _s2d_weight_grad(dw2: torch.Tensor, c: int) -> torch.Tensor:
 
 class _StemS2D(torch.autograd.Function):
     """7x7/2 (padding 3) convolution of a 3-channel image as the space-to-depth 4x4/1 convolution;
-    the weight gradient is folded back to 7x7 and, on a GPU, runs on the side stream into the
-    parameter's ``.grad`` view (``ops/_grad.py``). The image gets no gradient."""
+    returns ``(y, bn_partials)``. With ``kernel`` (bf16, csrc/conv_igemm.hip stem_conv_kernel) the
+    S2D tensor carries 16 channels (4 zero) and the forward emits the stem BatchNorm's partial
+    statistics; otherwise MIOpen runs the 12-channel form and ``bn_partials`` is None. The weight
+    gradient is folded back to 7x7 and, on a GPU, runs on the side stream into the parameter's
+    ``.grad`` view (``ops/_grad.py``). The image gets no gradient."""
 
     @staticmethod
-    def forward(ctx, x, weight):
-        xs = _s2d_input(x)
-        w2 = _s2d_weight(weight)
+    def forward(ctx, x, weight, kernel):
+        ctx.set_materialize_grads(False)
+        partial = None
+        if kernel:
+            C = _ext.load()
+            xs = C.stem_s2d(x, 16)
+            w2 = _s2d_weight(weight, 16)
+            y, partial = C.stem_conv_fwd(xs, w2)
+            ctx.mark_non_differentiable(partial)
+        else:
+            xs = _s2d_input(x)
+            w2 = _s2d_weight(weight)
+            y = F.conv2d(xs, w2)
         ctx.save_for_backward(xs, w2)
         ctx.weight = weight
-        return F.conv2d(xs, w2)
+        return y, partial
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dpartial):
         xs, w2 = ctx.saved_tensors
         weight = ctx.weight
+        if dy is None:
+            return None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
         args = (dy, xs, w2, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
         bwd = torch.ops.aten.convolution_backward
+        c = weight.shape[1]
         s = _grad.side_stream_for(weight)
         if s is None:
             dw2 = bwd(*args, [False, True, False])[1]
-            return None, _s2d_weight_grad(dw2, weight.shape[1]).to(weight.dtype)
+            return None, _s2d_weight_grad(dw2[:, :4 * c], c).to(weight.dtype), None
         _grad.fork(s, (dy, xs))
         with torch.cuda.stream(s):
             dw2 = bwd(*args, [False, True, False])[1]
-            _grad.target(weight).add_(_s2d_weight_grad(dw2, weight.shape[1]))
-        return None, None
+            _grad.target(weight).add_(_s2d_weight_grad(dw2[:, :4 * c], c))
+        return None, None, None
 
 
-def stem_conv(conv: nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+def stem_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> torch.Tensor:
     """The ResNet stem convolution: space-to-depth form on a GPU when it applies (7x7, stride 2,
     padding 3, 3 input channels, no bias, even H and W, image without gradient), else
     :func:`spatial_conv`. The S2D form is pinned to the 7x7 path only for zero padding, matching
-    input / weight dtypes and no autocast (its saved tensors keep their own dtype)."""
+    input / weight dtypes and no autocast (its saved tensors keep their own dtype). bf16 images of
+    width 122-506 with 64 output channels run on the stem kernel; with ``bn_stats`` its output
+    carries the following BatchNorm's partial statistics (``y._dca_bn_partials``)."""
     if (STEM_S2D and x.is_cuda and not x.requires_grad and conv.kernel_size == (7, 7)
             and conv.padding_mode == "zeros" and x.dtype == conv.weight.dtype
             and not torch.is_autocast_enabled()
             and conv.stride == (2, 2) and conv.padding == (3, 3) and conv.in_channels == 3
             and conv.groups == 1 and conv.bias is None and conv.dilation == (1, 1)
             and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0):
-        return _StemS2D.apply(x.contiguous(memory_format=torch.channels_last), conv.weight)
+        ws = (x.shape[3] + 6) // 2
+        kernel = (STEM_KERNEL and x.dtype == torch.bfloat16 and conv.out_channels == 64
+                  and 67 <= ws <= 256)
+        y, partial = _StemS2D.apply(x.contiguous(memory_format=torch.channels_last), conv.weight, kernel)
+        if bn_stats and partial is not None:
+            y._dca_bn_partials = partial
+        return y
     return spatial_conv(conv, x)
 
 

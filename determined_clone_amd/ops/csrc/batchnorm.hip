@@ -1040,27 +1040,17 @@ void bn_relu_pool_forward(BnDtype dt, const void* x, void* y, uint8_t* idx, int 
                           int C, const float* gamma, const float* beta, float* running_mean,
                           float* running_var, float momentum, float eps, float* save_mean,
                           float* save_invstd, int64_t* num_batches, float* workspace,
-                          const float* affine_scale, const float* affine_shift, hipStream_t st) {
+                          const float* affine_scale, const float* affine_shift, hipStream_t st,
+                          const float* given_partials, int given_blocks) {
   const PoolGeom g{H, W, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
   const int64_t M = static_cast<int64_t>(N) * H * W;
   const float* scale = affine_scale;
   const float* shift = affine_shift;
-  if (scale == nullptr) {  // training: batch statistics
-    ReduceGeom rg = reduce_geom(C);
-    int B = reduce_blocks(M, C, rg);
-    float* partial = workspace;
-    float* sc = workspace + static_cast<int64_t>(B) * 2 * C;
-    float* sh = sc + C;
-    switch (dt) {
-      case BnDtype::kBF16: launch_reduce<BF16>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, rg, st); break;
-      case BnDtype::kF16: launch_reduce<F16>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, rg, st); break;
-      default: launch_reduce<F32>(false, x, nullptr, nullptr, nullptr, nullptr, M, C, false, partial, B, rg, st); break;
-    }
-    hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
-                       C, M, gamma, beta, running_mean, running_var, momentum, eps, save_mean,
-                       save_invstd, sc, sh, num_batches);
-    scale = sc;
-    shift = sh;
+  if (scale == nullptr) {  // training: batch statistics (reduced here unless the conv epilogue did)
+    scale = forward_affine_from_stats(dt, x, M, C, gamma, beta, running_mean, running_var, momentum,
+                                      eps, save_mean, save_invstd, num_batches, workspace,
+                                      given_partials, given_blocks, st);
+    shift = scale + C;
   }
   const int64_t nout = static_cast<int64_t>(N) * g.Ho * g.Wo * C / 8;
   const int grid = stream_grid(nout, kBlock);

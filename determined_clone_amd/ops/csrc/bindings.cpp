@@ -24,7 +24,8 @@ void bn_relu_pool_forward(BnDtype dt, const void* x, void* y, uint8_t* idx, int 
                           int C, const float* gamma, const float* beta, float* running_mean,
                           float* running_var, float momentum, float eps, float* save_mean,
                           float* save_invstd, int64_t* num_batches, float* workspace,
-                          const float* affine_scale, const float* affine_shift, hipStream_t st);
+                          const float* affine_scale, const float* affine_shift, hipStream_t st,
+                          const float* given_partials = nullptr, int given_blocks = 0);
 void bn_relu_pool_backward(BnDtype dt, const void* dyp, const uint8_t* idx, const void* x, int N,
                            int H, int W, int C, const float* gamma, const float* save_mean,
                            const float* save_invstd, void* dx, float* dgamma, float* dbeta,
@@ -335,7 +336,8 @@ std::vector<Tensor> bn_bwd_train_dual(const Tensor& dy_in, const Tensor& x, cons
 // x: NHWC (channels_last) [N, C, H, W]. Returns (y_pool, save_mean, save_invstd, idx).
 std::vector<Tensor> bn_pool_fwd_train(const Tensor& x, const OptT& weight, const OptT& bias,
                                       const OptT& running_mean, const OptT& running_var,
-                                      const OptT& num_batches, double momentum, double eps) {
+                                      const OptT& num_batches, double momentum, double eps,
+                                      const OptT& partials) {
   CHECK_DEV(x);
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0,
               "bn_pool: channels_last [N, C%8==0, H, W] input required");
@@ -347,13 +349,17 @@ std::vector<Tensor> bn_pool_fwd_train(const Tensor& x, const OptT& weight, const
   Tensor idx = torch::empty({static_cast<int64_t>(N) * Ho * Wo * C}, x.options().dtype(at::kByte));
   Tensor save_mean = torch::empty({C}, fopt), save_invstd = torch::empty({C}, fopt);
   Tensor ws = torch::empty({dca::bn_workspace_floats(static_cast<int64_t>(N) * H * W, C)}, fopt);
+  // partials: (sum, sum^2) per block already reduced by x's producer (the stem conv epilogue)
+  const bool given = partials.has_value() && partials->defined();
+  check_partials(partials, C, x);
   dca::bn_relu_pool_forward(bn_dtype(x), x.data_ptr(), y.data_ptr(), idx.data_ptr<uint8_t>(), N, H, W, C,
                             ptr_or_null<float>(weight), ptr_or_null<float>(bias),
                             ptr_or_null<float>(running_mean), ptr_or_null<float>(running_var),
                             static_cast<float>(momentum), static_cast<float>(eps),
                             save_mean.data_ptr<float>(), save_invstd.data_ptr<float>(),
                             ptr_or_null<int64_t>(num_batches), ws.data_ptr<float>(), nullptr, nullptr,
-                            cur_stream());
+                            cur_stream(), given ? partials->data_ptr<float>() : nullptr,
+                            given ? static_cast<int>(partials->size(0)) : 0);
   return {y, save_mean, save_invstd, idx};
 }
 
@@ -591,7 +597,10 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("relu"), pybind11::arg("need_dres"), pybind11::arg("need_dweight"),
         pybind11::arg("dy2") = pybind11::none(), pybind11::arg("dweight_acc") = pybind11::none(),
         pybind11::arg("dbias_acc") = pybind11::none(), pybind11::arg("partials") = pybind11::none());
-  m.def("bn_pool_fwd_train", &bn_pool_fwd_train);
+  m.def("bn_pool_fwd_train", &bn_pool_fwd_train, pybind11::arg("x"), pybind11::arg("weight"),
+        pybind11::arg("bias"), pybind11::arg("running_mean"), pybind11::arg("running_var"),
+        pybind11::arg("num_batches"), pybind11::arg("momentum"), pybind11::arg("eps"),
+        pybind11::arg("partials") = pybind11::none());
   m.def("bn_pool_fwd_affine", &bn_pool_fwd_affine);
   m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("spatial_mean_bwd", &spatial_mean_bwd);

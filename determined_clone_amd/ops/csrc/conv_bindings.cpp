@@ -184,26 +184,52 @@ void strided_accumulate(Tensor& dx, const Tensor& small, int64_t s) {
                           static_cast<int>(Wo), static_cast<int>(s), stream());
 }
 
-// [N, 3, H, W] channels_last bf16 image -> [N, 12, (H+6)/2, (W+6)/2] channels_last (ops/conv.py
-// _s2d_input: the space-to-depth form of the 7x7/2 padding-3 stem convolution).
-Tensor stem_s2d(const Tensor& x) {
+// [N, 3, H, W] channels_last bf16 image -> [N, co, (H+6)/2, (W+6)/2] channels_last (ops/conv.py
+// _s2d_input: the space-to-depth form of the 7x7/2 padding-3 stem convolution; co = 12 or 16).
+Tensor stem_s2d(const Tensor& x, int64_t co) {
   const c10::DeviceGuard dg(x.device());
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3,
               "stem_s2d: bf16 [N, 3, H, W] GPU tensor required");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "stem_s2d: channels_last layout required");
+  TORCH_CHECK(co == 12 || co == 16, "stem_s2d: co must be 12 or 16");
   const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
   TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "stem_s2d: even H and W required");
-  TORCH_CHECK(N * (H + 6) * (W + 6) * 3 < (int64_t{1} << 40), "stem_s2d: too large");
-  Tensor xs = torch::empty({N, 12, (H + 6) / 2, (W + 6) / 2},
+  TORCH_CHECK(N * (H + 6) * (W + 6) * 4 < (int64_t{1} << 40), "stem_s2d: too large");
+  Tensor xs = torch::empty({N, co, (H + 6) / 2, (W + 6) / 2},
                            x.options().memory_format(at::MemoryFormat::ChannelsLast));
   if (xs.numel() == 0) return xs;
   dca::stem_s2d(x.data_ptr(), xs.data_ptr(), static_cast<int>(N), static_cast<int>(H),
-                static_cast<int>(W), stream());
+                static_cast<int>(W), static_cast<int>(co), stream());
   return xs;
 }
 
+// Stem convolution on the 16-channel S2D tensor (ops/conv.py _StemS2D): xs [N, 16, Hs, Ws] and
+// w16 [64, 16, 4, 4], both channels_last bf16 -> (y [N, 64, Hs-3, Ws-3] channels_last, partial
+// statistics [blocks, 2, 64] fp32 for the stem BatchNorm).
+std::vector<Tensor> stem_conv_fwd(const Tensor& xs, const Tensor& w16) {
+  const c10::DeviceGuard dg(xs.device());
+  TORCH_CHECK(xs.is_cuda() && xs.scalar_type() == at::kBFloat16 && xs.dim() == 4 && xs.size(1) == 16 &&
+                  xs.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_conv_fwd: channels_last bf16 [N, 16, Hs, Ws] input required");
+  TORCH_CHECK(w16.is_cuda() && w16.scalar_type() == at::kBFloat16 && w16.dim() == 4 &&
+                  w16.size(0) == 64 && w16.size(1) == 16 && w16.size(2) == 4 && w16.size(3) == 4 &&
+                  w16.is_contiguous(at::MemoryFormat::ChannelsLast) && w16.device() == xs.device(),
+              "stem_conv_fwd: channels_last bf16 [64, 16, 4, 4] weight required");
+  const int64_t N = xs.size(0), Hs = xs.size(2), Ws = xs.size(3);
+  TORCH_CHECK(Hs >= 4 && Ws - 3 >= 64 && Ws <= 256, "stem_conv_fwd: needs 67 <= Ws <= 256");
+  TORCH_CHECK(N * Hs * Ws * 32 < (int64_t{1} << 31) && N * ((Hs - 3) * (Ws - 3) + 127) / 128 < (int64_t{1} << 31),
+              "stem_conv_fwd: input too large for 32-bit buffer offsets");
+  Tensor y = torch::empty({N, 64, Hs - 3, Ws - 3}, xs.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int blocks = dca::stem_conv_blocks(static_cast<int>(N), static_cast<int>(Hs), static_cast<int>(Ws));
+  Tensor partial = torch::empty({blocks, 2, 64}, xs.options().dtype(at::kFloat));
+  dca::stem_conv_fwd(xs.data_ptr(), w16.data_ptr(), y.data_ptr(), partial.data_ptr<float>(),
+                     static_cast<int>(N), static_cast<int>(Hs), static_cast<int>(Ws), stream());
+  return {y, partial};
+}
+
 void register_conv_ops(pybind11::module& m) {
-  m.def("stem_s2d", &stem_s2d, pybind11::arg("x"));
+  m.def("stem_s2d", &stem_s2d, pybind11::arg("x"), pybind11::arg("co") = 12);
+  m.def("stem_conv_fwd", &stem_conv_fwd, pybind11::arg("xs"), pybind11::arg("w16"));
   m.def("strided_accumulate", &strided_accumulate, pybind11::arg("dx"), pybind11::arg("small"),
         pybind11::arg("stride"));
   m.def("conv_igemm_wgrad", &conv_igemm_wgrad, pybind11::arg("dy"), pybind11::arg("x"),

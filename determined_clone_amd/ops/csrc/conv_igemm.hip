@@ -777,50 +777,66 @@ void strided_accumulate(void* dx, const void* small, int N, int H, int W, int C,
 // Space-to-depth of the 3-channel stem image with its 3-pixel zero padding in the same pass:
 // x [N][H][W][3] (NHWC bf16) -> xs [N][(H+6)/2][(W+6)/2][12], channel (dy, dx, c) of output pixel
 // (i, j) = x[2i+dy-3][2j+dx-3][c] or 0 outside the image. Replaces ATen's pad (fill + copy) and
-// the strided reshape copy (423 us of the ResNet-50 bs-1024 step, profiles/round5_stem_s2d_kernel.txt).
-// Row kernel: each half-block (128 lanes) owns one output row; its two input rows (contiguous,
-// 6W bytes each) come in with 16-byte nontemporal loads into LDS, then every lane emits 8-byte
-// chunks (4 of an output pixel's 12 channels) so the stores are one contiguous run per row.
-// Needs 6W % 16 == 0 (W % 8 == 0); other widths take the per-pixel kernel below.
-constexpr int kS2dMaxW = 1024;
+// the strided reshape copy (423 us of the ResNet-50 bs-1024 step, profiles/round5_stem_conv_kernel_ab.txt).
+// Row kernel: a block owns output rows 2b and 2b+1 (n * Ho + i numbering); each half-block brings
+// its row's two input rows (contiguous, 6W bytes each) into LDS with 16-byte nontemporal loads,
+// then the block writes its 2 * Wo * 24 contiguous output bytes as 16-byte stores (8 channels a
+// lane, 16-byte aligned: 48 * Wo * b). Needs 6W % 16 == 0 (W % 8 == 0); other widths take the
+// per-pixel kernel below. Dynamic LDS: 4 input rows, 24W bytes. CO = 16 appends 4 zero channels
+// per pixel (the stem convolution kernel's 32-byte pixels).
+constexpr int kS2dMaxW = 2048;
+template <int CO>
 __global__ __launch_bounds__(256) void stem_s2d_rows_kernel(const uint16_t* __restrict__ x,
                                                             uint16_t* __restrict__ xs, int rows_out,
                                                             int Wo, int Ho, int W, int H) {
-  __shared__ uint4 tile[2][2][kS2dMaxW * 3 / 8];
+  extern __shared__ uint4 tile[];  // [half][dy][W * 3 / 8]
   const int h = threadIdx.x >> 7, lt = threadIdx.x & 127;
-  const int g = blockIdx.x * 2 + h;  // output row n * Ho + i
-  const bool live = g < rows_out;
-  const int n = live ? g / Ho : 0, i = live ? g - n * Ho : 0;
+  const int g0 = blockIdx.x * 2;
   const int row_vec = W * 3 / 8;  // 16-byte vectors per input row
-  if (live) {
+  if (g0 + h < rows_out) {
+    const int g = g0 + h, n = g / Ho, i = g - n * Ho;
     for (int idx = lt; idx < 2 * row_vec; idx += 128) {
       const int dy = idx >= row_vec, v = idx - dy * row_vec;
       const int r = 2 * i + dy - 3;
-      tile[h][dy][v] = (r >= 0 && r < H)
-                           ? ldnt16(x + (static_cast<int64_t>(n) * H + r) * W * 3 + v * 8)
-                           : make_uint4(0, 0, 0, 0);
+      tile[(2 * h + dy) * row_vec + v] =
+          (r >= 0 && r < H) ? ldnt16(x + (static_cast<int64_t>(n) * H + r) * W * 3 + v * 8)
+                            : make_uint4(0, 0, 0, 0);
     }
   }
   __syncthreads();
-  if (!live) return;
-  const uint16_t* t16 = reinterpret_cast<const uint16_t*>(&tile[h][0][0]);
-  const int row16 = kS2dMaxW * 3;  // LDS row stride in bf16
-  uint2* out = reinterpret_cast<uint2*>(xs + static_cast<int64_t>(g) * Wo * 12);
-  for (int k = lt; k < Wo * 3; k += 128) {
-    const int j = k / 3, q = k - 3 * j;
-    uint32_t v[4];
+  const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tile);
+  const int row_el = Wo * CO;                               // bf16 per output row
+  const int n_el = (g0 + 1 < rows_out ? 2 : 1) * row_el;    // this block's output elements
+  uint4* out = reinterpret_cast<uint4*>(xs + static_cast<int64_t>(g0) * row_el);
+  for (int k = threadIdx.x; k * 8 < n_el; k += 256) {
+    int e = 8 * k;
+    int rr = e >= row_el;
+    int rem = e - rr * row_el;
+    int j = rem / CO, ch = rem - CO * j;
+    uint32_t v[8];
 #pragma unroll
-    for (int e4 = 0; e4 < 4; ++e4) {
-      const int e = 4 * q + e4;  // channel (dy, dx, c) of output pixel j
-      const int dy = e / 6, dx = (e / 3) & 1, c = e % 3;
+    for (int e8 = 0; e8 < 8; ++e8) {
+      const int dy = ch >= 6, dx = (ch - 6 * dy) >= 3, c = ch - 6 * dy - 3 * dx;
       const int col = 2 * j + dx - 3;
-      v[e4] = (col >= 0 && col < W) ? t16[dy * row16 + col * 3 + c] : 0u;
+      v[e8] = (ch < 12 && rr < 2 && col >= 0 && col < W) ? t16[(2 * rr + dy) * row_vec * 8 + col * 3 + c] : 0u;
+      if (++ch == CO) {  // next output pixel (row_el is a multiple of CO: rows wrap on pixels)
+        ch = 0;
+        if (++j == Wo) { j = 0; ++rr; }
+      }
     }
-    out[k] = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+    if (8 * k + 8 <= n_el) {
+      out[k] = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
+    } else {  // odd row count and odd Wo: the last block's run ends inside a 16-byte chunk
+      uint16_t* o16 = reinterpret_cast<uint16_t*>(out + k);
+#pragma unroll
+      for (int e8 = 0; e8 < 8; ++e8)
+        if (e8 < n_el - 8 * k) o16[e8] = static_cast<uint16_t>(v[e8]);
+    }
   }
 }
 
 // Per-pixel fallback for widths the row kernel does not take: one lane per output pixel.
+template <int CO>
 __global__ __launch_bounds__(256) void stem_s2d_kernel(const uint16_t* __restrict__ x,
                                                        uint16_t* __restrict__ xs, int64_t n_pix,
                                                        int Wo, int Ho, int W, int H) {
@@ -830,7 +846,9 @@ __global__ __launch_bounds__(256) void stem_s2d_kernel(const uint16_t* __restric
     const int64_t ni = t / Wo;
     const int i = static_cast<int>(ni % Ho);
     const int64_t n = ni / Ho;
-    uint16_t v[12];
+    uint16_t v[CO];
+#pragma unroll
+    for (int e = 12; e < CO; ++e) v[e] = 0;
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
       const int r = 2 * i + dy - 3;
@@ -844,27 +862,195 @@ __global__ __launch_bounds__(256) void stem_s2d_kernel(const uint16_t* __restric
         for (int c = 0; c < 3; ++c) v[(dy * 2 + dx) * 3 + c] = ok ? __builtin_nontemporal_load(src + c) : 0;
       }
     }
-    uint2* dst = reinterpret_cast<uint2*>(xs + t * 12);
+    uint2* dst = reinterpret_cast<uint2*>(xs + t * CO);
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
+    for (int q = 0; q < CO / 4; ++q)
       dst[q] = make_uint2(v[4 * q] | (static_cast<uint32_t>(v[4 * q + 1]) << 16),
                           v[4 * q + 2] | (static_cast<uint32_t>(v[4 * q + 3]) << 16));
   }
 }
 
-void stem_s2d(const void* x, void* xs, int N, int H, int W, hipStream_t st) {
+template <int CO>
+void stem_s2d_launch(const void* x, void* xs, int N, int H, int W, hipStream_t st) {
   const int Ho = (H + 6) / 2, Wo = (W + 6) / 2;
   const int64_t rows_out = static_cast<int64_t>(N) * Ho;
   if (W % 8 == 0 && W <= kS2dMaxW && rows_out < (int64_t{1} << 31)) {
-    hipLaunchKernelGGL(stem_s2d_rows_kernel, dim3(static_cast<unsigned>((rows_out + 1) / 2)), dim3(256), 0,
-                       st, static_cast<const uint16_t*>(x), static_cast<uint16_t*>(xs),
+    hipLaunchKernelGGL(stem_s2d_rows_kernel<CO>, dim3(static_cast<unsigned>((rows_out + 1) / 2)), dim3(256),
+                       static_cast<size_t>(24) * W, st, static_cast<const uint16_t*>(x), static_cast<uint16_t*>(xs),
                        static_cast<int>(rows_out), Wo, Ho, W, H);
     return;
   }
   const int64_t n_pix = rows_out * Wo;
   const int64_t blocks = std::min<int64_t>((n_pix + 255) / 256, 256 * 64);
-  hipLaunchKernelGGL(stem_s2d_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st,
+  hipLaunchKernelGGL(stem_s2d_kernel<CO>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st,
                      static_cast<const uint16_t*>(x), static_cast<uint16_t*>(xs), n_pix, Wo, Ho, W, H);
+}
+
+void stem_s2d(const void* x, void* xs, int N, int H, int W, int co, hipStream_t st) {
+  if (co == 16) stem_s2d_launch<16>(x, xs, N, H, W, st);
+  else stem_s2d_launch<12>(x, xs, N, H, W, st);
+}
+
+// ---------------------------------------------------------------- ResNet stem convolution
+// The 7x7/2 pad-3 convolution of the 3-channel image (with the stem BatchNorm's statistics in the
+// epilogue), run on the space-to-depth tensor xs [N][Hs][Ws][16] (stem_s2d, CO = 16: channel
+// (dy, dx, c) + 4 zeros) as a 4x4/1 convolution with Kgemm = 4 (di) x 4 (dj) x 16 = 256:
+//   y[n][p][q][k] = sum_{di, dj, c} xs[n][p + di][q + dj][c] * w16[k][di][dj][c],  P = Hs - 3, Q = Ws - 3.
+// MIOpen ran it at 1.1 ms plus a 0.28 ms statistics pass for bs 1024 (round-5 step trace; ~1.15 GB
+// of traffic, 0.3 TFLOP). Structure:
+//  * persistent blocks (2 per CU) walk a contiguous range of 128-pixel tiles (tiles never cross an
+//    image: per image ceil(P*Q / 128)); all 64 output channels of a tile in one block;
+//  * the whole weight (64 x 256 bf16) lives in VGPRs for the kernel (32 bf16x8 fragments a lane);
+//  * a tile's pixels span at most 3 output rows (Q >= 64), so its input is the 6 contiguous S2D
+//    rows from its first row: one lane-linear buffer_load ... lds stream (out-of-range -> zeros),
+//    double-buffered across tiles. 16-B halves of a pixel are XOR-swizzled by bit 3 of the column
+//    on both sides so the 16 lanes of an MFMA fragment read hit distinct banks;
+//  * v_mfma_f32_32x32x16_bf16 on the transposed tile (rows = channels): every lane owns 4
+//    consecutive channels of one pixel -> 8-B LDS writes, 16-B coalesced stores, (sum, sum^2) of
+//    the bf16 outputs kept in registers across tiles and reduced once into partial[block][2][64].
+constexpr int kStemBM = 128, kStemRows = 6, kStemMaxWs = 256;
+
+__global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(
+    const uint16_t* __restrict__ xs, const uint16_t* __restrict__ w16, uint16_t* __restrict__ y,
+    float* __restrict__ partial, int N, int Hs, int Ws, int tiles_per_img, int win_chunks) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int P = Hs - 3, Q = Ws - 3, PQ = P * Q;
+  const int total = N * tiles_per_img;
+  const int t_begin = static_cast<int>(static_cast<int64_t>(blockIdx.x) * total / gridDim.x);
+  const int t_end = static_cast<int>(static_cast<int64_t>(blockIdx.x + 1) * total / gridDim.x);
+  uint16_t* win[2] = {lds, lds + win_chunks * 8};
+  uint16_t* Cs = lds + 2 * win_chunks * 8;  // [kStemBM][64 + 8]
+  constexpr int CS = 72;
+
+  // the weight in registers: fragment (ks, i) = w16[i * 32 + r32][ks * 16 + h * 8 .. + 8]
+  bf16x8 wf[16][2];
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      wf[ks][i] = *reinterpret_cast<const bf16x8*>(w16 + (i * 32 + r32) * 256 + ks * 16 + h * 8);
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(xs), 0, static_cast<int>(static_cast<uint32_t>(N * Hs * Ws) * 32u), 0x00020000);
+  // window loads: LDS chunk L (16 B) = pixel L/2 of the window, half (L & 1) ^ swizzle(column)
+  const int n_ins = win_chunks / kThreads;
+  auto issue = [&](int t, uint16_t* dst) {
+    const int n = t / tiles_per_img, p0 = (t - n * tiles_per_img) * kStemBM / Q;
+    const uint32_t base = static_cast<uint32_t>((n * Hs + p0) * Ws) * 32u;
+    const int used = kStemRows * Ws * 2;
+    for (int j = 0; j < n_ins; ++j) {
+      const int L = (j * 4 + wv) * 64 + lane;
+      const int pl = L >> 1, col = pl % Ws;
+      const uint32_t src = static_cast<uint32_t>(2 * pl + ((L & 1) ^ ((col >> 3) & 1))) * 16u;
+      blds16(xr, L < used ? base + src : kOOB, 0, dst + (j * 4 + wv) * 64 * 8);
+    }
+  };
+
+  const int cc = tid & 7, rr = tid >> 3;  // epilogue: 16-B chunk of a row, first row
+  float s8[8], q8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
+
+  // tile t's bf16 output (in Cs) -> 16-B coalesced stores + statistics. Runs one iteration late,
+  // before the next window's loads are issued, so the vmcnt(0) at the end of an iteration finds
+  // both the stores and the prefetch long done instead of waiting out a store's latency per tile.
+  auto store_out = [&](int t) {
+    const int n = t / tiles_per_img, m0 = (t - n * tiles_per_img) * kStemBM;
+    uint16_t* yt = y + (static_cast<int64_t>(n) * PQ + m0) * 64;
+    for (int row = rr; row < kStemBM; row += kThreads / 8) {
+      if (m0 + row >= PQ) break;
+      const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CS + cc * 8);
+      *reinterpret_cast<uint4*>(yt + row * 64 + cc * 8) = v;
+      const float f[8] = {bf16_lo(v.x), bf16_hi(v.x), bf16_lo(v.y), bf16_hi(v.y),
+                          bf16_lo(v.z), bf16_hi(v.z), bf16_lo(v.w), bf16_hi(v.w)};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] = fmaf(f[k], f[k], q8[k]); }
+    }
+  };
+
+  if (t_begin < t_end) issue(t_begin, win[0]);
+  wait_vmcnt<0>();
+  barrier_raw();
+  int buf = 0;
+  for (int t = t_begin; t < t_end; ++t) {
+    if (t > t_begin) store_out(t - 1);  // Cs holds tile t-1 (published by the last barrier)
+    if (t + 1 < t_end) issue(t + 1, win[buf ^ 1]);
+    const int n = t / tiles_per_img, m0 = (t - n * tiles_per_img) * kStemBM, p0 = m0 / Q;
+    int m = m0 + wv * 32 + r32;
+    if (m >= PQ) m = m0;  // masked pixel of the last tile: any valid address, never stored
+    const int p = m / Q, q = m - p * Q;
+    const int pix = (p - p0) * Ws + q;
+    const uint16_t* wb = win[buf];
+    f32x16 acc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+#pragma unroll
+    for (int di = 0; di < 4; ++di)
+#pragma unroll
+      for (int dj = 0; dj < 4; ++dj) {
+        const int ks = di * 4 + dj;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(
+            wb + (pix + di * Ws + dj) * 16 + ((h ^ (((q + dj) >> 3) & 1)) << 3));
+        acc[0] = mfma32(wf[ks][0], a, acc[0]);
+        acc[1] = mfma32(wf[ks][1], a, acc[1]);
+      }
+    // every wave has read Cs (store_out of tile t-1) before it is overwritten
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier_raw();
+    const int ml = wv * 32 + r32;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        uint2 pk;
+        pk.x = pack_bf16x2(acc[i][4 * q4 + 0], acc[i][4 * q4 + 1]);
+        pk.y = pack_bf16x2(acc[i][4 * q4 + 2], acc[i][4 * q4 + 3]);
+        *reinterpret_cast<uint2*>(Cs + ml * CS + i * 32 + 8 * q4 + 4 * h) = pk;
+      }
+    // Cs holds tile t, window t+1 landed, every wave is done with win[buf]
+    wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier_raw();
+    buf ^= 1;
+  }
+  if (t_begin < t_end) {
+    store_out(t_end - 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier_raw();  // Cs reads done before the statistics reuse the LDS
+  }
+  // per-block statistics: [32 rows][8 chunks][16] -> partial[block][0 / 1][64]
+  float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[rr * 128 + cc * 16 + k] = s8[k];
+    red[rr * 128 + cc * 16 + 8 + k] = q8[k];
+  }
+  __syncthreads();
+  if (tid < 128) {
+    float a = 0.f;
+    for (int j = 0; j < kThreads / 8; ++j) a += red[j * 128 + tid];
+    const int ch = (tid >> 4) * 8 + (tid & 7);
+    partial[(static_cast<int64_t>(blockIdx.x) * 2 + ((tid >> 3) & 1)) * 64 + ch] = a;
+  }
+}
+
+int stem_conv_blocks(int N, int Hs, int Ws) {
+  const int tiles = N * (((Hs - 3) * (Ws - 3) + kStemBM - 1) / kStemBM);
+  return std::max(1, std::min(tiles, 2 * 256));
+}
+
+void stem_conv_fwd(const void* xs, const void* w16, void* y, float* partial, int N, int Hs, int Ws,
+                   hipStream_t st) {
+  const int tiles_per_img = ((Hs - 3) * (Ws - 3) + kStemBM - 1) / kStemBM;
+  const int win_chunks = (kStemRows * Ws * 2 + kThreads - 1) / kThreads * kThreads;
+  const size_t lds = static_cast<size_t>(2 * win_chunks) * 16 + kStemBM * 72 * 2;
+  hipLaunchKernelGGL(stem_conv_kernel, dim3(stem_conv_blocks(N, Hs, Ws)), dim3(kThreads), lds, st,
+                     static_cast<const uint16_t*>(xs), static_cast<const uint16_t*>(w16),
+                     static_cast<uint16_t*>(y), partial, N, Hs, Ws, tiles_per_img, win_chunks);
 }
 
 void conv_flip_transpose(const void* w, void* wt, int K, int C, int RS, hipStream_t st) {

@@ -205,6 +205,57 @@ def test_stem_s2d_kernel_matches_pad_and_reshape(hw):
     assert torch.equal(xs, ref)
 
 
+@pytest.mark.parametrize("hw", [(224, 224), (96, 150), (130, 130)])
+def test_stem_conv_kernel_output_and_statistics(monkeypatch, hw):
+    """stem_conv_kernel (7x7/2 as a 4x4/1 MFMA conv on the 16-channel S2D tensor) equals the fp32
+    7x7 convolution, and its epilogue statistics equal (sum, sum^2) of the bf16 output it wrote
+    -- including a last tile of an image that is only partly filled (96x150, 130x130)."""
+    monkeypatch.setattr(conv, "STEM_KERNEL", True)
+    torch.manual_seed(0)
+    c = nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(3, 3, *hw, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = conv.stem_conv(c, x, bn_stats=True)
+    p = y._dca_bn_partials
+    assert p is not None and p.dtype == torch.float32 and p.shape[1:] == (2, 64)
+    ref = F.conv2d(x.float(), c.weight.float(), stride=2, padding=3)
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.shape == ref.shape
+    _close(y, ref, 2e-2, "stem kernel fwd")
+    yf = y.float()
+    torch.testing.assert_close(p[:, 0].sum(0), yf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(p[:, 1].sum(0), (yf * yf).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+
+
+def test_stem_bn_relu_pool_uses_conv_statistics(monkeypatch):
+    """ResNet stem with the conv-epilogue statistics: BN + ReLU + max-pool output, running stats
+    and the BN parameter gradients match the unfused fp32 reference."""
+    from determined_clone_amd.ops import batchnorm as bn_ops
+
+    monkeypatch.setattr(conv, "STEM_KERNEL", True)
+    torch.manual_seed(0)
+    c = nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+    bn = nn.BatchNorm2d(64).cuda()
+    bn.weight.data.uniform_(0.5, 1.5)
+    bn.bias.data.uniform_(-0.2, 0.2)
+    rm, rv = bn.running_mean.clone(), bn.running_var.clone()
+    x = torch.randn(4, 3, 224, 224, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = conv.stem_conv(c, x, bn_stats=True)
+    assert getattr(y, "_dca_bn_partials", None) is not None
+    out = bn_ops.batch_norm_relu_maxpool(y, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                         training=True, momentum=0.1, eps=1e-5,
+                                         num_batches_tracked=bn.num_batches_tracked)
+    yr = y.detach().float().requires_grad_(False)
+    w, b = bn.weight.detach().clone().requires_grad_(), bn.bias.detach().clone().requires_grad_()
+    ref = F.max_pool2d(F.relu(F.batch_norm(yr, rm, rv, w, b, True, 0.1, 1e-5)), 3, 2, 1)
+    _close(out, ref, 2e-2, "stem bn-relu-pool")
+    torch.testing.assert_close(bn.running_mean, rm, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(bn.running_var, rv, rtol=1e-3, atol=1e-4)
+    g = torch.randn_like(ref)
+    out.backward(g.to(out.dtype))
+    ref.backward(g)
+    _close(bn.weight.grad, w.grad, 2e-2, "stem bn dgamma")
+    _close(bn.bias.grad, b.grad, 2e-2, "stem bn dbeta")
+
+
 @pytest.mark.parametrize("side", [True, False])
 @pytest.mark.parametrize("hw", [(224, 224), (64, 48)])
 def test_stem_space_to_depth_matches_fp32(monkeypatch, side, hw):
