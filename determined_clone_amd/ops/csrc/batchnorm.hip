@@ -719,52 +719,64 @@ __global__ __launch_bounds__(kBlock) void bn_relu_pool_fwd_kernel(
   }
 }
 
-// Pre-pool gradient of 8 channels at input position (n, h, w): sum of pooled gradients whose
-// argmax is this position and whose ReLU passed.
+// BN-backward statistics and apply passes of the stem (BN + ReLU + max-pool), in quad form: one
+// thread per 2x2 block of pre-pool positions (rows 2hb, 2hb+1, columns 2wb, 2wb+1) and 8 channels. Such a block is covered by exactly the pooled windows
+// (hb + a, wb + b), a, b in {0, 1} (3x3 / stride 2 / padding 1), so the thread loads those 4
+// (gradient, slot byte) pairs ONCE for its 4 positions -- the per-position gather loaded them 4
+// times (9 loads per position -> 3): 0.95 -> 0.59 ms and 1.10 -> 0.92 ms for the bs-1024 stem,
+// +0.6 % on the ResNet-50 step (profiles/round5_stem_pool_bwd_quad_ab.txt).
 template <typename T>
-__device__ __forceinline__ void gather_pool_grad(const void* __restrict__ dyp, const uint8_t* __restrict__ idx,
-                                                 int64_t n, int h, int w, int c, int C, const PoolGeom& g,
-                                                 float* out) {
+__device__ __forceinline__ void gather_pool_grad_quad(const void* __restrict__ dyp,
+                                                      const uint8_t* __restrict__ idx, int64_t n,
+                                                      int hb, int wb, int c, int C,
+                                                      const PoolGeom& g, float (&gr)[4][8]) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) out[k] = 0.f;
+  for (int p = 0; p < 4; ++p)
 #pragma unroll
-  for (int dh = 0; dh < 2; ++dh) {
-    const int ho = (h + 1) / 2 - dh;
-    const int kh = h - 2 * ho + 1;
-    if (ho < 0 || ho >= g.Ho || kh > 2) continue;
+    for (int k = 0; k < 8; ++k) gr[p][k] = 0.f;
 #pragma unroll
-    for (int dw = 0; dw < 2; ++dw) {
-      const int wo = (w + 1) / 2 - dw;
-      const int kw = w - 2 * wo + 1;
-      if (wo < 0 || wo >= g.Wo || kw > 2) continue;
-      const uint32_t want = static_cast<uint32_t>(kh * 3 + kw) | 0x10u;
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int ho = hb + a, wo = wb + b;
+      if (ho >= g.Ho || wo >= g.Wo) continue;
       const int64_t off = ((n * g.Ho + ho) * g.Wo + wo) * C + c;
       const uint2 ib = *reinterpret_cast<const uint2*>(idx + off);
       float d[8];
       Vec8<T>::load(reinterpret_cast<const char*>(dyp) + off * Vec8<T>::bytes, d);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t byte = ((k < 4 ? ib.x : ib.y) >> (8 * (k & 3))) & 0xffu;
-        if (byte == want) out[k] += d[k];
+      for (int dh = 0; dh < 2; ++dh) {
+#pragma unroll
+        for (int dw = 0; dw < 2; ++dw) {
+          // position (2hb + dh, 2wb + dw) is tap (kh, kw) of window (ho, wo)
+          const int kh = dh + 1 - 2 * a, kw = dw + 1 - 2 * b;
+          if (kh < 0 || kh > 2 || kw < 0 || kw > 2) continue;
+          const uint32_t want = static_cast<uint32_t>(kh * 3 + kw) | 0x10u;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t byte = ((k < 4 ? ib.x : ib.y) >> (8 * (k & 3))) & 0xffu;
+            if (byte == want) gr[dh * 2 + dw][k] += d[k];
+          }
+        }
       }
     }
   }
 }
 
-// Row (n, h, w) of the pre-pool tensor; M < 2^31 is checked on the host (32-bit division).
-__device__ __forceinline__ void pool_row(int64_t r, const PoolGeom& g, int64_t& n, int& h, int& w) {
-  const uint32_t ru = static_cast<uint32_t>(r);
-  const uint32_t nh = ru / static_cast<uint32_t>(g.W);
-  w = static_cast<int>(ru - nh * static_cast<uint32_t>(g.W));
-  const uint32_t nn = nh / static_cast<uint32_t>(g.H);
-  h = static_cast<int>(nh - nn * static_cast<uint32_t>(g.H));
+// quad q -> (n, hb, wb); Q = N * Hb * Wb < 2^31 (host check)
+__device__ __forceinline__ void pool_quad(int64_t q, int Hb, int Wb, int64_t& n, int& hb, int& wb) {
+  const uint32_t qu = static_cast<uint32_t>(q);
+  const uint32_t nh = qu / static_cast<uint32_t>(Wb);
+  wb = static_cast<int>(qu - nh * static_cast<uint32_t>(Wb));
+  const uint32_t nn = nh / static_cast<uint32_t>(Hb);
+  hb = static_cast<int>(nh - nn * static_cast<uint32_t>(Hb));
   n = nn;
 }
 
-template <typename T, int U>
-__global__ __launch_bounds__(kBlock) void bn_pool_reduce_bwd_kernel(
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_pool_reduce_bwd_quad_kernel(
     const void* __restrict__ x, const void* __restrict__ dyp, const uint8_t* __restrict__ idx,
-    const float* __restrict__ mean, int64_t M, int C, int tpr, int rpi, PoolGeom g,
+    const float* __restrict__ mean, int64_t Qn, int C, int tpr, int rpi, PoolGeom g,
     float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
@@ -772,33 +784,32 @@ __global__ __launch_bounds__(kBlock) void bn_pool_reduce_bwd_kernel(
   const int c = (blockIdx.y * tpr + lc) * 8;
   const bool active = c < C;
   const int bx = static_cast<int>(gridDim.x) - 1 - static_cast<int>(blockIdx.x);
-  const RowRange rr = chunk_rows(M, rpi, bx, gridDim.x);
+  const RowRange rr = chunk_rows(Qn, rpi, bx, gridDim.x);
+  const int Hb = (g.H + 1) / 2, Wb = (g.W + 1) / 2;
   float s[8], q[8], mu[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; mu[k] = active ? mean[c + k] : 0.f; }
   if (active) {
-    int64_t r = rr.begin + r0;
-    for (; r < rr.end; r += U * rpi) {
-      Raw8<T> rx[U];
-      float gr[U][8];
+    for (int64_t r = rr.begin + r0; r < rr.end; r += rpi) {
+      int64_t n;
+      int hb, wb;
+      pool_quad(r, Hb, Wb, n, hb, wb);
+      Raw8<T> rx[4];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t ru = r + u * rpi;
-        if (ru < rr.end) {
-          rx[u] = ld8<T>(x, ru * C + c);
-          int64_t n;
-          int h, w;
-          pool_row(ru, g, n, h, w);
-          gather_pool_grad<T>(dyp, idx, n, h, w, c, C, g, gr[u]);
-        }
+      for (int p = 0; p < 4; ++p) {
+        const int h = 2 * hb + (p >> 1), w = 2 * wb + (p & 1);
+        if (h < g.H && w < g.W) rx[p] = ld8<T>(x, ((n * g.H + h) * g.W + w) * C + c);
       }
+      float gr[4][8];
+      gather_pool_grad_quad<T>(dyp, idx, n, hb, wb, c, C, g, gr);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (r + u * rpi < rr.end) {
+      for (int p = 0; p < 4; ++p) {
+        const int h = 2 * hb + (p >> 1), w = 2 * wb + (p & 1);
+        if (h < g.H && w < g.W) {
           float xv[8];
-          unpack8<T>(rx[u], xv);
+          unpack8<T>(rx[p], xv);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) { s[k] += gr[u][k]; q[k] = fmaf(gr[u][k], xv[k] - mu[k], q[k]); }
+          for (int k = 0; k < 8; ++k) { s[k] += gr[p][k]; q[k] = fmaf(gr[p][k], xv[k] - mu[k], q[k]); }
         }
       }
     }
@@ -817,43 +828,42 @@ __global__ __launch_bounds__(kBlock) void bn_pool_reduce_bwd_kernel(
   }
 }
 
-template <typename T, int U>
-__global__ __launch_bounds__(kBlock) void bn_pool_apply_bwd_kernel(
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_pool_apply_bwd_quad_kernel(
     const void* __restrict__ x, const void* __restrict__ dyp, const uint8_t* __restrict__ idx,
-    const float* __restrict__ coef, void* __restrict__ dx, int64_t M, int C, int tpr, int rpi,
+    const float* __restrict__ coef, void* __restrict__ dx, int64_t Qn, int C, int tpr, int rpi,
     PoolGeom g) {
   const int tid = threadIdx.x;
   const int lc = tid % tpr, r0 = tid / tpr;
   const BlkMap bm = apply_block_map(C, tpr);
   const int c = (bm.cg * tpr + lc) * 8;
   if (c >= C) return;
-  const RowRange rr = chunk_rows(M, rpi, bm.bx, bm.nb);
+  const RowRange rr = chunk_rows(Qn, rpi, bm.bx, bm.nb);
+  const int Hb = (g.H + 1) / 2, Wb = (g.W + 1) / 2;
   float k1[8], k2[8], k3[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { k1[k] = coef[c + k]; k2[k] = coef[C + c + k]; k3[k] = coef[2 * C + c + k]; }
-  for (int64_t r = rr.begin + r0; r < rr.end; r += U * rpi) {
-    Raw8<T> rx[U];
-    float gr[U][8];
+  for (int64_t r = rr.begin + r0; r < rr.end; r += rpi) {
+    int64_t n;
+    int hb, wb;
+    pool_quad(r, Hb, Wb, n, hb, wb);
+    Raw8<T> rx[4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t ru = r + u * rpi;
-      if (ru < rr.end) {
-        rx[u] = ld8<T>(x, ru * C + c);
-        int64_t n;
-        int h, w;
-        pool_row(ru, g, n, h, w);
-        gather_pool_grad<T>(dyp, idx, n, h, w, c, C, g, gr[u]);
-      }
+    for (int p = 0; p < 4; ++p) {
+      const int h = 2 * hb + (p >> 1), w = 2 * wb + (p & 1);
+      if (h < g.H && w < g.W) rx[p] = ld8<T>(x, ((n * g.H + h) * g.W + w) * C + c);
     }
+    float gr[4][8];
+    gather_pool_grad_quad<T>(dyp, idx, n, hb, wb, c, C, g, gr);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t ru = r + u * rpi;
-      if (ru < rr.end) {
+    for (int p = 0; p < 4; ++p) {
+      const int h = 2 * hb + (p >> 1), w = 2 * wb + (p & 1);
+      if (h < g.H && w < g.W) {
         float xv[8], o[8];
-        unpack8<T>(rx[u], xv);
+        unpack8<T>(rx[p], xv);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], gr[u][k], fmaf(k2[k], xv[k], k3[k]));
-        st8<T>(dx, ru * C + c, o);
+        for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], gr[p][k], fmaf(k2[k], xv[k], k3[k]));
+        st8<T>(dx, ((n * g.H + h) * g.W + w) * C + c, o);
       }
     }
   }
@@ -1071,20 +1081,23 @@ void bn_relu_pool_backward(BnDtype dt, const void* dyp, const uint8_t* idx, cons
   int B = reduce_blocks(M, C, rg);
   float* partial = workspace;
   float* coef = workspace + static_cast<int64_t>(B) * 2 * C;
-  dim3 grid(B, rg.cgroups);
   size_t lds = static_cast<size_t>(rg.rpi) * rg.tpr * 16 * sizeof(float);
+  const int64_t Qn = static_cast<int64_t>(N) * ((H + 1) / 2) * ((W + 1) / 2);
+  const int64_t qiters = (Qn + rg.rpi - 1) / rg.rpi;
+  if (B > qiters) B = static_cast<int>(qiters);
+  dim3 grid(B, rg.cgroups);
   switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL((bn_pool_reduce_bwd_kernel<BF16, 2>), grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
-    case BnDtype::kF16: hipLaunchKernelGGL((bn_pool_reduce_bwd_kernel<F16, 2>), grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
-    default: hipLaunchKernelGGL((bn_pool_reduce_bwd_kernel<F32, 2>), grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, M, C, rg.tpr, rg.rpi, g, partial); break;
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_pool_reduce_bwd_quad_kernel<BF16>, grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, Qn, C, rg.tpr, rg.rpi, g, partial); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_pool_reduce_bwd_quad_kernel<F16>, grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, Qn, C, rg.tpr, rg.rpi, g, partial); break;
+    default: hipLaunchKernelGGL(bn_pool_reduce_bwd_quad_kernel<F32>, grid, dim3(kBlock), lds, st, x, dyp, idx, save_mean, Qn, C, rg.tpr, rg.rpi, g, partial); break;
   }
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 7) / 8), dim3(kBlock), 0, st, partial, B,
                      C, M, gamma, save_mean, save_invstd, dgamma, dbeta, false, coef);
-  dim3 ag(apply_blocks(M, rg, ApplyTuning{kUApply, 2048}), rg.cgroups);
+  dim3 ag(apply_blocks(Qn, rg, ApplyTuning{1, 2048}), rg.cgroups);
   switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<BF16, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;
-    case BnDtype::kF16: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<F16, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;
-    default: hipLaunchKernelGGL((bn_pool_apply_bwd_kernel<F32, 2>), ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, M, C, rg.tpr, rg.rpi, g); break;
+    case BnDtype::kBF16: hipLaunchKernelGGL(bn_pool_apply_bwd_quad_kernel<BF16>, ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, Qn, C, rg.tpr, rg.rpi, g); break;
+    case BnDtype::kF16: hipLaunchKernelGGL(bn_pool_apply_bwd_quad_kernel<F16>, ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, Qn, C, rg.tpr, rg.rpi, g); break;
+    default: hipLaunchKernelGGL(bn_pool_apply_bwd_quad_kernel<F32>, ag, dim3(kBlock), 0, st, x, dyp, idx, coef, dx, Qn, C, rg.tpr, rg.rpi, g); break;
   }
 }
 
