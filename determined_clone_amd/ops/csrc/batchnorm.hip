@@ -723,45 +723,15 @@ __global__ __launch_bounds__(kBlock) void bn_relu_pool_fwd_kernel(
 // thread per 2x2 block of pre-pool positions (rows 2hb, 2hb+1, columns 2wb, 2wb+1) and 8 channels. Such a block is covered by exactly the pooled windows
 // (hb + a, wb + b), a, b in {0, 1} (3x3 / stride 2 / padding 1), so the thread loads those 4
 // (gradient, slot byte) pairs ONCE for its 4 positions -- the per-position gather loaded them 4
-// times (9 loads per position -> 3): 0.95 -> 0.59 ms and 1.10 -> 0.92 ms for the bs-1024 stem,
+// times (9 loads per position -> 3): 0.95 -> 0.45 ms and 1.10 -> 0.75 ms for the bs-1024 stem (with the prefetch below),
 // +0.6 % on the ResNet-50 step (profiles/round5_stem_pool_bwd_quad_ab.txt).
+// The loads of one quad (issued one quad ahead of their use: the passes are latency-bound at 4
+// waves per SIMD, so the next quad's 12 loads stay in flight while this one is computed).
 template <typename T>
-__device__ __forceinline__ void gather_pool_grad_quad(const void* __restrict__ dyp,
-                                                      const uint8_t* __restrict__ idx, int64_t n,
-                                                      int hb, int wb, int c, int C,
-                                                      const PoolGeom& g, float (&gr)[4][8]) {
-#pragma unroll
-  for (int p = 0; p < 4; ++p)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) gr[p][k] = 0.f;
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int ho = hb + a, wo = wb + b;
-      if (ho >= g.Ho || wo >= g.Wo) continue;
-      const int64_t off = ((n * g.Ho + ho) * g.Wo + wo) * C + c;
-      const uint2 ib = *reinterpret_cast<const uint2*>(idx + off);
-      float d[8];
-      Vec8<T>::load(reinterpret_cast<const char*>(dyp) + off * Vec8<T>::bytes, d);
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh) {
-#pragma unroll
-        for (int dw = 0; dw < 2; ++dw) {
-          // position (2hb + dh, 2wb + dw) is tap (kh, kw) of window (ho, wo)
-          const int kh = dh + 1 - 2 * a, kw = dw + 1 - 2 * b;
-          if (kh < 0 || kh > 2 || kw < 0 || kw > 2) continue;
-          const uint32_t want = static_cast<uint32_t>(kh * 3 + kw) | 0x10u;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const uint32_t byte = ((k < 4 ? ib.x : ib.y) >> (8 * (k & 3))) & 0xffu;
-            if (byte == want) gr[dh * 2 + dw][k] += d[k];
-          }
-        }
-      }
-    }
-  }
-}
+struct QuadLoads {
+  Raw8<T> x[4], dy[4];
+  uint2 ib[4];
+};
 
 // quad q -> (n, hb, wb); Q = N * Hb * Wb < 2^31 (host check)
 __device__ __forceinline__ void pool_quad(int64_t q, int Hb, int Wb, int64_t& n, int& hb, int& wb) {
@@ -771,6 +741,56 @@ __device__ __forceinline__ void pool_quad(int64_t q, int Hb, int Wb, int64_t& n,
   const uint32_t nn = nh / static_cast<uint32_t>(Hb);
   hb = static_cast<int>(nh - nn * static_cast<uint32_t>(Hb));
   n = nn;
+}
+
+template <typename T>
+__device__ __forceinline__ void load_quad(const void* __restrict__ x, const void* __restrict__ dyp,
+                                          const uint8_t* __restrict__ idx, int64_t n, int hb, int wb,
+                                          int c, int C, const PoolGeom& g, QuadLoads<T>& L) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int h = 2 * hb + (p >> 1), w = 2 * wb + (p & 1);
+    if (h < g.H && w < g.W) L.x[p] = ld8<T>(x, ((n * g.H + h) * g.W + w) * C + c);
+    const int ho = hb + (p >> 1), wo = wb + (p & 1);
+    L.ib[p] = make_uint2(0, 0);  // no window -> no slot matches
+    if (ho < g.Ho && wo < g.Wo) {
+      const int64_t off = ((n * g.Ho + ho) * g.Wo + wo) * C + c;
+      L.ib[p] = *reinterpret_cast<const uint2*>(idx + off);
+      L.dy[p] = ld8<T>(dyp, off);
+    }
+  }
+}
+
+// Pre-pool gradient of quad position p = (dh, dw), i.e. (2hb + dh, 2wb + dw): that position is
+// tap (kh, kw) = (dh + 1 - 2a, dw + 1 - 2b) of pooled window (hb + a, wb + b); it receives the
+// window's gradient when the window's slot byte names the tap with the ReLU bit set.
+template <typename T, int P>
+__device__ __forceinline__ void quad_grad(const QuadLoads<T>& L, float (&gp)[8]) {
+  constexpr int dh = P >> 1, dw = P & 1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) gp[k] = 0.f;
+#pragma unroll
+  for (int ab = 0; ab < 4; ++ab) {
+    const int kh = dh + 1 - 2 * (ab >> 1), kw = dw + 1 - 2 * (ab & 1);
+    if (kh < 0 || kh > 2 || kw < 0 || kw > 2) continue;
+    const uint32_t want = static_cast<uint32_t>(kh * 3 + kw) | 0x10u;
+    float d[8];
+    unpack8<T>(L.dy[ab], d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t byte = ((k < 4 ? L.ib[ab].x : L.ib[ab].y) >> (8 * (k & 3))) & 0xffu;
+      if (byte == want) gp[k] += d[k];
+    }
+  }
+}
+
+// the 4 positions of a quad, unrolled with compile-time P
+template <typename F>
+__device__ __forceinline__ void for_quad(F&& f) {
+  f(std::integral_constant<int, 0>{});
+  f(std::integral_constant<int, 1>{});
+  f(std::integral_constant<int, 2>{});
+  f(std::integral_constant<int, 3>{});
 }
 
 template <typename T>
@@ -789,29 +809,29 @@ __global__ __launch_bounds__(kBlock) void bn_pool_reduce_bwd_quad_kernel(
   float s[8], q[8], mu[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { s[k] = 0.f; q[k] = 0.f; mu[k] = active ? mean[c + k] : 0.f; }
-  if (active) {
+  if (active && rr.begin + r0 < rr.end) {
+    int64_t n;
+    int hb, wb;
+    pool_quad(rr.begin + r0, Hb, Wb, n, hb, wb);
+    QuadLoads<T> nxt;
+    load_quad<T>(x, dyp, idx, n, hb, wb, c, C, g, nxt);
     for (int64_t r = rr.begin + r0; r < rr.end; r += rpi) {
-      int64_t n;
-      int hb, wb;
-      pool_quad(r, Hb, Wb, n, hb, wb);
-      Raw8<T> rx[4];
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int h = 2 * hb + (p >> 1), w = 2 * wb + (p & 1);
-        if (h < g.H && w < g.W) rx[p] = ld8<T>(x, ((n * g.H + h) * g.W + w) * C + c);
+      const QuadLoads<T> cur = nxt;
+      const int chb = hb, cwb = wb;
+      if (r + rpi < rr.end) {
+        pool_quad(r + rpi, Hb, Wb, n, hb, wb);
+        load_quad<T>(x, dyp, idx, n, hb, wb, c, C, g, nxt);
       }
-      float gr[4][8];
-      gather_pool_grad_quad<T>(dyp, idx, n, hb, wb, c, C, g, gr);
+      for_quad([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        if (2 * chb + (p >> 1) < g.H && 2 * cwb + (p & 1) < g.W) {
+          float gp[8], xv[8];
+          quad_grad<T, p>(cur, gp);
+          unpack8<T>(cur.x[p], xv);
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int h = 2 * hb + (p >> 1), w = 2 * wb + (p & 1);
-        if (h < g.H && w < g.W) {
-          float xv[8];
-          unpack8<T>(rx[p], xv);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) { s[k] += gr[p][k]; q[k] = fmaf(gr[p][k], xv[k] - mu[k], q[k]); }
+          for (int k = 0; k < 8; ++k) { s[k] += gp[k]; q[k] = fmaf(gp[k], xv[k] - mu[k], q[k]); }
         }
-      }
+      });
     }
   }
   const int width = tpr * 16;
@@ -839,33 +859,36 @@ __global__ __launch_bounds__(kBlock) void bn_pool_apply_bwd_quad_kernel(
   const int c = (bm.cg * tpr + lc) * 8;
   if (c >= C) return;
   const RowRange rr = chunk_rows(Qn, rpi, bm.bx, bm.nb);
+  if (rr.begin + r0 >= rr.end) return;
   const int Hb = (g.H + 1) / 2, Wb = (g.W + 1) / 2;
   float k1[8], k2[8], k3[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { k1[k] = coef[c + k]; k2[k] = coef[C + c + k]; k3[k] = coef[2 * C + c + k]; }
+  int64_t n;
+  int hb, wb;
+  pool_quad(rr.begin + r0, Hb, Wb, n, hb, wb);
+  QuadLoads<T> nxt;
+  load_quad<T>(x, dyp, idx, n, hb, wb, c, C, g, nxt);
   for (int64_t r = rr.begin + r0; r < rr.end; r += rpi) {
-    int64_t n;
-    int hb, wb;
-    pool_quad(r, Hb, Wb, n, hb, wb);
-    Raw8<T> rx[4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int h = 2 * hb + (p >> 1), w = 2 * wb + (p & 1);
-      if (h < g.H && w < g.W) rx[p] = ld8<T>(x, ((n * g.H + h) * g.W + w) * C + c);
+    const QuadLoads<T> cur = nxt;
+    const int64_t cn = n;
+    const int chb = hb, cwb = wb;
+    if (r + rpi < rr.end) {
+      pool_quad(r + rpi, Hb, Wb, n, hb, wb);
+      load_quad<T>(x, dyp, idx, n, hb, wb, c, C, g, nxt);
     }
-    float gr[4][8];
-    gather_pool_grad_quad<T>(dyp, idx, n, hb, wb, c, C, g, gr);
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int h = 2 * hb + (p >> 1), w = 2 * wb + (p & 1);
+    for_quad([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      const int h = 2 * chb + (p >> 1), w = 2 * cwb + (p & 1);
       if (h < g.H && w < g.W) {
-        float xv[8], o[8];
-        unpack8<T>(rx[p], xv);
+        float gp[8], xv[8], o[8];
+        quad_grad<T, p>(cur, gp);
+        unpack8<T>(cur.x[p], xv);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], gr[p][k], fmaf(k2[k], xv[k], k3[k]));
-        st8<T>(dx, ((n * g.H + h) * g.W + w) * C + c, o);
+        for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], gp[k], fmaf(k2[k], xv[k], k3[k]));
+        st8<T>(dx, ((cn * g.H + h) * g.W + w) * C + c, o);
       }
-    }
+    });
   }
 }
 
