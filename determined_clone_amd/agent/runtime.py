@@ -104,6 +104,13 @@ def build_task(spec: Dict[str, Any], master_url: str, agent_id: str,
             raise RuntimeError(f"task {task_id}: {len(mine)} slots map to only {len(phys)} "
                                "GPU(s); --slots-per-gpu > 1 supports single-slot trials only")
         env["HIP_VISIBLE_DEVICES"] = ",".join(str(i) for i in phys)
+        if len(devices) > len({int(d.get("device_index", d["id"])) for d in devices}):
+            # --slots-per-gpu > 1: many single-slot trials share this node's cores. Split the
+            # agent's CPU-thread budget among the slots, or each trial process starts a full
+            # OpenMP / torch intra-op pool (16 trials x 16 threads on a 16-core share).
+            budget = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+            if "OMP_NUM_THREADS" not in _user_env(spec):
+                env["OMP_NUM_THREADS"] = str(max(1, budget * len(mine) // len(devices)))
     else:
         env["DET_SLOTS"] = str(max(len(mine), 1))
         # CPU slots: give each task its share of the host's cores so concurrent trials do not

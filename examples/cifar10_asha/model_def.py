@@ -21,9 +21,10 @@ class CIFARTrial(pytorch.PyTorchTrial):
             weight_decay=hp.get("weight_decay", 5e-4)))
 
     def _prep(self, x):
+        # fp16 records (the dataset's stored precision) -> fp32, NHWC on the GPU: one kernel
         if self.context.device.type == "cuda":
-            return x.contiguous(memory_format=torch.channels_last)
-        return x
+            return x.to(dtype=torch.float32, memory_format=torch.channels_last)
+        return x.float()
 
     def train_batch(self, batch, epoch_idx, batch_idx):
         x, y = batch
@@ -45,10 +46,11 @@ class CIFARTrial(pytorch.PyTorchTrial):
 
     def build_training_data_loader(self):
         n = int(self.context.get_hparams().get("train_records", 50000))
-        return pytorch.DataLoader(cifar.SyntheticCIFAR10(n, seed=0),
+        return pytorch.DataLoader(cifar.SyntheticCIFAR10(n, seed=0), collate_fn=cifar.collate,
                                   batch_size=self.context.get_per_slot_batch_size(), shuffle=True)
 
     def build_validation_data_loader(self):
         n = int(self.context.get_hparams().get("val_records", 10000))
         return pytorch.DataLoader(cifar.SyntheticCIFAR10(n, seed=1, label_noise=0.0),
+                                  collate_fn=cifar.collate,
                                   batch_size=self.context.get_per_slot_batch_size())

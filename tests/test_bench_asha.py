@@ -52,6 +52,14 @@ def test_synthetic_cifar_is_learnable_but_noisy():
 
     tr, va = SyntheticCIFAR10(2000, seed=0), SyntheticCIFAR10(500, seed=1, label_noise=0.0)
     assert tr.x.dtype == np.float16 and tr[0][0].shape == (3, 32, 32)
+    # the batched fetch (DataLoader __getitems__ + cifar.collate) equals per-record fetching
+    import torch
+
+    from determined_clone_amd.models.cifar import collate
+
+    bx, by = collate(tr.__getitems__([5, 0, 17]))
+    rx, ry = torch.utils.data.default_collate([tr[5], tr[0], tr[17]])
+    assert torch.equal(bx, rx) and torch.equal(by, ry)
     # nearest-class-mean on raw pixels is far from perfect (position jitter + low signal) ...
     means = np.stack([tr.x[tr.y == c].astype(np.float32).mean(0) for c in range(10)])
     pred = ((va.x.astype(np.float32)[:, None] - means[None]) ** 2).sum((2, 3, 4)).argmin(1)

@@ -63,3 +63,21 @@ def test_master_assigns_distinct_ports_on_shared_chief(tmp_path):
     assert p1 != p2 and all(s["rendezvous_port"] == p1 for s in started[0])
     m._allocation_done(m.allocations["c1"], 0, "done")
     assert p1 not in m.ports.in_use("node-a")
+
+
+def test_shared_gpu_slots_split_the_cpu_thread_budget(tmp_path, monkeypatch):
+    """--slots-per-gpu > 1: each single-slot trial gets its share of the agent's CPU threads
+    (OMP_NUM_THREADS), unless the experiment's environment sets it."""
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    devices = [{"id": i, "uuid": f"g0-{i}", "type": "rocm", "device_index": 0} for i in range(8)]
+    spec = dict(_spec(0, 29417), num_containers=1, slots=[3])
+    _, env = runtime.build_task(spec, "http://m:8080", "agent-1", devices, str(tmp_path), base_env={})
+    assert env["OMP_NUM_THREADS"] == "2"
+    spec["environment"] = {"environment_variables": ["OMP_NUM_THREADS=5"]}
+    _, env = runtime.build_task(spec, "http://m:8080", "agent-1", devices, str(tmp_path), base_env={})
+    assert env["OMP_NUM_THREADS"] == "5"
+    # one slot per GPU: unchanged (inherits the base environment)
+    one = [{"id": 0, "uuid": "g0", "type": "rocm", "device_index": 0}]
+    _, env = runtime.build_task(dict(spec, slots=[0], environment={}), "http://m:8080", "agent-1", one,
+                                str(tmp_path), base_env={})
+    assert "OMP_NUM_THREADS" not in env
