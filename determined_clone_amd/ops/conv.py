@@ -512,6 +512,10 @@ STEM_S2D_KERNEL = os.environ.get("DCA_STEM_S2D_KERNEL", "1") != "0"
 # the step measured -0.3..-2 % in five same-box A/Bs (profiles/round5_stem_conv_kernel_ab.txt).
 # DCA_STEM_KERNEL=1 opts in.
 STEM_KERNEL = os.environ.get("DCA_STEM_KERNEL", "0") == "1"
+# the stem weight gradient on the hand-written MFMA kernel (stem_wgrad_kernel) instead of MIOpen's
+# wrw -- the last kernel of every backward, on the critical path. OFF by default: the kernel is
+# correct but 1.25-1.31 ms against MIOpen's 1.11 (profiles/round5_stem_wgrad_kernel_ab.txt).
+STEM_WGRAD = os.environ.get("DCA_STEM_WGRAD", "0") == "1"
 
 
 def _s2d_input(x: torch.Tensor) -> torch.Tensor:
@@ -575,17 +579,22 @@ class _StemS2D(torch.autograd.Function):
         if dy is None:
             return None, None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
-        args = (dy, xs, w2, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
-        bwd = torch.ops.aten.convolution_backward
         c = weight.shape[1]
+        if (STEM_WGRAD and xs.shape[1] == 12 and xs.dtype == torch.bfloat16 and dy.shape[1] == 64
+                and dy.shape[3] <= 128):
+            # csrc/conv_igemm.hip stem_wgrad_kernel: [64][4][4][12] fp32 -> [64, 12, 4, 4]
+            def wgrad():
+                return _ext.load().stem_wgrad(dy, xs).permute(0, 3, 1, 2)
+        else:
+            def wgrad():
+                args = (dy, xs, w2, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+                return torch.ops.aten.convolution_backward(*args, [False, True, False])[1][:, :4 * c]
         s = _grad.side_stream_for(weight)
         if s is None:
-            dw2 = bwd(*args, [False, True, False])[1]
-            return None, _s2d_weight_grad(dw2[:, :4 * c], c).to(weight.dtype), None
+            return None, _s2d_weight_grad(wgrad(), c).to(weight.dtype), None
         _grad.fork(s, (dy, xs))
         with torch.cuda.stream(s):
-            dw2 = bwd(*args, [False, True, False])[1]
-            _grad.target(weight).add_(_s2d_weight_grad(dw2[:, :4 * c], c))
+            _grad.target(weight).add_(_s2d_weight_grad(wgrad(), c))
         return None, None, None
 
 

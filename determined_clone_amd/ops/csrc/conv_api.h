@@ -33,6 +33,11 @@ void stem_s2d(const void* x, void* xs, int N, int H, int W, int co, hipStream_t 
 // y [N][Hs-3][Ws-3][64] bf16 + BatchNorm partial statistics [stem_conv_blocks()][2][64] fp32.
 // Requires Ws - 3 >= 64 and Ws <= 256.
 int stem_conv_blocks(int N, int Hs, int Ws);
+// Stem weight gradient on the 12-channel S2D tensor: dy [N][Hs-3][Ws-3][64], xs [N][Hs][Ws][12] bf16
+// -> per-block fp32 partials ws [stem_wgrad_blocks(N)][64][4 (di)][4 (dj)][12] (summed by the
+// caller). Requires Ws - 3 <= 128.
+int stem_wgrad_blocks(int N);
+void stem_wgrad(const void* dy, const void* xs, float* ws, int N, int Hs, int Ws, hipStream_t st);
 void stem_conv_fwd(const void* xs, const void* w16, void* y, float* partial, int N, int Hs, int Ws,
                    hipStream_t st);
 // dx [N][H][W][C] += small [N][Ho][Wo][C] at rows s*i, columns s*j (bf16, C a multiple of 8).

@@ -227,9 +227,34 @@ std::vector<Tensor> stem_conv_fwd(const Tensor& xs, const Tensor& w16) {
   return {y, partial};
 }
 
+// Stem weight gradient (ops/conv.py _StemS2D.backward): dy [N, 64, P, Q] and the 12-channel S2D
+// image xs [N, 12, P+3, Q+3], channels_last bf16 -> dw [64, 4, 4, 12] fp32 ((di, dj, channel) order).
+Tensor stem_wgrad(const Tensor& dy, const Tensor& xs) {
+  const c10::DeviceGuard dg(dy.device());
+  TORCH_CHECK(xs.is_cuda() && xs.scalar_type() == at::kBFloat16 && xs.dim() == 4 && xs.size(1) == 12 &&
+                  xs.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_wgrad: channels_last bf16 [N, 12, Hs, Ws] image required");
+  const int64_t N = xs.size(0), Hs = xs.size(2), Ws = xs.size(3);
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N &&
+                  dy.size(1) == 64 && dy.size(2) == Hs - 3 && dy.size(3) == Ws - 3 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.device() == xs.device(),
+              "stem_wgrad: channels_last bf16 [N, 64, Hs-3, Ws-3] gradient required");
+  TORCH_CHECK(Hs >= 4 && Ws >= 4 && Ws - 3 <= 128, "stem_wgrad: output width must be <= 128");
+  TORCH_CHECK(N * Hs * Ws * 12 < (int64_t{1} << 40) && N * (Hs - 3) < (int64_t{1} << 31), "stem_wgrad: too large");
+  const int blocks = dca::stem_wgrad_blocks(static_cast<int>(N));
+  auto fopt = xs.options().dtype(at::kFloat);
+  Tensor ws = torch::empty({blocks, 64, 4, 4, 12}, fopt);
+  dca::stem_wgrad(dy.data_ptr(), xs.data_ptr(), ws.data_ptr<float>(), static_cast<int>(N),
+                  static_cast<int>(Hs), static_cast<int>(Ws), stream());
+  // per-block partials summed by ATen's tree reduction (fixed order; the 12 K outputs x 1 K
+  // partials leave a dedicated kernel too few workgroups: 0.5 ms at 6 blocks)
+  return ws.sum(0);
+}
+
 void register_conv_ops(pybind11::module& m) {
   m.def("stem_s2d", &stem_s2d, pybind11::arg("x"), pybind11::arg("co") = 12);
   m.def("stem_conv_fwd", &stem_conv_fwd, pybind11::arg("xs"), pybind11::arg("w16"));
+  m.def("stem_wgrad", &stem_wgrad, pybind11::arg("dy"), pybind11::arg("xs"));
   m.def("strided_accumulate", &strided_accumulate, pybind11::arg("dx"), pybind11::arg("small"),
         pybind11::arg("stride"));
   m.def("conv_igemm_wgrad", &conv_igemm_wgrad, pybind11::arg("dy"), pybind11::arg("x"),

@@ -531,6 +531,124 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_kernel(
     }
 }
 
+// ResNet stem weight gradient on the 12-channel space-to-depth image (ops/conv.py _StemS2D):
+//   dW[k][j] = sum_pix dy[pix][k] * xs[n][p + di][q * 12 + r],  j = di * 48 + r (r = dj * 12 + c),
+// i.e. the 4x4/1 conv's [64][4][4][12] gradient with K = the N*P*Q output pixels. For output row
+// (n, p) the im2col operand is never built: the 48-element run of tap row di at pixel q is the
+// contiguous S2D row slice starting at q * 12, so ds_read_b64_tr_b16 reads the B fragments straight
+// from 4 S2D rows in LDS (8-B aligned: 24 q + 2 r with r a multiple of 4) and the dy row
+// [128 px (112 + zero tail)][64 ch] gives the A fragments. One block per image (112 output rows),
+// S2D rows in a 4-slot ring (one new row per output row), fp32 partials per image summed by ATen.
+// Correct but SLOWER than MIOpen's wrw (1.25-1.31 ms vs 1.11 ms at bs 1024: each block walks its
+// 112 rows with one exposed load round trip per row; profiles/round5_stem_wgrad_kernel_ab.txt), so
+// opt-in (DCA_STEM_WGRAD=1);
+// 2 x 2 waves over the 64 x 192 result (one 32-channel half x 96 columns each), fp32 tile per block
+// -> stem_wgrad_reduce. MIOpen's wrw ran this in ~0.9 ms, the last kernel before the optimizer.
+constexpr int kStemWgPx = 128;     // dy pixels per LDS row tile (112 + zero tail)
+constexpr int kStemWgDyS = 72;     // dy LDS row stride (elements): 144-B rows, tr reads conflict-free
+
+__global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const uint16_t* __restrict__ dy,
+                                                              const uint16_t* __restrict__ xs,
+                                                              float* __restrict__ ws, int P, int Q,
+                                                              int Hs, int Ws) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* dyL = lds;                                  // [kStemWgPx][kStemWgDyS]
+  uint16_t* xsL = lds + kStemWgPx * kStemWgDyS;         // 4 S2D rows (4 * Ws * 12) + zero tail
+  const int row_el = Ws * 12;
+  const int xs_len = 4 * row_el + (kStemWgPx + 4 - Ws > 0 ? (kStemWgPx + 4 - Ws) * 12 : 0);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // zero the dy tail rows and the S2D tail once (never overwritten)
+  for (int e = tid; e < (kStemWgPx - Q) * kStemWgDyS; e += kThreads) dyL[Q * kStemWgDyS + e] = 0;
+  for (int e = 4 * row_el + tid; e < xs_len; e += kThreads) xsL[e] = 0;
+
+  const int wm = wv & 1, wj = wv >> 1;  // channels 32 wm .., columns 96 wj ..
+  const int h = lane >> 5, gq = (lane >> 2) & 3, gp = lane & 3, half16 = (lane >> 4) & 1;
+  f32x16 acc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+  // this lane's B columns: j = 96 wj + 32 t + half16 * 16 + 4 gp -> (tap row di, offset r)
+  int bdi[3], br[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int j = 96 * wj + 32 * t + half16 * 16 + 4 * gp;
+    bdi[t] = j / 48;
+    br[t] = j - bdi[t] * 48;
+  }
+  const int acol = 32 * wm + half16 * 16 + 4 * gp;
+
+  // One block per image (rows p = 0 .. P-1 in order). The S2D rows live in a 4-slot ring (row r in
+  // slot r & 3): output row p needs rows p .. p+3, so each step brings ONE new S2D row (p + 3) plus
+  // the dy row -- the loads of step p+1 are issued before step p is computed.
+  const int n = blockIdx.x;
+  const uint16_t* xs_img = xs + static_cast<int64_t>(n) * Hs * row_el;
+  const uint4* dy_img = reinterpret_cast<const uint4*>(dy + static_cast<int64_t>(n) * P * Q * 64);
+  constexpr int kDyV = (kStemWgPx * 8 + kThreads - 1) / kThreads;   // 16-B chunks per lane
+  constexpr int kXsV = (131 * 12 / 4 + kThreads - 1) / kThreads;     // 8-B chunks per lane (Ws <= 131)
+  const int row_v = row_el / 4;                                      // 8-B chunks per S2D row
+  uint4 rdy[kDyV];
+  uint2 rxs[kXsV];
+  auto load_step = [&](int p) {  // dy row p and S2D row p + 3
+#pragma unroll
+    for (int i = 0; i < kDyV; ++i) {
+      const int c = tid + i * kThreads;
+      if (c < Q * 8) rdy[i] = dy_img[static_cast<int64_t>(p) * Q * 8 + c];
+    }
+    const uint2* xsrc = reinterpret_cast<const uint2*>(xs_img + static_cast<int64_t>(p + 3) * row_el);
+#pragma unroll
+    for (int i = 0; i < kXsV; ++i) {
+      const int c = tid + i * kThreads;
+      if (c < row_v) rxs[i] = xsrc[c];
+    }
+  };
+  // S2D rows 0 .. 2 into slots 0 .. 2
+  for (int c = tid; c < 3 * row_v; c += kThreads)
+    reinterpret_cast<uint2*>(xsL)[c] = reinterpret_cast<const uint2*>(xs_img)[c];
+  load_step(0);
+  for (int p = 0; p < P; ++p) {
+    __syncthreads();  // previous step's fragments read
+#pragma unroll
+    for (int i = 0; i < kDyV; ++i) {
+      const int c = tid + i * kThreads;
+      if (c < Q * 8) *reinterpret_cast<uint4*>(dyL + (c >> 3) * kStemWgDyS + (c & 7) * 8) = rdy[i];
+    }
+    uint2* slot = reinterpret_cast<uint2*>(xsL + ((p + 3) & 3) * row_el);
+#pragma unroll
+    for (int i = 0; i < kXsV; ++i) {
+      const int c = tid + i * kThreads;
+      if (c < row_v) slot[c] = rxs[i];
+    }
+    __syncthreads();
+    if (p + 1 < P) load_step(p + 1);
+    int boff[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) boff[t] = ((p + bdi[t]) & 3) * row_el + br[t];
+#pragma unroll
+    for (int ks = 0; ks < kStemWgPx / 16; ++ks) {
+      const int px0 = 16 * ks + 8 * h + gq;  // + 4 for the second read
+      const bf16x8 a = cat8(tr_read(dyL + px0 * kStemWgDyS + acol),
+                            tr_read(dyL + (px0 + 4) * kStemWgDyS + acol));
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const bf16x8 b = cat8(tr_read(xsL + px0 * 12 + boff[t]), tr_read(xsL + (px0 + 4) * 12 + boff[t]));
+        acc[t] = mfma32(a, b, acc[t]);
+      }
+    }
+  }
+  // fp32 tile -> ws[block][k][j]
+  float* out = ws + static_cast<int64_t>(blockIdx.x) * 64 * 192;
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int j = 96 * wj + 32 * t + (lane & 31);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int k = 32 * wm + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      out[k * 192 + j] = acc[t][reg];
+    }
+  }
+}
+
 // dW (+)= sum over splits in a fixed order; 8 elements per thread. The workspace is in the
 // weight's [K][R][S][C] order; `kcrs` writes dW in [K][C][R][S] order instead (a contiguous NCHW
 // .grad view of a channels_last parameter).
@@ -1036,6 +1154,18 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(
     const int ch = (tid >> 4) * 8 + (tid & 7);
     partial[(static_cast<int64_t>(blockIdx.x) * 2 + ((tid >> 3) & 1)) * 64 + ch] = a;
   }
+}
+
+int stem_wgrad_blocks(int N) { return N; }
+
+void stem_wgrad(const void* dy, const void* xs, float* ws, int N, int Hs, int Ws, hipStream_t st) {
+  const int P = Hs - 3, Q = Ws - 3;
+  const int blocks = stem_wgrad_blocks(N);
+  const int tail = kStemWgPx + 4 - Ws > 0 ? (kStemWgPx + 4 - Ws) * 12 : 0;
+  const size_t lds = (static_cast<size_t>(kStemWgPx) * kStemWgDyS + 4 * Ws * 12 + tail) * 2;
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(blocks), dim3(kThreads), lds, st,
+                     static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(xs), ws, P, Q, Hs,
+                     Ws);
 }
 
 int stem_conv_blocks(int N, int Hs, int Ws) {

@@ -205,6 +205,25 @@ def test_stem_s2d_kernel_matches_pad_and_reshape(hw):
     assert torch.equal(xs, ref)
 
 
+@pytest.mark.parametrize("shape", [(4, 224, 224), (3, 96, 150), (2, 64, 48)])
+def test_stem_wgrad_kernel_matches_fp32(shape):
+    """stem_wgrad_kernel (im2col-free: B fragments transposed-read from 4 S2D rows in LDS) equals
+    the fp32 weight gradient of the 4x4/1 convolution on the 12-channel S2D image."""
+    from determined_clone_amd.ops import _ext
+
+    n, h, w = shape
+    torch.manual_seed(0)
+    x = torch.randn(n, 3, h, w, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xs = _ext.load().stem_s2d(x)
+    dy = torch.randn(n, 64, xs.shape[2] - 3, xs.shape[3] - 3, device="cuda").bfloat16()
+    dy = dy.contiguous(memory_format=torch.channels_last)
+    dw = _ext.load().stem_wgrad(dy, xs).permute(0, 3, 1, 2)
+    w2 = torch.zeros(64, 12, 4, 4, device="cuda")
+    ref = torch.ops.aten.convolution_backward(dy.float(), xs.float(), w2, None, [1, 1], [0, 0], [1, 1],
+                                              False, [0, 0], 1, [False, True, False])[1]
+    _close(dw, ref, 1e-3, "stem wgrad")
+
+
 @pytest.mark.parametrize("hw", [(224, 224), (96, 150), (130, 130)])
 def test_stem_conv_kernel_output_and_statistics(monkeypatch, hw):
     """stem_conv_kernel (7x7/2 as a 4x4/1 MFMA conv on the 16-channel S2D tensor) equals the fp32

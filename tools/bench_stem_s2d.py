@@ -62,6 +62,9 @@ def main():
         args = (dy, xs, w2, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])
         us = _time(lambda a: torch.ops.aten.convolution_backward(*a), args)
         print(f"{name:20s} {us:8.1f} us")
+    us = _time(lambda a: C.stem_wgrad(*a), (dy, xs12))
+    print(f"{'hip stem_wgrad':20s} {us:8.1f} us  {2.0 * y.numel() * 192 / us / 1e6:7.1f} TFLOP/s (S2D flops)  "
+          f"{(y.numel() + xs12.numel()) * 2 / us / 1e6:5.2f} TB/s")
 
 
 if __name__ == "__main__":
