@@ -539,9 +539,9 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_kernel(
 // from 4 S2D rows in LDS (8-B aligned: 24 q + 2 r with r a multiple of 4) and the dy row
 // [128 px (112 + zero tail)][64 ch] gives the A fragments. One block per image (112 output rows),
 // S2D rows in a 4-slot ring (one new row per output row), fp32 partials per image summed by ATen.
-// Correct but SLOWER than MIOpen's wrw (1.25-1.31 ms vs 1.11 ms at bs 1024: each block walks its
-// 112 rows with one exposed load round trip per row; profiles/round5_stem_wgrad_kernel_ab.txt), so
-// opt-in (DCA_STEM_WGRAD=1);
+// Correct but SLOWER than MIOpen's wrw (1.25-1.43 ms over five versions vs 1.11 ms at bs 1024;
+// this one, two steps of loads in flight, 1.43 ms -- the one-step ring measured 1.31:
+// profiles/round5_stem_wgrad_kernel_ab.txt), so opt-in (DCA_STEM_WGRAD=1);
 // 2 x 2 waves over the 64 x 192 result (one 32-channel half x 96 columns each), fp32 tile per block
 // -> stem_wgrad_reduce. MIOpen's wrw ran this in ~0.9 ms, the last kernel before the optimizer.
 constexpr int kStemWgPx = 128;     // dy pixels per LDS row tile (112 + zero tail)
@@ -587,40 +587,43 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const uint16_t* __
   constexpr int kDyV = (kStemWgPx * 8 + kThreads - 1) / kThreads;   // 16-B chunks per lane
   constexpr int kXsV = (131 * 12 / 4 + kThreads - 1) / kThreads;     // 8-B chunks per lane (Ws <= 131)
   const int row_v = row_el / 4;                                      // 8-B chunks per S2D row
-  uint4 rdy[kDyV];
-  uint2 rxs[kXsV];
-  auto load_step = [&](int p) {  // dy row p and S2D row p + 3
+  struct Regs {
+    uint4 dy[kDyV];
+    uint2 xs[kXsV];
+  };
+  auto load_step = [&](int p, Regs& R) __attribute__((always_inline)) {  // dy row p, S2D row p + 3
 #pragma unroll
     for (int i = 0; i < kDyV; ++i) {
       const int c = tid + i * kThreads;
-      if (c < Q * 8) rdy[i] = dy_img[static_cast<int64_t>(p) * Q * 8 + c];
+      if (c < Q * 8) R.dy[i] = dy_img[static_cast<int64_t>(p) * Q * 8 + c];
     }
     const uint2* xsrc = reinterpret_cast<const uint2*>(xs_img + static_cast<int64_t>(p + 3) * row_el);
 #pragma unroll
     for (int i = 0; i < kXsV; ++i) {
       const int c = tid + i * kThreads;
-      if (c < row_v) rxs[i] = xsrc[c];
+      if (c < row_v) R.xs[i] = xsrc[c];
     }
   };
-  // S2D rows 0 .. 2 into slots 0 .. 2
-  for (int c = tid; c < 3 * row_v; c += kThreads)
-    reinterpret_cast<uint2*>(xsL)[c] = reinterpret_cast<const uint2*>(xs_img)[c];
-  load_step(0);
-  for (int p = 0; p < P; ++p) {
-    __syncthreads();  // previous step's fragments read
+  // one step: this row's operands (loaded two steps earlier) -> LDS, the row two steps ahead into
+  // the same registers, then the MFMAs. Raw barriers + lgkmcnt(0): __syncthreads would also drain
+  // vmcnt, i.e. wait for the loads just issued for the next step.
+  auto step = [&](int p, Regs& R) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier_raw();  // previous step's fragments read
 #pragma unroll
     for (int i = 0; i < kDyV; ++i) {
       const int c = tid + i * kThreads;
-      if (c < Q * 8) *reinterpret_cast<uint4*>(dyL + (c >> 3) * kStemWgDyS + (c & 7) * 8) = rdy[i];
+      if (c < Q * 8) *reinterpret_cast<uint4*>(dyL + (c >> 3) * kStemWgDyS + (c & 7) * 8) = R.dy[i];
     }
     uint2* slot = reinterpret_cast<uint2*>(xsL + ((p + 3) & 3) * row_el);
 #pragma unroll
     for (int i = 0; i < kXsV; ++i) {
       const int c = tid + i * kThreads;
-      if (c < row_v) slot[c] = rxs[i];
+      if (c < row_v) slot[c] = R.xs[i];
     }
-    __syncthreads();
-    if (p + 1 < P) load_step(p + 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier_raw();
+    if (p + 2 < P) load_step(p + 2, R);
     int boff[3];
 #pragma unroll
     for (int t = 0; t < 3; ++t) boff[t] = ((p + bdi[t]) & 3) * row_el + br[t];
@@ -635,6 +638,16 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const uint16_t* __
         acc[t] = mfma32(a, b, acc[t]);
       }
     }
+  };
+  // S2D rows 0 .. 2 into slots 0 .. 2 (plain loads, published by the first step's barrier)
+  for (int c = tid; c < 3 * row_v; c += kThreads)
+    reinterpret_cast<uint2*>(xsL)[c] = reinterpret_cast<const uint2*>(xs_img)[c];
+  Regs ra, rb;
+  load_step(0, ra);
+  if (P > 1) load_step(1, rb);
+  for (int p = 0; p < P; p += 2) {
+    step(p, ra);
+    if (p + 1 < P) step(p + 1, rb);
   }
   // fp32 tile -> ws[block][k][j]
   float* out = ws + static_cast<int64_t>(blockIdx.x) * 64 * 192;
