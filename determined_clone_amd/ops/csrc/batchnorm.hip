@@ -719,6 +719,72 @@ __global__ __launch_bounds__(kBlock) void bn_relu_pool_fwd_kernel(
   }
 }
 
+// Forward in quad form: one thread per 2x2 block of pooled outputs (ho = 2hq + a, wo = 2wq + b)
+// and 8 channels. Their windows cover input rows 4hq-1 .. 4hq+3 and columns 4wq-1 .. 4wq+3: 25 loads
+// for 4 outputs instead of 36, each input vector applied to every window that contains it. Visiting
+// the 5x5 inputs row-major gives every window its taps in (kh, kw) order, so "first maximum wins"
+// is unchanged.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void bn_relu_pool_fwd_quad_kernel(
+    const void* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
+    void* __restrict__ y, uint8_t* __restrict__ idx, int64_t nthr, int C, PoolGeom g) {
+  const int c8 = C / 8;
+  const int Hq = (g.Ho + 1) / 2, Wq = (g.Wo + 1) / 2;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < nthr;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(t % c8) * 8;
+    const int64_t o = t / c8;  // (n, hq, wq)
+    const int wq = static_cast<int>(o % Wq);
+    const int hq = static_cast<int>((o / Wq) % Hq);
+    const int64_t n = o / (static_cast<int64_t>(Wq) * Hq);
+    float a8[8], b8[8], best[4][8];
+    uint32_t slot[4][8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { a8[k] = scale[c + k]; b8[k] = shift[c + k]; }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { best[q][k] = 0.f; slot[q][k] = 0xff; }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int h = 4 * hq - 1 + i;
+      if (h < 0 || h >= g.H) continue;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const int w = 4 * wq - 1 + j;
+        if (w < 0 || w >= g.W) continue;
+        float v[8];
+        Vec8<T>::load(reinterpret_cast<const char*>(x) + (((n * g.H + h) * g.W + w) * C + c) * Vec8<T>::bytes, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = fmaxf(fmaf(v[k], a8[k], b8[k]), 0.f);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int kh = i - 2 * (q >> 1), kw = j - 2 * (q & 1);
+          if (kh < 0 || kh > 2 || kw < 0 || kw > 2) continue;
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (slot[q][k] == 0xff || v[k] > best[q][k]) { best[q][k] = v[k]; slot[q][k] = kh * 3 + kw; }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ho = 2 * hq + (q >> 1), wo = 2 * wq + (q & 1);
+      if (ho >= g.Ho || wo >= g.Wo) continue;
+      const int64_t ot = ((n * g.Ho + ho) * g.Wo + wo) * c8 + c / 8;  // output vector index
+      Vec8<T>::store(reinterpret_cast<char*>(y) + ot * 8 * Vec8<T>::bytes, best[q]);
+      if (idx) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lo |= ((slot[q][k] | (best[q][k] > 0.f ? 0x10u : 0u)) & 0xffu) << (8 * k);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hi |= ((slot[q][4 + k] | (best[q][4 + k] > 0.f ? 0x10u : 0u)) & 0xffu) << (8 * k);
+        *reinterpret_cast<uint2*>(idx + ot * 8) = make_uint2(lo, hi);
+      }
+    }
+  }
+}
+
 // BN-backward statistics and apply passes of the stem (BN + ReLU + max-pool), in quad form: one
 // thread per 2x2 block of pre-pool positions (rows 2hb, 2hb+1, columns 2wb, 2wb+1) and 8 channels. Such a block is covered by exactly the pooled windows
 // (hb + a, wb + b), a, b in {0, 1} (3x3 / stride 2 / padding 1), so the thread loads those 4
@@ -1084,6 +1150,20 @@ void bn_relu_pool_forward(BnDtype dt, const void* x, void* y, uint8_t* idx, int 
                                       eps, save_mean, save_invstd, num_batches, workspace,
                                       given_partials, given_blocks, st);
     shift = scale + C;
+  }
+  static const bool quad = [] {
+    const char* e = std::getenv("DCA_BN_POOL_FWD_QUAD");
+    return !(e && e[0] == '0');
+  }();
+  if (quad) {
+    const int64_t nthr = static_cast<int64_t>(N) * ((g.Ho + 1) / 2) * ((g.Wo + 1) / 2) * (C / 8);
+    const int qgrid = stream_grid(nthr, kBlock);
+    switch (dt) {
+      case BnDtype::kBF16: hipLaunchKernelGGL(bn_relu_pool_fwd_quad_kernel<BF16>, dim3(qgrid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nthr, C, g); break;
+      case BnDtype::kF16: hipLaunchKernelGGL(bn_relu_pool_fwd_quad_kernel<F16>, dim3(qgrid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nthr, C, g); break;
+      default: hipLaunchKernelGGL(bn_relu_pool_fwd_quad_kernel<F32>, dim3(qgrid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nthr, C, g); break;
+    }
+    return;
   }
   const int64_t nout = static_cast<int64_t>(N) * g.Ho * g.Wo * C / 8;
   const int grid = stream_grid(nout, kBlock);
