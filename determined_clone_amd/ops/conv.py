@@ -516,6 +516,8 @@ STEM_KERNEL = os.environ.get("DCA_STEM_KERNEL", "0") == "1"
 # wrw -- the last kernel of every backward, on the critical path. OFF by default: the kernel is
 # correct but 1.25-1.31 ms against MIOpen's 1.11 (profiles/round5_stem_wgrad_kernel_ab.txt).
 STEM_WGRAD = os.environ.get("DCA_STEM_WGRAD", "0") == "1"
+# MIOpen stem convolution on the 16-channel S2D tensor (see _StemS2D.forward): OFF, -1.6 % measured
+STEM_S2D16 = os.environ.get("DCA_STEM_S2D16", "0") == "1"
 
 
 def _s2d_input(x: torch.Tensor) -> torch.Tensor:
@@ -564,6 +566,14 @@ class _StemS2D(torch.autograd.Function):
             w2 = _s2d_weight(weight, 16)
             y, partial = C.stem_conv_fwd(xs, w2)
             ctx.mark_non_differentiable(partial)
+        elif STEM_S2D16 and x.is_cuda and x.dtype == torch.bfloat16:
+            # 16-channel S2D (4 zero channels) on MIOpen: its weight gradient runs 0.95 ms against
+            # 1.12 ms at 12 channels standalone (tools/bench_stem_s2d.py), yet the step measured
+            # -1.6 % (profiles/round5_stem_conv_kernel_ab.txt) -- like the MFMA stem kernel, which
+            # also saves the 16-channel tensor; opt-in only
+            xs = _ext.load().stem_s2d(x, 16)
+            w2 = _s2d_weight(weight, 16)
+            y = F.conv2d(xs, w2)
         else:
             xs = _s2d_input(x)
             w2 = _s2d_weight(weight)
