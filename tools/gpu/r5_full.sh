@@ -1,6 +1,6 @@
 # round 5: full GPU tier + smoke + bench (the driver's round-end sequence) on the current tree
 set -o pipefail
-OUT=gpurun_out/r5f3
+OUT=gpurun_out/r5f4
 mkdir -p $OUT
 ( while sleep 30; do date +%T >> $OUT/heartbeat.txt; done ) &
 HB=$!
