@@ -1,6 +1,6 @@
 # round 5: stem BN+ReLU+maxpool backward in quad form (one thread per 2x2 block): tests, in-step A/B, kernel times
 set -o pipefail
-OUT=gpurun_out/r5q2
+OUT=gpurun_out/r5q3
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_ops_gpu.py -k "maxpool or stem" > $OUT/test.log 2>&1 || exit 1
