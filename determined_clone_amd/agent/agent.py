@@ -114,6 +114,13 @@ class _Task:
         self.killed = False
 
 
+def _names_image(spec: Dict[str, Any]) -> bool:
+    """True when the task's experiment config chose a container image (``environment.image``)."""
+    c = spec.get("container") or {}
+    img = c.get("image")
+    return bool(img if not isinstance(img, dict) else any(img.values()))
+
+
 class Agent:
     def __init__(self, master_url: str, agent_id: Optional[str] = None, pool: str = "default",
                  artificial_slots: int = 0, label: str = "", username: str = "admin",
@@ -138,6 +145,14 @@ class Agent:
         from determined_clone_amd.agent import containers
 
         self.containers = containers.make_runtime(container_runtime, self.id, container_socket, dev_root)
+        # "auto": containers only for tasks whose config names an image (environment.image);
+        # tasks without one keep the process runtime (zygote, per-agent MIOpen DB), so an agent
+        # on a host where a daemon answers does not move every task into a default image it may
+        # not be able to pull
+        self.container_auto = (container_runtime or "auto").lower() == "auto"
+        # allocations whose container is being created (pull / create / start on a worker thread)
+        # -> killed-while-launching flag
+        self._launching: Dict[str, threading.Event] = {}
         # pre-warmed fork server for task processes (exec/zygote.py), started in the background
         self.zygote = None
         self._zygote_done = threading.Event()
@@ -164,8 +179,14 @@ class Agent:
         wd = os.path.join(self.workdir, alloc.replace("/", "_"))
         ctx_dir = os.path.join(wd, "context")
         runtime.fetch_context(self.session, spec["task_id"], ctx_dir)
-        if self.containers is not None:
-            self._start_container(spec, wd, ctx_dir)
+        if self.containers is not None and (not self.container_auto or _names_image(spec)):
+            # off the action loop: an image pull can take minutes and must not stall kills, other
+            # starts or the master long-poll (reference: the agent pulls asynchronously)
+            killed = threading.Event()
+            with self._lock:
+                self._launching[spec["allocation_id"]] = killed
+            threading.Thread(target=self._start_container, args=(spec, wd, ctx_dir, killed),
+                             daemon=True, name=f"launch-{spec['allocation_id']}").start()
             return
         cmd, env = runtime.build_task(spec, self.master_url, self.id, self.devices, ctx_dir)
         if "MIOPEN_USER_DB_PATH" not in env:
@@ -201,19 +222,48 @@ class Agent:
         self._event(alloc, "RUNNING")
         threading.Thread(target=self._pump, args=(t,), daemon=True).start()
 
-    def _start_container(self, spec: Dict[str, Any], wd: str, ctx_dir: str) -> None:
+    def _start_container(self, spec: Dict[str, Any], wd: str, ctx_dir: str,
+                         killed: Optional[threading.Event] = None) -> None:
         """Run the task in a container (agent/containers.py): same command and DET_* environment
-        as the process runtime, seen through the container's mounts and device mapping."""
+        as the process runtime, seen through the container's mounts and device mapping. Runs on a
+        worker thread per allocation; a failure (pull, create, start) is reported as TERMINATED 1
+        and a kill that arrived meanwhile stops the container as soon as it exists."""
         alloc = spec["allocation_id"]
-        base = {k: v for k, v in os.environ.items() if k.startswith("DET_MASTER_CERT")}
-        cmd, env = runtime.build_task(spec, self.master_url, self.id, self.devices, ctx_dir, base_env=base)
-        mine = runtime.assigned_devices(spec, self.devices)
-        proc = self.containers.launch(spec, cmd, env, ctx_dir, mine, runtime.FRAMEWORK_ROOT)
+        try:
+            base = {k: v for k, v in os.environ.items() if k.startswith("DET_MASTER_CERT")}
+            cmd, env = runtime.build_task(spec, self.master_url, self.id, self.devices, ctx_dir, base_env=base)
+            if "MIOPEN_USER_DB_PATH" not in env:
+                # the agent's MIOpen find DB + kernel cache, bind-mounted at the same path, so
+                # containerised trials reuse what earlier trials found / compiled
+                from determined_clone_amd.ops import miopen_db
+
+                db, cache = miopen_db.task_dirs(self.workdir)
+                miopen_db.configure(env, db, cache)
+                spec = dict(spec)
+                c = dict(spec.get("container") or {})
+                c["bind_mounts"] = list(c.get("bind_mounts") or []) + [
+                    {"host_path": os.path.dirname(db), "container_path": os.path.dirname(db),
+                     "read_only": False}]
+                spec["container"] = c
+            mine = runtime.assigned_devices(spec, self.devices)
+            if killed is not None and killed.is_set():
+                raise RuntimeError("killed before its container started")
+            proc = self.containers.launch(spec, cmd, env, ctx_dir, mine, runtime.FRAMEWORK_ROOT)
+        except Exception as e:
+            logger.warning(f"container launch of {alloc} failed: {e}")
+            with self._lock:
+                self._launching.pop(alloc, None)
+            self._event(alloc, "TERMINATED", 137 if killed is not None and killed.is_set() else 1)
+            shutil.rmtree(wd, ignore_errors=True)
+            return
         t = _Task(spec, proc, wd)
         with self._lock:
             self.tasks[alloc] = t
+            self._launching.pop(alloc, None)
         self._event(alloc, "RUNNING")
         threading.Thread(target=self._pump, args=(t,), daemon=True).start()
+        if killed is not None and killed.is_set():  # kill arrived during the pull / create
+            self._kill(alloc)
 
     def _reattach(self) -> None:
         """After an agent restart: follow this agent's containers that are still running and
@@ -272,8 +322,12 @@ class Agent:
         return True
 
     def _kill(self, alloc: str, grace: float = 10.0) -> None:
-        t = self.tasks.get(alloc)
+        with self._lock:
+            t = self.tasks.get(alloc)
+            launching = self._launching.get(alloc)
         if t is None:
+            if launching is not None:
+                launching.set()  # _start_container stops it once it exists
             return
         t.killed = True
         if not self._signal(t, signal.SIGTERM):
@@ -344,10 +398,11 @@ def main() -> None:
     ap.add_argument("--slots-per-gpu", type=int, default=1,
                     help="expose each MI355X as this many slots (HP-search trials sharing a GPU)")
     ap.add_argument("--max-gpus", type=int, default=0, help="use only the first N GPUs (0 = all)")
-    ap.add_argument("--container-runtime", default="auto",
+    ap.add_argument("--container-runtime", default="process",
                     choices=["auto", "docker", "podman", "apptainer", "process"],
-                    help="run tasks in containers (auto: Docker or Podman when its socket answers, "
-                         "else process groups)")
+                    help="run tasks in containers: process (default) = process groups; auto = Docker "
+                         "or Podman when its socket answers, for tasks whose config sets "
+                         "environment.image (others stay process groups)")
     ap.add_argument("--container-socket", default=None, help="Docker / Podman API unix socket")
     ap.add_argument("--master-cert-file", default=None,
                     help="CA / self-signed cert of an HTTPS master, or 'noverify'")

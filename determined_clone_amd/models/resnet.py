@@ -98,11 +98,7 @@ class Bottleneck(nn.Module):
             # conv1 and the projection shortcut read the same x: one op, one input gradient
             # (the shortcut's strided backward-data is accumulated in place, ops/conv.py)
             ds_conv, ds_bn = self.downsample
-            if not conv_ops.DUAL:
-                y1 = pointwise_conv(self.conv1, x, self.bn1.training)
-                yd = pointwise_conv(ds_conv, x, ds_bn.training)
-            else:
-                y1, yd = pointwise_dual(self.conv1, ds_conv, x, self.bn1.training)
+            y1, yd = pointwise_dual(self.conv1, ds_conv, x, self.bn1.training)
             out = self.bn1(y1)
             if BN_DUAL and self.bn3.relu and not ds_bn.relu:
                 out = self.bn2(conv_ops.spatial_conv(self.conv2, out, self.bn2.training))

@@ -25,7 +25,6 @@ from typing import Optional
 import torch
 
 ENABLED = os.environ.get("DCA_DIRECT_GRAD", "1") != "0"
-CL_TARGETS = os.environ.get("DCA_WGRAD_STREAM_CL", "1") != "0"  # channels_last weights (A/B switch)
 
 
 def target(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -41,7 +40,7 @@ def target(p: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     # Requiring plain contiguity kept every 3x3 / 7x7 weight gradient of a channels_last ResNet
     # off the side stream: 17 MIOpen backward-weight calls, ~6.5 ms of a 80 ms step, on the
     # critical path -- profiles/round4_resnet50_step_breakdown_default.txt)
-    if not (g.is_contiguous() or (CL_TARGETS and g.dim() == 4 and g.stride() == p.stride()
+    if not (g.is_contiguous() or (g.dim() == 4 and g.stride() == p.stride()
                                   and g.is_contiguous(memory_format=torch.channels_last))):
         return None
     if g.dtype not in (torch.float32, torch.bfloat16):

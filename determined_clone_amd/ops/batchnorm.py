@@ -4,7 +4,7 @@ GPU path: `ops/csrc/batchnorm.hip` (NHWC, 2 HBM passes forward, 2 backward).
 CPU path: the plain PyTorch reference (`F.batch_norm` + add + relu) used by CPU tests and as the
 fp32 oracle for the GPU numerics tests.
 """
-from typing import Any, Optional
+from typing import Optional
 
 import torch
 import torch.nn.functional as F
@@ -37,22 +37,6 @@ class ResidualGradSink:
         self.grad = g if self.grad is None else self.grad + g
 
 
-FUSED_BWD_STATS_HITS = 0  # backward passes whose statistics came from a dgrad epilogue (tests)
-
-
-def fused_bwd_stats_source(x: torch.Tensor) -> Optional[Any]:
-    """The autograd node of the fused BatchNorm(+ReLU) that produced ``x`` when a consumer's
-    data-gradient kernel may reduce that BatchNorm's backward statistics in its epilogue: a
-    training-mode BN with ReLU, no residual, no extra upstream gradient sink in use. None
-    otherwise."""
-    node = getattr(x, "grad_fn", None)
-    if node is None or type(node).__name__ != "_BNActTrainBackward":
-        return None
-    if not getattr(node, "relu", False) or getattr(node, "has_res", True):
-        return None
-    return node
-
-
 class _BNActTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, num_batches, momentum,
@@ -78,21 +62,9 @@ class _BNActTrain(torch.autograd.Function):
         if ctx.out_sink is not None:
             ctx.out_sink.grad = None
         acc_w, acc_b = _direct_grad_targets(*ctx.params) if need_w else (None, None)
-        # statistics pass already done in the epilogue of the convolution data gradient that
-        # produced dy (ops/conv.py _IgemmConv, conv_igemm_dgrad_bn): skip it here
-        given = getattr(ctx, "_dca_given_partials", None)
-        partials = None
-        if given is not None:
-            ctx._dca_given_partials = None
-            part, src = given
-            if dy2 is None and src.data_ptr() == dy.data_ptr() and src.shape == dy.shape \
-                    and src.stride() == dy.stride():
-                partials = part
-                global FUSED_BWD_STATS_HITS
-                FUSED_BWD_STATS_HITS += 1
         dx, dgamma, dbeta, dres = _ext.load().bn_bwd_train(
             dy, x, mask, weight, mean, invstd, ctx.relu, ctx.has_res, need_w, dy2, acc_w, acc_b,
-            partials)
+            None)
         if acc_w is not None:
             need_w = False  # already accumulated into .grad by the finalize kernel
         dres_out = None
@@ -189,12 +161,23 @@ def batch_norm_act(x: torch.Tensor, weight: Optional[torch.Tensor], bias: Option
 
 
 # ----------------------------------------------------------------------------- dual (shortcut) fusion
+def _effective_momentum(m) -> float:
+    """torch's BatchNorm momentum: ``momentum``, or with ``momentum=None`` the cumulative average
+    1 / num_batches_tracked (read after this step's increment)."""
+    if m.momentum is not None:
+        return m.momentum
+    if m.training and m.num_batches_tracked is not None:
+        return 1.0 / float(m.num_batches_tracked.item())
+    return 0.0
+
+
 def reference_batch_norm_act_dual(x, bn, x2, bn2, relu=True):
-    """fp32 / CPU oracle: ``act(bn(x) + bn2(x2))`` with two ``nn.BatchNorm2d``-like modules."""
+    """fp32 / CPU oracle: ``act(bn(x) + bn2(x2))`` with two ``nn.BatchNorm2d``-like modules (their
+    ``num_batches_tracked`` already advanced for this step when ``momentum`` is None)."""
     y = F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.training,
-                     bn.momentum if bn.momentum is not None else 0.0, bn.eps)
+                     _effective_momentum(bn), bn.eps)
     y2 = F.batch_norm(x2, bn2.running_mean, bn2.running_var, bn2.weight, bn2.bias, bn2.training,
-                      bn2.momentum if bn2.momentum is not None else 0.0, bn2.eps)
+                      _effective_momentum(bn2), bn2.eps)
     y = y + y2
     return F.relu(y) if relu else y
 

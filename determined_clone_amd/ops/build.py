@@ -2,11 +2,17 @@
 
 No hipify, no torch JIT cache: every ``csrc/*.hip`` is compiled by ``hipcc --offload-arch=gfx950``
 and the pybind11 glue (``csrc/*.cpp``) by hipcc as host C++, then linked against the torch
-libraries of the running interpreter into ``ops/_C.so`` next to this file. Objects are rebuilt only
-when a source or header is newer (``python -m determined_clone_amd.ops.build [--force]``).
+libraries of the running interpreter into ``ops/_C.so`` next to this file
+(``python -m determined_clone_amd.ops.build [--force]``).
+
+Staleness is decided by CONTENT, not mtime: every object carries a sidecar with the hash of its
+source, the headers and the compile command, and is rebuilt when that differs. The hash of the whole
+``csrc/`` tree (:func:`source_hash`) is compiled into the extension (``_C.source_hash``), and
+``ops._ext.load()`` refuses a binary whose hash does not match the sources next to it.
 """
 import argparse
 import concurrent.futures
+import hashlib
 import os
 import pathlib
 import subprocess
@@ -47,53 +53,94 @@ def _common_flags(abi: int) -> List[str]:
 _FILE_FLAGS = {"attention": [] if os.environ.get("DCA_BUILD_SLP") else ["-fno-slp-vectorize"]}
 
 
-def _newer(src: pathlib.Path, obj: pathlib.Path, headers: List[pathlib.Path]) -> bool:
-    if not obj.exists():
-        return True
-    t = obj.stat().st_mtime
-    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
+def source_hash() -> str:
+    """sha256 over the names and bytes of every ``csrc/`` source and header plus the target arch and
+    per-file flags: the identity of a correct ``_C.so`` for this tree."""
+    h = hashlib.sha256()
+    h.update(f"arch={ARCH};flags={sorted(_FILE_FLAGS.items())}".encode())
+    for f in sorted(CSRC.iterdir()):
+        if f.suffix in (".hip", ".cpp", ".h"):
+            h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    return h.hexdigest()
 
 
-def _compile(cmd: List[str]) -> None:
+def _obj_key(src: pathlib.Path, headers: List[pathlib.Path], cmd: List[str]) -> str:
+    h = hashlib.sha256(" ".join(cmd[3:]).encode())  # flags (not the object path)
+    for f in [src] + headers:
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def _stale(obj: pathlib.Path, key: str) -> bool:
+    side = obj.with_suffix(obj.suffix + ".key")
+    return not obj.exists() or not side.exists() or side.read_text() != key
+
+
+def _compile(cmd: List[str], key: str = "") -> None:
     proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if proc.returncode != 0:
         raise RuntimeError("compile failed:\n" + " ".join(cmd) + "\n" + proc.stdout)
+    if key:  # record what the object was built from (after a successful compile only)
+        out = pathlib.Path(cmd[cmd.index("-o") + 1])
+        out.with_suffix(out.suffix + ".key").write_text(key)
 
 
 def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> pathlib.Path:
     inc, lib, abi = _torch_paths()
     BUILD.mkdir(exist_ok=True)
     headers = sorted(CSRC.glob("*.h"))
-    cmds, objs = [], []
+    jobs_list, objs = [], []
     for src in sorted(CSRC.glob("*.hip")):
         obj = BUILD / (src.stem + ".hip.o")
         objs.append(obj)
-        if force or _newer(src, obj, headers):
-            cmds.append([_hipcc(), "-c", str(src), "-o", str(obj), f"--offload-arch={ARCH}",
-                         "-munsafe-fp-atomics", f"-I{CSRC}"] + _common_flags(abi)
-                        + _FILE_FLAGS.get(src.stem, []))
+        cmd = [_hipcc(), "-c", str(src), "-o", str(obj), f"--offload-arch={ARCH}",
+               "-munsafe-fp-atomics", f"-I{CSRC}"] + _common_flags(abi) + _FILE_FLAGS.get(src.stem, [])
+        key = _obj_key(src, headers, cmd)
+        if force or _stale(obj, key):
+            jobs_list.append((cmd, key))
     py_inc = sysconfig.get_paths()["include"]
     for src in sorted(CSRC.glob("*.cpp")):
         obj = BUILD / (src.stem + ".cpp.o")
         objs.append(obj)
-        if force or _newer(src, obj, headers):
-            cmds.append([_hipcc(), "-c", str(src), "-o", str(obj), f"-I{CSRC}", f"-I{py_inc}",
-                         "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H"]
-                        + [f"-I{p}" for p in inc] + _common_flags(abi))
+        cmd = [_hipcc(), "-c", str(src), "-o", str(obj), f"-I{CSRC}", f"-I{py_inc}",
+               "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H"] + [f"-I{p}" for p in inc] \
+            + _common_flags(abi)
+        key = _obj_key(src, headers, cmd)
+        if force or _stale(obj, key):
+            jobs_list.append((cmd, key))
+    # the source hash as a linked-in symbol (bindings.cpp exposes it as _C.source_hash)
+    digest = source_hash()
+    hsrc, hobj = BUILD / "source_hash.cpp", BUILD / "source_hash.cpp.o"
+    objs.append(hobj)
+    hcode = f'extern "C" const char dca_source_hash[] = "{digest}";\n'
+    if not hsrc.exists() or hsrc.read_text() != hcode:
+        hsrc.write_text(hcode)
+    hcmd = [_hipcc(), "-c", str(hsrc), "-o", str(hobj), "-fPIC", "-O1"]
+    if force or _stale(hobj, digest):
+        jobs_list.append((hcmd, digest))
     jobs = jobs or min(8, os.cpu_count() or 4)
     with concurrent.futures.ThreadPoolExecutor(max_workers=jobs) as ex:
-        for cmd in cmds:
+        for cmd, _ in jobs_list:
             if verbose:
                 print(" ".join(cmd), flush=True)
-        list(ex.map(_compile, cmds))
-    if cmds or force or not TARGET.exists():
+        list(ex.map(lambda ck: _compile(*ck), jobs_list))
+    if jobs_list or force or not TARGET.exists() or linked_hash() != digest:
         link = [_hipcc(), "-shared", "-fPIC", "-o", str(TARGET)] + [str(o) for o in objs] + [
             f"--offload-arch={ARCH}", f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
             "-ltorch_hip", "-ltorch_python", "-lamdhip64", "-lhipblaslt", f"-Wl,-rpath,{lib}"]
         if verbose:
             print(" ".join(link), flush=True)
         _compile(link)
+        LINKED.write_text(digest)
     return TARGET
+
+
+LINKED = HERE / "_C.so.hash"  # next to _C.so (travels with it); the embedded hash stays authoritative
+
+
+def linked_hash() -> str:
+    """The source hash recorded when ``_C.so`` was last linked ("" if unknown)."""
+    return LINKED.read_text().strip() if LINKED.exists() and TARGET.exists() else ""
 
 
 def main() -> None:

@@ -34,7 +34,6 @@ from determined_clone_amd.ops import _ext, _grad
 # direction by timing both once, on the first training call (like cudnn.benchmark), and cached.
 _CHOICE = {}
 AUTOTUNE = os.environ.get("DCA_CONV_AUTOTUNE", "1") != "0"
-DUAL = os.environ.get("DCA_PW_DUAL", "1") != "0"  # pointwise_dual for downsampling blocks
 
 # Shipped decisions (like the MIOpen find DB and the TunableOp CSV in ops/tuned/): every
 # (direction, shape) this chooser met in the ResNet-50 bench (bs 1024, 256), the SD UNet bench and
@@ -165,9 +164,6 @@ def _choose(key, candidates) -> int:
         dist.broadcast_object_list(obj, src=0)
         best = int(obj[0])
     _CHOICE[key] = best
-    if os.environ.get("DCA_CONV_DEBUG") == "1":
-        print(f"[conv chooser] {key[0]} {key[1:]} us={[round(t, 1) for t in times]} -> {best}",
-              file=sys.stderr, flush=True)
     return best
 
 
@@ -183,13 +179,16 @@ def _from_rows(m: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
     return m.view(n, h, w, m.shape[1]).permute(0, 3, 1, 2)  # channels_last NCHW view
 
 
-# backward-data GEMM of a 1x1 conv accumulates into its input's deposited identity-shortcut
-# gradient (see _PointwiseLib); DCA_PW_ACC_RESIDUAL=0 keeps the two gradients separate
-ACC_RESIDUAL = os.environ.get("DCA_PW_ACC_RESIDUAL", "1") != "0"
+# The backward-data GEMM of a 1x1 conv accumulates into its input's deposited identity-shortcut
+# gradient (see _PointwiseLib; profiles/round3_shortcut_grad_accumulate_ab.txt), and a projection
+# shortcut's data gradient is added at the strided positions by a HIP kernel (csrc/conv_igemm.hip
+# strided_accumulate; ATen's strided add_ ran at 1.1-2.5 TB/s: round4_strided_accumulate_ab.txt).
 ACC_HITS = 0  # backward passes that took the accumulate path (tests)
-# projection-shortcut data gradient added at the strided positions by a HIP kernel
-# (csrc/conv_igemm.hip strided_accumulate); DCA_STRIDED_ACC=0 uses ATen's strided add_
-STRIDED_ACC = os.environ.get("DCA_STRIDED_ACC", "1") != "0"
+
+
+def _grad_sink(x: torch.Tensor):
+    """The residual-gradient sink of a fused-BN output (ops/batchnorm.py ResidualGradSink), if any."""
+    return getattr(x, "_dca_grad_sink", None)
 
 
 def _pw_forward(x: torch.Tensor, weight: torch.Tensor, stride: int) -> torch.Tensor:
@@ -266,7 +265,7 @@ class _PointwiseLib(torch.autograd.Function):
         ctx.stride = stride
         # x is a fused BN output whose identity-shortcut gradient arrives through a sink
         # (ops/batchnorm.py ResidualGradSink): the backward-data GEMM can accumulate into it
-        ctx.sink = getattr(x, "_dca_grad_sink", None) if ACC_RESIDUAL else None
+        ctx.sink = _grad_sink(x)
         return y, partial
 
     @staticmethod
@@ -366,7 +365,7 @@ class _PointwiseDual(torch.autograd.Function):
                 c2 = (lambda: bwd(*a2, [True, False, False])[0],
                       lambda: _from_rows(torch.mm(_rows(dy2, 1), W2), n, h, w))
                 pick = _choose(("dgrad", tuple(x.shape), w2.shape[0], 1, x.dtype), c2)
-                rows = _rows(dx, 1) if pick == 1 and ACC_RESIDUAL and \
+                rows = _rows(dx, 1) if pick == 1 and \
                     dx.is_contiguous(memory_format=torch.channels_last) else None
                 if rows is not None and rows.data_ptr() == dx.data_ptr():
                     rows.addmm_(_rows(dy2, 1), W2)  # beta = 1: no separate full-size add
@@ -375,7 +374,7 @@ class _PointwiseDual(torch.autograd.Function):
             else:
                 ho, wo = dy2.shape[2], dy2.shape[3]
                 small = torch.mm(_rows(dy2, 1), W2).view(n, ho, wo, cin)
-                if STRIDED_ACC and dx.dtype == torch.bfloat16 and cin % 8 == 0 and \
+                if dx.dtype == torch.bfloat16 and cin % 8 == 0 and \
                         dx.is_contiguous(memory_format=torch.channels_last):
                     # HIP kernel: 16-B lanes at HBM rate (ATen's strided add ran at 1.1-2.5 TB/s)
                     _ext.load().strided_accumulate(dx, small.permute(0, 3, 1, 2), st)
@@ -499,31 +498,19 @@ def _bgrad(dy: torch.Tensor, bias: torch.Tensor) -> Optional[torch.Tensor]:
 # kernel to 8x8 and fold it the same way -- it is exactly a 4x4 / stride-1 convolution on a
 # 115x115x12 image: 1119 us forward + 934 us weight gradient instead of 1716 + 1381
 # (profiles/round3_stem_conv_variants_find.txt); +0.5% end to end with its find-DB entries shipped
-# (profiles/round3_stem_s2d_ab.txt). DCA_STEM_S2D=0 runs the plain 7x7 convolution.
-STEM_S2D = os.environ.get("DCA_STEM_S2D", "1") != "0"
+# (profiles/round3_stem_s2d_ab.txt).
 
 
-# the stem image's pad + space-to-depth as one HIP pass (csrc/conv_igemm.hip stem_s2d_kernel);
-# DCA_STEM_S2D_KERNEL=0 keeps ATen's pad + reshape copies (A/B only).
-STEM_S2D_KERNEL = os.environ.get("DCA_STEM_S2D_KERNEL", "1") != "0"
-# the stem convolution itself on the hand-written kernel (stem_conv_kernel, BatchNorm statistics in
-# its epilogue). OFF by default: standalone it runs the bs-1024 stem in 0.84 ms against MIOpen's
-# 1.94 ms (+0.28 ms statistics pass), but in the step the kernels around it ran 1-8 % slower and
-# the step measured -0.3..-2 % in five same-box A/Bs (profiles/round5_stem_conv_kernel_ab.txt).
-# DCA_STEM_KERNEL=1 opts in.
-STEM_KERNEL = os.environ.get("DCA_STEM_KERNEL", "0") == "1"
-# the stem weight gradient on the hand-written MFMA kernel (stem_wgrad_kernel) instead of MIOpen's
-# wrw -- the last kernel of every backward, on the critical path. OFF by default: the kernel is
-# correct but 1.25-1.31 ms against MIOpen's 1.11 (profiles/round5_stem_wgrad_kernel_ab.txt).
-STEM_WGRAD = os.environ.get("DCA_STEM_WGRAD", "0") == "1"
-# MIOpen stem convolution on the 16-channel S2D tensor (see _StemS2D.forward): OFF, -1.6 % measured
-STEM_S2D16 = os.environ.get("DCA_STEM_S2D16", "0") == "1"
+# the stem image's pad + space-to-depth runs as one HIP pass (csrc/conv_igemm.hip stem_s2d_kernel).
+# (Measured and removed in round 6: an MFMA stem convolution kernel with the BatchNorm statistics in
+# its epilogue, a hand-written stem weight gradient and a 16-channel S2D tensor on MIOpen -- each
+# lost in the step: profiles/round5_stem_conv_kernel_ab.txt, round5_stem_wgrad_kernel_ab.txt.)
 
 
 def _s2d_input(x: torch.Tensor) -> torch.Tensor:
     """[N, 3, H, W] (NHWC memory) -> [N, 12, (H+6)/2, (W+6)/2] channels_last, channel (dy, dx, c)."""
     n, c, h, w = x.shape
-    if STEM_S2D_KERNEL and x.is_cuda and x.dtype == torch.bfloat16 and c == 3:
+    if x.is_cuda and x.dtype == torch.bfloat16 and c == 3:
         return _ext.load().stem_s2d(x)  # one pass, padding folded in (csrc/conv_igemm.hip)
     xn = F.pad(x.permute(0, 2, 3, 1), (0, 0, 3, 3, 3, 3))  # [N, H+6, W+6, C]
     hh, ww = (h + 6) // 2, (w + 6) // 2
@@ -531,13 +518,10 @@ def _s2d_input(x: torch.Tensor) -> torch.Tensor:
     return xs.permute(0, 3, 1, 2)
 
 
-def _s2d_weight(w: torch.Tensor, channels: int = 0) -> torch.Tensor:
-    """[K, C, 7, 7] -> [K, 4C, 4, 4] (channels_last), channel (dy, dx, c), tap (i, j) = (2i+dy, 2j+dx);
-    ``channels`` > 4C appends zero channels (the stem kernel's 16-channel pixels)."""
+def _s2d_weight(w: torch.Tensor) -> torch.Tensor:
+    """[K, C, 7, 7] -> [K, 4C, 4, 4] (channels_last), channel (dy, dx, c), tap (i, j) = (2i+dy, 2j+dx)."""
     k, c = w.shape[:2]
     wp = F.pad(w, (0, 1, 0, 1)).view(k, c, 4, 2, 4, 2).permute(0, 3, 5, 1, 2, 4).reshape(k, 4 * c, 4, 4)
-    if channels > 4 * c:
-        wp = F.pad(wp, (0, 0, 0, 0, 0, channels - 4 * c))
     return wp.contiguous(memory_format=torch.channels_last)
 
 
@@ -549,85 +533,54 @@ def _s2d_weight_grad(dw2: torch.Tensor, c: int) -> torch.Tensor:
 
 
 class _StemS2D(torch.autograd.Function):
-    """7x7/2 (padding 3) convolution of a 3-channel image as the space-to-depth 4x4/1 convolution;
-    returns ``(y, bn_partials)``. With ``kernel`` (bf16, csrc/conv_igemm.hip stem_conv_kernel) the
-    S2D tensor carries 16 channels (4 zero) and the forward emits the stem BatchNorm's partial
-    statistics; otherwise MIOpen runs the 12-channel form and ``bn_partials`` is None. The weight
-    gradient is folded back to 7x7 and, on a GPU, runs on the side stream into the parameter's
-    ``.grad`` view (``ops/_grad.py``). The image gets no gradient."""
+    """7x7/2 (padding 3) convolution of a 3-channel image as the space-to-depth 4x4/1 convolution
+    (MIOpen on the 12-channel form). The weight gradient is folded back to 7x7 and, on a GPU, runs on
+    the side stream into the parameter's ``.grad`` view (``ops/_grad.py``). The image gets no
+    gradient."""
 
     @staticmethod
-    def forward(ctx, x, weight, kernel):
+    def forward(ctx, x, weight):
         ctx.set_materialize_grads(False)
-        partial = None
-        if kernel:
-            C = _ext.load()
-            xs = C.stem_s2d(x, 16)
-            w2 = _s2d_weight(weight, 16)
-            y, partial = C.stem_conv_fwd(xs, w2)
-            ctx.mark_non_differentiable(partial)
-        elif STEM_S2D16 and x.is_cuda and x.dtype == torch.bfloat16:
-            # 16-channel S2D (4 zero channels) on MIOpen: its weight gradient runs 0.95 ms against
-            # 1.12 ms at 12 channels standalone (tools/bench_stem_s2d.py), yet the step measured
-            # -1.6 % (profiles/round5_stem_conv_kernel_ab.txt) -- like the MFMA stem kernel, which
-            # also saves the 16-channel tensor; opt-in only
-            xs = _ext.load().stem_s2d(x, 16)
-            w2 = _s2d_weight(weight, 16)
-            y = F.conv2d(xs, w2)
-        else:
-            xs = _s2d_input(x)
-            w2 = _s2d_weight(weight)
-            y = F.conv2d(xs, w2)
+        xs = _s2d_input(x)
+        w2 = _s2d_weight(weight)
         ctx.save_for_backward(xs, w2)
         ctx.weight = weight
-        return y, partial
+        return F.conv2d(xs, w2)
 
     @staticmethod
-    def backward(ctx, dy, _dpartial):
+    def backward(ctx, dy):
         xs, w2 = ctx.saved_tensors
         weight = ctx.weight
         if dy is None:
-            return None, None, None
+            return None, None
         dy = dy.contiguous(memory_format=torch.channels_last)
         c = weight.shape[1]
-        if (STEM_WGRAD and xs.shape[1] == 12 and xs.dtype == torch.bfloat16 and dy.shape[1] == 64
-                and dy.shape[3] <= 128):
-            # csrc/conv_igemm.hip stem_wgrad_kernel: [64][4][4][12] fp32 -> [64, 12, 4, 4]
-            def wgrad():
-                return _ext.load().stem_wgrad(dy, xs).permute(0, 3, 1, 2)
-        else:
-            def wgrad():
-                args = (dy, xs, w2, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
-                return torch.ops.aten.convolution_backward(*args, [False, True, False])[1][:, :4 * c]
+
+        def wgrad():
+            args = (dy, xs, w2, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+            return torch.ops.aten.convolution_backward(*args, [False, True, False])[1]
         s = _grad.side_stream_for(weight)
         if s is None:
-            return None, _s2d_weight_grad(wgrad(), c).to(weight.dtype), None
+            return None, _s2d_weight_grad(wgrad(), c).to(weight.dtype)
         _grad.fork(s, (dy, xs))
         with torch.cuda.stream(s):
             _grad.target(weight).add_(_s2d_weight_grad(wgrad(), c))
-        return None, None, None
+        return None, None
 
 
 def stem_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> torch.Tensor:
     """The ResNet stem convolution: space-to-depth form on a GPU when it applies (7x7, stride 2,
     padding 3, 3 input channels, no bias, even H and W, image without gradient), else
     :func:`spatial_conv`. The S2D form is pinned to the 7x7 path only for zero padding, matching
-    input / weight dtypes and no autocast (its saved tensors keep their own dtype). bf16 images of
-    width 122-506 with 64 output channels run on the stem kernel; with ``bn_stats`` its output
-    carries the following BatchNorm's partial statistics (``y._dca_bn_partials``)."""
-    if (STEM_S2D and x.is_cuda and not x.requires_grad and conv.kernel_size == (7, 7)
+    input / weight dtypes and no autocast (its saved tensors keep their own dtype). ``bn_stats`` is
+    accepted for call-site symmetry (the stem output carries no fused statistics)."""
+    if (x.is_cuda and not x.requires_grad and conv.kernel_size == (7, 7)
             and conv.padding_mode == "zeros" and x.dtype == conv.weight.dtype
             and not torch.is_autocast_enabled()
             and conv.stride == (2, 2) and conv.padding == (3, 3) and conv.in_channels == 3
             and conv.groups == 1 and conv.bias is None and conv.dilation == (1, 1)
             and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0):
-        ws = (x.shape[3] + 6) // 2
-        kernel = (STEM_KERNEL and x.dtype == torch.bfloat16 and conv.out_channels == 64
-                  and 67 <= ws <= 256)
-        y, partial = _StemS2D.apply(x.contiguous(memory_format=torch.channels_last), conv.weight, kernel)
-        if bn_stats and partial is not None:
-            y._dca_bn_partials = partial
-        return y
+        return _StemS2D.apply(x.contiguous(memory_format=torch.channels_last), conv.weight)
     return spatial_conv(conv, x)
 
 
@@ -640,11 +593,6 @@ def stem_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> torch
 # stride-1 data gradient 4.16 vs 5.56 ms. Stride-2 data gradients and every weight gradient stay
 # on MIOpen (the latter on the side stream). DCA_IGEMM=0 routes everything back to MIOpen.
 IGEMM = os.environ.get("DCA_IGEMM", "1") != "0"
-# stride-1 k x k data gradient whose input came from a fused BN+ReLU: with DCA_FUSE_BN_BWD_STATS=1
-# that BatchNorm's backward statistics pass runs in the dgrad epilogue (conv_igemm_dgrad_bn).
-# OFF by default: it saves one read of the gradient but lengthens the MFMA kernel's epilogue, and
-# measured -0.4 % on the ResNet-50 step (profiles/round5_dgrad_bn_stats_epilogue_ab.txt).
-FUSE_BN_BWD_STATS = os.environ.get("DCA_FUSE_BN_BWD_STATS", "0") == "1"
 
 
 def igemm_supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -670,12 +618,11 @@ class _IgemmConv(torch.autograd.Function):
     """k x k convolution on conv_igemm.hip; returns ``(y, bn_partials)``."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, stats, bn_src=None):
+    def forward(ctx, x, weight, stride, pad, stats):
         y, partial = _ext.load().conv_igemm_fwd(x, weight, stride, pad, stats)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         ctx.save_for_backward(x, weight)
         ctx.stride, ctx.pad = stride, pad
-        ctx.bn_src = bn_src  # autograd node of the BN(+ReLU) producing x (see backward)
         if partial is not None:
             ctx.mark_non_differentiable(partial)
         return y, partial
@@ -689,19 +636,11 @@ class _IgemmConv(torch.autograd.Function):
         dw = _wgrad(args, w) if ctx.needs_input_grad[1] else None
         dx = None
         if ctx.needs_input_grad[0]:
-            node = ctx.bn_src
-            if st == 1 and node is not None:
-                # x = relu(bn(x_bn)): the dgrad epilogue also reduces that BatchNorm's backward
-                # statistics (sum g*m, sum g*m*(x_bn - mean)) and hands them to its backward,
-                # which then skips its own statistics pass over dy and x_bn
-                x_bn, mask, _w, mean, _invstd = node.saved_tensors
-                dx, part = _ext.load().conv_igemm_dgrad_bn(dy, w, pad, x_bn, mask, mean)
-                node._dca_given_partials = (part, dx)
-            elif st == 1:
+            if st == 1:
                 dx = _ext.load().conv_igemm_dgrad(dy, w, pad)
             else:
                 dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None
 
 
 def spatial_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> torch.Tensor:
@@ -709,13 +648,8 @@ def spatial_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> to
     ``bn_stats`` the output carries the following BatchNorm's partial statistics), others on
     MIOpen with the weight (and bias) gradient on the side stream (``ops/_grad.py``)."""
     if igemm_supported(conv, x):
-        from determined_clone_amd.ops import batchnorm as bn_ops
-
-        src = bn_ops.fused_bwd_stats_source(x) if FUSE_BN_BWD_STATS and conv.stride[0] == 1 else None
         x = x.contiguous(memory_format=torch.channels_last)
-        if src is not None and not x.is_contiguous(memory_format=torch.channels_last):
-            src = None
-        y, partial = _IgemmConv.apply(x, conv.weight, conv.stride[0], conv.padding[0], bool(bn_stats), src)
+        y, partial = _IgemmConv.apply(x, conv.weight, conv.stride[0], conv.padding[0], bool(bn_stats))
         if partial is not None:
             y._dca_bn_partials = partial
         return y

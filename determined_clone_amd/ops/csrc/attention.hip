@@ -153,7 +153,7 @@ struct Strides {
 // XCDs, each with its own L2, so the query (or key) blocks of one (batch, head) -- which all stream
 // the same K/V (or Q/dO) tiles -- would be spread over 8 L2s and every tile fetched 8 times from
 // HBM / MALL. With remap, each XCD gets a contiguous range of grid positions (the bijective form,
-// valid for any grid size): the blocks of a (batch, head) share one L2. DCA_ATTN_XCD_REMAP=0 off.
+// valid for any grid size): the blocks of a (batch, head) share one L2.
 //
 // order 2 (heaviest first, causal): additionally, each XCD walks its (batch, head) pairs
 // x-slowest -- every pair's x = 0 block (the largest causal extent: the last query block of the
@@ -323,14 +323,10 @@ struct KVDma {
 // O^T += V^T P^T (no LDS round trip for P). V^T fragments come from the row-major V tile through
 // ds_read_b64_tr_b16 (hardware transpose), so K and V are staged exactly as they arrive from HBM.
 //
-// MSUM: the softmax row sums come out of the matrix core instead of 16 dependent v_add_f32 per
-// sub-tile: one more O^T-shaped MFMA pair per sub-tile with an all-ones A operand, whose every
-// row is sum_k P^T[k][q] (the same bf16 P the O product uses), rescaled with O by the deferred max.
-// The MFMA pipe runs at ~30% here while VALU issue and its dependency chains bound the loop.
-// ABL (timing-only ablations, wrong outputs; DCA_ATTN_ABL, never a default): bit 0 skips the
-// scale/max FMA before each exp, bit 1 the row-sum adds, bit 2 the exps, bit 3 the row max, bit 4
-// the K/V tile HBM loads after the first, bit 5 the LDS tile stores and their barriers.
-template <int D, bool CAUSAL, int KT, bool PIPE, bool MSUM = false, int ABL = 0, bool DMA = false>
+// (Measured and removed: row sums on the matrix core, -2..+1 %; 64 query rows per wave, -10..-24 %;
+// the timing-only ablations that chose the DMA ring -- profiles/round5_attention_dma_ring_ab.txt,
+// round4_attention_msum_ab.txt.)
+template <int D, bool CAUSAL, int KT, bool PIPE, bool DMA = false>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
@@ -369,8 +365,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   f32x16 oacc[D / 32];
 #pragma unroll
   for (int n = 0; n < D / 32; ++n) oacc[n] = zero16();
-  f32x16 lacc = zero16();  // MSUM: every register = this lane's query row sum
-  const bf16x8 ones8 = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
   float m = -INFINITY, l = 0.f;
   const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
   // tr-read lane address pieces (see T10: lane 4q+p of a 16-lane group -> row q, cols 4p..4p+3)
@@ -409,12 +403,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       if (kt + KT < k_end) dma.issue(smem + (stage ^ 1) * 2 * KT * D, smem + (stage ^ 1) * 2 * KT * D + KT * D, kt + KT, w);
       stage ^= 1;
     } else {
-      if constexpr ((ABL & 32) == 0) {
-        __syncthreads();
-        pf.store(Ks, Vs);
-        __syncthreads();
-      }
-      if ((ABL & 16) == 0 && kt + KT < k_end) pf.fetch(kt + KT);
+      __syncthreads();
+      pf.store(Ks, Vs);
+      __syncthreads();
+      if (kt + KT < k_end) pf.fetch(kt + KT);
     }
     if constexpr (PIPE) {
       // online softmax of one sub-tile's scores and O^T += V^T P^T
@@ -430,13 +422,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
           }
         }
         float mx = -INFINITY;
-        if constexpr ((ABL & 8) != 0) {
-          mx = sc[0];
-        } else {
   #pragma unroll
-          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[i]);
-          mx = half_max(mx);
-        }
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[i]);
+        mx = half_max(mx);
         // deferred max (T13): the running max m moves only when a score exceeds it by more than
         // kRescaleLog2 (p <= 2^kRescaleLog2 meanwhile: exact in the fp32 accumulators, 8 bits of
         // headroom in the bf16 P), so the D/2-multiply rescale of O and l runs on a few sub-tiles
@@ -450,26 +438,18 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
         float rs = 0.f;
   #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float t = (ABL & 1) ? sc[i] : fmaf(sc[i], scale_log2, -mref);
-          const float p = (ABL & 4) ? t : fast_exp2(t);
+          const float p = fast_exp2(fmaf(sc[i], scale_log2, -mref));
           sc[i] = p;
-          if constexpr (!MSUM && (ABL & 2) == 0) rs += p;
+          rs += p;
         }
-        if constexpr (!MSUM) {
-          rs = half_sum(rs);
-          l = l * alpha + rs;
-        }
+        rs = half_sum(rs);
+        l = l * alpha + rs;
         m = mnew;
         if (__any(upd)) {
   #pragma unroll
           for (int n = 0; n < D / 32; ++n) rescale16(oacc[n], alpha);
-          if constexpr (MSUM) rescale16(lacc, alpha);
         }
         const bf16x8 p0 = pack8(sc, 0), p1 = pack8(sc, 8);
-        if constexpr (MSUM) {
-          lacc = mfma32(ones8, p0, lacc);
-          lacc = mfma32(ones8, p1, lacc);
-        }
   #pragma unroll
         for (int n = 0; n < D / 32; ++n) {
   #pragma unroll
@@ -554,23 +534,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       for (int i = 0; i < 16; ++i) {
         const float p = fast_exp2(fmaf(sc[i], scale_log2, -mref));
         sc[i] = p;
-        if constexpr (!MSUM) rs += p;
+        rs += p;
       }
-      if constexpr (!MSUM) {
-        rs = half_sum(rs);
-        l = l * alpha + rs;
-      }
+      rs = half_sum(rs);
+      l = l * alpha + rs;
       m = mnew;
       if (__any(upd)) {
 #pragma unroll
         for (int n = 0; n < D / 32; ++n) rescale16(oacc[n], alpha);
-        if constexpr (MSUM) rescale16(lacc, alpha);
       }
       const bf16x8 p0 = pack8(sc, 0), p1 = pack8(sc, 8);
-      if constexpr (MSUM) {
-        lacc = mfma32(ones8, p0, lacc);
-        lacc = mfma32(ones8, p1, lacc);
-      }
 #pragma unroll
       for (int n = 0; n < D / 32; ++n) {
 #pragma unroll
@@ -583,7 +556,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
   }
   // 8-byte stores here: the widened form (store_rows) measured -2..-3% on this kernel at S >= 2048
   // (+1.5% at S 1024), +2.5-4% on the backward kernels (profiles/round3_attention_epilogue_ab.txt)
-  if constexpr (MSUM) l = lacc[0];
   if (my_q < Sq) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     uint16_t* orow = o + b * os.b + h * os.h + static_cast<int64_t>(my_q) * os.s;
@@ -598,176 +570,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(
       }
     if (hf == 0)
       lse[(static_cast<int64_t>(b) * H + h) * Sq + my_q] = l > 0.f ? m + log2f(l) : INFINITY;
-  }
-}
-
-// ------------------------------------------------------------------ forward, 64 query rows per wave
-// NW waves x 64 queries = 64 NW query rows per workgroup. Each wave runs TWO 32-query groups over
-// the same key sub-tile: the K fragments (ds_read_b128) and V^T fragments (ds_read_b64_tr_b16) are
-// read from LDS once and feed both groups' MFMAs (half the LDS reads per FLOP of attn_fwd_kernel),
-// and the two groups' softmax chains are independent, so inside ONE wave group 0's softmax (VALU)
-// issues under group 1's score MFMAs and group 1's softmax under group 0's P.V MFMAs -- the
-// MFMA / softmax ping-pong without relying on a co-resident wave. D = 128 needs ~490 VGPRs: one wave
-// per SIMD (NW = 4, one workgroup per CU). Same math, masks, deferred max and outputs as
-// attn_fwd_kernel (DCA_ATTN_FWD_W64=1 selects it). Measured 10-24 % SLOWER than attn_fwd_kernel
-// (2 / 1 waves per SIMD instead of 3-4 hide less latency; profiles/round5_attention_pmc_baseline.txt):
-// kept opt-in as the measured negative of the one-wave-per-SIMD structure.
-template <int D, bool CAUSAL, int NW>
-__global__ __launch_bounds__(NW * 64, (D == 128 ? 1 : 2)) void attn_fwd_w64_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
-    uint16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int H, Strides qs,
-    Strides ks, Strides vs, Strides os, float scale_log2, int order, const int* __restrict__ kvlen, int G) {
-  constexpr int KT = 64;
-  constexpr int QB = 64 * NW;
-  constexpr int NT = 64 * NW;
-  constexpr int RS = D + kPad;
-  constexpr int VPAD = D == 128 ? kTrPad : kPad;
-  constexpr int RSV = D + VPAD;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Ks = smem;
-  uint16_t* Vs = Ks + KT * RS;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, hf = lane >> 5;
-  const Blk blk = xcd_block(order);
-  const int b = blk.z, h = blk.y;
-  if (kvlen) Sk = min(Sk, max(kvlen[b], 1));
-  const int q_blk = (CAUSAL ? (gridDim.x - 1 - blk.x) : blk.x) * QB;
-  const int q0 = q_blk + w * 64;  // group g: queries q0 + 32 g + r
-  const uint16_t* qb = q + b * qs.b + h * qs.h;
-  const uint16_t* kb = k + b * ks.b + (h / G) * ks.h;
-  const uint16_t* vb = v + b * vs.b + (h / G) * vs.h;
-
-  bf16x8 qf[2][D / 16];
-  f32x16 oacc[2][D / 32];
-  float m[2], l[2];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int my_q = q0 + 32 * g + r;
-#pragma unroll
-    for (int s2 = 0; s2 < D / 16; ++s2)
-      qf[g][s2] = my_q < Sq ? load8(qb + static_cast<int64_t>(my_q) * qs.s + 16 * s2 + 8 * hf) : zero8();
-#pragma unroll
-    for (int n = 0; n < D / 32; ++n) oacc[g][n] = zero16();
-    m[g] = -INFINITY;
-    l[g] = 0.f;
-  }
-  const int k_end = CAUSAL ? min(Sk, q_blk + QB) : Sk;
-  const int tr_row = (r & 15) >> 2;
-  const int tr_col = 16 * (r >> 4) + 4 * (r & 3);
-
-  // online softmax of one group's 32-key sub-tile scores -> P fragments (and O rescale)
-  auto softmax = [&](f32x16& sc, const int g, const int kb0, const bool need_mask, bf16x8& p0, bf16x8& p1) {
-    const int my_q = q0 + 32 * g + r;
-    if (need_mask) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = kb0 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-        sc[i] = (key >= Sk || (CAUSAL && key > my_q)) ? -INFINITY : sc[i];
-      }
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[i]);
-    mx = half_max(mx);
-    const float mcand = mx * scale_log2;
-    const bool upd = mcand > m[g] + kRescaleLog2;
-    const float mnew = upd ? mcand : m[g];
-    const float mref = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = upd ? fast_exp2(m[g] - mref) : 1.f;
-    float rs = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = fast_exp2(fmaf(sc[i], scale_log2, -mref));
-      sc[i] = p;
-      rs += p;
-    }
-    rs = half_sum(rs);
-    l[g] = l[g] * alpha + rs;
-    m[g] = mnew;
-    if (__any(upd)) {
-#pragma unroll
-      for (int n = 0; n < D / 32; ++n) rescale16(oacc[g][n], alpha);
-    }
-    p0 = pack8(sc, 0);
-    p1 = pack8(sc, 8);
-  };
-
-  KVPrefetch<D, KT, VPAD, NT> pf;
-  pf.init(kb, ks, vb, vs, Sk);
-  pf.fetch(0);
-  for (int kt = 0; kt < k_end; kt += KT) {
-    __syncthreads();
-    pf.store(Ks, Vs);
-    __syncthreads();
-    if (kt + KT < k_end) pf.fetch(kt + KT);
-#pragma unroll
-    for (int sub = 0; sub < KT / 32; ++sub) {
-      const int kb0 = kt + 32 * sub;
-      if (kb0 >= k_end) break;
-      if (CAUSAL && kb0 > q0 + 63) break;  // wave-uniform: both groups fully masked from here
-      // group g needs any work (causal): its last query reaches this sub-tile
-      const bool live1 = !CAUSAL || kb0 <= q0 + 63;
-      const bool live0 = !CAUSAL || kb0 <= q0 + 31;
-      bf16x8 kf[D / 16];
-#pragma unroll
-      for (int s2 = 0; s2 < D / 16; ++s2) kf[s2] = load8(Ks + (32 * sub + r) * RS + 16 * s2 + 8 * hf);
-      // group 0's score chain first, then group 1's: group 0's softmax below issues while group
-      // 1's MFMAs are still in the matrix pipe
-      f32x16 s0 = zero16(), s1 = zero16();
-      if (live0) {
-#pragma unroll
-        for (int s2 = 0; s2 < D / 16; ++s2) s0 = mfma32(kf[s2], qf[0][s2], s0);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < D / 16; ++s2) s1 = mfma32(kf[s2], qf[1][s2], s1);
-      (void)live1;
-      const bool mask0 = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0);
-      const bool mask1 = (kb0 + 32 > Sk) || (CAUSAL && kb0 + 31 > q0 + 32);
-      bf16x8 a0, a1, c0, c1;
-      // V^T fragments of this sub-tile, shared by both groups
-      bf16x8 vf[D / 32][2];
-#pragma unroll
-      for (int n = 0; n < D / 32; ++n)
-#pragma unroll
-        for (int s3 = 0; s3 < 2; ++s3) {
-          const uint16_t* base = Vs + (32 * sub + 16 * s3 + 4 * hf + tr_row) * RSV + 32 * n + tr_col;
-          vf[n][s3] = cat8(tr_read(base), tr_read(base + 8 * RSV));
-        }
-      if (live0) {
-        softmax(s0, 0, kb0, mask0, a0, a1);  // VALU under group 1's score MFMAs
-#pragma unroll
-        for (int n = 0; n < D / 32; ++n) {
-          oacc[0][n] = mfma32(vf[n][0], a0, oacc[0][n]);
-          oacc[0][n] = mfma32(vf[n][1], a1, oacc[0][n]);
-        }
-      }
-      softmax(s1, 1, kb0, mask1, c0, c1);  // VALU under group 0's P.V MFMAs
-#pragma unroll
-      for (int n = 0; n < D / 32; ++n) {
-        oacc[1][n] = mfma32(vf[n][0], c0, oacc[1][n]);
-        oacc[1][n] = mfma32(vf[n][1], c1, oacc[1][n]);
-      }
-    }
-  }
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const int my_q = q0 + 32 * g + r;
-    if (my_q < Sq) {
-      const float inv = l[g] > 0.f ? 1.f / l[g] : 0.f;
-      uint16_t* orow = o + b * os.b + h * os.h + static_cast<int64_t>(my_q) * os.s;
-#pragma unroll
-      for (int n = 0; n < D / 32; ++n)
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg) {
-          uint2 pk;
-          pk.x = pack_bf16x2(oacc[g][n][4 * gg] * inv, oacc[g][n][4 * gg + 1] * inv);
-          pk.y = pack_bf16x2(oacc[g][n][4 * gg + 2] * inv, oacc[g][n][4 * gg + 3] * inv);
-          *reinterpret_cast<uint2*>(orow + 32 * n + 8 * gg + 4 * hf) = pk;
-        }
-      if (hf == 0)
-        lse[(static_cast<int64_t>(b) * H + h) * Sq + my_q] = l[g] > 0.f ? m[g] + log2f(l[g]) : INFINITY;
-    }
   }
 }
 
@@ -952,7 +754,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
 
 // QT = queries staged per LDS tile (one barrier pair per tile); each wave consumes it in 32-query
 // MFMA sub-tiles, so QT = 64 halves the barriers and staging passes per MFMA of QT = 32.
-template <int D, bool CAUSAL, int QT, bool SWZ = false>
+template <int D, bool CAUSAL, int QT>
 __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
     const uint16_t* __restrict__ dO, const float* __restrict__ lse, const float* __restrict__ delta,
@@ -961,9 +763,9 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     int order, const int* __restrict__ kvlen, int G) {
   constexpr int KB = 128;
   static_assert(QT == 32 || QT == 64, "query tile");
-  // SWZ: unpadded rows with the XOR chunk swizzle of KVDma (zero bank conflicts on both the row and
-  // the transposed reads; the padded rows measured 0.92 conflict cycles per LDS instruction)
-  constexpr int RS = SWZ ? D : D + kPad;
+  // padded rows (the XOR-swizzled unpadded layout of KVDma removed the 0.92 bank-conflict cycles per
+  // LDS instruction but measured neutral: profiles/round5_attention_dma_ring_ab.txt)
+  constexpr int RS = D + kPad;
   constexpr int CPR = D / 8;                 // 16-byte chunks per row
   constexpr int NPF = 2 * QT * CPR / 256;    // prefetched chunks per thread (Q and dO tiles)
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -1060,7 +862,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
     for (int j = 0; j < NPF; ++j) {
       const int cc = threadIdx.x + 256 * (j % PER);
       const int row = cc / CPR, ch = cc % CPR;
-      *reinterpret_cast<uint4*>((j >= PER ? dOs : Qs) + row * RS + (SWZ ? swz_off<D>(row, ch) : ch * 8)) = pf[j];
+      *reinterpret_cast<uint4*>((j >= PER ? dOs : Qs) + row * RS + ch * 8) = pf[j];
     }
     if (threadIdx.x < QT) {
       lse_s[threadIdx.x] = pl;
@@ -1096,7 +898,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
         bf16x8 qfr[D / 16], dofr[D / 16];
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          const int c = SWZ ? swz_off<D>(r, 2 * s + hf) : 16 * s + 8 * hf;
+          const int c = 16 * s + 8 * hf;
           qfr[s] = load8(Qh + r * RS + c);
           dofr[s] = load8(dOh + r * RS + c);
         }
@@ -1108,7 +910,7 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
       } else {
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
-          const int c = SWZ ? swz_off<D>(r, 2 * s + hf) : 16 * s + 8 * hf;
+          const int c = 16 * s + 8 * hf;
           sacc = mfma32(load8(Qh + r * RS + c), kf[s], sacc);
           dpacc = mfma32(load8(dOh + r * RS + c), vf[s], dpacc);
         }
@@ -1129,8 +931,8 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_kernel(
       for (int n = 0; n < D / 32; ++n) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const int off = (16 * s2 + 4 * hf + tr_row) * RS + (SWZ ? tr_off<D>(lane, n, false) : 32 * n + tr_col);
-          const int off8 = (16 * s2 + 4 * hf + tr_row + 8) * RS + (SWZ ? tr_off<D>(lane, n, true) : 32 * n + tr_col);
+          const int off = (16 * s2 + 4 * hf + tr_row) * RS + 32 * n + tr_col;
+          const int off8 = (16 * s2 + 4 * hf + tr_row + 8) * RS + 32 * n + tr_col;
           dvacc[n] = mfma32(cat8(tr_read(dOh + off), tr_read(dOh + off8)), s2 ? p1 : p0, dvacc[n]);
           dkacc[n] = mfma32(cat8(tr_read(Qh + off), tr_read(Qh + off8)), s2 ? s1 : s0, dkacc[n]);
         }
@@ -1390,227 +1192,36 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void attn_bwd_dkdv_dma_kernel
   store_rows<D>(dv + b * dvs.b + h * dvs.h + static_cast<int64_t>(my_key) * dvs.s, dvacc, 1.f, hf, my_key < SkT);
 }
 
-size_t fwd_lds(int D, int KT = 64) {  // K tile + V tile (see attn_fwd_kernel's VPAD)
-  return static_cast<size_t>(KT) * ((D + kPad) + (D + (D == 128 ? kTrPad : kPad))) * 2;
-}
-size_t bwd_dq_lds(int D, int KT = 64) { return 2 * static_cast<size_t>(KT) * (D + kPad) * 2; }
-
-// keys per LDS tile of the dQ kernel (DCA_ATTN_DQ_KT=128: half the barriers per MFMA, D = 64)
-int dq_kt() {
-  static const int kt = [] {
-    const char* e = std::getenv("DCA_ATTN_DQ_KT");
-    return (e && std::atoi(e) == 128) ? 128 : 64;
-  }();
-  return kt;
-}
-
 // workgroup order (see xcd_block): causal launches heaviest-first (2) -- fwd +12-38%, bwd
-// +10-23% over XCD remap alone at S 1024-4096 (profiles/round3_attention_lpt_order.txt);
-// DCA_ATTN_ORDER=xcd -> 1; DCA_ATTN_XCD_REMAP=0 -> 0 (hardware order)
-int attn_order(bool causal) {
-  static const int base = [] {
-    const char* e = std::getenv("DCA_ATTN_XCD_REMAP");
-    if (e && std::atoi(e) == 0) return 0;
-    const char* o = std::getenv("DCA_ATTN_ORDER");
-    return (o && std::string(o) == "xcd") ? 1 : 2;
-  }();
-  return (base == 2 && !causal) ? 1 : base;
-}
+// +10-23% over XCD remap alone at S 1024-4096 (profiles/round3_attention_lpt_order.txt); full
+// attention XCD-remapped (1).
+int attn_order(bool causal) { return causal ? 2 : 1; }
 
-// forward (D = 64): issue a sub-tile pair's score MFMAs before its softmaxes -- 377/477 ->
-// 395/523 TFLOP/s at S = 1024/2048 (profiles/round3_attention_ab.txt); DCA_ATTN_FWD_PIPE=0 off
-bool fwd_pipe() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCA_ATTN_FWD_PIPE");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
-
-// forward pipelining at D = 128: +1-3.5% D128 S4096 causal fwd in two same-box A/Bs
-// (profiles/round4_attention_branchfree_ab.txt, round4_attention_knobs.txt); DCA_ATTN_FWD_PIPE128=0 off
-bool fwd_pipe128() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCA_ATTN_FWD_PIPE128");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
-
-// dQ kernel (D = 64): issue a sub-tile pair's S / dP products before their softmax gradients
-// (DCA_ATTN_DQ_PIPE=1)
-bool dq_pipe() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCA_ATTN_DQ_PIPE");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-
-// forward row sums on the matrix core (attn_fwd_kernel MSUM; DCA_ATTN_FWD_MSUM=1)
-bool fwd_msum() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCA_ATTN_FWD_MSUM");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-
-// keys per LDS tile of the forward kernel (DCA_ATTN_FWD_KT=128: half the barriers per MFMA)
-int fwd_kt() {
-  static const int kt = [] {
-    const char* e = std::getenv("DCA_ATTN_FWD_KT");
-    return (e && std::atoi(e) == 128) ? 128 : 64;
-  }();
-  return kt;
-}
 size_t bwd_dkdv_lds(int D, int QT) {
   return 2 * static_cast<size_t>(QT) * (D + kPad) * 2 + 2 * static_cast<size_t>(QT) * sizeof(float);
 }
 
-// queries per LDS tile of the dK/dV kernel (DCA_ATTN_DKDV_QT=32 restores the 32-query tiles)
-int dkdv_qt() {
-  static const int qt = [] {
-    const char* e = std::getenv("DCA_ATTN_DKDV_QT");
-    return (e && std::atoi(e) == 32) ? 32 : 64;
-  }();
-  return qt;
-}
-
-// timing-only forward ablation bits (attn_fwd_kernel ABL): DCA_ATTN_ABL
-int fwd_ablation() {
-  static const int a = [] {
-    const char* e = std::getenv("DCA_ATTN_ABL");
-    return e ? std::atoi(e) : 0;
-  }();
-  return a;
-}
-
-// forward K / V tiles through the direct-to-LDS ring (KVDma): +1.5-8 % causal, +3-5 % full over the
-// register-staged tiles (profiles/round5_attention_dma_ring_ab.txt); DCA_ATTN_FWD_DMA=0 restores them
-bool fwd_dma() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCA_ATTN_FWD_DMA");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
-
-// backward tiles through the direct-to-LDS ring at D = 128 (dQ: K / V, dK/dV: Q / dO; bwd +2 %,
-// profiles/round5_attention_dma_ring_ab.txt): DCA_ATTN_BWD_DMA=0 disables. At D = 64 the dK/dV
-// kernel sits at 246 of its 256 registers and the swizzled offsets spill it (-50 %), and the dQ
-// kernel alone measured -1.5 % on the backward: both keep register staging unless
-// DCA_ATTN_BWD_DMA64=1 (dQ only)
-// dK/dV register-staged tiles in the swizzled unpadded layout (DCA_ATTN_DKDV_SWZ=1): removes the
-// padded layout's 0.92 bank-conflict cycles per LDS instruction but measured neutral (D64 S1024 -1 %,
-// S2048 +2 %, GPT-2 step +0.1 %: profiles/round5_attention_dma_ring_ab.txt), so off by default
-bool dkdv_swz() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCA_ATTN_DKDV_SWZ");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-bool bwd_dma64() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCA_ATTN_BWD_DMA64");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-bool bwd_dma() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCA_ATTN_BWD_DMA");
-    return !(e && std::atoi(e) == 0);
-  }();
-  return on;
-}
-
-// forward with 64 query rows per wave (attn_fwd_w64_kernel): DCA_ATTN_FWD_W64=1
-bool fwd_w64() {
-  static const bool on = [] {
-    const char* e = std::getenv("DCA_ATTN_FWD_W64");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-
+// Production configuration, each choice measured on MI355X (the A/B switches that chose them were
+// removed in round 6; their profiles stay):
+//  * forward: 64-key tiles through the 2-stage direct-to-LDS ring (KVDma, +1.5-8 % causal, +3-5 %
+//    full: profiles/round5_attention_dma_ring_ab.txt), score products of a sub-tile pair issued
+//    before their softmaxes (PIPE: D64 +5-10 %, D128 +1-3.5 %: round3_attention_ab.txt,
+//    round4_attention_knobs.txt); 128-key tiles measured slower (round4_attention_knobs.txt);
+//  * dQ: D = 128 through the DMA ring (+2 %); D = 64 register-staged 64-key tiles (the ring -1.5 %);
+//  * dK/dV: D = 128 through the DMA ring; D = 64 register-staged 64-query tiles (at 246 of 256
+//    VGPRs the ring's swizzled offsets spill it).
 template <int D, bool C>
 void launch_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse,
                 int B, int H, int Sq, int Sk, Strides qs, Strides ks, Strides vs, Strides os,
                 float scale_log2, const int* kvlen, int G, hipStream_t st) {
-  dim3 grid((Sq + 127) / 128, H, B);
-  if (fwd_w64()) {
-    // D = 64: 2 waves x 64 queries = the same 128-query blocks; D = 128: 4 waves (256-query
-    // blocks) so the K/V staging registers per thread halve (one wave per SIMD either way)
-    constexpr int NW = D == 128 ? 4 : 2;
-    grid.x = (Sq + 64 * NW - 1) / (64 * NW);
-    auto kern = attn_fwd_w64_kernel<D, C, NW>;
-    const size_t lds = fwd_lds(D, 64);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
-                       scale_log2, attn_order(C), kvlen, G);
-    return;
-  }
-  auto go = [&](auto ktag) {
-    constexpr int KT = decltype(ktag)::value;
-    const size_t lds = fwd_lds(D, KT);
-    auto launch = [&](auto kern) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-      hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
-                         scale_log2, attn_order(C), kvlen, G);
-    };
-    const bool ms = fwd_msum();
-    if constexpr (KT == 64) {
-      if (fwd_dma() && !ms && fwd_ablation() == 0) {
-        // K / V tiles through the 2-stage direct-to-LDS ring (KVDma)
-        const size_t lds2 = 2 * 2 * static_cast<size_t>(KT) * D * 2;
-        auto launch2 = [&](auto kern) {
-          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds2));
-          hipLaunchKernelGGL(kern, grid, dim3(256), lds2, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
-                             scale_log2, attn_order(C), kvlen, G);
-        };
-        if (fwd_pipe() && (D == 64 || fwd_pipe128())) launch2(attn_fwd_kernel<D, C, KT, true, false, 0, true>);
-        else launch2(attn_fwd_kernel<D, C, KT, false, false, 0, true>);
-        return;
-      }
-    }
-    // D = 128: the pipelined form fits without spills only without MSUM (246 VGPRs)
-    if (fwd_pipe() && (D == 64 || (!ms && fwd_pipe128()))) {
-      if constexpr (C && KT == 64) {
-        switch (fwd_ablation()) {
-          case 1: launch(attn_fwd_kernel<D, C, KT, true, false, 1>); return;
-          case 2: launch(attn_fwd_kernel<D, C, KT, true, false, 2>); return;
-          case 4: launch(attn_fwd_kernel<D, C, KT, true, false, 4>); return;
-          case 8: launch(attn_fwd_kernel<D, C, KT, true, false, 8>); return;
-          case 15: launch(attn_fwd_kernel<D, C, KT, true, false, 15>); return;
-          case 16: launch(attn_fwd_kernel<D, C, KT, true, false, 16>); return;
-          case 48: launch(attn_fwd_kernel<D, C, KT, true, false, 48>); return;
-          case 63: launch(attn_fwd_kernel<D, C, KT, true, false, 63>); return;
-          default: break;
-        }
-      }
-      if constexpr (D == 64) {
-        if (ms) launch(attn_fwd_kernel<D, C, KT, true, true>);
-        else launch(attn_fwd_kernel<D, C, KT, true>);
-      } else {
-        launch(attn_fwd_kernel<D, C, KT, true>);
-      }
-      return;
-    }
-    if (ms) launch(attn_fwd_kernel<D, C, KT, false, true>);
-    else launch(attn_fwd_kernel<D, C, KT, false>);
-  };
-  if constexpr (D == 64) {  // D = 128 at KT = 128 exceeds the register file (spills)
-    if (fwd_kt() == 128) {
-      go(std::integral_constant<int, 128>{});
-      return;
-    }
-  }
-  go(std::integral_constant<int, 64>{});
+  const dim3 grid((Sq + 127) / 128, H, B);
+  constexpr int KT = 64;
+  const size_t lds = 2 * 2 * static_cast<size_t>(KT) * D * 2;
+  auto kern = attn_fwd_kernel<D, C, KT, true, true>;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, q, k, v, o, lse, Sq, Sk, H, qs, ks, vs, os,
+                     scale_log2, attn_order(C), kvlen, G);
 }
 
 template <int D, bool C>
@@ -1625,54 +1236,19 @@ void launch_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const u
     hipLaunchKernelGGL(kern, dim3((Sq + 127) / 128, H, B), dim3(256), l1, st, q, k, v, o, dO, lse,
                        delta, dq, Sq, Sk, H, qs, ks, vs, os, dos, dqs, scale_log2, scale, attn_order(C), kvlen, G);
   };
-  bool dq_done = false;
-  if (bwd_dma() && (D == 128 || bwd_dma64())) {
-    // K / V tiles through the direct-to-LDS ring (KVDma)
-    const size_t l2 = 2 * 2 * static_cast<size_t>(64) * D * 2;
-    if constexpr (D == 64) {
-      if (dq_pipe()) dq_go(attn_bwd_dq_kernel<D, C, 64, true, true>, l2);
-      else dq_go(attn_bwd_dq_kernel<D, C, 64, false, true>, l2);
-    } else {
-      dq_go(attn_bwd_dq_kernel<D, C, 64, false, true>, l2);
-    }
-    dq_done = true;
-  }
-  if constexpr (D == 64) {
-    if (dq_done) {
-    } else if (dq_kt() == 128) {
-      dq_go(attn_bwd_dq_kernel<D, C, 128, false>, bwd_dq_lds(D, 128));
-      dq_done = true;
-    } else if (dq_pipe()) {
-      dq_go(attn_bwd_dq_kernel<D, C, 64, true>, bwd_dq_lds(D, 64));
-      dq_done = true;
-    }
-  }
-  if (!dq_done) dq_go(attn_bwd_dq_kernel<D, C, 64, false>, bwd_dq_lds(D, 64));
-  bool dkdv_done = false;
   if constexpr (D == 128) {
-    if (bwd_dma() && dkdv_qt() == 64) {
-      const size_t l2 = 2 * (2 * static_cast<size_t>(64) * D * 2 + 2 * 64 * sizeof(float));
-      auto kern = attn_bwd_dkdv_dma_kernel<D, C, 64>;
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l2));
-      hipLaunchKernelGGL(kern, dim3((Sk + 127) / 128, H / G, B), dim3(256), l2, st, q, k, v, dO, lse,
-                         delta, dk, dv, Sq, Sk, H, qs, ks, vs, dos, dks, dvs, scale_log2, scale,
-                         attn_order(C), kvlen, G);
-      dkdv_done = true;
-    }
-  }
-  if (dkdv_done) {
-  } else if (dkdv_qt() == 64 && dkdv_swz()) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64, true>), dim3((Sk + 127) / 128, H / G, B), dim3(256),
-                       bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
-                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen, G);
-  } else if (dkdv_qt() == 64) {
+    dq_go(attn_bwd_dq_kernel<D, C, 64, false, true>, 2 * 2 * static_cast<size_t>(64) * D * 2);
+    const size_t l2 = 2 * (2 * static_cast<size_t>(64) * D * 2 + 2 * 64 * sizeof(float));
+    auto kern = attn_bwd_dkdv_dma_kernel<D, C, 64>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(l2));
+    hipLaunchKernelGGL(kern, dim3((Sk + 127) / 128, H / G, B), dim3(256), l2, st, q, k, v, dO, lse,
+                       delta, dk, dv, Sq, Sk, H, qs, ks, vs, dos, dks, dvs, scale_log2, scale,
+                       attn_order(C), kvlen, G);
+  } else {
+    dq_go(attn_bwd_dq_kernel<D, C, 64, false>, 2 * static_cast<size_t>(64) * (D + kPad) * 2);
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 64>), dim3((Sk + 127) / 128, H / G, B), dim3(256),
                        bwd_dkdv_lds(D, 64), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
-                       vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen, G);
-  } else {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, 32>), dim3((Sk + 127) / 128, H / G, B), dim3(256),
-                       bwd_dkdv_lds(D, 32), st, q, k, v, dO, lse, delta, dk, dv, Sq, Sk, H, qs, ks,
                        vs, dos, dks, dvs, scale_log2, scale, attn_order(C), kvlen, G);
   }
 }

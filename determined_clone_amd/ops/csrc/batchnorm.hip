@@ -42,15 +42,7 @@ struct RowGeom {
 // At most 32 threads (256 channels, 512 B of bf16) per row: wide tensors are split over grid.y
 // channel groups, which multiplies the workgroups of the reduce passes without growing their
 // [blocks][2][C] partials.
-inline int max_tpr() {
-  // DCA_BN_MAXTPR (8..256, a power of two) overrides the cap (tuning sweeps only).
-  static const int v = [] {
-    const char* e = std::getenv("DCA_BN_MAXTPR");
-    int t = e ? std::atoi(e) : 32;
-    return (t >= 8 && t <= kBlock && (t & (t - 1)) == 0) ? t : 32;
-  }();
-  return v;
-}
+inline int max_tpr() { return 32; }
 inline RowGeom row_geom(int C) {
   int c8 = C / 8;
   RowGeom g;
@@ -69,7 +61,7 @@ inline ReduceGeom reduce_geom(int C) { return row_geom(C); }
 // the launcher may use a flat grid (gridDim.y == 1) whose FASTEST index is the channel group, so
 // the blocks that share a row range -- together covering whole rows -- run together and each row's
 // bytes are streamed at once, instead of one channel slice of every row per pass over the tensor
-// (blockIdx.y slowest). DCA_BN_APPLY_FLAT=0 keeps the 2-D grid.
+// (blockIdx.y slowest): C 1024-2048 apply 3.8-4.4 -> 5.2 TB/s (profiles/round4_bn_apply_flat_grid_ab.txt).
 struct BlkMap {
   int cg, bx, nb;
 };
@@ -508,17 +500,7 @@ struct ReduceTuning {
   int64_t elems_per_block, min_blocks, max_blocks, cap_floats;
 };
 inline const ReduceTuning& reduce_tuning() {
-  // DCA_BN_REDUCE="elems,min,max[,cap]" overrides the workgroup-count heuristic and the
-  // per-statistic partials cap (tuning sweeps only).
-  static const ReduceTuning t = [] {
-    ReduceTuning r{32768, 256, 2048, int64_t(1) << 18};
-    if (const char* e = std::getenv("DCA_BN_REDUCE")) {
-      long long a = 0, b = 0, c = 0, d = 0;
-      const int n = std::sscanf(e, "%lld,%lld,%lld,%lld", &a, &b, &c, &d);
-      if (n >= 3 && a > 0 && b > 0 && c >= b) r = {a, b, c, n == 4 && d > 0 ? d : r.cap_floats};
-    }
-    return r;
-  }();
+  static const ReduceTuning t{32768, 256, 2048, int64_t(1) << 18};
   return t;
 }
 
@@ -545,20 +527,10 @@ inline int reduce_blocks(int64_t M, int C, const ReduceGeom& g) {
 // grid with 4 rows per lane (tools/bench_bn.py, profiles/round4_bn_apply_oneshot_ab.txt; the
 // one-shot copy ceiling of this box is 6.16 TB/s, profiles/round4_hbm_streaming_ceilings.txt);
 // smaller tensors keep 4 rows per lane and the 2048-workgroup cap.
-// DCA_BN_APPLY="U,max_blocks" (U in 2 | 4 | 8) forces one geometry (A/B sweeps only).
 struct ApplyTuning {
   int u, max_blocks;
 };
 inline ApplyTuning apply_tuning(int64_t elems) {
-  static const ApplyTuning forced = [] {
-    ApplyTuning r{0, 0};
-    if (const char* e = std::getenv("DCA_BN_APPLY")) {
-      int u = 0, mb = 0;
-      if (std::sscanf(e, "%d,%d", &u, &mb) == 2 && (u == 2 || u == 4 || u == 8) && mb > 0) r = {u, mb};
-    }
-    return r;
-  }();
-  if (forced.u) return forced;
   if (elems >= (int64_t{1} << 25)) return {2, 1 << 30};
   return {kUApply, 2048};
 }
@@ -572,35 +544,15 @@ inline int apply_blocks(int64_t M, const RowGeom& g, const ApplyTuning& t) {
 }
 
 inline dim3 apply_grid(int64_t M, const RowGeom& g, const ApplyTuning& t) {
-  static const bool flat = [] {
-    const char* e = std::getenv("DCA_BN_APPLY_FLAT");
-    return !(e && std::atoi(e) == 0);
-  }();
   const int bx = apply_blocks(M, g, t);
-  if (flat && g.cgroups > 1 && static_cast<int64_t>(bx) * g.cgroups < (int64_t{1} << 31))
+  if (g.cgroups > 1 && static_cast<int64_t>(bx) * g.cgroups < (int64_t{1} << 31))
     return dim3(bx * g.cgroups, 1);  // see apply_block_map
   return dim3(bx, g.cgroups);
 }
 
 // Reduce-pass variant: the statistics passes stream with NONTEMPORAL loads by default (-3% on
 // the bs-1024 ResNet-50 BN shapes, fwd+bwd 32.3 -> 31.4 ms per step in tools/bench_bn.py,
-// profiles/round4_bn_reduce_nt_ab.txt). DCA_BN_REDUCE_VAR="U_bwd,nt" (A/B sweeps only): rows in
-// flight per lane in the backward pass (4 | 8) and nontemporal loads (0 | 1).
-struct ReduceVar {
-  int u_bwd;
-  bool nt;
-};
-inline const ReduceVar& reduce_var() {
-  static const ReduceVar v = [] {
-    ReduceVar r{kUReduceBwd, true};
-    if (const char* e = std::getenv("DCA_BN_REDUCE_VAR")) {
-      int u = 0, nt = 0;
-      if (std::sscanf(e, "%d,%d", &u, &nt) == 2 && (u == 4 || u == 8)) r = {u, nt != 0};
-    }
-    return r;
-  }();
-  return v;
-}
+// profiles/round4_bn_reduce_nt_ab.txt).
 
 template <typename T>
 void launch_reduce(bool bwd, const void* x, const void* dy, const void* dy2, const uint8_t* y,
@@ -611,21 +563,12 @@ void launch_reduce(bool bwd, const void* x, const void* dy, const void* dy2, con
   dim3 grid(B, g.cgroups);
   const bool dual = bwd && x2 != nullptr;
   size_t lds = static_cast<size_t>(g.rpi) * g.tpr * (dual ? 24 : 16) * sizeof(float);
-  const ReduceVar& v = reduce_var();
-#define DCA_RED(BW, UU, NTT, DU)                                                                     \
-  hipLaunchKernelGGL((bn_reduce_kernel<T, BW, UU, NTT, DU>), grid, dim3(kBlock), lds, st, x, dy, dy2, \
+#define DCA_RED(BW, UU, DU)                                                                       \
+  hipLaunchKernelGGL((bn_reduce_kernel<T, BW, UU, true, DU>), grid, dim3(kBlock), lds, st, x, dy, dy2, \
                      y, mean, M, C, g.tpr, g.rpi, relu, partial, x2, mean2, partial2)
-  if (dual) {
-    if (v.nt) DCA_RED(true, kUReduceBwd, true, true); else DCA_RED(true, kUReduceBwd, false, true);
-  } else if (bwd) {
-    if (v.u_bwd == 8) {
-      if (v.nt) DCA_RED(true, 8, true, false); else DCA_RED(true, 8, false, false);
-    } else {
-      if (v.nt) DCA_RED(true, kUReduceBwd, true, false); else DCA_RED(true, kUReduceBwd, false, false);
-    }
-  } else {
-    if (v.nt) DCA_RED(false, kUReduceFwd, true, false); else DCA_RED(false, kUReduceFwd, false, false);
-  }
+  if (dual) DCA_RED(true, kUReduceBwd, true);
+  else if (bwd) DCA_RED(true, kUReduceBwd, false);
+  else DCA_RED(false, kUReduceFwd, false);
 #undef DCA_RED
 }
 
@@ -673,51 +616,6 @@ void launch_apply_bwd(const void* dy, const void* dy2, const uint8_t* mask, cons
 struct PoolGeom {
   int H, W, Ho, Wo;
 };
-
-template <typename T>
-__global__ __launch_bounds__(kBlock) void bn_relu_pool_fwd_kernel(
-    const void* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
-    void* __restrict__ y, uint8_t* __restrict__ idx, int64_t nout, int C, PoolGeom g) {
-  const int c8 = C / 8;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < nout;
-       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int c = static_cast<int>(t % c8) * 8;
-    const int64_t o = t / c8;  // (n, ho, wo)
-    const int wo = static_cast<int>(o % g.Wo);
-    const int ho = static_cast<int>((o / g.Wo) % g.Ho);
-    const int64_t n = o / (static_cast<int64_t>(g.Wo) * g.Ho);
-    float a[8], b[8], best[8];
-    uint32_t slot[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { a[k] = scale[c + k]; b[k] = shift[c + k]; best[k] = 0.f; slot[k] = 0xff; }
-    for (int kh = 0; kh < 3; ++kh) {
-      const int h = 2 * ho - 1 + kh;
-      if (h < 0 || h >= g.H) continue;
-      for (int kw = 0; kw < 3; ++kw) {
-        const int w = 2 * wo - 1 + kw;
-        if (w < 0 || w >= g.W) continue;
-        float v[8];
-        Vec8<T>::load(reinterpret_cast<const char*>(x) +
-                          (((n * g.H + h) * g.W + w) * C + c) * Vec8<T>::bytes, v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float r = fmaxf(fmaf(v[k], a[k], b[k]), 0.f);
-          // first maximum wins (matches max_pool2d over the ReLU output)
-          if (slot[k] == 0xff || r > best[k]) { best[k] = r; slot[k] = kh * 3 + kw; }
-        }
-      }
-    }
-    Vec8<T>::store(reinterpret_cast<char*>(y) + t * 8 * Vec8<T>::bytes, best);
-    if (idx) {
-      uint32_t lo = 0, hi = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) lo |= ((slot[k] | (best[k] > 0.f ? 0x10u : 0u)) & 0xffu) << (8 * k);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) hi |= ((slot[4 + k] | (best[4 + k] > 0.f ? 0x10u : 0u)) & 0xffu) << (8 * k);
-      *reinterpret_cast<uint2*>(idx + t * 8) = make_uint2(lo, hi);
-    }
-  }
-}
 
 // Forward in quad form: one thread per 2x2 block of pooled outputs (ho = 2hq + a, wo = 2wq + b)
 // and 8 channels. Their windows cover input rows 4hq-1 .. 4hq+3 and columns 4wq-1 .. 4wq+3: 25 loads
@@ -1151,11 +1049,7 @@ void bn_relu_pool_forward(BnDtype dt, const void* x, void* y, uint8_t* idx, int 
                                       given_partials, given_blocks, st);
     shift = scale + C;
   }
-  static const bool quad = [] {
-    const char* e = std::getenv("DCA_BN_POOL_FWD_QUAD");
-    return !(e && e[0] == '0');
-  }();
-  if (quad) {
+  {
     const int64_t nthr = static_cast<int64_t>(N) * ((g.Ho + 1) / 2) * ((g.Wo + 1) / 2) * (C / 8);
     const int qgrid = stream_grid(nthr, kBlock);
     switch (dt) {
@@ -1163,14 +1057,6 @@ void bn_relu_pool_forward(BnDtype dt, const void* x, void* y, uint8_t* idx, int 
       case BnDtype::kF16: hipLaunchKernelGGL(bn_relu_pool_fwd_quad_kernel<F16>, dim3(qgrid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nthr, C, g); break;
       default: hipLaunchKernelGGL(bn_relu_pool_fwd_quad_kernel<F32>, dim3(qgrid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nthr, C, g); break;
     }
-    return;
-  }
-  const int64_t nout = static_cast<int64_t>(N) * g.Ho * g.Wo * C / 8;
-  const int grid = stream_grid(nout, kBlock);
-  switch (dt) {
-    case BnDtype::kBF16: hipLaunchKernelGGL(bn_relu_pool_fwd_kernel<BF16>, dim3(grid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nout, C, g); break;
-    case BnDtype::kF16: hipLaunchKernelGGL(bn_relu_pool_fwd_kernel<F16>, dim3(grid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nout, C, g); break;
-    default: hipLaunchKernelGGL(bn_relu_pool_fwd_kernel<F32>, dim3(grid), dim3(kBlock), 0, st, x, scale, shift, y, idx, nout, C, g); break;
   }
 }
 

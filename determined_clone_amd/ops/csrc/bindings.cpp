@@ -583,8 +583,11 @@ void register_conv_ops(pybind11::module& m);
 void register_groupnorm_ops(pybind11::module& m);
 void register_lt_ops(pybind11::module& m);
 
+extern "C" const char dca_source_hash[];  // ops/build.py: sha256 of the csrc/ tree
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "determined_clone_amd MI355X (gfx950) HIP kernels";
+  m.attr("source_hash") = pybind11::str(static_cast<const char*>(dca_source_hash));
   m.def("bn_fwd_train", &bn_fwd_train, pybind11::arg("x"), pybind11::arg("residual"),
         pybind11::arg("weight"), pybind11::arg("bias"), pybind11::arg("running_mean"),
         pybind11::arg("running_var"), pybind11::arg("num_batches"), pybind11::arg("momentum"),

@@ -99,39 +99,6 @@ Tensor conv_igemm_dgrad(const Tensor& dy_in, const Tensor& w, int64_t pad) {
   return dx;
 }
 
-// dx of a stride-1 convolution whose input was relu(bn(bn_x)) (bn_mask: that BatchNorm's ReLU
-// bits, bn_mean its saved mean): also returns the BatchNorm backward's [blocks][2][C] statistics
-// partials, reduced in the data-gradient epilogue (batchnorm bwd then skips its statistics pass).
-std::vector<Tensor> conv_igemm_dgrad_bn(const Tensor& dy_in, const Tensor& w, int64_t pad,
-                                        const Tensor& bn_x, const Tensor& bn_mask,
-                                        const Tensor& bn_mean) {
-  const Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
-  const c10::DeviceGuard dg(dy.device());
-  check_nhwc(dy, "conv_igemm_dgrad_bn");
-  TORCH_CHECK(w.dim() == 4 && w.size(0) == dy.size(1) && w.size(1) % 64 == 0 &&
-                  w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.scalar_type() == at::kBFloat16,
-              "conv_igemm_dgrad_bn: weight must be bf16 channels_last [K, C, R, S], C a multiple of 64");
-  const int64_t K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
-  TORCH_CHECK(R == S && pad <= R - 1, "conv_igemm_dgrad_bn: square kernels, padding < kernel");
-  Tensor wt = torch::empty({C, K, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
-  dca::conv_flip_transpose(w.data_ptr(), wt.data_ptr(), static_cast<int>(K), static_cast<int>(C),
-                           static_cast<int>(R * S), stream());
-  const dca::ConvGeom g = geom(dy, wt, 1, R - 1 - pad);
-  check_nhwc(bn_x, "conv_igemm_dgrad_bn (bn_x)");
-  TORCH_CHECK(bn_x.size(0) == g.N && bn_x.size(1) == g.K && bn_x.size(2) == g.P && bn_x.size(3) == g.Q,
-              "conv_igemm_dgrad_bn: bn_x must have the data gradient's shape");
-  TORCH_CHECK(bn_mask.scalar_type() == at::kByte && bn_mask.is_contiguous() &&
-                  bn_mask.numel() == static_cast<int64_t>(g.M) * g.K / 8 && bn_mask.device() == dy.device(),
-              "conv_igemm_dgrad_bn: bn_mask must be the BatchNorm's ReLU bitmask");
-  TORCH_CHECK(bn_mean.scalar_type() == at::kFloat && bn_mean.is_contiguous() && bn_mean.numel() == g.K,
-              "conv_igemm_dgrad_bn: bn_mean must be fp32 [C]");
-  Tensor dx = torch::empty({g.N, g.K, g.P, g.Q}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  Tensor partial = torch::empty({dca::conv_igemm_row_blocks(g), 2, g.K}, dy.options().dtype(at::kFloat));
-  dca::conv_igemm_fwd(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), partial.data_ptr<float>(), g,
-                      stream(), bn_x.data_ptr(), bn_mask.data_ptr<uint8_t>(), bn_mean.data_ptr<float>());
-  return {dx, partial};
-}
-
 // Weight gradient of y = conv2d(x, w, stride, pad) given dy; with `acc` (the parameter's
 // persistent .grad view, fp32 or bf16, [K, C, R, S] channels_last) it is added in place and
 // returned.
@@ -184,14 +151,14 @@ void strided_accumulate(Tensor& dx, const Tensor& small, int64_t s) {
                           static_cast<int>(Wo), static_cast<int>(s), stream());
 }
 
-// [N, 3, H, W] channels_last bf16 image -> [N, co, (H+6)/2, (W+6)/2] channels_last (ops/conv.py
-// _s2d_input: the space-to-depth form of the 7x7/2 padding-3 stem convolution; co = 12 or 16).
-Tensor stem_s2d(const Tensor& x, int64_t co) {
+// [N, 3, H, W] channels_last bf16 image -> [N, 12, (H+6)/2, (W+6)/2] channels_last (ops/conv.py
+// _s2d_input: the space-to-depth form of the 7x7/2 padding-3 stem convolution).
+Tensor stem_s2d(const Tensor& x) {
+  constexpr int64_t co = 12;
   const c10::DeviceGuard dg(x.device());
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) == 3,
               "stem_s2d: bf16 [N, 3, H, W] GPU tensor required");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "stem_s2d: channels_last layout required");
-  TORCH_CHECK(co == 12 || co == 16, "stem_s2d: co must be 12 or 16");
   const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
   TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "stem_s2d: even H and W required");
   TORCH_CHECK(N * (H + 6) * (W + 6) * 4 < (int64_t{1} << 40), "stem_s2d: too large");
@@ -199,62 +166,12 @@ Tensor stem_s2d(const Tensor& x, int64_t co) {
                            x.options().memory_format(at::MemoryFormat::ChannelsLast));
   if (xs.numel() == 0) return xs;
   dca::stem_s2d(x.data_ptr(), xs.data_ptr(), static_cast<int>(N), static_cast<int>(H),
-                static_cast<int>(W), static_cast<int>(co), stream());
+                static_cast<int>(W), stream());
   return xs;
 }
 
-// Stem convolution on the 16-channel S2D tensor (ops/conv.py _StemS2D): xs [N, 16, Hs, Ws] and
-// w16 [64, 16, 4, 4], both channels_last bf16 -> (y [N, 64, Hs-3, Ws-3] channels_last, partial
-// statistics [blocks, 2, 64] fp32 for the stem BatchNorm).
-std::vector<Tensor> stem_conv_fwd(const Tensor& xs, const Tensor& w16) {
-  const c10::DeviceGuard dg(xs.device());
-  TORCH_CHECK(xs.is_cuda() && xs.scalar_type() == at::kBFloat16 && xs.dim() == 4 && xs.size(1) == 16 &&
-                  xs.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "stem_conv_fwd: channels_last bf16 [N, 16, Hs, Ws] input required");
-  TORCH_CHECK(w16.is_cuda() && w16.scalar_type() == at::kBFloat16 && w16.dim() == 4 &&
-                  w16.size(0) == 64 && w16.size(1) == 16 && w16.size(2) == 4 && w16.size(3) == 4 &&
-                  w16.is_contiguous(at::MemoryFormat::ChannelsLast) && w16.device() == xs.device(),
-              "stem_conv_fwd: channels_last bf16 [64, 16, 4, 4] weight required");
-  const int64_t N = xs.size(0), Hs = xs.size(2), Ws = xs.size(3);
-  TORCH_CHECK(Hs >= 4 && Ws - 3 >= 64 && Ws <= 256, "stem_conv_fwd: needs 67 <= Ws <= 256");
-  TORCH_CHECK(N * Hs * Ws * 32 < (int64_t{1} << 31) && N * ((Hs - 3) * (Ws - 3) + 127) / 128 < (int64_t{1} << 31),
-              "stem_conv_fwd: input too large for 32-bit buffer offsets");
-  Tensor y = torch::empty({N, 64, Hs - 3, Ws - 3}, xs.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int blocks = dca::stem_conv_blocks(static_cast<int>(N), static_cast<int>(Hs), static_cast<int>(Ws));
-  Tensor partial = torch::empty({blocks, 2, 64}, xs.options().dtype(at::kFloat));
-  dca::stem_conv_fwd(xs.data_ptr(), w16.data_ptr(), y.data_ptr(), partial.data_ptr<float>(),
-                     static_cast<int>(N), static_cast<int>(Hs), static_cast<int>(Ws), stream());
-  return {y, partial};
-}
-
-// Stem weight gradient (ops/conv.py _StemS2D.backward): dy [N, 64, P, Q] and the 12-channel S2D
-// image xs [N, 12, P+3, Q+3], channels_last bf16 -> dw [64, 4, 4, 12] fp32 ((di, dj, channel) order).
-Tensor stem_wgrad(const Tensor& dy, const Tensor& xs) {
-  const c10::DeviceGuard dg(dy.device());
-  TORCH_CHECK(xs.is_cuda() && xs.scalar_type() == at::kBFloat16 && xs.dim() == 4 && xs.size(1) == 12 &&
-                  xs.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "stem_wgrad: channels_last bf16 [N, 12, Hs, Ws] image required");
-  const int64_t N = xs.size(0), Hs = xs.size(2), Ws = xs.size(3);
-  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N &&
-                  dy.size(1) == 64 && dy.size(2) == Hs - 3 && dy.size(3) == Ws - 3 &&
-                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.device() == xs.device(),
-              "stem_wgrad: channels_last bf16 [N, 64, Hs-3, Ws-3] gradient required");
-  TORCH_CHECK(Hs >= 4 && Ws >= 4 && Ws - 3 <= 128, "stem_wgrad: output width must be <= 128");
-  TORCH_CHECK(N * Hs * Ws * 12 < (int64_t{1} << 40) && N * (Hs - 3) < (int64_t{1} << 31), "stem_wgrad: too large");
-  const int blocks = dca::stem_wgrad_blocks(static_cast<int>(N));
-  auto fopt = xs.options().dtype(at::kFloat);
-  Tensor ws = torch::empty({blocks, 64, 4, 4, 12}, fopt);
-  dca::stem_wgrad(dy.data_ptr(), xs.data_ptr(), ws.data_ptr<float>(), static_cast<int>(N),
-                  static_cast<int>(Hs), static_cast<int>(Ws), stream());
-  // per-block partials summed by ATen's tree reduction (fixed order; the 12 K outputs x 1 K
-  // partials leave a dedicated kernel too few workgroups: 0.5 ms at 6 blocks)
-  return ws.sum(0);
-}
-
 void register_conv_ops(pybind11::module& m) {
-  m.def("stem_s2d", &stem_s2d, pybind11::arg("x"), pybind11::arg("co") = 12);
-  m.def("stem_conv_fwd", &stem_conv_fwd, pybind11::arg("xs"), pybind11::arg("w16"));
-  m.def("stem_wgrad", &stem_wgrad, pybind11::arg("dy"), pybind11::arg("xs"));
+  m.def("stem_s2d", &stem_s2d, pybind11::arg("x"));
   m.def("strided_accumulate", &strided_accumulate, pybind11::arg("dx"), pybind11::arg("small"),
         pybind11::arg("stride"));
   m.def("conv_igemm_wgrad", &conv_igemm_wgrad, pybind11::arg("dy"), pybind11::arg("x"),
@@ -264,6 +181,4 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stats"));
   m.def("conv_igemm_dgrad", &conv_igemm_dgrad, pybind11::arg("dy"), pybind11::arg("w"),
         pybind11::arg("pad"));
-  m.def("conv_igemm_dgrad_bn", &conv_igemm_dgrad_bn, pybind11::arg("dy"), pybind11::arg("w"),
-        pybind11::arg("pad"), pybind11::arg("bn_x"), pybind11::arg("bn_mask"), pybind11::arg("bn_mean"));
 }

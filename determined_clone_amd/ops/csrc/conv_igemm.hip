@@ -84,17 +84,14 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rsrc, uint32_t vof
       rsrc, (__attribute__((address_space(3))) void*)(lds_dst), 16, voff, soff, 0, 0);
 }
 
-// STATS (epilogue statistics into partial[mt][2][K], batchnorm.hip's layout):
-//   0 = none;
-//   1 = forward: (sum y, sum y^2) of the bf16 outputs -- the following BatchNorm's statistics;
-//   2 = backward: this launch is the DATA GRADIENT of a convolution whose input was
-//       relu(bn(bnx)); with g = the bf16 output and m = that BatchNorm's ReLU bit (bnmask),
-//       (sum g*m, sum g*m*(bnx - bnmean)) -- the BatchNorm backward's statistics pass, fused.
-template <int BM, int BN, int WM, int WN, int NSTAGE, int STATS>
+// STATS: the epilogue also reduces (sum y, sum y^2) of the bf16 outputs -- the following
+// BatchNorm's statistics -- into partial[mt][2][K] (batchnorm.hip's layout). (The backward form,
+// BatchNorm backward statistics in the data-gradient epilogue, measured -0.4 % on the step and was
+// removed: profiles/round5_dgrad_bn_stats_epilogue_ab.txt.)
+template <int BM, int BN, int WM, int WN, int NSTAGE, bool STATS>
 __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-    float* __restrict__ partial, ConvGeom g, const uint16_t* __restrict__ bnx,
-    const uint8_t* __restrict__ bnmask, const float* __restrict__ bnmean) {
+    float* __restrict__ partial, ConvGeom g) {
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM / WM, TN = BN / WN;  // wave tile: pixels x channels
   constexpr int FM = TM / 32, FN = TN / 32;
@@ -276,35 +273,22 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
   constexpr int CPR = BN / 8;          // 16-B chunks per output row
   constexpr int RPP = kThreads / CPR;  // rows per pass
   const int cc = tid % CPR, rr = tid / CPR;
-  float s8[8], q8[8], mu[8];
+  float s8[8], q8[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; mu[k] = STATS == 2 ? bnmean[n0 + cc * 8 + k] : 0.f; }
+  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
   for (int row = rr; row < BM; row += RPP) {
     if (m0 + row >= g.M) break;
     const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CS + cc * 8);
     const int64_t off = static_cast<int64_t>(m0 + row) * g.K + n0 + cc * 8;
     *reinterpret_cast<uint4*>(y + off) = v;
-    if (STATS) {
+    if constexpr (STATS) {
       const float f[8] = {bf16_lo(v.x), bf16_hi(v.x), bf16_lo(v.y), bf16_hi(v.y),
                           bf16_lo(v.z), bf16_hi(v.z), bf16_lo(v.w), bf16_hi(v.w)};
-      if (STATS == 1) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] = fmaf(f[k], f[k], q8[k]); }
-      } else {
-        const uint4 xv = *reinterpret_cast<const uint4*>(bnx + off);
-        const uint32_t mk = bnmask[off >> 3];
-        const float xf[8] = {bf16_lo(xv.x), bf16_hi(xv.x), bf16_lo(xv.y), bf16_hi(xv.y),
-                             bf16_lo(xv.z), bf16_hi(xv.z), bf16_lo(xv.w), bf16_hi(xv.w)};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float gk = ((mk >> k) & 1u) ? f[k] : 0.f;
-          s8[k] += gk;
-          q8[k] = fmaf(gk, xf[k] - mu[k], q8[k]);
-        }
-      }
+      for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] = fmaf(f[k], f[k], q8[k]); }
     }
   }
-  if (STATS) {
+  if constexpr (STATS) {
     // partial[mt][0][k] = sum, partial[mt][1][k] = sum of squares (batchnorm.hip layout)
     __syncthreads();
     float* red = reinterpret_cast<float*>(lds);  // [RPP][CPR * 16]
@@ -531,137 +515,6 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_kernel(
     }
 }
 
-// ResNet stem weight gradient on the 12-channel space-to-depth image (ops/conv.py _StemS2D):
-//   dW[k][j] = sum_pix dy[pix][k] * xs[n][p + di][q * 12 + r],  j = di * 48 + r (r = dj * 12 + c),
-// i.e. the 4x4/1 conv's [64][4][4][12] gradient with K = the N*P*Q output pixels. For output row
-// (n, p) the im2col operand is never built: the 48-element run of tap row di at pixel q is the
-// contiguous S2D row slice starting at q * 12, so ds_read_b64_tr_b16 reads the B fragments straight
-// from 4 S2D rows in LDS (8-B aligned: 24 q + 2 r with r a multiple of 4) and the dy row
-// [128 px (112 + zero tail)][64 ch] gives the A fragments. One block per image (112 output rows),
-// S2D rows in a 4-slot ring (one new row per output row), fp32 partials per image summed by ATen.
-// Correct but SLOWER than MIOpen's wrw (1.25-1.43 ms over five versions vs 1.11 ms at bs 1024;
-// this one, two steps of loads in flight, 1.43 ms -- the one-step ring measured 1.31:
-// profiles/round5_stem_wgrad_kernel_ab.txt), so opt-in (DCA_STEM_WGRAD=1);
-// 2 x 2 waves over the 64 x 192 result (one 32-channel half x 96 columns each), fp32 tile per block
-// -> stem_wgrad_reduce. MIOpen's wrw ran this in ~0.9 ms, the last kernel before the optimizer.
-constexpr int kStemWgPx = 128;     // dy pixels per LDS row tile (112 + zero tail)
-constexpr int kStemWgDyS = 72;     // dy LDS row stride (elements): 144-B rows, tr reads conflict-free
-
-__global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(const uint16_t* __restrict__ dy,
-                                                              const uint16_t* __restrict__ xs,
-                                                              float* __restrict__ ws, int P, int Q,
-                                                              int Hs, int Ws) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  uint16_t* dyL = lds;                                  // [kStemWgPx][kStemWgDyS]
-  uint16_t* xsL = lds + kStemWgPx * kStemWgDyS;         // 4 S2D rows (4 * Ws * 12) + zero tail
-  const int row_el = Ws * 12;
-  const int xs_len = 4 * row_el + (kStemWgPx + 4 - Ws > 0 ? (kStemWgPx + 4 - Ws) * 12 : 0);
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // zero the dy tail rows and the S2D tail once (never overwritten)
-  for (int e = tid; e < (kStemWgPx - Q) * kStemWgDyS; e += kThreads) dyL[Q * kStemWgDyS + e] = 0;
-  for (int e = 4 * row_el + tid; e < xs_len; e += kThreads) xsL[e] = 0;
-
-  const int wm = wv & 1, wj = wv >> 1;  // channels 32 wm .., columns 96 wj ..
-  const int h = lane >> 5, gq = (lane >> 2) & 3, gp = lane & 3, half16 = (lane >> 4) & 1;
-  f32x16 acc[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
-  // this lane's B columns: j = 96 wj + 32 t + half16 * 16 + 4 gp -> (tap row di, offset r)
-  int bdi[3], br[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int j = 96 * wj + 32 * t + half16 * 16 + 4 * gp;
-    bdi[t] = j / 48;
-    br[t] = j - bdi[t] * 48;
-  }
-  const int acol = 32 * wm + half16 * 16 + 4 * gp;
-
-  // One block per image (rows p = 0 .. P-1 in order). The S2D rows live in a 4-slot ring (row r in
-  // slot r & 3): output row p needs rows p .. p+3, so each step brings ONE new S2D row (p + 3) plus
-  // the dy row -- the loads of step p+1 are issued before step p is computed.
-  const int n = blockIdx.x;
-  const uint16_t* xs_img = xs + static_cast<int64_t>(n) * Hs * row_el;
-  const uint4* dy_img = reinterpret_cast<const uint4*>(dy + static_cast<int64_t>(n) * P * Q * 64);
-  constexpr int kDyV = (kStemWgPx * 8 + kThreads - 1) / kThreads;   // 16-B chunks per lane
-  constexpr int kXsV = (131 * 12 / 4 + kThreads - 1) / kThreads;     // 8-B chunks per lane (Ws <= 131)
-  const int row_v = row_el / 4;                                      // 8-B chunks per S2D row
-  struct Regs {
-    uint4 dy[kDyV];
-    uint2 xs[kXsV];
-  };
-  auto load_step = [&](int p, Regs& R) __attribute__((always_inline)) {  // dy row p, S2D row p + 3
-#pragma unroll
-    for (int i = 0; i < kDyV; ++i) {
-      const int c = tid + i * kThreads;
-      if (c < Q * 8) R.dy[i] = dy_img[static_cast<int64_t>(p) * Q * 8 + c];
-    }
-    const uint2* xsrc = reinterpret_cast<const uint2*>(xs_img + static_cast<int64_t>(p + 3) * row_el);
-#pragma unroll
-    for (int i = 0; i < kXsV; ++i) {
-      const int c = tid + i * kThreads;
-      if (c < row_v) R.xs[i] = xsrc[c];
-    }
-  };
-  // one step: this row's operands (loaded two steps earlier) -> LDS, the row two steps ahead into
-  // the same registers, then the MFMAs. Raw barriers + lgkmcnt(0): __syncthreads would also drain
-  // vmcnt, i.e. wait for the loads just issued for the next step.
-  auto step = [&](int p, Regs& R) __attribute__((always_inline)) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_raw();  // previous step's fragments read
-#pragma unroll
-    for (int i = 0; i < kDyV; ++i) {
-      const int c = tid + i * kThreads;
-      if (c < Q * 8) *reinterpret_cast<uint4*>(dyL + (c >> 3) * kStemWgDyS + (c & 7) * 8) = R.dy[i];
-    }
-    uint2* slot = reinterpret_cast<uint2*>(xsL + ((p + 3) & 3) * row_el);
-#pragma unroll
-    for (int i = 0; i < kXsV; ++i) {
-      const int c = tid + i * kThreads;
-      if (c < row_v) slot[c] = R.xs[i];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_raw();
-    if (p + 2 < P) load_step(p + 2, R);
-    int boff[3];
-#pragma unroll
-    for (int t = 0; t < 3; ++t) boff[t] = ((p + bdi[t]) & 3) * row_el + br[t];
-#pragma unroll
-    for (int ks = 0; ks < kStemWgPx / 16; ++ks) {
-      const int px0 = 16 * ks + 8 * h + gq;  // + 4 for the second read
-      const bf16x8 a = cat8(tr_read(dyL + px0 * kStemWgDyS + acol),
-                            tr_read(dyL + (px0 + 4) * kStemWgDyS + acol));
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const bf16x8 b = cat8(tr_read(xsL + px0 * 12 + boff[t]), tr_read(xsL + (px0 + 4) * 12 + boff[t]));
-        acc[t] = mfma32(a, b, acc[t]);
-      }
-    }
-  };
-  // S2D rows 0 .. 2 into slots 0 .. 2 (plain loads, published by the first step's barrier)
-  for (int c = tid; c < 3 * row_v; c += kThreads)
-    reinterpret_cast<uint2*>(xsL)[c] = reinterpret_cast<const uint2*>(xs_img)[c];
-  Regs ra, rb;
-  load_step(0, ra);
-  if (P > 1) load_step(1, rb);
-  for (int p = 0; p < P; p += 2) {
-    step(p, ra);
-    if (p + 1 < P) step(p + 1, rb);
-  }
-  // fp32 tile -> ws[block][k][j]
-  float* out = ws + static_cast<int64_t>(blockIdx.x) * 64 * 192;
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int j = 96 * wj + 32 * t + (lane & 31);
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int k = 32 * wm + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      out[k * 192 + j] = acc[t][reg];
-    }
-  }
-}
-
 // dW (+)= sum over splits in a fixed order; 8 elements per thread. The workspace is in the
 // weight's [K][R][S][C] order; `kcrs` writes dW in [K][C][R][S] order instead (a contiguous NCHW
 // .grad view of a channels_last parameter).
@@ -709,11 +562,7 @@ struct WgCfg {
 };
 
 WgCfg wgrad_cfg(const ConvGeom& g) {
-  static const int target = [] {
-    const char* e = std::getenv("DCA_IGEMM_WG_BLOCKS");  // tuning sweeps only
-    const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : 1024;
-  }();
+  constexpr int target = 1024;  // workgroups to aim for (tiles x pixel splits)
   WgCfg c;
   c.bko = g.K % 128 == 0 ? 128 : 64;
   c.bc = g.C % 128 == 0 ? 128 : 64;
@@ -751,44 +600,20 @@ struct Cfg {
 };
 
 Cfg pick(const ConvGeom& g) {
-  static const int force_bm = [] {
-    const char* e = std::getenv("DCA_IGEMM_BM");  // tuning sweeps only
-    return e ? std::atoi(e) : 0;
-  }();
-  static const int force_bn = [] {
-    const char* e = std::getenv("DCA_IGEMM_BN");
-    return e ? std::atoi(e) : 0;
-  }();
   Cfg c;
   c.bn = g.K % 128 == 0 ? 128 : 64;
-  if (force_bn == 64 || (force_bn == 128 && g.K % 128 == 0)) c.bn = force_bn;
   // 256 x 64 (80 KB of stages) and 128 x 128 (64 KB) both keep two workgroups per CU; 256 x 128
   // (96 KB) would keep one and measured 10-20% slower (profiles/round4_igemm_v2_stages.txt)
   c.bm = c.bn == 64 ? 256 : 128;
-  if (force_bm == 128 || force_bm == 256) c.bm = force_bm;
   return c;
 }
 
-// LDS ring depth: 2 (two workgroups per CU fit for tiles up to 80 KB of stages, which measured
-// faster than a 3-deep ring at one workgroup per CU: profiles/round4_igemm_v2_stages.txt);
-// DCA_IGEMM_STAGES=3 for sweeps.
-int stages() {
-  static const int v = [] {
-    const char* e = std::getenv("DCA_IGEMM_STAGES");
-    return e && std::atoi(e) == 3 ? 3 : 2;
-  }();
-  return v;
-}
-
-struct BnSrc {
-  const void* x;
-  const uint8_t* mask;
-  const float* mean;
-};
-
-template <int BM, int BN, int NSTAGE, int STATS>
-void launch_fwd_n(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                  hipStream_t st, const BnSrc& bn) {
+// LDS ring depth 2: two workgroups per CU fit for tiles up to 80 KB of stages, which measured
+// faster than a 3-deep ring at one workgroup per CU (profiles/round4_igemm_v2_stages.txt).
+template <int BM, int BN, bool STATS>
+void launch_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
+                hipStream_t st) {
+  constexpr int NSTAGE = 2;
   constexpr int WM = BN >= 128 ? 2 : 4, WN = 4 / WM;
   constexpr size_t stage = static_cast<size_t>(BM + BN) * kBK * 2 * NSTAGE;
   constexpr size_t epi = static_cast<size_t>(BM) * (BN + 8) * 2;
@@ -803,28 +628,15 @@ void launch_fwd_n(const void* x, const void* w, void* y, float* partial, const C
   (void)attr;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, st,
                      static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w),
-                     static_cast<uint16_t*>(y), partial, g, static_cast<const uint16_t*>(bn.x),
-                     bn.mask, bn.mean);
+                     static_cast<uint16_t*>(y), partial, g);
 }
 
-template <int BM, int BN, int STATS>
-void launch_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                hipStream_t st, const BnSrc& bn) {
-  if (stages() == 3) launch_fwd_n<BM, BN, 3, STATS>(x, w, y, partial, g, st, bn);
-  else launch_fwd_n<BM, BN, 2, STATS>(x, w, y, partial, g, st, bn);
-}
-
-template <int STATS>
+template <bool STATS>
 void fwd_dispatch(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                  hipStream_t st, const BnSrc& bn) {
+                  hipStream_t st) {
   const Cfg c = pick(g);
-  if (c.bn == 128) {
-    if (c.bm == 256) launch_fwd<256, 128, STATS>(x, w, y, partial, g, st, bn);
-    else launch_fwd<128, 128, STATS>(x, w, y, partial, g, st, bn);
-  } else {
-    if (c.bm == 256) launch_fwd<256, 64, STATS>(x, w, y, partial, g, st, bn);
-    else launch_fwd<128, 64, STATS>(x, w, y, partial, g, st, bn);
-  }
+  if (c.bn == 128) launch_fwd<128, 128, STATS>(x, w, y, partial, g, st);
+  else launch_fwd<256, 64, STATS>(x, w, y, partial, g, st);
 }
 
 }  // namespace
@@ -836,11 +648,9 @@ int conv_igemm_row_blocks(const ConvGeom& g) {
 }
 
 void conv_igemm_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                    hipStream_t st, const void* bn_x, const uint8_t* bn_mask, const float* bn_mean) {
-  const BnSrc bn{bn_x, bn_mask, bn_mean};
-  if (partial && bn_x) fwd_dispatch<2>(x, w, y, partial, g, st, bn);
-  else if (partial) fwd_dispatch<1>(x, w, y, partial, g, st, bn);
-  else fwd_dispatch<0>(x, w, y, nullptr, g, st, bn);
+                    hipStream_t st) {
+  if (partial) fwd_dispatch<true>(x, w, y, partial, g, st);
+  else fwd_dispatch<false>(x, w, y, nullptr, g, st);
 }
 
 int64_t conv_igemm_wgrad_ws_floats(const ConvGeom& g) {
@@ -913,8 +723,7 @@ void strided_accumulate(void* dx, const void* small, int N, int H, int W, int C,
 // its row's two input rows (contiguous, 6W bytes each) into LDS with 16-byte nontemporal loads,
 // then the block writes its 2 * Wo * 24 contiguous output bytes as 16-byte stores (8 channels a
 // lane, 16-byte aligned: 48 * Wo * b). Needs 6W % 16 == 0 (W % 8 == 0); other widths take the
-// per-pixel kernel below. Dynamic LDS: 4 input rows, 24W bytes. CO = 16 appends 4 zero channels
-// per pixel (the stem convolution kernel's 32-byte pixels).
+// per-pixel kernel below. Dynamic LDS: 4 input rows, 24W bytes.
 constexpr int kS2dMaxW = 2048;
 template <int CO>
 __global__ __launch_bounds__(256) void stem_s2d_rows_kernel(const uint16_t* __restrict__ x,
@@ -1017,183 +826,8 @@ void stem_s2d_launch(const void* x, void* xs, int N, int H, int W, hipStream_t s
                      static_cast<const uint16_t*>(x), static_cast<uint16_t*>(xs), n_pix, Wo, Ho, W, H);
 }
 
-void stem_s2d(const void* x, void* xs, int N, int H, int W, int co, hipStream_t st) {
-  if (co == 16) stem_s2d_launch<16>(x, xs, N, H, W, st);
-  else stem_s2d_launch<12>(x, xs, N, H, W, st);
-}
-
-// ---------------------------------------------------------------- ResNet stem convolution
-// The 7x7/2 pad-3 convolution of the 3-channel image (with the stem BatchNorm's statistics in the
-// epilogue), run on the space-to-depth tensor xs [N][Hs][Ws][16] (stem_s2d, CO = 16: channel
-// (dy, dx, c) + 4 zeros) as a 4x4/1 convolution with Kgemm = 4 (di) x 4 (dj) x 16 = 256:
-//   y[n][p][q][k] = sum_{di, dj, c} xs[n][p + di][q + dj][c] * w16[k][di][dj][c],  P = Hs - 3, Q = Ws - 3.
-// MIOpen ran it at 1.1 ms plus a 0.28 ms statistics pass for bs 1024 (round-5 step trace; ~1.15 GB
-// of traffic, 0.3 TFLOP). Structure:
-//  * persistent blocks (2 per CU) walk a contiguous range of 128-pixel tiles (tiles never cross an
-//    image: per image ceil(P*Q / 128)); all 64 output channels of a tile in one block;
-//  * the whole weight (64 x 256 bf16) lives in VGPRs for the kernel (32 bf16x8 fragments a lane);
-//  * a tile's pixels span at most 3 output rows (Q >= 64), so its input is the 6 contiguous S2D
-//    rows from its first row: one lane-linear buffer_load ... lds stream (out-of-range -> zeros),
-//    double-buffered across tiles. 16-B halves of a pixel are XOR-swizzled by bit 3 of the column
-//    on both sides so the 16 lanes of an MFMA fragment read hit distinct banks;
-//  * v_mfma_f32_32x32x16_bf16 on the transposed tile (rows = channels): every lane owns 4
-//    consecutive channels of one pixel -> 8-B LDS writes, 16-B coalesced stores, (sum, sum^2) of
-//    the bf16 outputs kept in registers across tiles and reduced once into partial[block][2][64].
-constexpr int kStemBM = 128, kStemRows = 6, kStemMaxWs = 256;
-
-__global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(
-    const uint16_t* __restrict__ xs, const uint16_t* __restrict__ w16, uint16_t* __restrict__ y,
-    float* __restrict__ partial, int N, int Hs, int Ws, int tiles_per_img, int win_chunks) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int r32 = lane & 31, h = lane >> 5;
-  const int P = Hs - 3, Q = Ws - 3, PQ = P * Q;
-  const int total = N * tiles_per_img;
-  const int t_begin = static_cast<int>(static_cast<int64_t>(blockIdx.x) * total / gridDim.x);
-  const int t_end = static_cast<int>(static_cast<int64_t>(blockIdx.x + 1) * total / gridDim.x);
-  uint16_t* win[2] = {lds, lds + win_chunks * 8};
-  uint16_t* Cs = lds + 2 * win_chunks * 8;  // [kStemBM][64 + 8]
-  constexpr int CS = 72;
-
-  // the weight in registers: fragment (ks, i) = w16[i * 32 + r32][ks * 16 + h * 8 .. + 8]
-  bf16x8 wf[16][2];
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      wf[ks][i] = *reinterpret_cast<const bf16x8*>(w16 + (i * 32 + r32) * 256 + ks * 16 + h * 8);
-
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(xs), 0, static_cast<int>(static_cast<uint32_t>(N * Hs * Ws) * 32u), 0x00020000);
-  // window loads: LDS chunk L (16 B) = pixel L/2 of the window, half (L & 1) ^ swizzle(column)
-  const int n_ins = win_chunks / kThreads;
-  auto issue = [&](int t, uint16_t* dst) {
-    const int n = t / tiles_per_img, p0 = (t - n * tiles_per_img) * kStemBM / Q;
-    const uint32_t base = static_cast<uint32_t>((n * Hs + p0) * Ws) * 32u;
-    const int used = kStemRows * Ws * 2;
-    for (int j = 0; j < n_ins; ++j) {
-      const int L = (j * 4 + wv) * 64 + lane;
-      const int pl = L >> 1, col = pl % Ws;
-      const uint32_t src = static_cast<uint32_t>(2 * pl + ((L & 1) ^ ((col >> 3) & 1))) * 16u;
-      blds16(xr, L < used ? base + src : kOOB, 0, dst + (j * 4 + wv) * 64 * 8);
-    }
-  };
-
-  const int cc = tid & 7, rr = tid >> 3;  // epilogue: 16-B chunk of a row, first row
-  float s8[8], q8[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
-
-  // tile t's bf16 output (in Cs) -> 16-B coalesced stores + statistics. Runs one iteration late,
-  // before the next window's loads are issued, so the vmcnt(0) at the end of an iteration finds
-  // both the stores and the prefetch long done instead of waiting out a store's latency per tile.
-  auto store_out = [&](int t) {
-    const int n = t / tiles_per_img, m0 = (t - n * tiles_per_img) * kStemBM;
-    uint16_t* yt = y + (static_cast<int64_t>(n) * PQ + m0) * 64;
-    for (int row = rr; row < kStemBM; row += kThreads / 8) {
-      if (m0 + row >= PQ) break;
-      const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CS + cc * 8);
-      *reinterpret_cast<uint4*>(yt + row * 64 + cc * 8) = v;
-      const float f[8] = {bf16_lo(v.x), bf16_hi(v.x), bf16_lo(v.y), bf16_hi(v.y),
-                          bf16_lo(v.z), bf16_hi(v.z), bf16_lo(v.w), bf16_hi(v.w)};
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] = fmaf(f[k], f[k], q8[k]); }
-    }
-  };
-
-  if (t_begin < t_end) issue(t_begin, win[0]);
-  wait_vmcnt<0>();
-  barrier_raw();
-  int buf = 0;
-  for (int t = t_begin; t < t_end; ++t) {
-    if (t > t_begin) store_out(t - 1);  // Cs holds tile t-1 (published by the last barrier)
-    if (t + 1 < t_end) issue(t + 1, win[buf ^ 1]);
-    const int n = t / tiles_per_img, m0 = (t - n * tiles_per_img) * kStemBM, p0 = m0 / Q;
-    int m = m0 + wv * 32 + r32;
-    if (m >= PQ) m = m0;  // masked pixel of the last tile: any valid address, never stored
-    const int p = m / Q, q = m - p * Q;
-    const int pix = (p - p0) * Ws + q;
-    const uint16_t* wb = win[buf];
-    f32x16 acc[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-#pragma unroll
-    for (int di = 0; di < 4; ++di)
-#pragma unroll
-      for (int dj = 0; dj < 4; ++dj) {
-        const int ks = di * 4 + dj;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(
-            wb + (pix + di * Ws + dj) * 16 + ((h ^ (((q + dj) >> 3) & 1)) << 3));
-        acc[0] = mfma32(wf[ks][0], a, acc[0]);
-        acc[1] = mfma32(wf[ks][1], a, acc[1]);
-      }
-    // every wave has read Cs (store_out of tile t-1) before it is overwritten
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_raw();
-    const int ml = wv * 32 + r32;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) {
-        uint2 pk;
-        pk.x = pack_bf16x2(acc[i][4 * q4 + 0], acc[i][4 * q4 + 1]);
-        pk.y = pack_bf16x2(acc[i][4 * q4 + 2], acc[i][4 * q4 + 3]);
-        *reinterpret_cast<uint2*>(Cs + ml * CS + i * 32 + 8 * q4 + 4 * h) = pk;
-      }
-    // Cs holds tile t, window t+1 landed, every wave is done with win[buf]
-    wait_vmcnt<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_raw();
-    buf ^= 1;
-  }
-  if (t_begin < t_end) {
-    store_out(t_end - 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_raw();  // Cs reads done before the statistics reuse the LDS
-  }
-  // per-block statistics: [32 rows][8 chunks][16] -> partial[block][0 / 1][64]
-  float* red = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    red[rr * 128 + cc * 16 + k] = s8[k];
-    red[rr * 128 + cc * 16 + 8 + k] = q8[k];
-  }
-  __syncthreads();
-  if (tid < 128) {
-    float a = 0.f;
-    for (int j = 0; j < kThreads / 8; ++j) a += red[j * 128 + tid];
-    const int ch = (tid >> 4) * 8 + (tid & 7);
-    partial[(static_cast<int64_t>(blockIdx.x) * 2 + ((tid >> 3) & 1)) * 64 + ch] = a;
-  }
-}
-
-int stem_wgrad_blocks(int N) { return N; }
-
-void stem_wgrad(const void* dy, const void* xs, float* ws, int N, int Hs, int Ws, hipStream_t st) {
-  const int P = Hs - 3, Q = Ws - 3;
-  const int blocks = stem_wgrad_blocks(N);
-  const int tail = kStemWgPx + 4 - Ws > 0 ? (kStemWgPx + 4 - Ws) * 12 : 0;
-  const size_t lds = (static_cast<size_t>(kStemWgPx) * kStemWgDyS + 4 * Ws * 12 + tail) * 2;
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(blocks), dim3(kThreads), lds, st,
-                     static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(xs), ws, P, Q, Hs,
-                     Ws);
-}
-
-int stem_conv_blocks(int N, int Hs, int Ws) {
-  const int tiles = N * (((Hs - 3) * (Ws - 3) + kStemBM - 1) / kStemBM);
-  return std::max(1, std::min(tiles, 2 * 256));
-}
-
-void stem_conv_fwd(const void* xs, const void* w16, void* y, float* partial, int N, int Hs, int Ws,
-                   hipStream_t st) {
-  const int tiles_per_img = ((Hs - 3) * (Ws - 3) + kStemBM - 1) / kStemBM;
-  const int win_chunks = (kStemRows * Ws * 2 + kThreads - 1) / kThreads * kThreads;
-  const size_t lds = static_cast<size_t>(2 * win_chunks) * 16 + kStemBM * 72 * 2;
-  hipLaunchKernelGGL(stem_conv_kernel, dim3(stem_conv_blocks(N, Hs, Ws)), dim3(kThreads), lds, st,
-                     static_cast<const uint16_t*>(xs), static_cast<const uint16_t*>(w16),
-                     static_cast<uint16_t*>(y), partial, N, Hs, Ws, tiles_per_img, win_chunks);
+void stem_s2d(const void* x, void* xs, int N, int H, int W, hipStream_t st) {
+  stem_s2d_launch<12>(x, xs, N, H, W, st);
 }
 
 void conv_flip_transpose(const void* w, void* wt, int K, int C, int RS, hipStream_t st) {

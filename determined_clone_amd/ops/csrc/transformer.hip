@@ -663,11 +663,8 @@ inline int ln_grid(int64_t rows) {
 
 int ln_bwd_blocks(int64_t rows) {
   // 512-4096 blocks measure within 15% of each other at GPT-2-medium rows (2.7-3.1 TB/s,
-  // tools/bench_tx_bwd.py); DCA_LN_BWD_BLOCKS overrides for tuning
-  static const int cap = [] {
-    const char* e = std::getenv("DCA_LN_BWD_BLOCKS");
-    return e ? std::atoi(e) : 1024;
-  }();
+  // tools/bench_tx_bwd.py)
+  constexpr int cap = 1024;
   int64_t g = (rows + kWaves - 1) / kWaves;
   return static_cast<int>(g < cap ? (g < 1 ? 1 : g) : cap);
 }
@@ -698,30 +695,16 @@ void layernorm_fwd(TDtype dt, const void* x, const void* res, void* sum_out, voi
 
 // Row-group kernel launch shape (D <= kLnColsumMaxD): W waves per row, R rows per group step.
 int ln_rg_waves(int D) { return D <= 512 ? 1 : D <= 1024 ? 2 : 4; }
-int ln_rg_rows() {
-  static const int r = [] {
-    const char* e = std::getenv("DCA_LN_BWD_ROWS");
-    return e && std::atoi(e) == 4 ? 4 : 2;
-  }();
-  return r;
-}
+// 2 rows per group step (4 measured slower: profiles/round5_ln_bwd_row_group_sweep.txt)
+int ln_rg_rows() { return 2; }
 int ln_rg_blocks(int64_t rows, int D) {
-  // DCA_LN_BWD_BLOCKS overrides (tuning); the default fills every CU with two 8-wave blocks
-  static const int cap = [] {
-    const char* e = std::getenv("DCA_LN_BWD_BLOCKS");
-    return e ? std::atoi(e) : 512;
-  }();
+  // fills every CU with two 8-wave blocks
+  constexpr int cap = 512;
   const int64_t per = static_cast<int64_t>(8 / ln_rg_waves(D)) * ln_rg_rows();
   const int64_t g = (rows + per - 1) / per;
   return static_cast<int>(g < cap ? (g < 1 ? 1 : g) : cap);
 }
-bool ln_rg_path(int D) {
-  static const bool off = [] {
-    const char* e = std::getenv("DCA_LN_BWD_RG");
-    return e && e[0] == '0';
-  }();
-  return !off && D <= kLnColsumMaxD;
-}
+bool ln_rg_path(int D) { return D <= kLnColsumMaxD; }
 
 int64_t ln_bwd_partial_floats(int64_t rows, int D, bool colsum) {
   const int blocks = ln_rg_path(D) ? ln_rg_blocks(rows, D) : ln_bwd_blocks(rows);
@@ -798,11 +781,8 @@ void bias_gelu_fwd(TDtype dt, const void* x, const void* bias, bool bias_bf16, v
 }
 
 int bias_gelu_bwd_row_blocks(int64_t rows) {
-  // row slabs (grid.y); DCA_BGB_BLOCKS overrides (tuning)
-  static const int cap = [] {
-    const char* e = std::getenv("DCA_BGB_BLOCKS");
-    return e ? std::atoi(e) : 256;
-  }();
+  // row slabs (grid.y; profiles/round5_bias_gelu_bwd_sweep_and_ln_rg_ab.txt)
+  constexpr int cap = 256;
   return static_cast<int>(rows < cap ? (rows < 1 ? 1 : rows) : cap);
 }
 

@@ -38,11 +38,10 @@ class _GroupNormAct(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
-TORCH_FALLBACK = os.environ.get("DCA_GN_TORCH", "0") == "1"  # A/B switch only
 
 
 def _gpu_ok(x: torch.Tensor, weight: Optional[torch.Tensor], groups: int) -> bool:
-    if TORCH_FALLBACK or not x.is_cuda or x.dim() != 4 or x.dtype not in (torch.bfloat16, torch.float32):
+    if not x.is_cuda or x.dim() != 4 or x.dtype not in (torch.bfloat16, torch.float32):
         return False
     C = x.shape[1]
     if C % 8 or C % groups or not x.is_contiguous(memory_format=torch.channels_last):

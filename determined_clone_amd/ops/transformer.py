@@ -186,9 +186,8 @@ class _BiasGelu(torch.autograd.Function):
         return dx, db.to(ctx.bias.dtype)
 
 
-_WGRAD_SPLITK = os.environ.get("DCA_WGRAD_SPLITK", "1") != "0"
-# K-slices of the split-K weight gradient (A/B knob; 4 measured best in isolation)
-_WGRAD_SPLITS = int(os.environ.get("DCA_WGRAD_SPLITS", "4"))
+# K-slices of the split-K weight gradient (4 measured best: profiles/round5_gpt2_wgrad_splitk_ab.txt)
+_WGRAD_SPLITS = 4
 # linear-layer weight gradients on the side stream (ops/_grad.py); A/B switch
 LINEAR_SIDE_STREAM = os.environ.get("DCA_LINEAR_WGRAD_STREAM", "1") != "0"
 
@@ -201,7 +200,7 @@ def _wgrad_splits(tokens: int, m: int, n: int) -> int:
     split-K. Splitting K four ways as one batched GEMM fills the chip: measured on MI355X at 16k
     tokens (tools/bench_wgrad.py, profiles/r9_wgrad_splitk.txt) 1024x1024 111 -> 64 us,
     3072x1024 166 -> 115 us, 4096x1024 166 -> 145 us, 1024x4096 161 -> 143 us."""
-    if not _WGRAD_SPLITK or tokens < 8192 or tokens % 4 or m * n > 16 * 2 ** 20:
+    if tokens < 8192 or tokens % 4 or m * n > 16 * 2 ** 20:
         return 1
     if (m * n) % 8 or tokens % _WGRAD_SPLITS:  # splitk_accumulate: 8 elements per thread
         return 1

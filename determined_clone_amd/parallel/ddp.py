@@ -61,6 +61,7 @@ class GradientSync:
         self.buckets: List[_Bucket] = []
         self._param_bucket = {}
         self._next = 0
+        self._comm_keep: List[torch.Tensor] = []
         self._hooks = []
         self._build(bucket_mb, first_bucket_mb)
         self._register_hooks()
@@ -141,6 +142,7 @@ class GradientSync:
         backward and before the optimizer step."""
         if self.world == 1 or not self.enabled:
             return
+        self._comm_keep = []  # last sync's low-precision copies: their readers ran long ago
         for b in self.buckets[self._next:]:
             if not b.launched:
                 self._launch(b)
@@ -154,9 +156,11 @@ class GradientSync:
             if b.comm is not None:
                 b.buf.grad[b.start:b.end].copy_(b.comm)
                 if b.comm.is_cuda:
-                    # allocated on the comm stream, last read here: keep it alive until this
-                    # stream's copy has run before the allocator can hand it out again
-                    b.comm.record_stream(torch.cuda.current_stream())
+                    # allocated on the comm stream, last read by this stream's copy: kept alive by
+                    # reference until the next sync (not record_stream, which pins freed blocks
+                    # behind the lagging stream -- the slow mode of ops/_grad.py); by then the
+                    # copy has long run and the comm stream's next kernels wait on later events
+                    self._comm_keep.append(b.comm)
                 b.comm = None
             if manual_div:
                 b.buf.grad[b.start:b.end].div_(self.world)

@@ -549,6 +549,12 @@ class _PyTorchTrialController:
             self.core_context.train.set_status("validating")
         self.context.reset_reducers()
         self.context._sync_buffers()
+        # ZeRO overlap_param_gather: evaluation / metric code may read parameters directly
+        # (p.data, tied weights) -- every in-flight all-gather lands first
+        for o in list(getattr(self.context, "optimizers", [])) + list(self.context.models):
+            wait = getattr(o, "wait_params", None)
+            if callable(wait):
+                wait()
         for m in self.context.models:
             m.eval()
         t0 = time.time()

@@ -474,6 +474,10 @@ class DeepSpeedEngine(torch.nn.Module):
             self._autotune.on_step()  # may end a dsat measurement run (SystemExit)
 
     def zero_grad(self) -> None:
+        # a user-called zero_grad may precede code that reads parameters outside a module forward
+        # (tied / functionally used weights): wait for in-flight all-gathers first. The engine's
+        # own post-step zero_grad (step()) does not, so the gathers still overlap the next forward.
+        self.wait_params()
         self.optimizer.zero_grad()
 
     def wait_params(self) -> None:

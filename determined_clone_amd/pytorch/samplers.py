@@ -52,8 +52,10 @@ class DistributedSampler(torch.utils.data.Sampler):
 
 
 class DistributedBatchSampler(torch.utils.data.BatchSampler):
-    """Shard a batch sampler: each global batch of ``batch_size * num_workers`` records is split
-    so rank r gets its contiguous ``batch_size`` slice."""
+    """Shard a batch sampler across ``num_workers`` ranks by dealing whole batches round-robin:
+    rank r yields batches r, r + num_workers, r + 2 * num_workers, ... of the wrapped sampler (each
+    unchanged). Built on a per-slot batch sampler, the ``num_workers`` consecutive per-slot batches
+    that one step consumes together form that step's global batch."""
 
     def __init__(self, batch_sampler, num_workers: int, rank: int) -> None:
         self._batch_sampler = batch_sampler

@@ -38,6 +38,8 @@ class FakeDocker:
         self.sock_path = sock_path
         self.images = set()
         self.pulls: List[Dict[str, Any]] = []
+        self.pull_gate = threading.Event()  # cleared: image pulls block until it is set
+        self.pull_gate.set()
         self.creates: List[Dict[str, Any]] = []
         self.containers: Dict[str, _Container] = {}
         self.lock = threading.Lock()
@@ -103,6 +105,7 @@ class FakeDocker:
                 dec = json.loads(base64.urlsafe_b64decode(auth + "===")) if auth else None
                 ref = q["fromImage"] + (f":{q['tag']}" if q.get("tag") else "")
                 self.pulls.append({"image": ref, "auth": dec})
+                self.pull_gate.wait(60)  # a slow registry
                 self.images.add(ref)
                 self._send(h, 200, b'{"status":"Pulling from fake"}\n{"status":"Download complete"}\n')
             elif path == "/containers/create":

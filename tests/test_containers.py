@@ -282,3 +282,70 @@ def test_entrypoint_sources_hook(tmp_path):
     out = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, check=True).stdout
     assert out.strip() == "42"
     assert runtime.with_startup_hook(["true"], str(tmp_path / "nohook")) == ["true"]
+
+
+def test_slow_pull_does_not_block_the_agent_and_kill_during_launch(docker):
+    """the container launch (pull / create / start) runs on a worker thread per
+    allocation, so a slow pull returns the action loop at once; a kill that arrives during the pull
+    ends the task as soon as its container exists (TERMINATED 137), and a failed launch reports
+    TERMINATED 1 instead of hanging."""
+    tmp = tempfile.mkdtemp(prefix="det-sp-")
+    m = Master(os.path.join(tmp, "m.db"))
+    srv = MasterServer(m, "127.0.0.1", 0).start()
+    try:
+        agent = Agent(m.master_url, "agent-p", artificial_slots=1, container_runtime="docker",
+                      container_socket=docker.sock_path)
+        events = []
+        agent._event = lambda alloc, state, exit_code=None: events.append((alloc, state, exit_code))
+        ctx = os.path.join(tmp, "ctx")
+        os.makedirs(ctx)
+        from determined_clone_amd.agent import runtime as rt_mod
+
+        monkeypatch = pytest.MonkeyPatch()
+        monkeypatch.setattr(rt_mod, "fetch_context", lambda session, task_id, d: os.makedirs(d, exist_ok=True))
+        monkeypatch.setattr(rt_mod, "build_task", lambda spec, *a, **k: (
+            [sys.executable, "-c", "import time; time.sleep(30)"], {"DET_TASK_ID": spec["task_id"]}))
+        monkeypatch.setattr(rt_mod, "assigned_devices", lambda spec, devices: [])
+        spec = {"allocation_id": "task-5.0", "task_id": "task-5", "slots": 0, "env": {},
+                "container": {"image": "registry.example/slow:1", "force_pull_image": True},
+                "entrypoint": [sys.executable, "-c", "import time; time.sleep(30)"]}
+        docker.pull_gate.clear()
+        t0 = time.time()
+        agent._start(spec)
+        assert time.time() - t0 < 5.0  # returned while the pull is still blocked
+        assert "task-5.0" in agent._launching and "task-5.0" not in agent.tasks
+        agent._kill("task-5.0")
+        docker.pull_gate.set()
+        t0 = time.time()
+        while not any(e[1] == "TERMINATED" for e in events) and time.time() - t0 < 30:
+            time.sleep(0.1)
+        assert any(e[0] == "task-5.0" and e[1] == "TERMINATED" and e[2] in (137, -9, -15, 143)
+                   for e in events), events
+        assert not agent._launching
+        agent.stop()
+        monkeypatch.undo()
+    finally:
+        docker.pull_gate.set()
+        srv.stop()
+
+
+def test_auto_runtime_keeps_imageless_tasks_as_processes(docker, monkeypatch):
+    """with ``auto`` a task whose config names no image runs as a process group (zygote,
+    per-agent MIOpen DB); only ``environment.image`` moves a task into a container."""
+    from determined_clone_amd.agent import agent as agent_mod
+
+    assert agent_mod._names_image({"container": {"image": {"cpu": "a", "rocm": "b"}}})
+    assert not agent_mod._names_image({"container": {"image": None}})
+    assert not agent_mod._names_image({})
+    tmp = tempfile.mkdtemp(prefix="det-au-")
+    m, srv, agent, s = _cluster(tmp, container_runtime="auto", container_socket=docker.sock_path)
+    try:
+        assert isinstance(agent.containers, containers.EngineRuntime)
+        cfg = CONFIG.split("environment:")[0] + "resources: {shm_size: 4 gb}\n"
+        n = len(docker.creates)
+        st, logs = _run_experiment(s, _ctx(tmp), cfg)
+        assert st == "COMPLETED", logs[-30:]
+        assert len(docker.creates) == n  # no container was created
+    finally:
+        agent.stop()
+        srv.stop()

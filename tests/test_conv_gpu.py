@@ -205,76 +205,6 @@ def test_stem_s2d_kernel_matches_pad_and_reshape(hw):
     assert torch.equal(xs, ref)
 
 
-@pytest.mark.parametrize("shape", [(4, 224, 224), (3, 96, 150), (2, 64, 48)])
-def test_stem_wgrad_kernel_matches_fp32(shape):
-    """stem_wgrad_kernel (im2col-free: B fragments transposed-read from 4 S2D rows in LDS) equals
-    the fp32 weight gradient of the 4x4/1 convolution on the 12-channel S2D image."""
-    from determined_clone_amd.ops import _ext
-
-    n, h, w = shape
-    torch.manual_seed(0)
-    x = torch.randn(n, 3, h, w, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    xs = _ext.load().stem_s2d(x)
-    dy = torch.randn(n, 64, xs.shape[2] - 3, xs.shape[3] - 3, device="cuda").bfloat16()
-    dy = dy.contiguous(memory_format=torch.channels_last)
-    dw = _ext.load().stem_wgrad(dy, xs).permute(0, 3, 1, 2)
-    w2 = torch.zeros(64, 12, 4, 4, device="cuda")
-    ref = torch.ops.aten.convolution_backward(dy.float(), xs.float(), w2, None, [1, 1], [0, 0], [1, 1],
-                                              False, [0, 0], 1, [False, True, False])[1]
-    _close(dw, ref, 1e-3, "stem wgrad")
-
-
-@pytest.mark.parametrize("hw", [(224, 224), (96, 150), (130, 130)])
-def test_stem_conv_kernel_output_and_statistics(monkeypatch, hw):
-    """stem_conv_kernel (7x7/2 as a 4x4/1 MFMA conv on the 16-channel S2D tensor) equals the fp32
-    7x7 convolution, and its epilogue statistics equal (sum, sum^2) of the bf16 output it wrote
-    -- including a last tile of an image that is only partly filled (96x150, 130x130)."""
-    monkeypatch.setattr(conv, "STEM_KERNEL", True)
-    torch.manual_seed(0)
-    c = nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
-    x = torch.randn(3, 3, *hw, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    y = conv.stem_conv(c, x, bn_stats=True)
-    p = y._dca_bn_partials
-    assert p is not None and p.dtype == torch.float32 and p.shape[1:] == (2, 64)
-    ref = F.conv2d(x.float(), c.weight.float(), stride=2, padding=3)
-    assert y.is_contiguous(memory_format=torch.channels_last) and y.shape == ref.shape
-    _close(y, ref, 2e-2, "stem kernel fwd")
-    yf = y.float()
-    torch.testing.assert_close(p[:, 0].sum(0), yf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
-    torch.testing.assert_close(p[:, 1].sum(0), (yf * yf).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
-
-
-def test_stem_bn_relu_pool_uses_conv_statistics(monkeypatch):
-    """ResNet stem with the conv-epilogue statistics: BN + ReLU + max-pool output, running stats
-    and the BN parameter gradients match the unfused fp32 reference."""
-    from determined_clone_amd.ops import batchnorm as bn_ops
-
-    monkeypatch.setattr(conv, "STEM_KERNEL", True)
-    torch.manual_seed(0)
-    c = nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
-    bn = nn.BatchNorm2d(64).cuda()
-    bn.weight.data.uniform_(0.5, 1.5)
-    bn.bias.data.uniform_(-0.2, 0.2)
-    rm, rv = bn.running_mean.clone(), bn.running_var.clone()
-    x = torch.randn(4, 3, 224, 224, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    y = conv.stem_conv(c, x, bn_stats=True)
-    assert getattr(y, "_dca_bn_partials", None) is not None
-    out = bn_ops.batch_norm_relu_maxpool(y, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                         training=True, momentum=0.1, eps=1e-5,
-                                         num_batches_tracked=bn.num_batches_tracked)
-    yr = y.detach().float().requires_grad_(False)
-    w, b = bn.weight.detach().clone().requires_grad_(), bn.bias.detach().clone().requires_grad_()
-    ref = F.max_pool2d(F.relu(F.batch_norm(yr, rm, rv, w, b, True, 0.1, 1e-5)), 3, 2, 1)
-    _close(out, ref, 2e-2, "stem bn-relu-pool")
-    torch.testing.assert_close(bn.running_mean, rm, rtol=1e-3, atol=1e-4)
-    torch.testing.assert_close(bn.running_var, rv, rtol=1e-3, atol=1e-4)
-    g = torch.randn_like(ref)
-    out.backward(g.to(out.dtype))
-    ref.backward(g)
-    _close(bn.weight.grad, w.grad, 2e-2, "stem bn dgamma")
-    _close(bn.bias.grad, b.grad, 2e-2, "stem bn dbeta")
-
-
 @pytest.mark.parametrize("side", [True, False])
 @pytest.mark.parametrize("hw", [(224, 224), (64, 48)])
 def test_stem_space_to_depth_matches_fp32(monkeypatch, side, hw):
@@ -284,7 +214,6 @@ def test_stem_space_to_depth_matches_fp32(monkeypatch, side, hw):
     from determined_clone_amd.parallel.flat import FlatParamSpace
 
     monkeypatch.setattr(_grad, "SIDE_STREAM", side)
-    monkeypatch.setattr(conv, "STEM_S2D", True)
     torch.manual_seed(0)
     c = nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
     FlatParamSpace([[c.weight]])  # persistent .grad view (side-stream accumulation target)
@@ -318,8 +247,9 @@ def test_pointwise_dgrad_accumulates_into_shortcut_gradient(monkeypatch):
     # the GEMM for every stride-1 backward-data (where the accumulate path applies), MIOpen otherwise
     monkeypatch.setattr(conv_ops, "_choose", lambda key, cands: 1 if key[0] == "dgrad" else 0)
     grads = []
+    real_sink = conv_ops._grad_sink
     for acc in (False, True):
-        monkeypatch.setattr(conv_ops, "ACC_RESIDUAL", acc)
+        monkeypatch.setattr(conv_ops, "_grad_sink", real_sink if acc else (lambda x: None))
         hits = conv_ops.ACC_HITS
         model = copy.deepcopy(base)
         F.cross_entropy(model(x).float(), y).backward()
@@ -468,59 +398,3 @@ def test_strided_accumulate_matches_strided_add(shape):
     want[:, :, ::s, ::s] += small
     _ext.load().strided_accumulate(dx, small, s)
     torch.testing.assert_close(dx, want, atol=0, rtol=0)
-
-
-@pytest.mark.parametrize("shape", [(4, 64, 56, 56), (2, 128, 28, 28), (8, 256, 14, 14), (4, 512, 7, 7)])
-def test_igemm_dgrad_bn_statistics_epilogue(shape):
-    """conv_igemm_dgrad_bn: the stride-1 3x3 data gradient plus, from its epilogue, the backward
-    statistics of the BN+ReLU that produced the convolution input -- (sum g*m, sum g*m*(x - mean))
-    over the bf16 gradient g -- against the same sums in fp32 over the returned gradient."""
-    from determined_clone_amd.ops import _ext
-
-    C = _ext.load()
-    torch.manual_seed(0)
-    N, c, H, W = shape
-    k = c
-    dy = torch.randn(N, k, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    w = (torch.randn(k, c, 3, 3, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
-    x_bn = torch.randn(N, c, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    mean = torch.randn(c, device="cuda") * 0.1
-    keep = torch.rand(N, c, H, W, device="cuda") > 0.4
-    rows = keep.permute(0, 2, 3, 1).reshape(-1, c)
-    bits = (rows.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1)
-    mask = bits.to(torch.uint8).contiguous()
-    dx_ref = C.conv_igemm_dgrad(dy, w, 1)
-    dx, part = C.conv_igemm_dgrad_bn(dy, w, 1, x_bn, mask, mean)
-    assert torch.equal(dx, dx_ref)  # the epilogue statistics leave the gradient untouched
-    g = dx.float().permute(0, 2, 3, 1).reshape(-1, c) * rows
-    xr = x_bn.float().permute(0, 2, 3, 1).reshape(-1, c)
-    want_s, want_q = g.sum(0), (g * (xr - mean)).sum(0)
-    got = part.sum(0)
-    torch.testing.assert_close(got[0], want_s, atol=2e-2, rtol=1e-3)
-    torch.testing.assert_close(got[1], want_q, atol=5e-2, rtol=1e-3)
-
-
-def test_bottleneck_bn1_backward_statistics_fused_in_conv2_dgrad(monkeypatch):
-    """In a stride-1 bottleneck, bn1's backward takes its statistics from conv2's dgrad epilogue
-    (counted) and the block's gradients match the unfused path (DCA_FUSE_BN_BWD_STATS=0)."""
-    from determined_clone_amd.models import resnet
-    from determined_clone_amd.ops import batchnorm as bn_ops
-
-    torch.manual_seed(0)
-    blk = resnet.to_mi355x_layout(resnet.Bottleneck(256, 64, stride=1)).cuda()
-    x = torch.randn(8, 256, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    outs = []
-    for fused in (True, False):
-        monkeypatch.setattr(conv, "FUSE_BN_BWD_STATS", fused)
-        for p in blk.parameters():
-            p.grad = None
-        before = bn_ops.FUSED_BWD_STATS_HITS
-        xi = x.clone().requires_grad_(True)
-        y = blk(xi)
-        y.float().square().mean().backward()
-        assert (bn_ops.FUSED_BWD_STATS_HITS - before) == (1 if fused else 0)
-        outs.append((xi.grad.float(), {n: p.grad.float().clone() for n, p in blk.named_parameters()}))
-    (g1, p1), (g2, p2) = outs
-    torch.testing.assert_close(g1, g2, atol=2e-3, rtol=2e-2)
-    for n in p1:
-        torch.testing.assert_close(p1[n], p2[n], atol=2e-3, rtol=2e-2, msg=n)
