@@ -67,16 +67,134 @@ class CheckpointState(enum.Enum):
 
 
 class OrderBy(enum.Enum):
-    ASC = "ASC"
-    DESC = "DESC"
-    ASCENDING = "ASC"
-    DESCENDING = "DESC"
+    """Ascending or descending order of a sorted list (reference common/experimental/_util.py)."""
+
+    ASCENDING = "ORDER_BY_ASC"
+    ASC = "ORDER_BY_ASC"
+    DESCENDING = "ORDER_BY_DESC"
+    DESC = "ORDER_BY_DESC"
+
+
+_WARN_DEPRECATED_ORDER = False  # set once the classes below exist (enum creation reads members)
+
+
+class _DeprecatedOrderBy(enum.Enum):
+    """Per-object order enums kept for reference compatibility; ``OrderBy`` replaces them."""
+
+    def __getattribute__(self, name: str) -> Any:
+        if _WARN_DEPRECATED_ORDER:
+            import warnings
+
+            warnings.warn(f"'{type(self).__name__}' is deprecated; use 'experimental.OrderBy' instead.",
+                          FutureWarning, stacklevel=2)
+        return super().__getattribute__(name)
+
+
+class ExperimentOrderBy(_DeprecatedOrderBy):
+    ASCENDING = "ORDER_BY_ASC"
+    DESCENDING = "ORDER_BY_DESC"
+
+
+class TrialOrderBy(_DeprecatedOrderBy):
+    ASCENDING = "ORDER_BY_ASC"
+    ASC = "ORDER_BY_ASC"
+    DESCENDING = "ORDER_BY_DESC"
+    DESC = "ORDER_BY_DESC"
+
+
+class ModelOrderBy(_DeprecatedOrderBy):
+    ASCENDING = "ORDER_BY_ASC"
+    ASC = "ORDER_BY_ASC"
+    DESCENDING = "ORDER_BY_DESC"
+    DESC = "ORDER_BY_DESC"
+
+
+class CheckpointOrderBy(_DeprecatedOrderBy):
+    ASC = "ORDER_BY_ASC"
+    DESC = "ORDER_BY_DESC"
+
+
+_WARN_DEPRECATED_ORDER = True
+
+
+def _descending(order_by: Any, default: bool = False) -> bool:
+    """True for any DESC member of OrderBy / a per-object order enum, or the string forms."""
+    if order_by is None:
+        return default
+    v = order_by.value if isinstance(order_by, enum.Enum) else str(order_by)
+    return v.upper() in ("ORDER_BY_DESC", "DESC", "DESCENDING")
+
+
+class ExperimentSortBy(enum.Enum):
+    """Experiment list sort keys (reference common/experimental/experiment.py:41)."""
+
+    ID = "SORT_BY_ID"
+    DESCRIPTION = "SORT_BY_DESCRIPTION"
+    START_TIME = "SORT_BY_START_TIME"
+    END_TIME = "SORT_BY_END_TIME"
+    STATE = "SORT_BY_STATE"
+    NUM_TRIALS = "SORT_BY_NUM_TRIALS"
+    PROGRESS = "SORT_BY_PROGRESS"
+    USER = "SORT_BY_USER"
+    NAME = "SORT_BY_NAME"
+    FORKED_FROM = "SORT_BY_FORKED_FROM"
+    RESOURCE_POOL = "SORT_BY_RESOURCE_POOL"
+    PROJECT_ID = "SORT_BY_PROJECT_ID"
+    CHECKPOINT_SIZE = "SORT_BY_CHECKPOINT_SIZE"
+    CHECKPOINT_COUNT = "SORT_BY_CHECKPOINT_COUNT"
+    SEARCHER_METRIC_VAL = "SORT_BY_SEARCHER_METRIC_VAL"
+
+
+class TrialSortBy(enum.Enum):
+    """Trial list sort keys (reference common/experimental/trial.py:537)."""
+
+    UNSPECIFIED = "SORT_BY_UNSPECIFIED"
+    ID = "SORT_BY_ID"
+    START_TIME = "SORT_BY_START_TIME"
+    END_TIME = "SORT_BY_END_TIME"
+    STATE = "SORT_BY_STATE"
+    BEST_VALIDATION_METRIC = "SORT_BY_BEST_VALIDATION_METRIC"
+    LATEST_VALIDATION_METRIC = "SORT_BY_LATEST_VALIDATION_METRIC"
+    BATCHES_PROCESSED = "SORT_BY_BATCHES_PROCESSED"
+    DURATION = "SORT_BY_DURATION"
+    RESTARTS = "SORT_BY_RESTARTS"
+    CHECKPOINT_SIZE = "SORT_BY_CHECKPOINT_SIZE"
+
+
+class ModelSortBy(enum.Enum):
+    """Model list sort keys (reference common/experimental/model.py:152)."""
+
+    UNSPECIFIED = "SORT_BY_UNSPECIFIED"
+    NAME = "SORT_BY_NAME"
+    DESCRIPTION = "SORT_BY_DESCRIPTION"
+    CREATION_TIME = "SORT_BY_CREATION_TIME"
+    LAST_UPDATED_TIME = "SORT_BY_LAST_UPDATED_TIME"
+    NUM_VERSIONS = "SORT_BY_NUM_VERSIONS"
+    WORKSPACE = "SORT_BY_WORKSPACE"
+
+
+class CheckpointSortBy(enum.Enum):
+    """Checkpoint list sort keys (reference common/experimental/checkpoint/_checkpoint.py:78)."""
+
+    UUID = "SORT_BY_UUID"
+    TRIAL_ID = "SORT_BY_TRIAL_ID"
+    BATCH_NUMBER = "SORT_BY_BATCH_NUMBER"
+    END_TIME = "SORT_BY_END_TIME"
+    STATE = "SORT_BY_STATE"
+    SEARCHER_METRIC = "SORT_BY_SEARCHER_METRIC"
+
+
+def _sorted(items: List[Any], key: Callable[[Any], Any], desc: bool) -> List[Any]:
+    """Stable sort with missing (None) keys last in either direction."""
+    have = [i for i in items if key(i) is not None]
+    miss = [i for i in items if key(i) is None]
+    return sorted(have, key=key, reverse=desc) + miss
 
 
 class DownloadMode(enum.Enum):
-    AUTO = "AUTO"
-    DIRECT = "DIRECT"
-    MASTER = "MASTER"
+    DIRECT = "direct"
+    MASTER = "master"
+    AUTO = "auto"
 
 
 def _enum(cls: Any, v: Any) -> Any:
@@ -236,8 +354,23 @@ class Checkpoint:
         return f"Checkpoint(uuid={self.uuid!r}, trial_id={getattr(self, 'trial_id', None)})"
 
 
-def _sort_checkpoints(cks: List[Checkpoint], sort_by: Optional[str], smaller_is_better: bool,
-                      order_by: Optional[OrderBy]) -> List[Checkpoint]:
+def _sort_checkpoints(cks: List[Checkpoint], sort_by: Any, smaller_is_better: bool,
+                      order_by: Any, searcher_metric: Optional[str] = None) -> List[Checkpoint]:
+    """``sort_by``: a :class:`CheckpointSortBy` or the name of a validation metric."""
+    if isinstance(order_by, enum.Enum) and not isinstance(order_by, OrderBy):
+        order_by = OrderBy.DESC if _descending(order_by) else OrderBy.ASC
+    if isinstance(sort_by, CheckpointSortBy):
+        if sort_by == CheckpointSortBy.SEARCHER_METRIC:
+            if searcher_metric is None:
+                raise ValueError("SEARCHER_METRIC sorting needs the experiment's searcher.metric")
+            sort_by = searcher_metric
+        else:
+            keyf = {CheckpointSortBy.UUID: lambda c: c.uuid,
+                    CheckpointSortBy.TRIAL_ID: lambda c: c.trial_id,
+                    CheckpointSortBy.BATCH_NUMBER: lambda c: c.steps_completed,
+                    CheckpointSortBy.END_TIME: lambda c: c.report_time,
+                    CheckpointSortBy.STATE: lambda c: c.state.value if isinstance(c.state, enum.Enum) else c.state}[sort_by]
+            return _sorted(cks, keyf, _descending(order_by))
     if sort_by is None:
         key: Callable[[Checkpoint], Any] = lambda c: c.report_time or 0  # noqa: E731
         desc = order_by != OrderBy.ASC
@@ -250,6 +383,76 @@ def _sort_checkpoints(cks: List[Checkpoint], sort_by: Optional[str], smaller_is_
             return sorted(cks, key=lambda c: -key(c) if key(c) != float("inf") else float("inf"))
         return sorted(cks, key=key)
     return sorted(cks, key=key, reverse=desc)
+
+
+def _ts(v: Any) -> Any:
+    """Comparable form of a timestamp (ISO string or epoch number)."""
+    return v if v is None or isinstance(v, (int, float)) else str(v)
+
+
+def _trial_key(sort_by: "TrialSortBy", session: Session, smaller_is_better: bool) -> Callable[[Any], Any]:
+    def vmetric(t: Any, which: str) -> Any:
+        v = (t.summary_metrics.get(which) or {}) if isinstance(t.summary_metrics, dict) else {}
+        if which == "best" and t.best_validation is not None:
+            bv = t.best_validation
+            return bv.get("searcher_metric") if isinstance(bv, dict) else bv
+        m = v.get("searcher_metric") if isinstance(v, dict) else None
+        return m if m is None or smaller_is_better else -m
+
+    def duration(t: Any) -> Any:
+        try:
+            import datetime
+
+            f = datetime.datetime.fromisoformat
+            end = t.end_time or datetime.datetime.now(datetime.timezone.utc).isoformat()
+            return (f(str(end).replace("Z", "+00:00")) - f(str(t.start_time).replace("Z", "+00:00"))).total_seconds()
+        except Exception:
+            return None
+
+    def ck_size(t: Any) -> Any:
+        rows = session.get(f"/api/v1/trials/{t.id}/checkpoints")["checkpoints"]
+        return sum(int(c.get("size") or sum(int(x) for x in (c.get("resources") or {}).values())) for c in rows)
+
+    return {TrialSortBy.ID: lambda t: t.id, TrialSortBy.START_TIME: lambda t: _ts(t.start_time),
+            TrialSortBy.END_TIME: lambda t: _ts(t.end_time),
+            TrialSortBy.STATE: lambda t: t.state.value if isinstance(t.state, enum.Enum) else t.state,
+            TrialSortBy.BEST_VALIDATION_METRIC: lambda t: vmetric(t, "best"),
+            TrialSortBy.LATEST_VALIDATION_METRIC: lambda t: vmetric(t, "latest_validation"),
+            TrialSortBy.BATCHES_PROCESSED: lambda t: t.steps_completed,
+            TrialSortBy.DURATION: duration, TrialSortBy.RESTARTS: lambda t: t.restarts,
+            TrialSortBy.CHECKPOINT_SIZE: ck_size}[sort_by]
+
+
+def _experiment_key(sort_by: "ExperimentSortBy", session: Session) -> Callable[[Any], Any]:
+    def trials(e: Any) -> List[Dict[str, Any]]:
+        return session.get(f"/api/v1/experiments/{e.id}/trials")["trials"]
+
+    def checkpoints(e: Any) -> List[Dict[str, Any]]:
+        return session.get(f"/api/v1/experiments/{e.id}/checkpoints")["checkpoints"]
+
+    def metric_val(e: Any) -> Any:
+        scfg = e.config.get("searcher", {}) if isinstance(e.config, dict) else {}
+        vals = []
+        for t in trials(e):
+            bv = t.get("best_validation")
+            v = bv.get("searcher_metric") if isinstance(bv, dict) else bv
+            if v is not None:
+                vals.append(v)
+        if not vals:
+            return None
+        return min(vals) if scfg.get("smaller_is_better", True) else max(vals)
+
+    return {ExperimentSortBy.ID: lambda e: e.id, ExperimentSortBy.DESCRIPTION: lambda e: e.description or "",
+            ExperimentSortBy.START_TIME: lambda e: _ts(e.start_time), ExperimentSortBy.END_TIME: lambda e: _ts(e.end_time),
+            ExperimentSortBy.STATE: lambda e: e.state.value if isinstance(e.state, enum.Enum) else e.state,
+            ExperimentSortBy.NUM_TRIALS: lambda e: len(trials(e)), ExperimentSortBy.PROGRESS: lambda e: e.progress,
+            ExperimentSortBy.USER: lambda e: e.username, ExperimentSortBy.NAME: lambda e: e.name or "",
+            ExperimentSortBy.FORKED_FROM: lambda e: e.parent_id,
+            ExperimentSortBy.RESOURCE_POOL: lambda e: ((e.config.get("resources") or {}).get("resource_pool") or ""),
+            ExperimentSortBy.PROJECT_ID: lambda e: e.project_id,
+            ExperimentSortBy.CHECKPOINT_SIZE: lambda e: sum(int(c.get("size") or 0) for c in checkpoints(e)),
+            ExperimentSortBy.CHECKPOINT_COUNT: lambda e: len(checkpoints(e)),
+            ExperimentSortBy.SEARCHER_METRIC_VAL: metric_val}[sort_by]
 
 
 class Trial:
@@ -310,10 +513,11 @@ class Trial:
                          order_by: Optional[OrderBy] = None, max_results: Optional[int] = None) -> List[Checkpoint]:
         cks = [Checkpoint(self._session, c["uuid"], c)
                for c in self._session.get(f"/api/v1/trials/{self.id}/checkpoints")["checkpoints"]]
-        sib = True
+        sib, metric = True, None
         if sort_by is not None and getattr(self, "experiment_id", None) is not None:
-            sib = bool(self._session.get(f"/api/v1/experiments/{self.experiment_id}")["config"]["searcher"].get("smaller_is_better", True))
-        out = _sort_checkpoints(cks, sort_by, sib, order_by)
+            scfg = self._session.get(f"/api/v1/experiments/{self.experiment_id}")["config"]["searcher"]
+            sib, metric = bool(scfg.get("smaller_is_better", True)), scfg.get("metric")
+        out = _sort_checkpoints(cks, sort_by, sib, order_by, metric)
         return out[:max_results] if max_results else out
 
     get_checkpoints = list_checkpoints
@@ -394,6 +598,7 @@ class Experiment:
         self.job_id = d.get("job_id")
         self.searcher_type = d.get("searcher_type")
         self.unmanaged = bool(d.get("unmanaged"))
+        self.username = d.get("username", d.get("user"))
 
     def reload(self) -> None:
         self._hydrate(self._session.get(f"/api/v1/experiments/{self._id}")["experiment"])
@@ -462,11 +667,20 @@ class Experiment:
         untar_to(base64.b64decode(b64), out)
         return out
 
-    def list_trials(self, sort_by: Optional[str] = None, order_by: Optional[OrderBy] = None) -> List[Trial]:
+    def list_trials(self, sort_by: Any = None, order_by: Any = None) -> List[Trial]:
+        """Trials of this experiment; ``sort_by`` a :class:`TrialSortBy` (or "best_validation"),
+        ``order_by`` an :class:`OrderBy` (reference Experiment.list_trials)."""
         params = {"sort_by": "best_validation"} if sort_by == "best_validation" else None
         ts = [Trial(self._session, t["id"], t)
               for t in self._session.get(f"/api/v1/experiments/{self._id}/trials", params=params)["trials"]]
-        if order_by == OrderBy.DESC and sort_by is None:
+        if isinstance(sort_by, TrialSortBy) and sort_by != TrialSortBy.UNSPECIFIED:
+            sib = True
+            if sort_by in (TrialSortBy.BEST_VALIDATION_METRIC, TrialSortBy.LATEST_VALIDATION_METRIC):
+                self.reload()
+                sib = bool(self.config.get("searcher", {}).get("smaller_is_better", True))
+            desc = _descending(order_by, default=False)
+            return _sorted(ts, _trial_key(sort_by, self._session, sib), desc)
+        if _descending(order_by) and sort_by is None:
             ts.reverse()
         return ts
 
@@ -500,9 +714,15 @@ class Experiment:
         cks = [Checkpoint(self._session, c["uuid"], c)
                for c in self._session.get(f"/api/v1/experiments/{self._id}/checkpoints")["checkpoints"]]
         self.reload()
-        sib = bool(self.config.get("searcher", {}).get("smaller_is_better", True))
-        out = _sort_checkpoints(cks, sort_by, sib, order_by)
+        scfg = self.config.get("searcher", {})
+        out = _sort_checkpoints(cks, sort_by, bool(scfg.get("smaller_is_better", True)), order_by,
+                                scfg.get("metric"))
         return out[:max_results] if max_results else out
+
+    def delete_tensorboard_files(self) -> None:
+        """Delete this experiment's TensorBoard event files from checkpoint storage (reference
+        experiment.py:604, DELETE /api/v1/experiments/{id}/tensorboard-files)."""
+        self._session.delete(f"/api/v1/experiments/{self._id}/tensorboard-files")
 
     def top_checkpoint(self, sort_by: Optional[str] = None, smaller_is_better: Optional[bool] = None) -> Checkpoint:
         top = self.top_n_checkpoints(1, sort_by, smaller_is_better)
@@ -564,8 +784,23 @@ class ModelVersion:
     def delete(self) -> None:
         self._session.delete(self._url())
 
+    def reload(self) -> None:
+        """Refresh from the master (reference model.py:133, GetModelVersion)."""
+        self._hydrate(self._session.get(self._url())["model_version"])
+
+    def iter_metrics(self, group: Optional[str] = None) -> Iterable[TrialMetrics]:
+        """Metrics of the tasks that reported using this model version
+        (``core_context.experimental.report_task_using_model_version``; reference model.py:101,
+        GetTrialMetricsByModelVersion with trial source INFERENCE)."""
+        params: Dict[str, Any] = {"trial_source_info_type": "TRIAL_SOURCE_INFO_TYPE_INFERENCE"}
+        rows = self._session.get(f"{self._url()}/metrics", params=params)["metrics"]
+        for r in rows:
+            if group is None or r.get("group") == group:
+                yield TrialMetrics._from_api(r["trial_id"], r)
+
     def get_metrics(self, group: Optional[str] = None) -> Iterable[TrialMetrics]:
-        return self.checkpoint.get_metrics(group) if self.checkpoint else iter(())
+        """Deprecated alias of :meth:`iter_metrics`."""
+        return self.iter_metrics(group)
 
     def __repr__(self) -> str:
         return f"ModelVersion(model={self.model_name!r}, version={self.version})"
@@ -899,7 +1134,19 @@ class Determined:
     def list_experiments(self, experiment_ids: Optional[List[int]] = None,
                          labels: Optional[List[str]] = None, users: Optional[List[str]] = None,
                          states: Optional[List[ExperimentState]] = None,
-                         project_id: Optional[int] = None) -> List[Experiment]:
+                         project_id: Optional[int] = None, sort_by: Any = None,
+                         order_by: Any = None) -> List[Experiment]:
+        """Experiments, optionally filtered and sorted by an :class:`ExperimentSortBy` in
+        :class:`OrderBy` order (reference Determined.list_experiments)."""
+        out = self._list_experiments(experiment_ids, labels, users, states, project_id)
+        if sort_by is None:
+            return out
+        return _sorted(out, _experiment_key(ExperimentSortBy(sort_by) if not isinstance(sort_by, ExperimentSortBy)
+                                            else sort_by, self._session), _descending(order_by))
+
+    def _list_experiments(self, experiment_ids: Optional[List[int]], labels: Optional[List[str]],
+                          users: Optional[List[str]], states: Optional[List[ExperimentState]],
+                          project_id: Optional[int]) -> List[Experiment]:
         params: Dict[str, Any] = {}
         if states:
             params["states"] = [s.value if isinstance(s, ExperimentState) else s for s in states]
@@ -911,6 +1158,8 @@ class Determined:
             if experiment_ids and e["id"] not in experiment_ids:
                 continue
             if labels and not set(labels) & set(e.get("labels") or []):
+                continue
+            if users and e.get("username", e.get("user")) not in users:
                 continue
             out.append(Experiment(self._session, e["id"], e))
         return out
@@ -965,7 +1214,7 @@ class Determined:
     def get_model_by_id(self, model_id: int) -> Model:
         return self.get_model(model_id)
 
-    def list_models(self, sort_by: Optional[str] = None, order_by: OrderBy = OrderBy.ASC,
+    def list_models(self, sort_by: Any = None, order_by: Any = OrderBy.ASC,
                     name: Optional[str] = None, description: Optional[str] = None,
                     model_id: Optional[int] = None, workspace_names: Optional[List[str]] = None) -> List[Model]:
         ms = [Model(self._session, m) for m in self._session.get("/api/v1/models")["models"]]
@@ -978,10 +1227,20 @@ class Determined:
         if workspace_names:
             ids = {self.get_workspace(w).id for w in workspace_names}
             ms = [m for m in ms if m.workspace_id in ids]
+        if isinstance(sort_by, ModelSortBy):
+            sort_by = {ModelSortBy.UNSPECIFIED: None, ModelSortBy.NAME: "name",
+                       ModelSortBy.DESCRIPTION: "description", ModelSortBy.CREATION_TIME: "creation_time",
+                       ModelSortBy.LAST_UPDATED_TIME: "last_updated_time",
+                       ModelSortBy.NUM_VERSIONS: "num_versions", ModelSortBy.WORKSPACE: "workspace"}[sort_by]
+        ws_names: Dict[Any, str] = {}
+        if sort_by == "workspace":
+            ws_names = {w.id: w.name for w in self.list_workspaces()}
         key = {"name": lambda m: m.name, "description": lambda m: m.description or "",
                "creation_time": lambda m: m.creation_time or 0,
-               "last_updated_time": lambda m: m.last_updated_time or 0}.get(sort_by or "name", lambda m: m.name)
-        return sorted(ms, key=key, reverse=order_by == OrderBy.DESC)
+               "last_updated_time": lambda m: m.last_updated_time or 0,
+               "num_versions": lambda m: len(m.list_versions()),
+               "workspace": lambda m: ws_names.get(m.workspace_id, "")}.get(sort_by or "name", lambda m: m.name)
+        return sorted(ms, key=key, reverse=_descending(order_by))
 
     get_models = list_models
 
@@ -1094,3 +1353,6 @@ stream_trials_metrics = _export("stream_trials_metrics")
 iter_trials_metrics = _export("iter_trials_metrics")
 stream_trials_training_metrics = _export("stream_trials_training_metrics")
 stream_trials_validation_metrics = _export("stream_trials_validation_metrics")
+
+# reference name of the OAuth client record (common/experimental/oauth2_scim_client.py)
+Oauth2ScimClient = OAuthClient

@@ -18,3 +18,4 @@ for m in normal; do
   timeout -s KILL 200 rocprofv3 --pmc $P1 --kernel-include-regex "conv_fwd_kernel" --output-format csv -d $OUT/pmc1_$m -o run -- python tools/probe_contention.py --mode $m --steps 2 --warmup 2 > $OUT/pmc1_$m.log 2>&1 || exit 1
   timeout -s KILL 200 rocprofv3 --pmc $P2 --kernel-include-regex "conv_fwd_kernel" --output-format csv -d $OUT/pmc2_$m -o run -- python tools/probe_contention.py --mode $m --steps 2 --warmup 2 > $OUT/pmc2_$m.log 2>&1 || exit 1
 done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || exit 1
