@@ -14,7 +14,7 @@ import io
 import json
 import tarfile
 import time
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 from determined_clone_amd.master.db import dec, now
 from determined_clone_amd.master.experiment import TERMINAL, experiment_row_to_api, trial_row_to_api
@@ -166,22 +166,15 @@ def get_slot(r: Req) -> Any:
 
 # =========================================================================== experiments (bulk, search, files)
 def _bulk_ids(r: Req) -> List[int]:
+    """Experiment ids of a bulk action: ``experiment_ids``, or every experiment matching
+    ``filters`` (BulkExperimentFilters, one SQL query: experiment_filter.bulk_filter_sql)."""
+    from determined_clone_amd.master.experiment_filter import bulk_filter_sql
+
     ids = [int(i) for i in r.body.get("experiment_ids") or []]
     f = r.body.get("filters")
     if f is not None:
-        for row in r.m.db.all("SELECT * FROM experiments ORDER BY id"):
-            d = experiment_row_to_api(row, r.m.experiments.get(row["id"]))
-            if f.get("project_id") and d["project_id"] != f["project_id"]:
-                continue
-            if f.get("states") and d["state"] not in f["states"]:
-                continue
-            if "archived" in f and f["archived"] is not None and d["archived"] != bool(f["archived"]):
-                continue
-            if f.get("name") and f["name"] not in (d["name"] or ""):
-                continue
-            if f.get("labels") and not set(f["labels"]) <= set(d["labels"] or []):
-                continue
-            ids.append(d["id"])
+        where, params = bulk_filter_sql(f)
+        ids += [row["id"] for row in r.m.db.all(f"SELECT e.id FROM experiments e WHERE {where}", params)]
     return sorted(set(ids))
 
 
@@ -288,29 +281,83 @@ def model_def_file(r: Req) -> Any:
     raise HTTPError(404, f"file {want!r} not in the model definition")
 
 
+# sort columns of SearchExperiments (reference api_experiment.go orderColMap + hp. / metric keys)
+_SEARCH_SORT = {"id": "e.id", "name": "json_extract(e.config, '$.name')",
+                "description": "json_extract(e.config, '$.description')", "startTime": "e.start_time",
+                "endTime": "e.end_time", "state": "e.state", "progress": "e.progress",
+                "user": "e.owner_id", "forkedFrom": "e.parent_id", "projectId": "e.project_id",
+                "resourcePool": "json_extract(e.config, '$.resources.resource_pool')",
+                "searcherType": "json_extract(e.config, '$.searcher.name')",
+                "searcherMetric": "json_extract(e.config, '$.searcher.metric')",
+                "searcherMetricsVal": "bt.best_validation",
+                "numTrials": "(SELECT COUNT(*) FROM trials t WHERE t.experiment_id = e.id)",
+                "tags": "json_extract(e.config, '$.labels')"}
+
+
+def _search_order(sort: Optional[str]) -> Tuple[str, List[Any]]:
+    from determined_clone_amd.master import experiment_filter as EF
+
+    if not sort:
+        return "e.id ASC", []
+    parts, params, has_id = [], [], False
+    for item in sort.split(","):
+        key, _, direction = item.partition("=")
+        direction = direction or "asc"
+        if direction not in ("asc", "desc"):
+            raise HTTPError(400, f"invalid sort direction: {direction}")
+        d = "ASC" if direction == "asc" else "DESC"
+        if key.startswith("hp."):
+            expr = "json_extract(e.config, ?)"
+            params.append("$.hyperparameters" + EF._json_path(*key[3:].split("."))[1:])
+        elif "." in key:
+            try:
+                grp, name, qual = EF.parse_metric_name(key)
+            except EF.FilterError as ex:
+                raise HTTPError(400, str(ex))
+            expr = "json_extract(bt.summary_metrics, ?)"
+            params.append(EF._json_path(grp, name) + "." + qual)
+        elif key in _SEARCH_SORT:
+            expr = _SEARCH_SORT[key]
+            has_id = has_id or key == "id"
+        else:
+            raise HTTPError(400, f"invalid sort col: {key}")
+        parts.append(f"({expr}) IS NULL, {expr} {d}")  # NULLS LAST either way
+        if expr.count("?"):
+            params.append(params[-1])  # the expression appears twice
+    if not has_id:
+        parts.append("e.id ASC")
+    return ", ".join(parts), params
+
+
 @route("GET", "/api/v1/experiments-search")
 def search_experiments(r: Req) -> Any:
-    """Experiments with their best trial (reference: SearchExperiments), filtered by project,
-    name substring and state, sorted by ``sort`` (``field[=asc|desc]``)."""
-    rows = r.m.db.all("SELECT * FROM experiments ORDER BY id")
-    out = []
-    for row in rows:
-        d = experiment_row_to_api(row, r.m.experiments.get(row["id"]))
-        if r.qget("project_id") and str(d["project_id"]) != r.qget("project_id"):
-            continue
-        flt = r.qget("filter")
-        if flt and flt not in (d["name"] or "") and flt != d["state"]:
-            continue
-        e = r.m.experiments.get(row["id"])
-        smaller = e.smaller_is_better if e else True
-        best = r.m.db.one("SELECT * FROM trials WHERE experiment_id=? AND best_validation IS NOT NULL "
-                          f"ORDER BY best_validation {'ASC' if smaller else 'DESC'} LIMIT 1", [row["id"]])
-        out.append({"experiment": d, "best_trial": trial_row_to_api(best) if best else None})
-    sort = r.qget("sort")
-    if sort:
-        key, _, order = sort.partition("=")
-        out.sort(key=lambda x: (x["experiment"].get(key) is None, x["experiment"].get(key)),
-                 reverse=order == "desc")
+    """Experiments with their best trial (reference: SearchExperiments, api_experiment.go:2523):
+    the ``filter`` experiment-filter DSL (master/experiment_filter.py), ``project_id``, ``sort``
+    (``col=asc|desc[,...]``; experiment columns, ``hp.*``, ``<group>.<metric>.<qualifier>``),
+    ``offset`` / ``limit`` -- one SQL query with the best trial joined (no per-experiment query)."""
+    from determined_clone_amd.master import experiment_filter as EF
+
+    where, params = "1", []
+    flt = r.qget("filter")
+    if flt:
+        try:
+            where, params = EF.compile_filter(flt)
+        except EF.FilterError as ex:
+            raise HTTPError(400, str(ex))
+    if r.qget("project_id"):
+        where = f"({where}) AND e.project_id = ?"
+        params = params + [_int(r.qget("project_id"))]
+    order, oparams = _search_order(r.qget("sort"))
+    rows = r.m.db.all(f"SELECT e.*, bt.id AS _bt_id FROM {EF.FROM_BEST_TRIAL} WHERE {where} ORDER BY {order}",
+                      params + oparams)
+    best = {}
+    bt_ids = [row["_bt_id"] for row in rows if row["_bt_id"] is not None]
+    for i in range(0, len(bt_ids), 500):
+        chunk = bt_ids[i:i + 500]
+        for t in r.m.db.all(f"SELECT * FROM trials WHERE id IN ({','.join('?' * len(chunk))})", chunk):
+            best[t["id"]] = trial_row_to_api(t)
+    out = [{"experiment": experiment_row_to_api(row, r.m.experiments.get(row["id"])),
+            "best_trial": best.get(row["_bt_id"])} for row in rows]
     p = S._paginate(out, r)
     return {"experiments": p["items"], "pagination": p["pagination"]}
 

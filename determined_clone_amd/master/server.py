@@ -845,7 +845,14 @@ for _kind, _path in (("COMMAND", "commands"), ("SHELL", "shells"), ("NOTEBOOK", 
             if isinstance(ep, str):
                 ep = ["bash", "-c", ep]
             if kind == "TENSORBOARD" and not ep:
-                ep = ["python3", "-m", "determined_clone_amd.exec.tensorboard"] + [str(x) for x in r.body.get("experiment_ids", [])]
+                eids = [int(x) for x in r.body.get("experiment_ids") or []]
+                if r.body.get("filters") is not None:  # reference api_tensorboard.go:484-487
+                    from determined_clone_amd.master.experiment_filter import bulk_filter_sql
+
+                    where, params = bulk_filter_sql(r.body["filters"])
+                    eids = [row["id"] for row in r.m.db.all(
+                        f"SELECT e.id FROM experiments e WHERE {where} ORDER BY e.id", params)]
+                ep = ["python3", "-m", "determined_clone_amd.exec.tensorboard"] + [str(x) for x in eids]
             if kind == "NOTEBOOK" and not ep:
                 ep = ["python3", "-m", "determined_clone_amd.exec.notebook"]
             if kind == "SHELL" and not ep:

@@ -284,17 +284,49 @@ function experimentActions(e) {
   return out;
 }
 
+// Experiment-list filter box -> the reference's filter-group JSON (master/experiment_filter.py):
+// clauses separated by ";", each "<column> <op> <value>" with op one of = != < <= > >= contains
+// notContains isEmpty notEmpty; columns: experiment fields (name, state, tags, numTrials, ...),
+// hp.<name>, or <group>.<metric>.<min|max|mean|last> (e.g. validation.val_loss.min < 0.1).
+function parseExperimentFilter(text, showArchived) {
+  const children = [];
+  for (const raw of text.split(";")) {
+    const m = raw.trim().match(/^(\S+)\s+(=|!=|<=|>=|<|>|contains|notContains|isEmpty|notEmpty)\s*(.*)$/);
+    if (!m) continue;
+    const [, col, op, rest] = m;
+    let value = rest.trim().replace(/^["']|["']$/g, "");
+    const num = value !== "" && !isNaN(Number(value));
+    const node = { kind: "field", columnName: col, operator: op, value: op.endsWith("Empty") ? null : (num ? Number(value) : value) };
+    if (col.startsWith("hp.")) Object.assign(node, { location: "LOCATION_TYPE_HYPERPARAMETERS", type: num ? "COLUMN_TYPE_NUMBER" : "COLUMN_TYPE_TEXT" });
+    else if (/\.(min|max|mean|last)$/.test(col)) Object.assign(node, { location: col.startsWith("training.") ? "LOCATION_TYPE_TRAINING" : "LOCATION_TYPE_VALIDATIONS", type: num ? "COLUMN_TYPE_NUMBER" : "COLUMN_TYPE_TEXT" });
+    children.push(node);
+  }
+  return { filterGroup: { kind: "group", conjunction: "and", children }, showArchived };
+}
+
 async function pageExperiments(params) {
   const q = new URLSearchParams();
   if (params.get("archived") !== "all") q.set("archived", "false");
   if (params.get("state")) q.append("states", params.get("state"));
   if (params.get("project")) q.set("project_id", params.get("project"));
-  const r = await api.get("/api/v1/experiments?" + q);
+  let r;
+  const ftext = params.get("filter") || "";
+  if (ftext) {  // the filter DSL runs on the search route (SearchExperiments)
+    const fq = new URLSearchParams({ filter: JSON.stringify(parseExperimentFilter(ftext, params.get("archived") === "all")) });
+    if (params.get("project")) fq.set("project_id", params.get("project"));
+    const sr = await api.get("/api/v1/experiments-search?" + fq);
+    const rows = sr.experiments.map((x) => x.experiment).filter((e) => !params.get("state") || e.state === params.get("state"));
+    r = { experiments: rows, pagination: { total: rows.length } };
+  } else {
+    r = await api.get("/api/v1/experiments?" + q);
+  }
+  const fbox = h("input", { type: "text", size: 48, value: ftext, placeholder: "filter: name contains resnet; validation.val_loss.min < 0.5; hp.lr > 0.01",
+    onchange: (ev) => nav("#/experiments", { state: params.get("state"), archived: params.get("archived"), filter: ev.target.value }) });
   const state = h("select", { onchange: (ev) => nav("#/experiments", { state: ev.target.value, archived: params.get("archived") }) },
     ["", "ACTIVE", "PAUSED", "COMPLETED", "CANCELED", "ERROR"].map((s) => h("option", { value: s, selected: s === (params.get("state") || "") }, s || "all states")));
   const arch = h("label", {}, h("input", { type: "checkbox", checked: params.get("archived") === "all",
-    onchange: (ev) => nav("#/experiments", { state: params.get("state"), archived: ev.target.checked ? "all" : "" }) }), " show archived");
-  return h("div", {}, h("h1", {}, "Experiments"), h("div", { class: "toolbar" }, state, arch,
+    onchange: (ev) => nav("#/experiments", { state: params.get("state"), archived: ev.target.checked ? "all" : "", filter: ftext }) }), " show archived");
+  return h("div", {}, h("h1", {}, "Experiments"), h("div", { class: "toolbar" }, fbox, state, arch,
     h("span", { class: "muted" }, `${r.pagination.total} experiments`)), experimentTable(r.experiments));
 }
 

@@ -2,6 +2,7 @@
 metric streams, workloads, metric reports, user settings, slots, job stats, NTSC priority,
 resource accounting, project/workspace archive + move, resource-pool bindings, route precedence."""
 import base64
+import json
 import os
 import shutil
 import tempfile
@@ -62,8 +63,16 @@ def test_files_labels_search_and_streams(env):
     assert s.get(f"/api/v1/experiments/{eid}")["experiment"]["labels"] == ["a", "b"]
     s.delete(f"/api/v1/experiments/{eid}/labels/a")
     assert s.get("/api/v1/experiment/labels")["labels"] == ["b"]
-    res = s.get("/api/v1/experiments-search", params={"filter": "api-extra"})["experiments"]
+    flt = {"filterGroup": {"kind": "group", "conjunction": "and", "children": [
+        {"kind": "field", "columnName": "name", "operator": "contains", "value": "API-EXTRA"},
+        {"kind": "field", "location": "LOCATION_TYPE_VALIDATIONS", "type": "COLUMN_TYPE_NUMBER",
+         "columnName": "validation.val_loss.last", "operator": "notEmpty"}]}, "showArchived": False}
+    res = s.get("/api/v1/experiments-search", params={"filter": json.dumps(flt), "sort": "id=desc"})["experiments"]
     assert res[0]["experiment"]["id"] == eid and res[0]["best_trial"] is not None
+    flt["filterGroup"]["children"][0]["value"] = "no-such-name"
+    assert s.get("/api/v1/experiments-search", params={"filter": json.dumps(flt)})["experiments"] == []
+    with pytest.raises(Exception):  # malformed filter: 400, not an empty list
+        s.get("/api/v1/experiments-search", params={"filter": '{"filterGroup": {"kind": "group"}}'})
     names = s.get("/api/v1/experiments/metrics-stream/metric-names", params={"ids": eid})
     assert "val_loss" in names["validation_metrics"] and "loss" in names["training_metrics"]
     assert s.get(f"/api/v1/experiments/{eid}/metrics-stream/batches",

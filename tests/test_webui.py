@@ -117,3 +117,31 @@ def test_ui_pages_against_live_master(server, tmp_path):
                  "/api/v1/workspaces", "/api/v1/workspaces/1/projects", "/api/v1/projects/1",
                  "/api/v1/webhooks", "/api/v1/master/logs?after_id=0&tail=500", "/api/v1/users"):
         assert isinstance(call("GET", path, token=tok), dict), path
+
+
+def test_experiment_list_filter_box_builds_reference_filter_json(tmp_path):
+    """The experiment list's filter box turns "col op value; ..." into the reference's
+    filter-group JSON; the master's compiler (master/experiment_filter.py) accepts it."""
+    import json
+    import re
+    import shutil
+    import subprocess
+
+    from determined_clone_amd.master import experiment_filter as EF
+
+    node = shutil.which("node")
+    if node is None:
+        pytest.skip("node not installed")
+    src = open(APP_JS).read()
+    fn = re.search(r"function parseExperimentFilter\(.*?\n}\n", src, re.S).group(0)
+    script = tmp_path / "f.js"
+    script.write_text(fn + "\nconsole.log(JSON.stringify(parseExperimentFilter("
+                      "'name contains resnet; validation.val_loss.min < 0.5; hp.lr >= 0.01; description notEmpty; "
+                      "hp.model = efficientdet_d0', false)));\n")
+    out = json.loads(subprocess.run([node, str(script)], capture_output=True, text=True, check=True).stdout)
+    kids = out["filterGroup"]["children"]
+    assert [k["columnName"] for k in kids] == ["name", "validation.val_loss.min", "hp.lr", "description", "hp.model"]
+    assert kids[1]["location"] == "LOCATION_TYPE_VALIDATIONS" and kids[1]["value"] == 0.5
+    assert kids[2]["location"] == "LOCATION_TYPE_HYPERPARAMETERS" and kids[2]["type"] == "COLUMN_TYPE_NUMBER"
+    assert kids[3]["value"] is None and kids[4]["type"] == "COLUMN_TYPE_TEXT"
+    EF.compile_filter(out)
