@@ -18,7 +18,7 @@ import pathlib
 import subprocess
 import sys
 import sysconfig
-from typing import List
+from typing import List, Optional, Sequence
 
 HERE = pathlib.Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
@@ -85,22 +85,29 @@ def _compile(cmd: List[str], key: str = "") -> None:
         out.with_suffix(out.suffix + ".key").write_text(key)
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> pathlib.Path:
+def build(force: bool = False, verbose: bool = False, jobs: int = 0, defines: Sequence[str] = (),
+          target: Optional[pathlib.Path] = None) -> pathlib.Path:
+    """Build ``_C.so`` (or, with ``defines`` / ``target``, an A/B variant of it in its own object
+    directory -- loaded through ``DCA_OPS_SO``, never by default)."""
     inc, lib, abi = _torch_paths()
-    BUILD.mkdir(exist_ok=True)
+    variant = bool(defines) or target is not None
+    TARGET_ = target or TARGET
+    BUILD_ = BUILD if not variant else BUILD / ("variant_" + hashlib.sha1(" ".join(defines).encode()).hexdigest()[:10])
+    dflags = [f"-D{d}" for d in defines]
+    BUILD_.mkdir(parents=True, exist_ok=True)
     headers = sorted(CSRC.glob("*.h"))
     jobs_list, objs = [], []
     for src in sorted(CSRC.glob("*.hip")):
-        obj = BUILD / (src.stem + ".hip.o")
+        obj = BUILD_ / (src.stem + ".hip.o")
         objs.append(obj)
         cmd = [_hipcc(), "-c", str(src), "-o", str(obj), f"--offload-arch={ARCH}",
-               "-munsafe-fp-atomics", f"-I{CSRC}"] + _common_flags(abi) + _FILE_FLAGS.get(src.stem, [])
+               "-munsafe-fp-atomics", f"-I{CSRC}"] + _common_flags(abi) + _FILE_FLAGS.get(src.stem, []) + dflags
         key = _obj_key(src, headers, cmd)
         if force or _stale(obj, key):
             jobs_list.append((cmd, key))
     py_inc = sysconfig.get_paths()["include"]
     for src in sorted(CSRC.glob("*.cpp")):
-        obj = BUILD / (src.stem + ".cpp.o")
+        obj = BUILD_ / (src.stem + ".cpp.o")
         objs.append(obj)
         cmd = [_hipcc(), "-c", str(src), "-o", str(obj), f"-I{CSRC}", f"-I{py_inc}",
                "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H"] + [f"-I{p}" for p in inc] \
@@ -110,7 +117,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> pathlib.
             jobs_list.append((cmd, key))
     # the source hash as a linked-in symbol (bindings.cpp exposes it as _C.source_hash)
     digest = source_hash()
-    hsrc, hobj = BUILD / "source_hash.cpp", BUILD / "source_hash.cpp.o"
+    hsrc, hobj = BUILD_ / "source_hash.cpp", BUILD_ / "source_hash.cpp.o"
     objs.append(hobj)
     hcode = f'extern "C" const char dca_source_hash[] = "{digest}";\n'
     if not hsrc.exists() or hsrc.read_text() != hcode:
@@ -124,6 +131,11 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> pathlib.
             if verbose:
                 print(" ".join(cmd), flush=True)
         list(ex.map(lambda ck: _compile(*ck), jobs_list))
+    if variant:
+        if jobs_list or force or not TARGET_.exists():
+            _compile([_hipcc(), "-shared", "-fPIC", "-o", str(TARGET_)] + [str(o) for o in objs]
+                     + _link_flags(lib))
+        return TARGET_
     if jobs_list or force or not TARGET.exists() or linked_hash() != digest:
         link = [_hipcc(), "-shared", "-fPIC", "-o", str(TARGET)] + [str(o) for o in objs] + [
             f"--offload-arch={ARCH}", f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
@@ -133,6 +145,11 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0) -> pathlib.
         _compile(link)
         LINKED.write_text(digest)
     return TARGET
+
+
+def _link_flags(lib: str) -> List[str]:
+    return [f"--offload-arch={ARCH}", f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
+            "-ltorch_hip", "-ltorch_python", "-lamdhip64", "-lhipblaslt", f"-Wl,-rpath,{lib}"]
 
 
 LINKED = HERE / "_C.so.hash"  # next to _C.so (travels with it); the embedded hash stays authoritative
@@ -148,8 +165,12 @@ def main() -> None:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=0)
+    ap.add_argument("-D", dest="defines", action="append", default=[],
+                    help="A/B variant: compile with this define (needs --out)")
+    ap.add_argument("--out", default=None, help="A/B variant: output .so path (load via DCA_OPS_SO)")
     args = ap.parse_args()
-    out = build(force=args.force, verbose=args.verbose, jobs=args.jobs)
+    out = build(force=args.force, verbose=args.verbose, jobs=args.jobs, defines=args.defines,
+                target=pathlib.Path(args.out).resolve() if args.out else None)
     print(f"built {out}")
 
 

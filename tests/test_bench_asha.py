@@ -65,3 +65,20 @@ def test_synthetic_cifar_is_learnable_but_noisy():
     pred = ((va.x.astype(np.float32)[:, None] - means[None]) ** 2).sum((2, 3, 4)).argmin(1)
     acc = (pred == va.y).mean()
     assert 0.15 < acc < 0.95, acc
+
+
+def test_bench_asha_sixteen_trials_on_eight_fake_gpus(tmp_path):
+    """BASELINE config "16 concurrent trials gang-scheduled across 8 MI355X" --
+    the agent reports 8 ROCm devices with 2 slots each (trials run on the CPU here): 16 trials
+    run at once, never more than 2 on one GPU, all 8 GPUs used."""
+    out = subprocess.run(
+        [sys.executable, os.path.join(ROOT, "tools", "bench_asha.py"), "--cpu", "--fake-gpus", "8",
+         "--slots-per-gpu", "2", "--max-trials", "16", "--max-concurrent", "16", "--epochs", "1",
+         "--records-per-epoch", "128", "--batch", "64", "--timeout", "600"],
+        capture_output=True, text=True, timeout=900, cwd=str(tmp_path))
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["experiment_state"] == "COMPLETED" and res["trials_completed"] == 16
+    assert res["n_gpus"] == 8 and res["config"]["slots_per_gpu"] == 2
+    assert res["max_concurrent_trials"] == 16 and res["max_trials_per_gpu"] <= 2
+    assert res["gpus_used"] == 8

@@ -52,3 +52,40 @@ def test_bench_gpus_flag_launches_ranks_itself():
     assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 4
     assert r["backend"] == "gloo"  # CPU here; "nccl" (RCCL) on the GPU box
     assert r["device"] == "cpu" and "host memory" in r["data"]
+
+
+def _one_json_line(out):
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+def _clean_env():
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def test_bench_eight_ranks_world_size_eight():
+    """the driver's 8-GPU launch shape (``bench.py --gpus 8``, no launcher) forms
+    an 8-rank process group and reports the 8-rank aggregate (gloo on CPU, tiny batch)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1",
+           "--warmup", "1", "--batch", "1"]
+    r = _one_json_line(subprocess.run(cmd, cwd=ROOT, env=_clean_env(), capture_output=True, text=True,
+                                      timeout=900))
+    assert r["n_gpus"] == 8 and r["world_size"] == 8 and r["backend"] == "gloo"
+    assert r["config"]["parallelism"] == "dp8" and r["config"]["global_batch"] == 8
+    assert abs(r["value"] - 8 / (r["ms_per_step"] / 1000.0)) / r["value"] < 0.01
+
+
+def test_bench_gpt2_eight_ranks_zero2():
+    """``tools/bench_gpt2.py --gpus 8``: the GPT-2 DeepSpeedTrial ZeRO-2 bench at 8 ranks (a tiny
+    GPT on CPU; the MI355X run uses gpt2-medium)."""
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "bench_gpt2.py"), "--gpus", "8", "--model", "tiny",
+           "--micro", "1", "--seq", "64", "--steps", "1", "--warmup", "1"]
+    r = _one_json_line(subprocess.run(cmd, cwd=ROOT, env=_clean_env(), capture_output=True, text=True,
+                                      timeout=900))
+    assert r["n_gpus"] == 8 and r["world_size"] == 8 and r["backend"] == "gloo"
+    assert r["config"]["parallelism"] == "zero2-dp8" and r["config"]["global_batch"] == 8

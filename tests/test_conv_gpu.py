@@ -271,6 +271,8 @@ IGEMM_SHAPES = [
     (2, 64, 56, 64, 1), (2, 128, 56, 128, 2), (3, 128, 28, 128, 1), (2, 256, 28, 256, 2),
     (4, 256, 14, 256, 1), (3, 512, 14, 512, 2), (5, 512, 7, 512, 1), (1, 64, 5, 128, 1),
     (1, 192, 9, 64, 2),
+    # ragged last pixel tiles, stride 2, C != K (also ran the removed 8-wave kernel: round6_igemm_big_tile_ab.txt)
+    (2, 128, 14, 256, 1), (1, 256, 9, 128, 2), (3, 64, 11, 256, 1), (2, 512, 7, 128, 1),
 ]
 
 
@@ -307,13 +309,17 @@ def test_conv_igemm_forward_stats_and_dgrad(shape):
         _close(C.conv_igemm_dgrad(dy, w, 1), dref, 1e-2, "dx")
 
 
-def test_conv_igemm_asymmetric_weight_orientation():
+@pytest.mark.parametrize("ck", [(64, 64), (128, 256), (256, 128)])
+def test_conv_igemm_asymmetric_weight_orientation(ck):
     """A weight that is non-zero at ONE tap and ONE (k, c) pair: catches transposed taps /
-    swapped channel maps that random data can hide."""
+    swapped channel maps that random data can hide (4-wave kernel at 64 x 64, the 8-wave big-tile
+    kernel shapes at K = 256 / 128)."""
     C = _ext.load()
-    x, w = _igemm_inputs(2, 64, 9, 64)
+    c, k = ck
+    x, w = _igemm_inputs(2, c, 9, k)
     w = torch.zeros_like(w)
     w[5, 17, 0, 2] = 1.0  # k=5 reads channel 17 at tap (r=0, s=2)
+    w[k - 3, c - 2, 2, 1] = -2.0  # last channel tiles, another tap
     y, _ = C.conv_igemm_fwd(x, w, 1, 1, False)
     ref = F.conv2d(x.float(), w.float(), padding=1)
     torch.testing.assert_close(y.float(), ref, atol=0, rtol=0)

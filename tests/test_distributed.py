@@ -52,11 +52,12 @@ def _worker_sync(rank: int, world: int, port: int, fused: bool, agg: int, out_di
         else:
             opt = ctx.wrap_optimizer(orig, fused=fused)
         x, y = _data(8 * agg)
+        b = 8 // world  # per-rank share of each 8-record global micro batch
         for step in range(3):
             for micro in range(agg):
                 ctx._current_batch_idx = step * agg + micro
-                lo = (micro * world + rank) * 4
-                xb, yb = x[lo:lo + 4], y[lo:lo + 4]
+                lo = micro * 8 + rank * b
+                xb, yb = x[lo:lo + b], y[lo:lo + b]
                 loss = torch.nn.functional.mse_loss(model(xb), yb)
                 ctx.backward(loss)
                 ctx.step_optimizer(opt)
@@ -83,18 +84,21 @@ def _reference(agg: int, scheduled: bool = False):
     return model.state_dict()
 
 
-@pytest.mark.parametrize("fused,agg", [(False, 1), (True, 1), (True, 2), (False, 2)])
-def test_data_parallel_matches_single_process(fused, agg):
-    world = 2
+@pytest.mark.parametrize("world,fused,agg", [(2, False, 1), (2, True, 1), (2, True, 2), (2, False, 2),
+                                             (4, True, 1), (8, True, 2), (8, False, 1)])
+def test_data_parallel_matches_single_process(world, fused, agg):
+    """Bucketed all-reduce DDP at 2 ranks and at the driver's 4 / 8-rank layouts (VERDICT r5 #5;
+    676 parameters: not a multiple of 8), every rank bit-identical, equal to one process on the
+    full batch."""
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_worker_sync, args=(world, _free_port(), fused, agg, d), nprocs=world,
                            start_method="spawn")
         ref = _reference(agg)
-        r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
-        r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)
+        outs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
         for k in ref:
-            torch.testing.assert_close(r0[k], r1[k], atol=0, rtol=0)
-            torch.testing.assert_close(r0[k], ref[k], atol=1e-5, rtol=1e-5)
+            for o in outs[1:]:
+                torch.testing.assert_close(outs[0][k], o[k], atol=0, rtol=0)
+            torch.testing.assert_close(outs[0][k], ref[k], atol=1e-5, rtol=1e-5)
 
 
 def test_data_parallel_original_optimizer_object_drives_fused_replacement():

@@ -98,14 +98,20 @@ def _reference(kind, max_norm):
     return m, opt
 
 
-@pytest.mark.parametrize("stage,kind,max_norm,bucket_mb,defer", [
-    (1, "adam", 0.0, 64.0, False),
-    (2, "adam", 0.0, 0.002, True),   # many small buckets: hooks fire bucket by bucket
-    (2, "adamw", 0.05, 0.002, False),  # global-norm clipping across shards
-    (2, "sgd", 0.0, 0.001, True),
+@pytest.mark.parametrize("world,stage,kind,max_norm,bucket_mb,defer", [
+    (2, 1, "adam", 0.0, 64.0, False),
+    (2, 2, "adam", 0.0, 0.002, True),   # many small buckets: hooks fire bucket by bucket
+    (2, 2, "adamw", 0.05, 0.002, False),  # global-norm clipping across shards
+    (2, 2, "sgd", 0.0, 0.001, True),
+    # the driver's 8-GPU layout: 1764 parameters (not a multiple of 8, so the
+    # last shard is padded), 500-float buckets (boundaries inside the 640- and 960-element weights),
+    # 8 deferred gathers in flight, clipping over 8 shards
+    (4, 2, "adamw", 0.05, 0.002, True),
+    (8, 1, "adam", 0.0, 64.0, False),
+    (8, 2, "adamw", 0.05, 0.002, True),
 ])
-def test_zero_matches_full_batch(stage, kind, max_norm, bucket_mb, defer):
-    world = 2
+def test_zero_matches_full_batch(world, stage, kind, max_norm, bucket_mb, defer):
+    assert sum(p.numel() for p in _model().parameters()) % 8 != 0  # padded last shard at world 8
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), stage, kind, max_norm, bucket_mb, d, defer),
                  nprocs=world, join=True)
@@ -158,6 +164,10 @@ def test_lamb_rejected():
         zero.zero_optimizer_for("lamb")
 
 
+def _rs_len(world):
+    return 3 + 5 * world + 7  # room for the offset-3 bucket plus an untouched tail
+
+
 def _rs_worker(rank, world, port, out_dir):
     """In-place bucket reduce-scatter exactly as ZeroShardMixin._launch issues it: the output is
     the rank's own chunk of the bucket, a view into the reduced input."""
@@ -169,7 +179,7 @@ def _rs_worker(rank, world, port, out_dir):
     chunk = 5
     res = {}
     for start in (0, 3):  # a bucket at offset 0 and one further into the flat buffer
-        flat = torch.arange(40, dtype=torch.float32) + 1000 * rank
+        flat = torch.arange(_rs_len(world), dtype=torch.float32) + 1000 * rank
         full = flat[start:start + world * chunk]
         out = full[rank * chunk:(rank + 1) * chunk]
         before = flat.clone()
@@ -183,7 +193,7 @@ def _rs_worker(rank, world, port, out_dir):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_inplace_reduce_scatter_offsets_per_bucket(world):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_rs_worker, args=(world, _free_port(), d), nprocs=world, join=True)
@@ -196,11 +206,11 @@ def test_inplace_reduce_scatter_offsets_per_bucket(world):
             # own chunk == sum over ranks of that chunk; everything else untouched
             want = sum(outs[q][start][1][lo:hi] for q in range(world))
             torch.testing.assert_close(after[lo:hi], want)
-            mask = torch.ones(40, dtype=torch.bool)
+            mask = torch.ones(_rs_len(world), dtype=torch.bool)
             mask[lo:hi] = False
             torch.testing.assert_close(after[mask], before[mask])
             # output = input + rank * chunk: the value at chunk offset i is the sum of element
             # (start + r*chunk + i) over ranks
-            base = torch.arange(40, dtype=torch.float32)[lo:hi]
+            base = torch.arange(_rs_len(world), dtype=torch.float32)[lo:hi]
             torch.testing.assert_close(after[lo:hi], world * base + 1000 * sum(range(world)))
         torch.testing.assert_close(o["avg"], torch.tensor([(world + 1) / 2]))

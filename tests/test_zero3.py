@@ -51,12 +51,12 @@ def _engine(stage: int, micro: int = 4, grouped: bool = True):
     return eng
 
 
-def _train(eng, steps=3, rank=0, world=1):
-    n = 4 // world
+def _train(eng, steps=3, rank=0, world=1, gb=4):
+    n = gb // world
     losses = []
     for step in range(steps):
         for micro in range(2):
-            x, y = _data(step, micro)
+            x, y = _data(step, micro, gb)
             x, y = x[rank * n:(rank + 1) * n], y[rank * n:(rank + 1) * n]
             _, loss = eng(x, y)
             eng.backward(loss)
@@ -88,24 +88,24 @@ def test_stage3_single_process_matches_stage0():
     assert all(u.full.untyped_storage().size() == 0 for u in z3.units)
 
 
-def _worker(rank: int, world: int, port: int, out: str) -> None:
+def _worker(rank: int, world: int, port: int, out: str, gb: int = 4) -> None:
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
-    eng = _engine(3, micro=4 // world)
+    eng = _engine(3, micro=gb // world)
     shard = sum(u.shard_numel for u in eng._z3.units)
     full = sum(u.padded for u in eng._z3.units)
     assert shard * world == full
-    losses = _train(eng, rank=rank, world=world)
+    losses = _train(eng, rank=rank, world=world, gb=gb)
     eng.save_checkpoint(out, tag="t")
     sd = eng.module_state_dict()
     # resume from the checkpoint in a fresh stage-3 engine and take one more step
-    eng2 = _engine(3, micro=4 // world)
+    eng2 = _engine(3, micro=gb // world)
     eng2.load_checkpoint(out, tag="t")
     sd2 = eng2.module_state_dict()
     for k in sd:
         assert torch.equal(sd[k], sd2[k]), k
-    more = _train(eng, steps=1, rank=rank, world=world)
-    more2 = _train(eng2, steps=1, rank=rank, world=world)
+    more = _train(eng, steps=1, rank=rank, world=world, gb=gb)
+    more2 = _train(eng2, steps=1, rank=rank, world=world, gb=gb)
     assert more2 == more
     sd_more = eng2.module_state_dict()
     if rank == 0:
@@ -114,22 +114,26 @@ def _worker(rank: int, world: int, port: int, out: str) -> None:
     torch.distributed.destroy_process_group()
 
 
-def test_stage3_two_ranks_matches_single_process(tmp_path):
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+@pytest.mark.parametrize("world", [2, 8])
+def test_stage3_multi_rank_matches_single_process(tmp_path, world):
+    """2 ranks, and the driver's 8-rank layout (per-unit shards padded to 8, 8
+    reduce-scatters / all-gathers per unit) against one process on the full batch."""
+    gb = 4 if world == 2 else 8
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), gb), nprocs=world, join=True)
     res = torch.load(tmp_path / "final.pt", weights_only=True)
-    ref = _engine(0)
-    _train(ref)
+    ref = _engine(0, micro=gb)
+    _train(ref, gb=gb)
     for k, v in ref.module_state_dict().items():
         torch.testing.assert_close(res["sd"][k], v, rtol=1e-4, atol=2e-5, msg=k)
     # resume the 2-rank checkpoint on ONE rank: the optimizer shards are re-partitioned (not
     # reset), so the next step equals the 2-rank resumed run's next step
-    eng1 = _engine(3, micro=4)
+    eng1 = _engine(3, micro=gb)
     eng1.load_checkpoint(tmp_path, tag="t")
-    _train(eng1, steps=1)  # full batch on one rank == the two half batches
+    _train(eng1, steps=1, gb=gb)  # full batch on one rank == the per-rank slices
     for k, v in res["sd_more"].items():
         torch.testing.assert_close(eng1.module_state_dict()[k], v, rtol=1e-4, atol=2e-5, msg=k)
     # consolidated checkpoint weights load into an unpartitioned engine
-    eng0 = _engine(0)
+    eng0 = _engine(0, micro=gb)
     eng0.load_checkpoint(tmp_path, tag="t", load_optimizer_states=False)
     for k, v in ref.module_state_dict().items():
         torch.testing.assert_close(eng0.module_state_dict()[k], v, rtol=1e-4, atol=2e-5, msg=k)

@@ -34,6 +34,7 @@ ROOT = os.path.dirname(HERE)
 sys.path.insert(0, ROOT)
 
 import yaml  # noqa: E402
+from typing import Dict, List, Tuple  # noqa: E402
 
 from determined_clone_amd.agent import Agent  # noqa: E402
 from determined_clone_amd.common.api import Session  # noqa: E402
@@ -105,6 +106,9 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--timeout", type=float, default=3000.0)
     ap.add_argument("--cpu", action="store_true", help="artificial CPU slots (plumbing check)")
+    ap.add_argument("--fake-gpus", type=int, default=0,
+                    help="CPU rehearsal of the 8-GPU layout: the agent reports N ROCm devices "
+                         "(--slots-per-gpu each) while the trials run on the CPU")
     ap.add_argument("--hip-graph", type=int, default=None, choices=(0, 1),
                     help="override the example's optimizations.hip_graph (A/B)")
     ap.add_argument("--trace", action="store_true",
@@ -115,14 +119,39 @@ def main() -> None:
     m = Master(os.path.join(tmp, "m.db"),
                checkpoint_storage={"type": "shared_fs", "host_path": os.path.join(tmp, "ckpt")})
     srv = MasterServer(m, "127.0.0.1", 0).start()
-    from determined_clone_amd.agent.agent import _detect_physical
+    from determined_clone_amd.agent import agent as agent_mod
 
-    phys = [d for d in _detect_physical() if d["type"] == "rocm"]
+    if args.fake_gpus:
+        fake = [{"id": i, "uuid": f"fake-gpu-{i}", "type": "rocm", "brand": "AMD", "gfx_target": "gfx950"}
+                for i in range(args.fake_gpus)]
+        agent_mod._detect_physical = lambda artificial_slots=0: [dict(d) for d in fake]
+    phys = [d for d in agent_mod._detect_physical() if d["type"] == "rocm"]
     n_gpus = min(args.gpus, len(phys)) if args.gpus and phys else len(phys)
     spg = args.slots_per_gpu or max(1, -(-args.max_concurrent // max(1, n_gpus)))
-    agent = Agent(m.master_url, "agent-0", artificial_slots=args.max_concurrent if args.cpu else 0,
+    use_cpu_slots = args.cpu and not args.fake_gpus
+    agent = Agent(m.master_url, "agent-0", artificial_slots=args.max_concurrent if use_cpu_slots else 0,
                   workdir=os.path.join(tmp, "agent"), slots_per_gpu=spg,
-                  max_gpus=n_gpus if not args.cpu else 0).start_background()
+                  max_gpus=n_gpus if not use_cpu_slots else 0)
+    # allocation timeline: (time, +1/-1, allocation, physical devices) -> concurrency overall / per GPU
+    timeline: List[Tuple[float, int, str, Tuple[int, ...]]] = []
+    devices_of: Dict[str, Tuple[int, ...]] = {}
+    orig_start, orig_event = agent._start, agent._event
+
+    def _start(spec):
+        from determined_clone_amd.agent import runtime as rt
+
+        devs = tuple(sorted({int(d.get("device_index", d["id"])) for d in rt.assigned_devices(spec, agent.devices)}))
+        devices_of[spec["allocation_id"]] = devs
+        timeline.append((time.time(), 1, spec["allocation_id"], devs))
+        return orig_start(spec)
+
+    def _event(alloc, state, exit_code=None):
+        if state == "TERMINATED" and alloc in devices_of:
+            timeline.append((time.time(), -1, alloc, devices_of.pop(alloc)))
+        return orig_event(alloc, state, exit_code)
+
+    agent._start, agent._event = _start, _event
+    agent.start_background()
     s = Session(m.master_url)
     s.token = s.post("/api/v1/auth/login", {"username": "admin", "password": ""})["token"]
     try:
@@ -154,6 +183,13 @@ def main() -> None:
         vals = sorted(t["best_validation"] for t in done if t.get("best_validation") is not None)
         best = vals[0] if vals else None
         startup = _startup_share(m, s, trials)
+        conc, per_dev, peak, peak_dev = 0, {}, 0, 0
+        for _t, d, _a, devs in sorted(timeline, key=lambda e: (e[0], e[1])):
+            conc += d
+            peak = max(peak, conc)
+            for g in devs:
+                per_dev[g] = per_dev.get(g, 0) + d
+                peak_dev = max(peak_dev, per_dev[g])
         if args.trace:
             _print_trace(s, trials)
         if state != "COMPLETED":
@@ -171,6 +207,8 @@ def main() -> None:
             if vals else None,
             "startup_share": startup["share"], "startup_mean_s": startup["mean_s"],
             "allocations": startup["allocations"],
+            "max_concurrent_trials": peak, "max_trials_per_gpu": peak_dev,
+            "gpus_used": len({g for e in timeline for g in e[3]}),
             "dtype": "bf16" if not args.cpu else "fp32", "data": "synthetic CIFAR-10-shaped",
             "config": {"model": "cifar10_cnn", "searcher": "adaptive_asha", "max_trials": args.max_trials,
                        "max_concurrent_trials": args.max_concurrent, "slots_per_gpu": spg,
