@@ -312,8 +312,8 @@ def test_conv_igemm_forward_stats_and_dgrad(shape):
 @pytest.mark.parametrize("ck", [(64, 64), (128, 256), (256, 128)])
 def test_conv_igemm_asymmetric_weight_orientation(ck):
     """A weight that is non-zero at ONE tap and ONE (k, c) pair: catches transposed taps /
-    swapped channel maps that random data can hide (4-wave kernel at 64 x 64, the 8-wave big-tile
-    kernel shapes at K = 256 / 128)."""
+    swapped channel maps that random data can hide (the 256 x 64 tile at K = 64, 128 x 128 tiles
+    with several channel tiles at K = 256 / 128)."""
     C = _ext.load()
     c, k = ck
     x, w = _igemm_inputs(2, c, 9, k)
