@@ -8,7 +8,8 @@ every line of those files that calls an in-place tensor collective (``reduce_sca
 ``all_gather_into_tensor``) or uses ``ReduceOp.AVG``, whether some rank executed it -- the lines
 the 8-GPU RCCL run takes.
 
-Usage: python tools/collective_coverage.py [> profiles/round5_collective_coverage.txt]
+Usage: python tools/collective_coverage.py [--world 8] [> profiles/round6_collective_coverage_w8.txt]
+(``--world 8``: every worker at the driver's 8-rank layout.)
 """
 import glob
 import json
@@ -64,23 +65,29 @@ def _free_port() -> int:
 
 
 def main() -> None:
+    import argparse
+
     import torch.multiprocessing as mp
 
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=2, choices=(2, 4, 8))
+    w = ap.parse_args().world
+    gb = 4 if w == 2 else 8  # global (micro) batch the per-rank slices are cut from
     runs = [
-        ("tests.test_zero._worker", lambda d: (2, _free_port(), 1, "adam", 0.0, 64.0, d, False)),
-        ("tests.test_zero._worker", lambda d: (2, _free_port(), 2, "adamw", 0.05, 0.002, d, False)),
-        ("tests.test_zero._worker", lambda d: (2, _free_port(), 2, "sgd", 0.0, 0.001, d, True)),
-        ("tests.test_zero3._worker", lambda d: (2, _free_port(), d)),
-        ("tests.test_distributed._worker_sync", lambda d: (2, _free_port(), True, 1, d)),
-        ("tests.test_distributed._worker_sync", lambda d: (2, _free_port(), False, 2, d)),
-        ("tests.test_deepspeed_trial._engine_worker", lambda d: (2, _free_port(), 2, d, True)),
-        ("tests.test_deepspeed_trial._engine_worker", lambda d: (2, _free_port(), 1, d, False)),
+        ("tests.test_zero._worker", lambda d: (w, _free_port(), 1, "adam", 0.0, 64.0, d, False)),
+        ("tests.test_zero._worker", lambda d: (w, _free_port(), 2, "adamw", 0.05, 0.002, d, False)),
+        ("tests.test_zero._worker", lambda d: (w, _free_port(), 2, "sgd", 0.0, 0.001, d, True)),
+        ("tests.test_zero3._worker", lambda d: (w, _free_port(), d, gb)),
+        ("tests.test_distributed._worker_sync", lambda d: (w, _free_port(), True, 1, d)),
+        ("tests.test_distributed._worker_sync", lambda d: (w, _free_port(), False, 2, d)),
+        ("tests.test_deepspeed_trial._engine_worker", lambda d: (w, _free_port(), 2, d, True, gb)),
+        ("tests.test_deepspeed_trial._engine_worker", lambda d: (w, _free_port(), 1, d, False, gb)),
     ]
     cov_dir = tempfile.mkdtemp(prefix="collcov-")
     for fn_path, mk in runs:
         with tempfile.TemporaryDirectory() as d:
-            mp.spawn(_traced, args=(fn_path, mk(d), cov_dir), nprocs=2, join=True)
-        print(f"ran {fn_path} x2 ranks", flush=True)
+            mp.spawn(_traced, args=(fn_path, mk(d), cov_dir), nprocs=w, join=True)
+        print(f"ran {fn_path} x{w} ranks", flush=True)
     executed = set()
     for f in glob.glob(os.path.join(cov_dir, "*.json")):
         executed.update((a, b) for a, b in json.load(open(f)))
