@@ -84,14 +84,34 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rsrc, uint32_t vof
       rsrc, (__attribute__((address_space(3))) void*)(lds_dst), 16, voff, soff, 0, 0);
 }
 
-// STATS: the epilogue also reduces (sum y, sum y^2) of the bf16 outputs -- the following
-// BatchNorm's statistics -- into partial[mt][2][K] (batchnorm.hip's layout). (The backward form,
-// BatchNorm backward statistics in the data-gradient epilogue, measured -0.4 % on the step and was
-// removed: profiles/round5_dgrad_bn_stats_epilogue_ab.txt.)
-template <int BM, int BN, int WM, int WN, int NSTAGE, bool STATS>
+// GELU(tanh) derivative of transformer.hip's bias_gelu (same formula, so the fused and the
+// separate backward agree): d/dx [x s(u)] = s + x s (1 - s) 2 u',  s = sigmoid(2u).
+__device__ __forceinline__ float gelu_tanh_grad_f(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float u = k0 * fmaf(k1 * x2, x, x);
+  const float s = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
+  return fmaf(x * s * (1.f - s), 2.f * k0 * fmaf(3.f * k1, x2, 1.f), s);
+}
+
+// Epilogue modes (EPI):
+//   kEpiNone  -- store y;
+//   kEpiStats -- also reduce (sum y, sum y^2) of the bf16 outputs -- the following BatchNorm's
+//                statistics -- into partial[mt][2][K] (batchnorm.hip's layout). (The backward form,
+//                BatchNorm backward statistics in the data-gradient epilogue, measured -0.4 % on the
+//                step and was removed: profiles/round5_dgrad_bn_stats_epilogue_ab.txt.)
+//   kEpiDGelu -- the kernel runs as the GEMM dH = dY W2 of a transformer MLP's output projection
+//                (R = S = 1, one pixel per token) and stores dZ = dH * gelu'(z + bias) instead of dH
+//                (z [M][K] bf16 = the saved pre-activation, bias fp32 [K]); partial[mt][0][K]
+//                receives the column sums of dZ (the fc1 bias gradient). This deletes the separate
+//                bias-GELU backward pass (read dH + z, write dZ) and dH's round trip through HBM.
+constexpr int kEpiNone = 0, kEpiStats = 1, kEpiDGelu = 2;
+template <int BM, int BN, int WM, int WN, int NSTAGE, int EPI>
 __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-    float* __restrict__ partial, ConvGeom g) {
+    float* __restrict__ partial, ConvGeom g, const uint16_t* __restrict__ ez,
+    const float* __restrict__ ebias) {
+  constexpr bool STATS = EPI == kEpiStats;
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM / WM, TN = BN / WN;  // wave tile: pixels x channels
   constexpr int FM = TM / 32, FN = TN / 32;
@@ -273,13 +293,33 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
   constexpr int CPR = BN / 8;          // 16-B chunks per output row
   constexpr int RPP = kThreads / CPR;  // rows per pass
   const int cc = tid % CPR, rr = tid / CPR;
-  float s8[8], q8[8];
+  float s8[8], q8[8], eb[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { s8[k] = 0.f; q8[k] = 0.f; }
+  for (int k = 0; k < 8; ++k) {
+    s8[k] = 0.f;
+    q8[k] = 0.f;
+    eb[k] = EPI == kEpiDGelu ? ebias[n0 + cc * 8 + k] : 0.f;
+  }
   for (int row = rr; row < BM; row += RPP) {
     if (m0 + row >= g.M) break;
     const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CS + cc * 8);
     const int64_t off = static_cast<int64_t>(m0 + row) * g.K + n0 + cc * 8;
+    if constexpr (EPI == kEpiDGelu) {
+      const uint4 zv = ldnt16(ez + off);  // the pre-activation, read once
+      const float dh[8] = {bf16_lo(v.x), bf16_hi(v.x), bf16_lo(v.y), bf16_hi(v.y),
+                           bf16_lo(v.z), bf16_hi(v.z), bf16_lo(v.w), bf16_hi(v.w)};
+      const float zf[8] = {bf16_lo(zv.x), bf16_hi(zv.x), bf16_lo(zv.y), bf16_hi(zv.y),
+                           bf16_lo(zv.z), bf16_hi(zv.z), bf16_lo(zv.w), bf16_hi(zv.w)};
+      float dz[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        dz[k] = dh[k] * gelu_tanh_grad_f(zf[k] + eb[k]);
+        s8[k] += dz[k];
+      }
+      *reinterpret_cast<uint4*>(y + off) = make_uint4(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]),
+                                                      pack_bf16x2(dz[4], dz[5]), pack_bf16x2(dz[6], dz[7]));
+      continue;
+    }
     *reinterpret_cast<uint4*>(y + off) = v;
     if constexpr (STATS) {
       const float f[8] = {bf16_lo(v.x), bf16_hi(v.x), bf16_lo(v.y), bf16_hi(v.y),
@@ -288,8 +328,9 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
       for (int k = 0; k < 8; ++k) { s8[k] += f[k]; q8[k] = fmaf(f[k], f[k], q8[k]); }
     }
   }
-  if constexpr (STATS) {
-    // partial[mt][0][k] = sum, partial[mt][1][k] = sum of squares (batchnorm.hip layout)
+  if constexpr (EPI != kEpiNone) {
+    // partial[mt][0][k] = sum, partial[mt][1][k] = sum of squares (batchnorm.hip layout; the
+    // dGELU mode fills [0] only)
     __syncthreads();
     float* red = reinterpret_cast<float*>(lds);  // [RPP][CPR * 16]
     constexpr int width = CPR * 16;
@@ -402,51 +443,74 @@ __global__ __launch_bounds__(kThreads, 2) void conv_wgrad_kernel(
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(x), 0, static_cast<int>(static_cast<uint32_t>(g.N * g.H * g.W) * g.C * 2u),
       0x00020000);
-  int xb_n[IB], xb_p[IB], xb_q[IB];
-  uint32_t xb_c[IB];  // byte offset of this lane's channel chunk within a pixel row
+  // Loader state, all carried incrementally (round 6: the per-stage address math -- three 32-bit
+  // multiplies, a 64-bit multiply-add and a data-dependent carry loop per x row -- was ~150 VALU
+  // per 16 MFMAs in the ISA, more than the matrix work):
+  //  * dy rows: byte offset of (row m, channel k0 + chunk) advanced by kWM * K * 2 per stage;
+  //  * x rows: the output pixel's (p, q), its input coordinates (ih, iw) at this workgroup's tap and
+  //    the byte offset of x[n][ih][iw][c0 + chunk], advanced by kWM pixels per stage with at most one
+  //    q-wrap and one p-wrap (kWM % Q < Q and (kWM / Q) % P + 1 <= P); the offset may leave the
+  //    tensor while the tap is a padding tap (unsigned wrap-around), it is only used when valid.
+  uint32_t dy_vo[IA];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    const int j = wv + 4 * i;
+    const int row = j * (64 / LA) + lane / LA;
+    const int chunk = (lane % LA) ^ wswz<RA>(row);
+    dy_vo[i] = (static_cast<uint32_t>(mb + row) * g.K + static_cast<uint32_t>(k0 + chunk * 8)) * 2u;
+  }
+  const uint32_t dy_step = static_cast<uint32_t>(kWM) * g.K * 2u;
+  const int C2 = g.C * 2;
+  const int st = g.stride;
+  int xq[IB], xp[IB], xih[IB], xiw[IB];
+  uint32_t xvo[IB];
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
     const int j = wv + 4 * i;
     const int row = j * (64 / LB) + lane / LB;
     const int m = mb + row;
-    xb_n[i] = fdiv(m, PQ, inv_pq);
-    const int rem = m - xb_n[i] * PQ;
-    xb_p[i] = fdiv(rem, g.Q, inv_q);
-    xb_q[i] = rem - xb_p[i] * g.Q;
-    xb_c[i] = static_cast<uint32_t>((c0 + ((lane % LB) ^ wswz<RB>(row)) * 8) * 2);
+    const int n = fdiv(m, PQ, inv_pq);
+    const int rem = m - n * PQ;
+    xp[i] = fdiv(rem, g.Q, inv_q);
+    xq[i] = rem - xp[i] * g.Q;
+    xih[i] = xp[i] * st - g.pad + r;
+    xiw[i] = xq[i] * st - g.pad + s;
+    xvo[i] = static_cast<uint32_t>((n * g.H + xih[i]) * g.W + xiw[i]) * static_cast<uint32_t>(C2) +
+             static_cast<uint32_t>((c0 + ((lane % LB) ^ wswz<RB>(row)) * 8) * 2);
   }
+  // per-stage deltas (uniform): kWM pixels = dn images + dp rows + dq columns
   const int dq = kWM % g.Q, dp = (kWM / g.Q) % g.P, dn = kWM / PQ;
+  const uint32_t a_q = static_cast<uint32_t>(st * C2), a_p = static_cast<uint32_t>(st * g.W * C2),
+                 a_n = static_cast<uint32_t>(g.H * g.W * C2);
+  const uint32_t d_step = dn * a_n + dp * a_p + dq * a_q;
+  const uint32_t d_qwrap = a_p - static_cast<uint32_t>(g.Q) * a_q;  // q -= Q, p += 1
+  const uint32_t d_pwrap = a_n - static_cast<uint32_t>(g.P) * a_p;  // p -= P, n += 1
 
   auto stage = [&](int m_base, int buf) {
     uint16_t* As = lds + buf * STAGE;
     uint16_t* Bs = As + kWM * BKO;
+    const int lim = me - m_base;  // rows of this stage inside the split
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
       const int j = wv + 4 * i;                  // instruction index within the tile
       const int row = j * (64 / LA) + lane / LA;
-      const int chunk = (lane % LA) ^ wswz<RA>(row);
-      const int m = m_base + row;
-      const uint32_t vo =
-          m < me ? (static_cast<uint32_t>(m) * g.K + static_cast<uint32_t>(k0 + chunk * 8)) * 2u : kOOB;
-      blds16(dyr, vo, 0, As + j * 512);
+      blds16(dyr, row < lim ? dy_vo[i] : kOOB, 0, As + j * 512);
+      dy_vo[i] += dy_step;
     }
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       const int j = wv + 4 * i;
       const int row = j * (64 / LB) + lane / LB;
-      const int m = m_base + row;
-      const int ih = xb_p[i] * g.stride - g.pad + r, iw = xb_q[i] * g.stride - g.pad + s;
-      const bool ok = m < me && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
-                      static_cast<unsigned>(iw) < static_cast<unsigned>(g.W);
-      const uint32_t vo =
-          ok ? static_cast<uint32_t>((xb_n[i] * g.H + ih) * g.W + iw) * static_cast<uint32_t>(g.C) * 2u + xb_c[i]
-             : kOOB;
-      blds16(xr, vo, 0, Bs + j * 512);
+      const bool ok = row < lim && static_cast<unsigned>(xih[i]) < static_cast<unsigned>(g.H) &&
+                      static_cast<unsigned>(xiw[i]) < static_cast<unsigned>(g.W);
+      blds16(xr, ok ? xvo[i] : kOOB, 0, Bs + j * 512);
       // advance this row by kWM pixels
-      int q = xb_q[i] + dq, p = xb_p[i] + dp, n = xb_n[i] + dn;
-      if (q >= g.Q) { q -= g.Q; ++p; }
-      while (p >= g.P) { p -= g.P; ++n; }
-      xb_q[i] = q; xb_p[i] = p; xb_n[i] = n;
+      int q = xq[i] + dq, p = xp[i] + dp;
+      int ih = xih[i] + dp * st, iw = xiw[i] + dq * st;
+      uint32_t vo = xvo[i] + d_step;
+      if (q >= g.Q) { q -= g.Q; iw -= g.Q * st; ++p; ih += st; vo += d_qwrap; }
+      if (p >= g.P) { p -= g.P; ih -= g.P * st; vo += d_pwrap; }
+      xq[i] = q; xp[i] = p; xih[i] = ih; xiw[i] = iw; xvo[i] = vo;
     }
   };
 
@@ -610,16 +674,16 @@ Cfg pick(const ConvGeom& g) {
 
 // LDS ring depth 2: two workgroups per CU fit for tiles up to 80 KB of stages, which measured
 // faster than a 3-deep ring at one workgroup per CU (profiles/round4_igemm_v2_stages.txt).
-template <int BM, int BN, bool STATS>
+template <int BM, int BN, int EPI>
 void launch_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                hipStream_t st) {
+                hipStream_t st, const void* ez, const float* ebias) {
   constexpr int NSTAGE = 2;
   constexpr int WM = BN >= 128 ? 2 : 4, WN = 4 / WM;
   constexpr size_t stage = static_cast<size_t>(BM + BN) * kBK * 2 * NSTAGE;
   constexpr size_t epi = static_cast<size_t>(BM) * (BN + 8) * 2;
   constexpr size_t lds = stage > epi ? stage : epi;
   const int grid = static_cast<int>((static_cast<int64_t>(g.M) + BM - 1) / BM * (g.K / BN));
-  auto kern = conv_fwd_kernel<BM, BN, WM, WN, NSTAGE, STATS>;
+  auto kern = conv_fwd_kernel<BM, BN, WM, WN, NSTAGE, EPI>;
   static const bool attr = [&] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
@@ -628,15 +692,15 @@ void launch_fwd(const void* x, const void* w, void* y, float* partial, const Con
   (void)attr;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, st,
                      static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w),
-                     static_cast<uint16_t*>(y), partial, g);
+                     static_cast<uint16_t*>(y), partial, g, static_cast<const uint16_t*>(ez), ebias);
 }
 
-template <bool STATS>
+template <int EPI>
 void fwd_dispatch(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                  hipStream_t st) {
+                  hipStream_t st, const void* ez = nullptr, const float* ebias = nullptr) {
   const Cfg c = pick(g);
-  if (c.bn == 128) launch_fwd<128, 128, STATS>(x, w, y, partial, g, st);
-  else launch_fwd<256, 64, STATS>(x, w, y, partial, g, st);
+  if (c.bn == 128) launch_fwd<128, 128, EPI>(x, w, y, partial, g, st, ez, ebias);
+  else launch_fwd<256, 64, EPI>(x, w, y, partial, g, st, ez, ebias);
 }
 
 }  // namespace
@@ -649,8 +713,13 @@ int conv_igemm_row_blocks(const ConvGeom& g) {
 
 void conv_igemm_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
                     hipStream_t st) {
-  if (partial) fwd_dispatch<true>(x, w, y, partial, g, st);
-  else fwd_dispatch<false>(x, w, y, nullptr, g, st);
+  if (partial) fwd_dispatch<kEpiStats>(x, w, y, partial, g, st);
+  else fwd_dispatch<kEpiNone>(x, w, y, nullptr, g, st);
+}
+
+void conv_igemm_fwd_dgelu(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
+                          const void* z, const float* bias, hipStream_t st) {
+  fwd_dispatch<kEpiDGelu>(x, w, y, partial, g, st, z, bias);
 }
 
 int64_t conv_igemm_wgrad_ws_floats(const ConvGeom& g) {
