@@ -308,9 +308,13 @@ class _GeluLinear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = _weight_grad(w_param, dy2, h.reshape(-1, h.shape[-1]))
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[3]:
-            dz, partial = _ext.load().linear_dgelu(dy2, weight, z, ctx.fc_bias)
+            if weight.shape[1] % 256 == 0:  # the 256 x 256 tile GEMM (csrc/gemm.hip)
+                dz, partial = _ext.load().gemm_nt_dgelu(dy2, weight.t().contiguous(), z, ctx.fc_bias)
+            else:  # 128-column tiles (the implicit-GEMM kernel of csrc/conv_igemm.hip)
+                dz, partial = _ext.load().linear_dgelu(dy2, weight, z, ctx.fc_bias)
+                partial = partial[:, 0]
             if ctx.needs_input_grad[3]:
-                col = partial[:, 0].sum(0)
+                col = partial.sum(0)
                 acc = _grad.target(ctx.fc_bias)
                 if acc is not None:
                     acc.add_(col)
