@@ -126,7 +126,8 @@ class MLP(nn.Module):
         self.proj = nn.Linear(cfg.mlp_ratio * E, E)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return T.gelu_linear(T.linear(x, self.fc.weight), self.fc.bias, self.proj.weight, self.proj.bias)
+        h = T.bias_gelu(T.linear(x, self.fc.weight), self.fc.bias)
+        return T.linear(h, self.proj.weight, self.proj.bias)
 
 
 class Block(nn.Module):

@@ -582,7 +582,6 @@ void register_transformer_ops(pybind11::module& m);
 void register_conv_ops(pybind11::module& m);
 void register_groupnorm_ops(pybind11::module& m);
 void register_lt_ops(pybind11::module& m);
-void register_gemm_ops(pybind11::module& m);
 
 extern "C" const char dca_source_hash[];  // ops/build.py: sha256 of the csrc/ tree
 
@@ -628,5 +627,4 @@ PYBIND11_MODULE(_C, m) {
   register_conv_ops(m);
   register_groupnorm_ops(m);
   register_lt_ops(m);
-  register_gemm_ops(m);
 }

@@ -15,11 +15,6 @@ int conv_igemm_row_blocks(const ConvGeom& g);
 // partial (optional): [row blocks][2][K] fp32 (sum y, sum y^2) of the bf16 output.
 void conv_igemm_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
                     hipStream_t st);
-// The same GEMM (R = S = 1) storing dZ = y * gelu'(z + bias) instead of y, with the column sums
-// of dZ in partial[row blocks][0][K] (transformer MLP backward: dH = dY W2 fused with the GELU
-// backward and the fc1 bias gradient). z [M][K] bf16, bias fp32 [K].
-void conv_igemm_fwd_dgelu(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                          const void* z, const float* bias, hipStream_t st);
 // Weight gradient dW (bf16 or fp32; accumulate adds into it) from dy [M][K] and x, stored
 // [K][R][S][C] (channels_last) or, with dw_kcrs, [K][C][R][S]; ws: conv_igemm_wgrad_ws_floats(g)
 // fp32 scratch.

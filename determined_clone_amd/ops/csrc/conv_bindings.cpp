@@ -131,46 +131,6 @@ Tensor conv_igemm_wgrad(const Tensor& dy_in, const Tensor& x, const Tensor& w, i
   return out;
 }
 
-// GPT-2 MLP backward through the projection and the GELU in one GEMM:
-//   dz = (dy @ w2) * gelu'(z + bias)      dy [T, E], w2 [E, F] (nn.Linear weight), z [T, F]
-// with the bias-gradient column sums of dz in `partial` [blocks, 2, F] (row 0 of each block).
-// It is the implicit-GEMM forward kernel on a 1x1 "image" (N = T rows) with the dGELU epilogue.
-std::vector<Tensor> linear_dgelu(const Tensor& dy_in, const Tensor& w2, const Tensor& z_in,
-                                 const Tensor& bias) {
-  const Tensor dy = dy_in.contiguous();
-  const Tensor z = z_in.contiguous();
-  const c10::DeviceGuard dg(dy.device());
-  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && z.scalar_type() == at::kBFloat16 &&
-                  w2.scalar_type() == at::kBFloat16 && w2.dim() == 2 && w2.is_contiguous(),
-              "linear_dgelu: bf16 GPU tensors, contiguous [E, F] weight");
-  const int64_t E = w2.size(0), F = w2.size(1);
-  TORCH_CHECK(E % 64 == 0 && F % 64 == 0, "linear_dgelu: both weight dims must be multiples of 64");
-  TORCH_CHECK(dy.size(-1) == E && z.size(-1) == F && bias.numel() == F && bias.is_cuda(),
-              "linear_dgelu: dy [..., E], z [..., F], bias [F]");
-  const int64_t T = dy.numel() / E;
-  TORCH_CHECK(z.numel() / F == T, "linear_dgelu: dy and z row counts differ");
-  TORCH_CHECK(T * F < (int64_t{1} << 30) && T * E < (int64_t{1} << 30),
-              "linear_dgelu: tensors too large for 32-bit byte offsets");
-  Tensor wt = torch::empty({F, E}, w2.options());
-  dca::conv_flip_transpose(w2.data_ptr(), wt.data_ptr(), static_cast<int>(E), static_cast<int>(F), 1,
-                           stream());
-  const Tensor b = bias.to(at::kFloat).contiguous();
-  dca::ConvGeom g;
-  g.N = static_cast<int>(T);
-  g.C = static_cast<int>(E);
-  g.K = static_cast<int>(F);
-  g.H = g.W = g.P = g.Q = g.R = g.S = 1;
-  g.stride = 1;
-  g.pad = 0;
-  g.M = static_cast<int>(T);
-  std::vector<int64_t> shape(z.sizes().begin(), z.sizes().end());
-  Tensor dz = torch::empty(shape, z.options());
-  Tensor partial = torch::empty({dca::conv_igemm_row_blocks(g), 2, F}, dy.options().dtype(at::kFloat));
-  dca::conv_igemm_fwd_dgelu(dy.data_ptr(), wt.data_ptr(), dz.data_ptr(), partial.data_ptr<float>(), g,
-                            z.data_ptr(), b.data_ptr<float>(), stream());
-  return {dz, partial};
-}
-
 }  // namespace
 
 // dx (channels_last [N, C, H, W]) += small (channels_last [N, C, Ho, Wo]) at the stride-s
@@ -219,8 +179,6 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("acc") = pybind11::none());
   m.def("conv_igemm_fwd", &conv_igemm_fwd, pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stats"));
-  m.def("linear_dgelu", &linear_dgelu, pybind11::arg("dy"), pybind11::arg("w2"), pybind11::arg("z"),
-        pybind11::arg("bias"));
   m.def("conv_igemm_dgrad", &conv_igemm_dgrad, pybind11::arg("dy"), pybind11::arg("w"),
         pybind11::arg("pad"));
 }

@@ -84,33 +84,17 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t rsrc, uint32_t vof
       rsrc, (__attribute__((address_space(3))) void*)(lds_dst), 16, voff, soff, 0, 0);
 }
 
-// GELU(tanh) derivative of transformer.hip's bias_gelu (same formula, so the fused and the
-// separate backward agree): d/dx [x s(u)] = s + x s (1 - s) 2 u',  s = sigmoid(2u).
-__device__ __forceinline__ float gelu_tanh_grad_f(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float x2 = x * x;
-  const float u = k0 * fmaf(k1 * x2, x, x);
-  const float s = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
-  return fmaf(x * s * (1.f - s), 2.f * k0 * fmaf(3.f * k1, x2, 1.f), s);
-}
-
 // Epilogue modes (EPI):
 //   kEpiNone  -- store y;
 //   kEpiStats -- also reduce (sum y, sum y^2) of the bf16 outputs -- the following BatchNorm's
 //                statistics -- into partial[mt][2][K] (batchnorm.hip's layout). (The backward form,
 //                BatchNorm backward statistics in the data-gradient epilogue, measured -0.4 % on the
 //                step and was removed: profiles/round5_dgrad_bn_stats_epilogue_ab.txt.)
-//   kEpiDGelu -- the kernel runs as the GEMM dH = dY W2 of a transformer MLP's output projection
-//                (R = S = 1, one pixel per token) and stores dZ = dH * gelu'(z + bias) instead of dH
-//                (z [M][K] bf16 = the saved pre-activation, bias fp32 [K]); partial[mt][0][K]
-//                receives the column sums of dZ (the fc1 bias gradient). This deletes the separate
-//                bias-GELU backward pass (read dH + z, write dZ) and dH's round trip through HBM.
-constexpr int kEpiNone = 0, kEpiStats = 1, kEpiDGelu = 2;
+constexpr int kEpiNone = 0, kEpiStats = 1;
 template <int BM, int BN, int WM, int WN, int NSTAGE, int EPI>
 __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-    float* __restrict__ partial, ConvGeom g, const uint16_t* __restrict__ ez,
-    const float* __restrict__ ebias) {
+    float* __restrict__ partial, ConvGeom g) {
   constexpr bool STATS = EPI == kEpiStats;
   static_assert(WM * WN == 4, "4 waves");
   constexpr int TM = BM / WM, TN = BN / WN;  // wave tile: pixels x channels
@@ -293,33 +277,16 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
   constexpr int CPR = BN / 8;          // 16-B chunks per output row
   constexpr int RPP = kThreads / CPR;  // rows per pass
   const int cc = tid % CPR, rr = tid / CPR;
-  float s8[8], q8[8], eb[8];
+  float s8[8], q8[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     s8[k] = 0.f;
     q8[k] = 0.f;
-    eb[k] = EPI == kEpiDGelu ? ebias[n0 + cc * 8 + k] : 0.f;
   }
   for (int row = rr; row < BM; row += RPP) {
     if (m0 + row >= g.M) break;
     const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CS + cc * 8);
     const int64_t off = static_cast<int64_t>(m0 + row) * g.K + n0 + cc * 8;
-    if constexpr (EPI == kEpiDGelu) {
-      const uint4 zv = ldnt16(ez + off);  // the pre-activation, read once
-      const float dh[8] = {bf16_lo(v.x), bf16_hi(v.x), bf16_lo(v.y), bf16_hi(v.y),
-                           bf16_lo(v.z), bf16_hi(v.z), bf16_lo(v.w), bf16_hi(v.w)};
-      const float zf[8] = {bf16_lo(zv.x), bf16_hi(zv.x), bf16_lo(zv.y), bf16_hi(zv.y),
-                           bf16_lo(zv.z), bf16_hi(zv.z), bf16_lo(zv.w), bf16_hi(zv.w)};
-      float dz[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        dz[k] = dh[k] * gelu_tanh_grad_f(zf[k] + eb[k]);
-        s8[k] += dz[k];
-      }
-      *reinterpret_cast<uint4*>(y + off) = make_uint4(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]),
-                                                      pack_bf16x2(dz[4], dz[5]), pack_bf16x2(dz[6], dz[7]));
-      continue;
-    }
     *reinterpret_cast<uint4*>(y + off) = v;
     if constexpr (STATS) {
       const float f[8] = {bf16_lo(v.x), bf16_hi(v.x), bf16_lo(v.y), bf16_hi(v.y),
@@ -329,8 +296,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
     }
   }
   if constexpr (EPI != kEpiNone) {
-    // partial[mt][0][k] = sum, partial[mt][1][k] = sum of squares (batchnorm.hip layout; the
-    // dGELU mode fills [0] only)
+    // partial[mt][0][k] = sum, partial[mt][1][k] = sum of squares (batchnorm.hip layout)
     __syncthreads();
     float* red = reinterpret_cast<float*>(lds);  // [RPP][CPR * 16]
     constexpr int width = CPR * 16;
@@ -676,7 +642,7 @@ Cfg pick(const ConvGeom& g) {
 // faster than a 3-deep ring at one workgroup per CU (profiles/round4_igemm_v2_stages.txt).
 template <int BM, int BN, int EPI>
 void launch_fwd(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                hipStream_t st, const void* ez, const float* ebias) {
+                hipStream_t st) {
   constexpr int NSTAGE = 2;
   constexpr int WM = BN >= 128 ? 2 : 4, WN = 4 / WM;
   constexpr size_t stage = static_cast<size_t>(BM + BN) * kBK * 2 * NSTAGE;
@@ -692,15 +658,15 @@ void launch_fwd(const void* x, const void* w, void* y, float* partial, const Con
   (void)attr;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, st,
                      static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w),
-                     static_cast<uint16_t*>(y), partial, g, static_cast<const uint16_t*>(ez), ebias);
+                     static_cast<uint16_t*>(y), partial, g);
 }
 
 template <int EPI>
 void fwd_dispatch(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                  hipStream_t st, const void* ez = nullptr, const float* ebias = nullptr) {
+                  hipStream_t st) {
   const Cfg c = pick(g);
-  if (c.bn == 128) launch_fwd<128, 128, EPI>(x, w, y, partial, g, st, ez, ebias);
-  else launch_fwd<256, 64, EPI>(x, w, y, partial, g, st, ez, ebias);
+  if (c.bn == 128) launch_fwd<128, 128, EPI>(x, w, y, partial, g, st);
+  else launch_fwd<256, 64, EPI>(x, w, y, partial, g, st);
 }
 
 }  // namespace
@@ -715,11 +681,6 @@ void conv_igemm_fwd(const void* x, const void* w, void* y, float* partial, const
                     hipStream_t st) {
   if (partial) fwd_dispatch<kEpiStats>(x, w, y, partial, g, st);
   else fwd_dispatch<kEpiNone>(x, w, y, nullptr, g, st);
-}
-
-void conv_igemm_fwd_dgelu(const void* x, const void* w, void* y, float* partial, const ConvGeom& g,
-                          const void* z, const float* bias, hipStream_t st) {
-  fwd_dispatch<kEpiDGelu>(x, w, y, partial, g, st, z, bias);
 }
 
 int64_t conv_igemm_wgrad_ws_floats(const ConvGeom& g) {

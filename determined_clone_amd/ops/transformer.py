@@ -118,8 +118,7 @@ class _LayerNorm(torch.autograd.Function):
         # projection) whose dy is exactly this LayerNorm's dx -- its bias gradient is reduced in
         # the LN backward pass instead of by a separate column sum (``_Linear.backward``)
         ctx.bias_node = residual.grad_fn if (FUSE_LN_BIAS_GRAD and res is not None and res is residual and
-                                             type(residual.grad_fn).__name__ in ("_LinearBackward",
-                                                                         "_GeluLinearBackward")) else None
+                                             type(residual.grad_fn).__name__ == "_LinearBackward") else None
         if res is not None:
             return y, s
         return y
@@ -279,74 +278,6 @@ class _Linear(torch.autograd.Function):
         if b_param is not None and ctx.needs_input_grad[2]:
             db = _bias_grad(b_param, dy2)
         return dx, dw, db
-
-
-class _GeluLinear(torch.autograd.Function):
-    """``y = gelu_tanh(z + fc_bias) @ w.T + b``: a transformer MLP's activation and output
-    projection, whose backward runs the data gradient through the projection *and* the GELU as
-    one MFMA GEMM (``linear_dgelu``: the implicit-GEMM kernel of conv_igemm.hip with a dGELU
-    epilogue that reads z once, stores dZ = (dY W) * gelu'(z + fc_bias) and reduces the fc bias
-    gradient's per-tile column sums). dH never goes to HBM and the separate bias-GELU backward
-    pass is gone. Inputs are ordered like ``_Linear``'s (x, weight, bias) so the consuming
-    LayerNorm's fused bias-gradient hand-off (``_LayerNorm.backward``) applies unchanged."""
-
-    @staticmethod
-    def forward(ctx, z, weight, bias, fc_bias):
-        z = z.contiguous()
-        h = _ext.load().bias_gelu(z, _bias_arg(fc_bias))
-        ctx.save_for_backward(z, h, weight)
-        ctx.params = (weight, bias)
-        ctx.fc_bias = fc_bias
-        return F.linear(h, weight, bias)
-
-    @staticmethod
-    def backward(ctx, dy):
-        z, h, weight = ctx.saved_tensors
-        w_param, b_param = ctx.params
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        dz = dw = db = dfb = None
-        if ctx.needs_input_grad[1]:
-            dw = _weight_grad(w_param, dy2, h.reshape(-1, h.shape[-1]))
-        if ctx.needs_input_grad[0] or ctx.needs_input_grad[3]:
-            if weight.shape[1] % 256 == 0:  # the 256 x 256 tile GEMM (csrc/gemm.hip)
-                dz, partial = _ext.load().gemm_nt_dgelu(dy2, weight.t().contiguous(), z, ctx.fc_bias)
-            else:  # 128-column tiles (the implicit-GEMM kernel of csrc/conv_igemm.hip)
-                dz, partial = _ext.load().linear_dgelu(dy2, weight, z, ctx.fc_bias)
-                partial = partial[:, 0]
-            if ctx.needs_input_grad[3]:
-                col = partial.sum(0)
-                acc = _grad.target(ctx.fc_bias)
-                if acc is not None:
-                    acc.add_(col)
-                else:
-                    dfb = col.to(ctx.fc_bias.dtype)
-        given = getattr(ctx, "_dca_bias_given", None)
-        if given is not None:
-            ctx._dca_bias_given = None
-            if dy.data_ptr() == given.data_ptr() and dy.shape == given.shape and dy.stride() == given.stride():
-                return dz, dw, None, dfb
-            dy2 = (dy - given).reshape(-1, dy.shape[-1])
-        if b_param is not None and ctx.needs_input_grad[2]:
-            db = _bias_grad(b_param, dy2)
-        return dz, dw, db, dfb
-
-
-# the fused MLP backward of _GeluLinear (A/B switch; off = bias_gelu + linear as separate ops)
-FUSE_MLP_DGELU = os.environ.get("DCA_FUSE_MLP_DGELU", "0") == "1"
-
-
-def gelu_linear(z: torch.Tensor, fc_bias: torch.Tensor, weight: torch.Tensor,
-                bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``linear(bias_gelu(z, fc_bias), weight, bias)`` -- the MLP's second half -- with the fused
-    projection + dGELU backward on the GPU when the shapes fit the kernel."""
-    E, Fd = weight.shape
-    ok = (FUSE_MLP_DGELU and _gpu_ok(z) and z.dtype == torch.bfloat16 and weight.dtype == z.dtype and
-          fc_bias is not None and (bias is None or bias.dtype == z.dtype) and E % 64 == 0 and
-          Fd % 64 == 0 and z.shape[-1] == Fd and z.numel() < 2 ** 30 and
-          z.numel() // Fd * E < 2 ** 30 and not torch.is_autocast_enabled())
-    if not ok:
-        return linear(bias_gelu(z, fc_bias), weight, bias)
-    return _GeluLinear.apply(z, weight, bias, fc_bias)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -515,6 +446,6 @@ def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: b
     return _FlashAttention.apply(q, k, v, causal, float(scale), _kv_len(key_lengths, q.shape[0], q.device))
 
 
-__all__ = ["layer_norm", "bias_gelu", "gelu_linear", "rope", "rope_tables", "flash_attention",
+__all__ = ["layer_norm", "bias_gelu", "rope", "rope_tables", "flash_attention",
            "flash_attention_qkvpacked", "cross_entropy",
            "reference_layer_norm", "reference_bias_gelu", "reference_rope", "reference_attention"]

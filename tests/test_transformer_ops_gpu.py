@@ -493,73 +493,3 @@ def test_hipblaslt_epilogue_probe_runs():
     assert C.lt_probe(1, 1024, 4096, 1024, True, False, -1, -1, False) > 0
     assert C.lt_probe(4, 1024, 4096, 1024, True, False, 0, -1, True) > 0
 
-
-@pytest.mark.parametrize("T_,E,F", [(333, 768, 3072), (8192, 768, 3072), (1000, 1024, 4096), (96, 64, 128)])
-def test_linear_dgelu_kernel(T_, E, F):
-    """linear_dgelu (the implicit-GEMM kernel with the dGELU epilogue) against fp32 torch:
-    dz = (dy @ w2) * gelu'(z + b) and the per-tile column sums of dz (the fc bias gradient)."""
-    C = _C()
-    torch.manual_seed(0)
-    dy = torch.randn(T_, E, device="cuda").bfloat16()
-    w2 = (torch.randn(E, F, device="cuda") * E ** -0.5).bfloat16()
-    z = torch.randn(T_, F, device="cuda").bfloat16()
-    b = torch.randn(F, device="cuda") * 0.5
-    dz, partial = C.linear_dgelu(dy, w2, z, b)
-    zr = (z.float() + b).requires_grad_(True)
-    torch.nn.functional.gelu(zr, approximate="tanh").backward(dy.float() @ w2.float())
-    assert dz.shape == (T_, F) and dz.dtype == torch.bfloat16
-    assert _rel(dz, zr.grad) < 1e-2
-    assert _rel(partial[:, 0].sum(0), zr.grad.sum(0)) < 1e-2
-
-
-@pytest.mark.parametrize("ln_consumer", [False, True])
-def test_gelu_linear_fused_backward(ln_consumer, monkeypatch):
-    """gelu_linear (fused projection + dGELU backward) against the unfused bias_gelu + linear
-    pair and an fp32 autograd reference: input, weight and both bias gradients, accumulated into
-    flat .grad views over two backward passes; the LayerNorm bias hand-off still applies."""
-    _C()
-    monkeypatch.setattr(T, "FUSE_MLP_DGELU", True)
-    torch.manual_seed(0)
-    E, F = 768, 3072
-    z = torch.randn(4, 512, F, device="cuda").bfloat16()
-    g = torch.randn(4, 512, E, device="cuda").bfloat16()
-    resid = torch.randn(4, 512, E, device="cuda").bfloat16()
-    w = (torch.randn(E, F, device="cuda") * 0.02).bfloat16()
-    bias = torch.randn(E, device="cuda").bfloat16()
-    fb = (torch.randn(F, device="cuda") * 0.5).bfloat16()
-    out = {}
-    for mode in ("fused", "unfused"):
-        ps = [torch.nn.Parameter(t.clone()) for t in (w, bias, fb)]
-        space, calls = _flat(ps)
-        zs = z.clone().requires_grad_(True)
-        for _ in range(2):
-            if mode == "fused":
-                y = T.gelu_linear(zs, ps[2], ps[0], ps[1])
-                assert type(y.grad_fn).__name__ == "_GeluLinearBackward"
-            else:
-                y = T.linear(T.bias_gelu(zs, ps[2]), ps[0], ps[1])
-            if ln_consumer:
-                o, s = T.layer_norm(resid, None, None, 1e-5, residual=y)
-                loss = (o.float() * g.float()).sum() + s.float().square().mean()
-            else:
-                loss = (y.float() * g.float()).sum()
-            loss.backward()
-        from determined_clone_amd.ops import _grad
-
-        _grad.join()
-        assert len(calls) == 2 * 3
-        out[mode] = [zs.grad.float()] + [p.grad.float().clone() for p in ps]
-    zr = z.float().requires_grad_(True)
-    pr = [t.float().requires_grad_(True) for t in (w, bias, fb)]
-    for _ in range(2):
-        yr = torch.nn.functional.linear(T.reference_bias_gelu(zr, pr[2]), pr[0], pr[1])
-        if ln_consumer:
-            o, s = T.reference_layer_norm(resid.float(), None, None, 1e-5, residual=yr)
-            lr = (o * g.float()).sum() + s.square().mean()
-        else:
-            lr = (yr * g.float()).sum()
-        lr.backward()
-    ref = [zr.grad] + [p.grad for p in pr]
-    for a, b, r in zip(out["fused"], out["unfused"], ref):
-        assert _rel(a, r) < 2e-2
-        assert _rel(a, b) < 2e-2
