@@ -590,11 +590,9 @@ def stem_conv(conv: nn.Conv2d, x: torch.Tensor, bn_stats: bool = False) -> torch
 # is skipped), the stride-1 data gradient runs on the same kernel (flipped, transposed weight).
 # Measured at bs 1024 against MIOpen (tools/bench_igemm.py, profiles/round4_igemm_v2_stages.txt):
 # forward at parity (5.23 vs 5.18 ms per step, before counting the statistics pass it removes),
-# stride-1 data gradient 4.16 vs 5.56 ms. 3x3 stride-2 data gradients run as four parity-class
-# implicit GEMMs (conv_igemm_dgrad_s2); weight gradients are chosen per shape (see _wgrad).
-# DCA_IGEMM=0 routes everything back to MIOpen.
+# stride-1 data gradient 4.16 vs 5.56 ms. Stride-2 data gradients and every weight gradient stay
+# on MIOpen (the latter on the side stream). DCA_IGEMM=0 routes everything back to MIOpen.
 IGEMM = os.environ.get("DCA_IGEMM", "1") != "0"
-IGEMM_DGRAD_S2 = os.environ.get("DCA_IGEMM_DGRAD_S2", "1") != "0"  # A/B switch (0: MIOpen)
 
 
 def igemm_supported(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -640,10 +638,6 @@ class _IgemmConv(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if st == 1:
                 dx = _ext.load().conv_igemm_dgrad(dy, w, pad)
-            elif (IGEMM_DGRAD_S2 and st == 2 and pad == 1 and w.shape[2] == 3 and w.shape[3] == 3
-                  and x.shape[2] == 2 * dy.shape[2] and x.shape[3] == 2 * dy.shape[3]):
-                # parity-class implicit GEMMs: no zero-filled, atomically accumulated dx (MIOpen)
-                dx = _ext.load().conv_igemm_dgrad_s2(dy, w, x.shape[2], x.shape[3])
             else:
                 dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
         return dx, dw, None, None, None

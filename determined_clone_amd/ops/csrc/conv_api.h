@@ -9,10 +9,6 @@ namespace dca {
 // y [N][P][Q][K], all bf16; C and K multiples of 64; N*H*W*C and N*P*Q*K below 2^31.
 struct ConvGeom {
   int N, H, W, C, K, P, Q, R, S, stride, pad, M;  // M = N*P*Q
-  // Output placement (forward kernel): os = 0 stores y[m][K] densely; os > 0 stores output pixel
-  // (n, p, q) at row (n * OH + p * os + oa) * OW + q * os + ob of an [N][OH][OW][K] tensor -- one
-  // parity class of a stride-2 data gradient (conv_igemm_dgrad_s2).
-  int os = 0, oa = 0, ob = 0, OH = 0, OW = 0;
 };
 // Row blocks of the forward = first dimension of its [blocks][2][K] BatchNorm partial statistics.
 int conv_igemm_row_blocks(const ConvGeom& g);

@@ -99,56 +99,6 @@ Tensor conv_igemm_dgrad(const Tensor& dy_in, const Tensor& w, int64_t pad) {
   return dx;
 }
 
-// dx of a 3x3, stride-2, padding-1 convolution (the downsampling 3x3 of a ResNet block) without
-// MIOpen's zero-filled, atomically accumulated dx: output pixel (2i + a, 2j + b) only receives the
-// taps r with r = a + 1 - 2t (t = 0, 1 -> input row i + t), so each parity class (a, b) is a
-// stride-1 implicit GEMM over dy with a 1x1, 1x2, 2x1 or 2x2 kernel (padding 0; the row / column past
-// dy's edge reads as zero) whose epilogue stores straight into the class's interleaved dx positions.
-// Every dx element is written exactly once (H = 2P, W = 2Q).
-Tensor conv_igemm_dgrad_s2(const Tensor& dy_in, const Tensor& w, int64_t H, int64_t W) {
-  const Tensor dy = dy_in.contiguous(at::MemoryFormat::ChannelsLast);
-  const c10::DeviceGuard dg(dy.device());
-  check_nhwc(dy, "conv_igemm_dgrad_s2");
-  TORCH_CHECK(w.dim() == 4 && w.size(0) == dy.size(1) && w.size(1) % 64 == 0 && w.size(2) == 3 &&
-                  w.size(3) == 3 && w.scalar_type() == at::kBFloat16,
-              "conv_igemm_dgrad_s2: bf16 3x3 weight [K, C, 3, 3], C a multiple of 64");
-  const int64_t N = dy.size(0), K = dy.size(1), P = dy.size(2), Q = dy.size(3), C = w.size(1);
-  TORCH_CHECK(H == 2 * P && W == 2 * Q, "conv_igemm_dgrad_s2: input must be exactly twice the output size");
-  TORCH_CHECK(N * C * H * W < (int64_t{1} << 30), "conv_igemm_dgrad_s2: dx too large for 32-bit offsets");
-  Tensor dx = torch::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  for (int a = 0; a < 2; ++a)
-    for (int b = 0; b < 2; ++b) {
-      // taps of this class in input-offset order t = 0, 1: r = a + 1 - 2t
-      const std::vector<int64_t> rs = a == 0 ? std::vector<int64_t>{1} : std::vector<int64_t>{2, 0};
-      const std::vector<int64_t> ss = b == 0 ? std::vector<int64_t>{1} : std::vector<int64_t>{2, 0};
-      const Tensor ri = torch::tensor(rs, torch::dtype(torch::kLong)).to(w.device());
-      const Tensor si = torch::tensor(ss, torch::dtype(torch::kLong)).to(w.device());
-      // [C][Rc][Sc][K] = channels_last [C, K, Rc, Sc]
-      const Tensor wc = w.index_select(2, ri).index_select(3, si).permute({1, 0, 2, 3})
-                            .contiguous(at::MemoryFormat::ChannelsLast);
-      dca::ConvGeom g;
-      g.N = static_cast<int>(N);
-      g.H = static_cast<int>(P);
-      g.W = static_cast<int>(Q);
-      g.C = static_cast<int>(K);
-      g.K = static_cast<int>(C);
-      g.R = static_cast<int>(rs.size());
-      g.S = static_cast<int>(ss.size());
-      g.stride = 1;
-      g.pad = 0;
-      g.P = static_cast<int>(P);
-      g.Q = static_cast<int>(Q);
-      g.M = static_cast<int>(N * P * Q);
-      g.os = 2;
-      g.oa = a;
-      g.ob = b;
-      g.OH = static_cast<int>(H);
-      g.OW = static_cast<int>(W);
-      dca::conv_igemm_fwd(dy.data_ptr(), wc.data_ptr(), dx.data_ptr(), nullptr, g, stream());
-    }
-  return dx;
-}
-
 // Weight gradient of y = conv2d(x, w, stride, pad) given dy; with `acc` (the parameter's
 // persistent .grad view, fp32 or bf16, [K, C, R, S] channels_last) it is added in place and
 // returned.
@@ -229,8 +179,6 @@ void register_conv_ops(pybind11::module& m) {
         pybind11::arg("acc") = pybind11::none());
   m.def("conv_igemm_fwd", &conv_igemm_fwd, pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("stats"));
-  m.def("conv_igemm_dgrad_s2", &conv_igemm_dgrad_s2, pybind11::arg("dy"), pybind11::arg("w"),
-        pybind11::arg("H"), pybind11::arg("W"));
   m.def("conv_igemm_dgrad", &conv_igemm_dgrad, pybind11::arg("dy"), pybind11::arg("w"),
         pybind11::arg("pad"));
 }

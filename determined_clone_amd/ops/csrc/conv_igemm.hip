@@ -286,12 +286,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_fwd_kernel(
   for (int row = rr; row < BM; row += RPP) {
     if (m0 + row >= g.M) break;
     const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CS + cc * 8);
-    int64_t orow = m0 + row;
-    if (g.os) {  // a parity class of a stride-2 data gradient: interleaved placement
-      const int n = (m0 + row) / PQ, rem = m0 + row - n * PQ, p = rem / g.Q, q = rem - p * g.Q;
-      orow = (static_cast<int64_t>(n) * g.OH + p * g.os + g.oa) * g.OW + q * g.os + g.ob;
-    }
-    const int64_t off = orow * g.K + n0 + cc * 8;
+    const int64_t off = static_cast<int64_t>(m0 + row) * g.K + n0 + cc * 8;
     *reinterpret_cast<uint4*>(y + off) = v;
     if constexpr (STATS) {
       const float f[8] = {bf16_lo(v.x), bf16_hi(v.x), bf16_lo(v.y), bf16_hi(v.y),
