@@ -214,3 +214,87 @@ def test_inplace_reduce_scatter_offsets_per_bucket(world):
             base = torch.arange(_rs_len(world), dtype=torch.float32)[lo:hi]
             torch.testing.assert_close(after[lo:hi], world * base + 1000 * sum(range(world)))
         torch.testing.assert_close(o["avg"], torch.tensor([(world + 1) / 2]))
+
+
+class _LazyWork:
+    """An all_gather_into_tensor that runs only when waited for: the behaviour of RCCL's async
+    collectives (gloo's host collectives complete inside the call, which hides deferral bugs)."""
+
+    def __init__(self, fn, args, kwargs):
+        self.fn, self.args, self.kwargs, self.done = fn, args, kwargs, False
+
+    def wait(self):
+        if not self.done:
+            self.fn(*self.args, **self.kwargs)
+            self.done = True
+        return True
+
+
+class _Functional(torch.nn.Module):
+    """Uses a child's weight functionally (the child's own forward never runs, so its forward
+    pre-hook -- where deferred gathers are normally waited for -- never fires)."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.a = torch.nn.Linear(16, 40)
+        self.b = torch.nn.Linear(40, 4)
+
+    def forward(self, x):
+        return torch.nn.functional.linear(torch.tanh(self.a(x)), self.b.weight, self.b.bias)
+
+
+def _lazy_worker(rank, world, port, out_dir):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    dist = torch.distributed
+    real = dist.all_gather_into_tensor
+
+    def lazy(*a, async_op=False, **k):
+        if not async_op:
+            return real(*a, **k)
+        return _LazyWork(real, a, k)
+    dist.all_gather_into_tensor = lazy
+    m = _Functional()
+    opt = zero.zero_optimizer_for("adam")(_groups(m), lr=0.05, stage=2, bucket_mb=0.002,
+                                          first_bucket_mb=0.0005)
+    opt.attach_module(m)
+    x, y = _data()
+    per = x.shape[0] // world
+    deferred = []
+    for _ in range(STEPS):
+        # the contract for parameters read outside their module's forward: wait_params() first
+        # (DeepSpeed engine zero_grad / the trial controller's evaluation entry do this)
+        deferred.append(len(opt._gather_pending))
+        opt.wait_params()
+        opt.zero_grad()
+        xb, yb = x[rank * per:(rank + 1) * per], y[rank * per:(rank + 1) * per]
+        torch.nn.functional.mse_loss(m(xb), yb).backward()
+        opt.finish_grad_sync()
+        opt.step()
+    opt.wait_params()
+    torch.save({"params": {k: v.detach().clone() for k, v in m.state_dict().items()},
+                "deferred": deferred}, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_deferred_param_gather_with_functional_weight_use():
+    """with overlap_param_gather the post-step all-gathers stay in flight (lazily, as on
+    RCCL) and only a module's own forward pre-hook waits for them; a parent that reads a child's
+    weight functionally must call wait_params() first. With that contract the 2-rank ZeRO-2 run
+    equals the full-batch reference, and the gathers really were deferred after every step."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_lazy_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        outs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    ref = _Functional()
+    opt = fopt.FusedAdam(_groups(ref), lr=0.05)
+    x, y = _data()
+    for _ in range(STEPS):
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(ref(x), y).backward()
+        opt.step()
+    for o in outs:
+        assert o["deferred"][0] == 0 and all(n > 0 for n in o["deferred"][1:]), o["deferred"]
+        for k, v in ref.state_dict().items():
+            torch.testing.assert_close(o["params"][k], v, atol=1e-5, rtol=1e-5)
