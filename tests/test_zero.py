@@ -55,9 +55,13 @@ def _count_collectives():
     return calls
 
 
-def _worker(rank, world, port, stage, kind, max_norm, bucket_mb, out_dir, defer=False):
+def _worker(rank, world, port, stage, kind, max_norm, bucket_mb, out_dir, defer=False, lazy=False):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    if lazy:  # RCCL-like async collectives: data moves only at wait()
+        from tests import lazy_collectives
+
+        lazy_collectives.install()
     calls = _count_collectives()
     m = _model()
     cls = zero.zero_optimizer_for(kind)
@@ -98,22 +102,26 @@ def _reference(kind, max_norm):
     return m, opt
 
 
-@pytest.mark.parametrize("world,stage,kind,max_norm,bucket_mb,defer", [
-    (2, 1, "adam", 0.0, 64.0, False),
-    (2, 2, "adam", 0.0, 0.002, True),   # many small buckets: hooks fire bucket by bucket
-    (2, 2, "adamw", 0.05, 0.002, False),  # global-norm clipping across shards
-    (2, 2, "sgd", 0.0, 0.001, True),
+@pytest.mark.parametrize("world,stage,kind,max_norm,bucket_mb,defer,lazy", [
+    (2, 1, "adam", 0.0, 64.0, False, False),
+    (2, 2, "adam", 0.0, 0.002, True, False),   # many small buckets: hooks fire bucket by bucket
+    (2, 2, "adamw", 0.05, 0.002, False, False),  # global-norm clipping across shards
+    (2, 2, "sgd", 0.0, 0.001, True, False),
     # the driver's 8-GPU layout: 1764 parameters (not a multiple of 8, so the
     # last shard is padded), 500-float buckets (boundaries inside the 640- and 960-element weights),
     # 8 deferred gathers in flight, clipping over 8 shards
-    (4, 2, "adamw", 0.05, 0.002, True),
-    (8, 1, "adam", 0.0, 64.0, False),
-    (8, 2, "adamw", 0.05, 0.002, True),
+    (4, 2, "adamw", 0.05, 0.002, True, False),
+    (8, 1, "adam", 0.0, 64.0, False, False),
+    (8, 2, "adamw", 0.05, 0.002, True, False),
+    # RCCL-like lazy collectives (tests/lazy_collectives.py): a reduce-scatter / gather output read
+    # before its wait would show here
+    (2, 2, "adamw", 0.05, 0.002, True, True),
+    (4, 1, "adam", 0.0, 0.002, True, True),
 ])
-def test_zero_matches_full_batch(world, stage, kind, max_norm, bucket_mb, defer):
+def test_zero_matches_full_batch(world, stage, kind, max_norm, bucket_mb, defer, lazy):
     assert sum(p.numel() for p in _model().parameters()) % 8 != 0  # padded last shard at world 8
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), stage, kind, max_norm, bucket_mb, d, defer),
+        mp.spawn(_worker, args=(world, _free_port(), stage, kind, max_norm, bucket_mb, d, defer, lazy),
                  nprocs=world, join=True)
         ref, ref_opt = _reference(kind, max_norm)
         outs = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
@@ -216,20 +224,6 @@ def test_inplace_reduce_scatter_offsets_per_bucket(world):
         torch.testing.assert_close(o["avg"], torch.tensor([(world + 1) / 2]))
 
 
-class _LazyWork:
-    """An all_gather_into_tensor that runs only when waited for: the behaviour of RCCL's async
-    collectives (gloo's host collectives complete inside the call, which hides deferral bugs)."""
-
-    def __init__(self, fn, args, kwargs):
-        self.fn, self.args, self.kwargs, self.done = fn, args, kwargs, False
-
-    def wait(self):
-        if not self.done:
-            self.fn(*self.args, **self.kwargs)
-            self.done = True
-        return True
-
-
 class _Functional(torch.nn.Module):
     """Uses a child's weight functionally (the child's own forward never runs, so its forward
     pre-hook -- where deferred gathers are normally waited for -- never fires)."""
@@ -247,14 +241,10 @@ class _Functional(torch.nn.Module):
 def _lazy_worker(rank, world, port, out_dir):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
-    dist = torch.distributed
-    real = dist.all_gather_into_tensor
+    from tests import lazy_collectives
 
-    def lazy(*a, async_op=False, **k):
-        if not async_op:
-            return real(*a, **k)
-        return _LazyWork(real, a, k)
-    dist.all_gather_into_tensor = lazy
+    lazy_collectives.install()  # RCCL-like: gathers / reduce-scatters move data only at wait()
+    dist = torch.distributed
     m = _Functional()
     opt = zero.zero_optimizer_for("adam")(_groups(m), lr=0.05, stage=2, bucket_mb=0.002,
                                           first_bucket_mb=0.0005)

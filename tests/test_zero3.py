@@ -88,9 +88,13 @@ def test_stage3_single_process_matches_stage0():
     assert all(u.full.untyped_storage().size() == 0 for u in z3.units)
 
 
-def _worker(rank: int, world: int, port: int, out: str, gb: int = 4) -> None:
+def _worker(rank: int, world: int, port: int, out: str, gb: int = 4, lazy: bool = False) -> None:
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    if lazy:  # RCCL-like async collectives: data moves only at wait() (tests/lazy_collectives.py)
+        from tests import lazy_collectives
+
+        lazy_collectives.install()
     eng = _engine(3, micro=gb // world)
     shard = sum(u.shard_numel for u in eng._z3.units)
     full = sum(u.padded for u in eng._z3.units)
@@ -114,12 +118,13 @@ def _worker(rank: int, world: int, port: int, out: str, gb: int = 4) -> None:
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_stage3_multi_rank_matches_single_process(tmp_path, world):
+@pytest.mark.parametrize("world,lazy", [(2, False), (8, False), (2, True), (4, True)])
+def test_stage3_multi_rank_matches_single_process(tmp_path, world, lazy):
     """2 ranks, and the driver's 8-rank layout (per-unit shards padded to 8, 8
-    reduce-scatters / all-gathers per unit) against one process on the full batch."""
+    reduce-scatters / all-gathers per unit) against one process on the full batch; ``lazy``: the
+    per-unit gathers and reduce-scatters complete only when waited for (RCCL semantics)."""
     gb = 4 if world == 2 else 8
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), gb), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), gb, lazy), nprocs=world, join=True)
     res = torch.load(tmp_path / "final.pt", weights_only=True)
     ref = _engine(0, micro=gb)
     _train(ref, gb=gb)
