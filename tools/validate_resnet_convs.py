@@ -5,7 +5,8 @@ computed in 64-image chunks (torch.nn.grad on fp32 copies of the same bf16 input
 
 The shipped tuning artefacts pick kernels by speed alone; this checks, at the exact shapes the
 bench runs, that what they picked computes the right numbers (profiles/round6_tuned_gemm_validation.txt).
-Prints one JSON line per distinct convolution and a summary. Usage: python tools/validate_resnet_convs.py"""
+Prints one JSON line per distinct convolution and a summary.
+Usage: python tools/validate_resnet_convs.py [--batch 1024]"""
 import json
 import os
 import sys
@@ -110,6 +111,12 @@ def check(kind, convs, shape, bn_stats, g):
 
 
 def main():
+    global BATCH
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=BATCH)
+    BATCH = ap.parse_args().batch
     torch.manual_seed(0)
     model = resnet.to_mi355x_layout(resnet.resnet50()).cuda().train()
     calls = record_calls(model)
